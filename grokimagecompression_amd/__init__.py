@@ -1,0 +1,269 @@
+"""grokimagecompression_amd -- MI355X-native JPEG 2000 hot path, Grok-compatible.
+
+Python host mirror of the reference's compress / decompress entry points
+(grk_compress / grk_decompress, Grok v5.1.0) over the C ABI in
+include/grk_mi355x.h (libgrk_mi355x.so, built in-tree under lib/).
+
+    import grokimagecompression_amd as grk
+    codec = grk.Codec(device=0)
+    j2k = codec.compress(img, prec=8)                 # img: (c,h,w) int32 numpy or torch.cuda tensor
+    out = codec.decompress(j2k)                       # numpy (c,h,w) int32
+    out = codec.decompress(j2k, device_out=True)      # torch.cuda tensor
+
+The product path never falls back to the CPU: if the extension is missing or
+no gfx950 device is present, every entry point raises GrkGpuError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgrk_mi355x.so")
+MAXC = 16
+
+__all__ = ["Codec", "CParams", "GrkGpuError", "lib", "build", "read_header"]
+
+
+class GrkGpuError(RuntimeError):
+    pass
+
+
+class ImageDesc(ctypes.Structure):
+    _fields_ = [("x0", ctypes.c_uint32), ("y0", ctypes.c_uint32), ("x1", ctypes.c_uint32), ("y1", ctypes.c_uint32),
+                ("numcomps", ctypes.c_uint32), ("prec", ctypes.c_uint32 * MAXC), ("sgnd", ctypes.c_int32 * MAXC)]
+
+
+class CParams(ctypes.Structure):
+    """grk_cparameters subset (grok.h:447-570)."""
+    _fields_ = [("numresolution", ctypes.c_uint32), ("cblockw_init", ctypes.c_uint32),
+                ("cblockh_init", ctypes.c_uint32), ("irreversible", ctypes.c_int32), ("tcp_mct", ctypes.c_int32),
+                ("tile_size_on", ctypes.c_int32), ("cp_tdx", ctypes.c_uint32), ("cp_tdy", ctypes.c_uint32),
+                ("cp_tx0", ctypes.c_uint32), ("cp_ty0", ctypes.c_uint32)]
+
+    @classmethod
+    def make(cls, numresolution=6, cblk=(64, 64), irreversible=False, mct=-1, tiles=None, tile_offset=(0, 0)):
+        p = cls()
+        lib().grkgpu_default_cparams(ctypes.byref(p))
+        p.numresolution = numresolution
+        p.cblockw_init, p.cblockh_init = cblk
+        p.irreversible = 1 if irreversible else 0
+        p.tcp_mct = mct
+        if tiles:
+            p.tile_size_on = 1
+            p.cp_tdx, p.cp_tdy = tiles
+            p.cp_tx0, p.cp_ty0 = tile_offset
+        return p
+
+    @classmethod
+    def from_cli(cls, args):
+        """Map grk_compress command-line options (-I -n -b -t -T -Y) to params;
+        returns (params, image_offset)."""
+        kw, off, i = {}, (0, 0), 0
+        while i < len(args):
+            a = args[i]
+            if a == "-I":
+                kw["irreversible"] = True
+            elif a == "-n":
+                kw["numresolution"] = int(args[i + 1]); i += 1
+            elif a == "-b":
+                kw["cblk"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
+            elif a == "-t":
+                kw["tiles"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
+            elif a == "-T":
+                kw["tile_offset"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
+            elif a == "-Y":
+                kw["mct"] = int(args[i + 1]); i += 1
+            elif a == "-d":
+                off = tuple(int(v) for v in args[i + 1].split(",")); i += 1
+            else:
+                raise ValueError("unsupported grk_compress option %s" % a)
+            i += 1
+        return cls.make(**kw), off
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("h2d_ms", ctypes.c_float), ("dcshift_mct_ms", ctypes.c_float), ("dwt_ms", ctypes.c_float),
+                ("t1_ms", ctypes.c_float), ("gather_ms", ctypes.c_float), ("d2h_ms", ctypes.c_float),
+                ("host_t2_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("num_cblks", ctypes.c_uint64),
+                ("cs_bytes", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+_EXPORTS = None
+
+
+def build():
+    """Compile libgrk_mi355x.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GrkGpuError("libgrk_mi355x.so not built (run grokimagecompression_amd.build()); "
+                              "there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        P, U32, I32, VP = ctypes.POINTER, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p
+        L.grkgpu_version.restype = ctypes.c_char_p
+        L.grkgpu_last_error.restype = ctypes.c_char_p
+        L.grkgpu_create.argtypes = [ctypes.c_int, P(VP)]
+        L.grkgpu_destroy.argtypes = [VP]
+        L.grkgpu_set_stream.argtypes = [VP, VP]
+        L.grkgpu_get_stats.argtypes = [VP, P(Stats)]
+        L.grkgpu_default_cparams.argtypes = [P(CParams)]
+        L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
+                                      P(ctypes.c_size_t)]
+        L.grkgpu_read_header.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P(ImageDesc)]
+        L.grkgpu_decompress.argtypes = [VP, ctypes.c_char_p, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
+        L.grkgpu_free.argtypes = [VP]
+        L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
+        L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
+        L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
+        L.grkgpu_dwt_inv.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
+        L.grkgpu_t1_scratch_bytes.restype = ctypes.c_size_t
+        L.grkgpu_t1_encode_blocks.argtypes = [VP, U32, VP, VP, VP, VP, VP]
+        L.grkgpu_t1_decode_blocks.argtypes = [VP, U32, VP, VP, VP, VP]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise GrkGpuError("grkgpu error %d: %s" % (rc, lib().grkgpu_last_error().decode()))
+
+
+def read_header(buf):
+    d = ImageDesc()
+    _check(lib().grkgpu_read_header(bytes(buf), len(buf), ctypes.byref(d)))
+    return d
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(device):
+    torch = _torch()
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Codec:
+    """One HIP context (device, stream, device-memory arenas) per instance."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self._ctx = ctypes.c_void_p()
+        _check(lib().grkgpu_create(device, ctypes.byref(self._ctx)))
+
+    def close(self):
+        if self._ctx:
+            lib().grkgpu_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        s = Stats()
+        _check(lib().grkgpu_get_stats(self._ctx, ctypes.byref(s)))
+        return s.as_dict()
+
+    def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False):
+        """img: (c,h,w) int32 numpy array (host) or torch tensor on cuda:<device>.
+        Returns the .j2k codestream as bytes."""
+        params = params or CParams.make()
+        c, h, w = img.shape
+        d = ImageDesc()
+        d.x0, d.y0 = offset
+        d.x1, d.y1 = offset[0] + w, offset[1] + h
+        d.numcomps = c
+        for k in range(c):
+            d.prec[k] = prec
+            d.sgnd[k] = 1 if sgnd else 0
+        on_dev = not isinstance(img, np.ndarray)
+        if on_dev:
+            torch = _torch()
+            assert img.dtype == torch.int32 and img.is_cuda and img.is_contiguous()
+            lib().grkgpu_set_stream(self._ctx, _stream_handle(img.device))
+            ptrs = (ctypes.c_void_p * c)(*[img[k].data_ptr() for k in range(c)])
+        else:
+            img = np.ascontiguousarray(img, dtype=np.int32)
+            ptrs = (ctypes.c_void_p * c)(*[img[k].ctypes.data for k in range(c)])
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _check(lib().grkgpu_compress(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0,
+                                     ctypes.byref(out), ctypes.byref(n)))
+        b = ctypes.string_at(out, n.value)
+        lib().grkgpu_free(out)
+        return b
+
+    def decompress(self, buf, device_out=False, out=None):
+        """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
+        device_out / out is a cuda tensor)."""
+        buf = bytes(buf)
+        d = read_header(buf)
+        c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
+        on_dev = device_out or (out is not None and not isinstance(out, np.ndarray))
+        if on_dev:
+            torch = _torch()
+            if out is None:
+                out = torch.empty((c, h, w), dtype=torch.int32, device="cuda:%d" % self.device)
+            lib().grkgpu_set_stream(self._ctx, _stream_handle(out.device))
+            ptrs = (ctypes.c_void_p * c)(*[out[k].data_ptr() for k in range(c)])
+        else:
+            if out is None:
+                out = np.empty((c, h, w), dtype=np.int32)
+            ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
+        _check(lib().grkgpu_decompress(self._ctx, buf, len(buf), None, ptrs, 1 if on_dev else 0))
+        return out
+
+
+# ---- stage entry points on torch device tensors (per-kernel parity tests) ----
+
+def dwt_fwd(t, x0, y0, numres, irreversible):
+    """In-place forward DWT of a (h,w) int32 cuda tensor (Mallat layout)."""
+    torch = _torch()
+    h, w = t.shape
+    scratch = torch.empty(2 * h * w + 256, dtype=torch.int32, device=t.device)
+    _check(lib().grkgpu_dwt_fwd(t.data_ptr(), scratch.data_ptr(), x0, y0, x0 + w, y0 + h, numres,
+                                1 if irreversible else 0, _stream_handle(t.device)))
+    return t
+
+
+def dwt_inv(t, x0, y0, numres, irreversible):
+    torch = _torch()
+    h, w = t.shape
+    scratch = torch.empty(2 * h * w + 256, dtype=torch.int32, device=t.device)
+    _check(lib().grkgpu_dwt_inv(t.data_ptr(), scratch.data_ptr(), x0, y0, x0 + w, y0 + h, numres,
+                                1 if irreversible else 0, _stream_handle(t.device)))
+    return t
+
+
+def dcshift_mct_fwd(planes, shifts, mct, irreversible):
+    """planes: (c,h,w) int32 cuda tensor, modified in place."""
+    c, h, w = planes.shape
+    ptrs = (ctypes.c_void_p * c)(*[planes[k].data_ptr() for k in range(c)])
+    sh = (ctypes.c_int32 * c)(*shifts)
+    _check(lib().grkgpu_dcshift_mct_fwd(ptrs, c, w, h, w, sh, mct, 1 if irreversible else 0,
+                                        _stream_handle(planes.device)))
+    return planes
+
+
+def mct_inv_dcshift(planes, prec, sgnd, mct, irreversible):
+    c, h, w = planes.shape
+    ptrs = (ctypes.c_void_p * c)(*[planes[k].data_ptr() for k in range(c)])
+    pr = (ctypes.c_uint32 * c)(*([prec] * c))
+    sg = (ctypes.c_int32 * c)(*([1 if sgnd else 0] * c))
+    _check(lib().grkgpu_mct_inv_dcshift(ptrs, c, w, h, w, pr, sg, mct, 1 if irreversible else 0,
+                                        _stream_handle(planes.device)))
+    return planes

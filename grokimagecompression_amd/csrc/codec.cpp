@@ -1,0 +1,754 @@
+// codec.cpp -- tile pipeline (the reference's TileProcessor, "tcd") turned into
+// a HIP dispatch layer, plus the extern "C" API of include/grk_mi355x.h.
+//
+// Encode (TileProcessor::encode_tile, TileProcessor.cpp:951-1025):
+//   H2D planes (if host) -> per tile: DC shift + MCT kernel -> per component
+//   DWT levels -> ONE T1 launch over every code-block of every tile ->
+//   D2H per-block results -> gather kernel packs block bytes -> D2H ->
+//   host Tier-2 + headers.
+// Decode (TileProcessor::decode_tile, TileProcessor.cpp:1069-1179):
+//   host header + Tier-2 parse -> H2D codestream -> ONE T1 decode launch ->
+//   per tile/component inverse DWT levels -> inverse MCT + DC shift.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/grk_mi355x.h"
+#include "codestream.h"
+#include "grk_device.h"
+
+using namespace grkgpu;
+
+static thread_local std::string g_err;
+static int set_err(int code, const std::string &msg) { g_err = msg; return code; }
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return set_err(GRKGPU_EHIP, std::string(#expr ": ") + hipGetErrorString(e_));    \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr; cap = 0;
+        size_t nb = bytes + bytes / 8 + 256;
+        hipError_t e = hipMalloc(&p, nb);
+        if (e == hipSuccess) cap = nb;
+        return e;
+    }
+    template <typename T> T *as() const { return (T *)p; }
+    ~DevBuf() { if (p) hipFree(p); }
+};
+
+struct HostBuf {  // pinned host staging
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr; cap = 0;
+        size_t nb = bytes + bytes / 8 + 256;
+        hipError_t e = hipHostMalloc(&p, nb, hipHostMallocDefault);
+        if (e == hipSuccess) cap = nb;
+        return e;
+    }
+    template <typename T> T *as() const { return (T *)p; }
+    ~HostBuf() { if (p) hipHostFree(p); }
+};
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct grkgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs;
+    HostBuf h_results, h_packed, h_gather, h_blocks;
+    hipEvent_t ev[8] = {};
+    grkgpu_stats stats = {};
+};
+
+static int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return set_err(GRKGPU_ENODEV, "no HIP device available (MI355X / gfx950 required; no CPU fallback)");
+    if (device < 0 || device >= n) return set_err(GRKGPU_ENODEV, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return set_err(GRKGPU_ENODEV, "hipGetDeviceProperties failed");
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return set_err(GRKGPU_ENODEV, std::string("unsupported device arch ") + prop.gcnArchName + " (gfx950 required)");
+    return GRKGPU_OK;
+}
+
+extern "C" {
+
+const char *grkgpu_version(void) { return "grk-mi355x 0.1.0 (Grok 5.1.0 codestream-compatible)"; }
+const char *grkgpu_last_error(void) { return g_err.c_str(); }
+
+int grkgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void grkgpu_default_cparams(grkgpu_cparams *p) {
+    memset(p, 0, sizeof(*p));
+    p->numresolution = 6;
+    p->cblockw_init = 64;
+    p->cblockh_init = 64;
+    p->irreversible = 0;
+    p->tcp_mct = -1;
+}
+
+int grkgpu_create(int device, grkgpu_ctx **out) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(device));
+    auto *c = new grkgpu_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_err(GRKGPU_EHIP, "hipStreamCreate failed");
+    }
+    c->own_stream = true;
+    for (auto &e : c->ev) hipEventCreate(&e);
+    *out = c;
+    return GRKGPU_OK;
+}
+
+void grkgpu_destroy(grkgpu_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    for (auto &e : c->ev) if (e) hipEventDestroy(e);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int grkgpu_set_stream(grkgpu_ctx *c, void *stream) {
+    if (!c) return set_err(GRKGPU_EINVAL, "null ctx");
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    c->stream = (hipStream_t)stream;
+    c->own_stream = false;
+    return GRKGPU_OK;
+}
+
+int grkgpu_get_stats(grkgpu_ctx *c, grkgpu_stats *out) {
+    if (!c || !out) return set_err(GRKGPU_EINVAL, "null arg");
+    *out = c->stats;
+    return GRKGPU_OK;
+}
+
+void grkgpu_free(void *p) { free(p); }
+
+size_t grkgpu_t1_scratch_bytes(void) { return sizeof(BlockRows); }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// shared helpers
+// ---------------------------------------------------------------------------
+static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *p, CodingParams &cp) {
+    if (!img || !p) return set_err(GRKGPU_EINVAL, "null image/params");
+    if (img->numcomps < 1 || img->numcomps > 16) return set_err(GRKGPU_EINVAL, "numcomps must be 1..16");
+    if (img->x1 <= img->x0 || img->y1 <= img->y0) return set_err(GRKGPU_EINVAL, "empty image");
+    if (p->numresolution < 1 || p->numresolution > 33) return set_err(GRKGPU_EINVAL, "numresolution must be 1..33");
+    auto pow2 = [](uint32_t v) { return v >= 4 && v <= 64 && (v & (v - 1)) == 0; };
+    if (!pow2(p->cblockw_init) || !pow2(p->cblockh_init))
+        return set_err(GRKGPU_EINVAL, "code-block dimensions must be powers of two in [4, 64]");
+    cp.numcomps = img->numcomps;
+    cp.image = {img->x0, img->y0, img->x1, img->y1};
+    for (uint32_t k = 0; k < img->numcomps; ++k) {
+        if (img->prec[k] < 1 || img->prec[k] > 16) return set_err(GRKGPU_EUNSUPPORTED, "precision must be 1..16");
+        cp.prec[k] = img->prec[k];
+        cp.sgnd[k] = img->sgnd[k] ? 1 : 0;
+        cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
+    }
+    cp.numres = p->numresolution;
+    cp.cblkw = (uint32_t)floorlog2((int32_t)p->cblockw_init);
+    cp.cblkh = (uint32_t)floorlog2((int32_t)p->cblockh_init);
+    cp.irrev = p->irreversible ? 1 : 0;
+    cp.mct = p->tcp_mct < 0 ? (img->numcomps >= 3 ? 1 : 0) : (p->tcp_mct ? 1 : 0);
+    if (cp.mct && img->numcomps < 3) cp.mct = 0;
+    if (p->tile_size_on) {
+        if (!p->cp_tdx || !p->cp_tdy) return set_err(GRKGPU_EINVAL, "zero tile size");
+        if (p->cp_tx0 > img->x0 || p->cp_ty0 > img->y0 || (uint64_t)p->cp_tx0 + p->cp_tdx <= img->x0 ||
+            (uint64_t)p->cp_ty0 + p->cp_tdy <= img->y0)
+            return set_err(GRKGPU_EINVAL, "tile origin must satisfy tx0 <= x0 < tx0 + tdx");
+        cp.tdx = p->cp_tdx; cp.tdy = p->cp_tdy; cp.tx0 = p->cp_tx0; cp.ty0 = p->cp_ty0;
+        cp.tw = ceildiv(img->x1 - cp.tx0, cp.tdx);
+        cp.th = ceildiv(img->y1 - cp.ty0, cp.tdy);
+    } else {
+        cp.tx0 = cp.ty0 = 0;
+        cp.tdx = img->x1; cp.tdy = img->y1;
+        cp.tw = cp.th = 1;
+    }
+    if ((uint64_t)cp.tw * cp.th > 65535) return set_err(GRKGPU_EINVAL, "too many tiles");
+    generate_qcd(cp);
+    return GRKGPU_OK;
+}
+
+// Forward DWT of one tile-component: src -> coef (Mallat), ll scratch ping-pong.
+static hipError_t run_dwt_fwd(const int32_t *src, int32_t *coef, int32_t *llA, int32_t *llB, const TileComp &tc,
+                              int irrev, hipStream_t s) {
+    const uint32_t stride = tc.r.w();
+    const int32_t *in = src;
+    uint32_t instride = stride;
+    int32_t *bufs[2] = {llA, llB};
+    int flip = 0;
+    for (int lvl = 0; lvl + 1 < (int)tc.numres; ++lvl) {
+        const Rect &cur = tc.res[tc.numres - 1 - lvl].r;
+        const Rect &nxt = tc.res[tc.numres - 2 - lvl].r;
+        bool last = lvl + 2 == (int)tc.numres;
+        int32_t *llout = last ? coef : bufs[flip];
+        uint32_t llstride = last ? stride : nxt.w();
+        if (cur.w() && cur.h()) {
+            hipError_t e = launch_dwt_fwd_level(in, instride, llout, llstride, coef, stride, (int)cur.w(),
+                                                (int)cur.h(), (int)(cur.x0 & 1), (int)(cur.y0 & 1), (int)nxt.w(),
+                                                (int)nxt.h(), irrev, s);
+            if (e != hipSuccess) return e;
+        }
+        in = llout;
+        instride = llstride;
+        flip ^= 1;
+    }
+    if (tc.numres == 1)
+        return hipMemcpyAsync(coef, src, sizeof(int32_t) * (size_t)tc.r.w() * tc.r.h(), hipMemcpyDeviceToDevice, s);
+    return hipSuccess;
+}
+
+// Inverse DWT: coef (Mallat) -> dst, ll scratch ping-pong.
+static hipError_t run_dwt_inv(const int32_t *coef, int32_t *dst, int32_t *llA, int32_t *llB, const TileComp &tc,
+                              int irrev, hipStream_t s) {
+    const uint32_t stride = tc.r.w();
+    if (tc.numres == 1)
+        return hipMemcpyAsync(dst, coef, sizeof(int32_t) * (size_t)tc.r.w() * tc.r.h(), hipMemcpyDeviceToDevice, s);
+    const int32_t *ll = coef;
+    uint32_t llstride = stride;
+    int32_t *bufs[2] = {llA, llB};
+    int flip = 0;
+    for (uint32_t r = 1; r < tc.numres; ++r) {
+        const Rect &lo = tc.res[r - 1].r;
+        const Rect &cur = tc.res[r].r;
+        bool last = r + 1 == tc.numres;
+        int32_t *out = last ? dst : bufs[flip];
+        uint32_t ostride = last ? stride : cur.w();
+        if (cur.w() && cur.h()) {
+            hipError_t e = launch_dwt_inv_level(ll, llstride, coef, stride, out, ostride, (int)cur.w(), (int)cur.h(),
+                                                (int)(cur.x0 & 1), (int)(cur.y0 & 1), (int)lo.w(), (int)lo.h(),
+                                                irrev, s);
+            if (e != hipSuccess) return e;
+        }
+        ll = out;
+        llstride = ostride;
+        flip ^= 1;
+    }
+    return hipSuccess;
+}
+
+template <typename F>
+static void for_each_cblk(TileComp &tc, F f) {
+    for (uint32_t resno = 0; resno < tc.numres; ++resno) {
+        Resolution &res = tc.res[resno];
+        for (uint32_t b = 0; b < res.numbands; ++b) {
+            Band &band = res.bands[b];
+            for (auto &pr : band.precs)
+                for (auto &c : pr.cblks) f(band, c);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// encode
+// ---------------------------------------------------------------------------
+extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                               const int32_t *const *planes, int planes_on_device, uint8_t **out, size_t *outlen) {
+    if (!c || !planes || !out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    int rc = setup_params(img, p, cp);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    double t_start = now_ms();
+    const uint32_t nc = cp.numcomps, iw = cp.image.w(), ih = cp.image.h();
+    const uint64_t plane = (uint64_t)iw * ih;
+
+    // geometry for every tile, arena offsets, block table
+    const uint32_t ntiles = cp.tw * cp.th;
+    std::vector<Tile> tiles(ntiles);
+    uint64_t arena = 0, max_tc = 0;
+    std::vector<EncBlock> eb;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        Tile &tile = tiles[t];
+        tile.index = t;
+        tile.r = tile_rect(cp, t);
+        tile.comps.resize(nc);
+        for (uint32_t k = 0; k < nc; ++k) {
+            TileComp &tc = tile.comps[k];
+            build_tilecomp(tc, tile.r, cp, k, true);
+            tc.arena_off = arena;
+            uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
+            arena += (area + 63) & ~63ull;
+            max_tc = std::max(max_tc, area);
+            for_each_cblk(tc, [&](Band &band, Cblk &cb) {
+                cb.gidx = (uint32_t)eb.size();
+                EncBlock b;
+                b.coef_off = tc.arena_off + (uint64_t)cb.by * tile.r.w() + cb.bx;
+                b.out_off = 0;
+                b.stride = tile.r.w();
+                b.w = cb.r.w();
+                b.h = cb.r.h();
+                b.orient = band.bandno;
+                b.qmfbid = cp.irrev ? 0 : 1;
+                b.inv_step = (int32_t)band.inv_step;
+                eb.push_back(b);
+            });
+        }
+    }
+    const uint32_t nblk = (uint32_t)eb.size();
+    uint64_t out_total = 0;
+    for (auto &b : eb) {  // MQ output slab: w*h*4 bytes (+ the zero pad byte before)
+        out_total += 16;
+        b.out_off = out_total;
+        out_total += ((uint64_t)b.w * b.h * 4 + 64 + 15) & ~15ull;
+    }
+    HIPCHK(c->work.ensure(arena * 4 + 256));
+    HIPCHK(c->coef.ensure(arena * 4 + 256));
+    HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
+    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(BlockRows) + 256));
+    HIPCHK(c->mqout.ensure(out_total + 256));
+    HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
+    HIPCHK(c->results.ensure((size_t)nblk * sizeof(EncResult) + 256));
+    HIPCHK(c->h_results.ensure((size_t)nblk * sizeof(EncResult) + 256));
+    HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
+
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    // input planes on the device
+    PlanePtrs src{};
+    if (planes_on_device) {
+        for (uint32_t k = 0; k < nc; ++k) src.p[k] = (int32_t *)planes[k];
+    } else {
+        HIPCHK(c->img.ensure(plane * nc * 4 + 256));
+        for (uint32_t k = 0; k < nc; ++k) {
+            src.p[k] = c->img.as<int32_t>() + plane * k;
+            HIPCHK(hipMemcpyAsync(src.p[k], planes[k], plane * 4, hipMemcpyHostToDevice, s));
+        }
+    }
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    ShiftArr sh{};
+    for (uint32_t k = 0; k < nc; ++k) sh.v[k] = cp.shift[k];
+    int32_t *llA = c->ll.as<int32_t>(), *llB = llA + (max_tc / 2 + 64);
+    for (auto &tile : tiles) {
+        PlanePtrs tsrc{}, tdst{};
+        for (uint32_t k = 0; k < nc; ++k) {
+            tsrc.p[k] = src.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+            tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
+        }
+        HIPCHK(launch_dcshift_mct_fwd(tsrc, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+    }
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    for (auto &tile : tiles)
+        for (uint32_t k = 0; k < nc; ++k) {
+            const TileComp &tc = tile.comps[k];
+            HIPCHK(run_dwt_fwd(c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off, llA, llB,
+                               tc, cp.irrev, s));
+        }
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    memcpy(c->h_blocks.p, eb.data(), (size_t)nblk * sizeof(EncBlock));
+    HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(EncBlock), hipMemcpyHostToDevice, s));
+    HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<BlockRows>(),
+                            c->mqout.as<uint8_t>(), c->results.as<EncResult>(), s));
+    HIPCHK(hipEventRecord(c->ev[4], s));
+    HIPCHK(hipMemcpyAsync(c->h_results.p, c->results.p, (size_t)nblk * sizeof(EncResult), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const EncResult *res = c->h_results.as<EncResult>();
+
+    // pack block bytes: layer 0 takes every pass -> passes[last].rate bytes
+    std::vector<BlockT2> bt(nblk);
+    std::vector<GatherItem> gi;
+    gi.reserve(nblk);
+    uint64_t packed = 0;
+    for (uint32_t i = 0; i < nblk; ++i) {
+        const EncResult &r = res[i];
+        if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
+        bt[i].numbps = r.numbps;
+        bt[i].numpasses = r.numpasses;
+        bt[i].rate = r.rate;
+        bt[i].datalen = r.numpasses ? r.rate[r.numpasses - 1] : 0;
+        bt[i].packed_off = packed;
+        if (bt[i].datalen) {
+            if (bt[i].datalen > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+            gi.push_back({eb[i].out_off, packed, bt[i].datalen, 0});
+        }
+        packed += bt[i].datalen;
+    }
+    HIPCHK(c->gather.ensure(gi.size() * sizeof(GatherItem) + 256));
+    HIPCHK(c->h_gather.ensure(gi.size() * sizeof(GatherItem) + 256));
+    HIPCHK(c->packed.ensure(packed + 256));
+    HIPCHK(c->h_packed.ensure(packed + 256));
+    memcpy(c->h_gather.p, gi.data(), gi.size() * sizeof(GatherItem));
+    HIPCHK(hipEventRecord(c->ev[5], s));
+    HIPCHK(hipMemcpyAsync(c->gather.p, c->h_gather.p, gi.size() * sizeof(GatherItem), hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather(c->mqout.as<uint8_t>(), c->gather.as<GatherItem>(), (uint32_t)gi.size(),
+                         c->packed.as<uint8_t>(), s));
+    HIPCHK(hipEventRecord(c->ev[6], s));
+    HIPCHK(hipMemcpyAsync(c->h_packed.p, c->packed.p, packed, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->ev[7], s));
+    HIPCHK(hipStreamSynchronize(s));
+    double t_t2 = now_ms();
+
+    // host Tier-2 + headers (j2k_encode :2059, j2k_write_sot :5065, T2::encode_packets)
+    ByteBuf cs;
+    cs.v.reserve(packed + packed / 16 + 4096);
+    write_main_header(cs, cp);
+    const uint8_t *pk = c->h_packed.as<uint8_t>();
+    for (auto &tile : tiles) {
+        size_t sot = cs.size();
+        cs.put16(0xFF90); cs.put16(10); cs.put16(tile.index); cs.put32(0); cs.put8(0); cs.put8(1);
+        cs.put16(0xFF93);
+        for (uint32_t resno = 0; resno < cp.numres; ++resno)  // LRCP, one layer
+            for (uint32_t k = 0; k < nc; ++k) {
+                TileComp &tc = tile.comps[k];
+                Resolution &r = tc.res[resno];
+                for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) encode_packet(tc, resno, precno, bt, pk, cs);
+            }
+        cs.set32(sot + 6, (uint32_t)(cs.size() - sot));
+    }
+    cs.put16(0xFFD9);
+    double t_end = now_ms();
+    uint8_t *o = (uint8_t *)malloc(cs.size());
+    if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
+    memcpy(o, cs.v.data(), cs.size());
+    *out = o;
+    *outlen = cs.size();
+
+    grkgpu_stats &st = c->stats;
+    memset(&st, 0, sizeof(st));
+    hipEventElapsedTime(&st.h2d_ms, c->ev[0], c->ev[1]);
+    hipEventElapsedTime(&st.dcshift_mct_ms, c->ev[1], c->ev[2]);
+    hipEventElapsedTime(&st.dwt_ms, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&st.t1_ms, c->ev[3], c->ev[4]);
+    hipEventElapsedTime(&st.gather_ms, c->ev[5], c->ev[6]);
+    hipEventElapsedTime(&st.d2h_ms, c->ev[6], c->ev[7]);
+    st.host_t2_ms = (float)(t_end - t_t2);
+    st.total_ms = (float)(t_end - t_start);
+    st.num_cblks = nblk;
+    st.cs_bytes = cs.size();
+    return GRKGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decode
+// ---------------------------------------------------------------------------
+extern "C" int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img) {
+    if (!cs || !img) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    size_t sot = 0;
+    std::string err;
+    if (!parse_main_header(cs, len, cp, sot, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
+    memset(img, 0, sizeof(*img));
+    img->x0 = cp.image.x0; img->y0 = cp.image.y0; img->x1 = cp.image.x1; img->y1 = cp.image.y1;
+    img->numcomps = cp.numcomps;
+    for (uint32_t k = 0; k < cp.numcomps; ++k) { img->prec[k] = cp.prec[k]; img->sgnd[k] = cp.sgnd[k]; }
+    return GRKGPU_OK;
+}
+
+static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
+
+extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
+                                 int32_t *const *planes, int planes_on_device) {
+    if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
+    double t_start = now_ms();
+    CodingParams cp;
+    size_t pos = 0;
+    std::string err;
+    if (!parse_main_header(csb, len, cp, pos, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
+    if (img) {
+        int rc = grkgpu_read_header(csb, len, img);
+        if (rc) return rc;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th, iw = cp.image.w(), ih = cp.image.h();
+    const uint64_t plane = (uint64_t)iw * ih;
+
+    // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
+    std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
+    while (pos + 2 <= len) {
+        uint32_t m = rd16(csb + pos);
+        if (m == 0xFFD9) break;
+        if (m != 0xFF90 || pos + 12 > len) return set_err(GRKGPU_ECORRUPT, "expected SOT");
+        uint32_t isot = rd16(csb + pos + 4), psot = rd32(csb + pos + 6);
+        if (isot >= ntiles) return set_err(GRKGPU_ECORRUPT, "bad tile index");
+        size_t sot = pos;
+        size_t end = psot ? sot + psot : len - 2;
+        if (end > len) end = len;
+        pos += 12;
+        while (pos + 4 <= end && rd16(csb + pos) != 0xFF93) {
+            uint32_t mm = rd16(csb + pos);
+            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5F)
+                return set_err(GRKGPU_EUNSUPPORTED, "tile-part header coding markers not supported");
+            pos += 2 + rd16(csb + pos + 2);
+        }
+        pos += 2;
+        if (pos > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part");
+        tparts[isot].push_back({pos, end - pos});
+        pos = end;
+    }
+
+    // host Tier-2 over every tile; code-block segments -> DecBlock table
+    std::vector<Tile> tiles(ntiles);
+    uint64_t arena = 0, max_tc = 0;
+    std::vector<DecBlock> db;
+    std::vector<uint8_t> extra;  // concatenated multi-chunk segments
+    std::vector<uint8_t> tilebuf;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        Tile &tile = tiles[t];
+        tile.index = t;
+        tile.r = tile_rect(cp, t);
+        tile.comps.resize(nc);
+        for (uint32_t k = 0; k < nc; ++k) {
+            build_tilecomp(tile.comps[k], tile.r, cp, k, false);
+            tile.comps[k].arena_off = arena;
+            uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
+            arena += (area + 63) & ~63ull;
+            max_tc = std::max(max_tc, area);
+        }
+        // tile data: single tile-part -> decode in place; else concatenate
+        const uint8_t *td;
+        size_t tlen;
+        uint64_t base;
+        bool contiguous = tparts[t].size() <= 1;
+        if (contiguous) {
+            td = tparts[t].empty() ? csb : csb + tparts[t][0].first;
+            tlen = tparts[t].empty() ? 0 : tparts[t][0].second;
+            base = tparts[t].empty() ? 0 : tparts[t][0].first;
+        } else {
+            tilebuf.clear();
+            for (auto &pp : tparts[t]) tilebuf.insert(tilebuf.end(), csb + pp.first, csb + pp.first + pp.second);
+            td = tilebuf.data();
+            tlen = tilebuf.size();
+            base = 0;
+        }
+        size_t off = 0;
+        bool stop = false;
+        for (uint32_t layno = 0; layno < cp.numlayers && !stop; ++layno)
+            for (uint32_t resno = 0; resno < cp.numres && !stop; ++resno)
+                for (uint32_t k = 0; k < nc && !stop; ++k) {
+                    Resolution &r = tile.comps[k].res[resno];
+                    for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) {
+                        if (off >= tlen) { stop = true; break; }
+                        int64_t used = decode_packet(tile.comps[k], resno, precno, layno, td + off, tlen - off, base + off);
+                        if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
+                        off += (size_t)used;
+                    }
+                }
+        for (uint32_t k = 0; k < nc; ++k) {
+            TileComp &tc = tile.comps[k];
+            for_each_cblk(tc, [&](Band &band, Cblk &cb) {
+                DecBlock d{};
+                d.dst_off = tc.arena_off + (uint64_t)cb.by * tile.r.w() + cb.bx;
+                d.dstride = tile.r.w();
+                d.w = cb.r.w();
+                d.h = cb.r.h();
+                d.orient = band.bandno;
+                d.irrev = cp.irrev;
+                d.step = band.stepsize;
+                d.numpasses = cb.numpasses;
+                d.numbps = cb.numbps;
+                d.len = cb.seglen;
+                if (cb.chunks.size() == 1 && contiguous) {
+                    d.data_off = cb.chunks[0].first;
+                } else if (!cb.chunks.empty()) {
+                    d.data_off = (uint64_t)len + extra.size();  // placed after the codestream
+                    for (auto &ch : cb.chunks) {
+                        const uint8_t *srcp = contiguous ? csb + ch.first : tilebuf.data() + ch.first;
+                        extra.insert(extra.end(), srcp, srcp + ch.second);
+                    }
+                } else {
+                    d.len = 0;
+                }
+                db.push_back(d);
+            });
+        }
+    }
+    const uint32_t nblk = (uint32_t)db.size();
+    double t_t2 = now_ms();
+    HIPCHK(c->cs.ensure(len + extra.size() + 256));
+    HIPCHK(c->coef.ensure(arena * 4 + 256));
+    HIPCHK(c->work.ensure(arena * 4 + 256));
+    HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
+    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(BlockRows) + 256));
+    HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
+    HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
+    HIPCHK(c->h_packed.ensure(len + extra.size() + 256));
+    memcpy(c->h_packed.p, csb, len);
+    if (!extra.empty()) memcpy(c->h_packed.as<uint8_t>() + len, extra.data(), extra.size());
+    memcpy(c->h_blocks.p, db.data(), (size_t)nblk * sizeof(DecBlock));
+
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    HIPCHK(hipMemcpyAsync(c->cs.p, c->h_packed.p, len + extra.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<BlockRows>(),
+                            c->coef.as<int32_t>(), s));
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    int32_t *llA = c->ll.as<int32_t>(), *llB = llA + (max_tc / 2 + 64);
+    for (auto &tile : tiles)
+        for (uint32_t k = 0; k < nc; ++k) {
+            const TileComp &tc = tile.comps[k];
+            HIPCHK(run_dwt_inv(c->coef.as<int32_t>() + tc.arena_off, c->work.as<int32_t>() + tc.arena_off, llA, llB,
+                               tc, cp.irrev, s));
+        }
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    PlanePtrs dst{};
+    if (planes_on_device) {
+        for (uint32_t k = 0; k < nc; ++k) dst.p[k] = planes[k];
+    } else {
+        HIPCHK(c->img.ensure(plane * nc * 4 + 256));
+        for (uint32_t k = 0; k < nc; ++k) dst.p[k] = c->img.as<int32_t>() + plane * k;
+    }
+    ShiftArr sh{}, mn{}, mx{};
+    for (uint32_t k = 0; k < nc; ++k) {
+        sh.v[k] = cp.shift[k];
+        if (cp.sgnd[k]) { mn.v[k] = -(1 << (cp.prec[k] - 1)); mx.v[k] = (1 << (cp.prec[k] - 1)) - 1; }
+        else { mn.v[k] = 0; mx.v[k] = (1 << cp.prec[k]) - 1; }
+    }
+    for (auto &tile : tiles) {
+        PlanePtrs tsrc{}, tdst{};
+        for (uint32_t k = 0; k < nc; ++k) {
+            tsrc.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
+            tdst.p[k] = dst.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+        }
+        HIPCHK(launch_mct_inv_dcshift(tsrc, tile.r.w(), tile.r.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev, s));
+    }
+    HIPCHK(hipEventRecord(c->ev[4], s));
+    if (!planes_on_device)
+        for (uint32_t k = 0; k < nc; ++k)
+            HIPCHK(hipMemcpyAsync(planes[k], dst.p[k], plane * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->ev[5], s));
+    HIPCHK(hipStreamSynchronize(s));
+    double t_end = now_ms();
+    grkgpu_stats &st = c->stats;
+    memset(&st, 0, sizeof(st));
+    hipEventElapsedTime(&st.h2d_ms, c->ev[0], c->ev[1]);
+    hipEventElapsedTime(&st.t1_ms, c->ev[1], c->ev[2]);
+    hipEventElapsedTime(&st.dwt_ms, c->ev[2], c->ev[3]);
+    hipEventElapsedTime(&st.dcshift_mct_ms, c->ev[3], c->ev[4]);
+    hipEventElapsedTime(&st.d2h_ms, c->ev[4], c->ev[5]);
+    st.host_t2_ms = (float)(t_t2 - t_start);
+    st.total_ms = (float)(t_end - t_start);
+    st.num_cblks = nblk;
+    st.cs_bytes = len;
+    return GRKGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stage entry points
+// ---------------------------------------------------------------------------
+extern "C" int grkgpu_dcshift_mct_fwd(int32_t *const *planes, uint32_t numcomps, uint32_t w, uint32_t h,
+                                      uint32_t stride, const int32_t *shift, int32_t mct, int32_t irreversible,
+                                      void *stream) {
+    if (!planes || !shift || numcomps < 1 || numcomps > 16) return set_err(GRKGPU_EINVAL, "bad arguments");
+    int rc = check_device(0);
+    if (rc) return rc;
+    PlanePtrs p{};
+    ShiftArr sh{};
+    for (uint32_t k = 0; k < numcomps; ++k) { p.p[k] = planes[k]; sh.v[k] = shift[k]; }
+    HIPCHK(launch_dcshift_mct_fwd(p, stride, p, w, h, numcomps, sh, mct, irreversible, (hipStream_t)stream));
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps, uint32_t w, uint32_t h,
+                                      uint32_t stride, const uint32_t *prec, const int32_t *sgnd, int32_t mct,
+                                      int32_t irreversible, void *stream) {
+    if (!planes || !prec || !sgnd || numcomps < 1 || numcomps > 16 || stride != w)
+        return set_err(GRKGPU_EINVAL, "bad arguments (stride must equal w)");
+    int rc = check_device(0);
+    if (rc) return rc;
+    PlanePtrs p{};
+    ShiftArr sh{}, mn{}, mx{};
+    for (uint32_t k = 0; k < numcomps; ++k) {
+        p.p[k] = planes[k];
+        sh.v[k] = sgnd[k] ? 0 : (1 << (prec[k] - 1));
+        if (sgnd[k]) { mn.v[k] = -(1 << (prec[k] - 1)); mx.v[k] = (1 << (prec[k] - 1)) - 1; }
+        else { mn.v[k] = 0; mx.v[k] = (1 << prec[k]) - 1; }
+    }
+    HIPCHK(launch_mct_inv_dcshift(p, w, h, p, w, numcomps, sh, mn, mx, mct, irreversible, (hipStream_t)stream));
+    return GRKGPU_OK;
+}
+
+static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                      uint32_t numres, int32_t irrev, void *stream, bool inverse) {
+    if (!buf || !scratch || x1 <= x0 || y1 <= y0 || numres < 1 || numres > 33)
+        return set_err(GRKGPU_EINVAL, "bad arguments");
+    int rc = check_device(0);
+    if (rc) return rc;
+    CodingParams cp;
+    cp.numcomps = 1;
+    cp.image = {x0, y0, x1, y1};
+    cp.prec[0] = 8;
+    cp.numres = numres;
+    cp.irrev = irrev;
+    generate_qcd(cp);
+    TileComp tc;
+    build_tilecomp(tc, cp.image, cp, 0, !inverse);
+    uint64_t area = (uint64_t)(x1 - x0) * (y1 - y0);
+    // scratch: [0, area) = temporary full buffer, [area, 2*area) = LL ping-pong
+    int32_t *tmp = scratch, *llA = scratch + area, *llB = llA + (area / 2 + 32);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(tmp, buf, area * 4, hipMemcpyDeviceToDevice, s));
+    if (!inverse) { HIPCHK(run_dwt_fwd(tmp, buf, llA, llB, tc, irrev, s)); }
+    else { HIPCHK(run_dwt_inv(tmp, buf, llA, llB, tc, irrev, s)); }
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_dwt_fwd(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                              uint32_t numres, int32_t irreversible, void *stream) {
+    return dwt_common(buf, scratch, x0, y0, x1, y1, numres, irreversible, stream, false);
+}
+
+extern "C" int grkgpu_dwt_inv(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                              uint32_t numres, int32_t irreversible, void *stream) {
+    return dwt_common(buf, scratch, x0, y0, x1, y1, numres, irreversible, stream, true);
+}
+
+static_assert(sizeof(grkgpu_enc_block) == sizeof(EncBlock), "EncBlock ABI");
+static_assert(sizeof(grkgpu_enc_result) == sizeof(EncResult), "EncResult ABI");
+static_assert(sizeof(grkgpu_dec_block) == sizeof(DecBlock), "DecBlock ABI");
+
+extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
+                                       void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream) {
+    if (!blocks || !coef || !scratch || !out || !results) return set_err(GRKGPU_EINVAL, "null argument");
+    int rc = check_device(0);
+    if (rc) return rc;
+    HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, (BlockRows *)scratch, out,
+                            (EncResult *)results, (hipStream_t)stream));
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t nblocks, const uint8_t *data,
+                                       void *scratch, int32_t *dst, void *stream) {
+    if (!blocks || !data || !scratch || !dst) return set_err(GRKGPU_EINVAL, "null argument");
+    int rc = check_device(0);
+    if (rc) return rc;
+    HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (BlockRows *)scratch, dst,
+                            (hipStream_t)stream));
+    return GRKGPU_OK;
+}

@@ -1,0 +1,473 @@
+// codestream.cpp -- host geometry, quantisation parameters, Tier-2 packets and
+// headers for the MI355X JPEG 2000 path (see codestream.h).
+#include "codestream.h"
+
+#include <math.h>
+
+#include <algorithm>
+
+namespace grkgpu {
+
+// ---------------------------------------------------------------------------
+// quantisation parameters -- param_qcd::generate (codestream/HTParams.cpp:164)
+// ---------------------------------------------------------------------------
+namespace {
+// BIBO gains (HTParams.cpp:105-149) and sqrt energy gains (HTParams.cpp:49-84)
+const float kBibo53L[34] = {1.0000e+00f, 1.5000e+00f, 1.6250e+00f, 1.6875e+00f, 1.6963e+00f, 1.7067e+00f,
+    1.7116e+00f, 1.7129e+00f, 1.7141e+00f, 1.7145e+00f, 1.7151e+00f, 1.7152e+00f, 1.7155e+00f, 1.7155e+00f,
+    1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f,
+    1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f,
+    1.7156e+00f, 1.7156e+00f, 1.7156e+00f, 1.7156e+00f};
+const float kBibo53H[34] = {2.0000e+00f, 2.5000e+00f, 2.7500e+00f, 2.8047e+00f, 2.8198e+00f, 2.8410e+00f,
+    2.8558e+00f, 2.8601e+00f, 2.8628e+00f, 2.8656e+00f, 2.8662e+00f, 2.8667e+00f, 2.8669e+00f, 2.8670e+00f,
+    2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f,
+    2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f,
+    2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f};
+const float kGain97L[34] = {1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f,
+    8.2388e+00f, 1.1652e+01f, 1.6479e+01f, 2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f,
+    1.3183e+02f, 1.8643e+02f, 2.6366e+02f, 3.7287e+02f, 5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f,
+    2.1093e+03f, 2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f, 1.1932e+04f, 1.6874e+04f, 2.3864e+04f,
+    3.3748e+04f, 4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
+const float kGain97H[34] = {1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f,
+    1.1809e+01f, 1.6701e+01f, 2.3620e+01f, 3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f,
+    1.8896e+02f, 2.6723e+02f, 3.7792e+02f, 5.3446e+02f, 7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f,
+    3.0233e+03f, 4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f, 1.7103e+04f, 2.4187e+04f, 3.4205e+04f,
+    4.8373e+04f, 6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
+
+int rev_bits(float g) { return (int)std::ceil(std::log((double)g) / M_LN2); }
+
+StepSize irrev_step(float delta) {
+    StepSize s;
+    while (delta < 1.0f) { s.expn++; delta *= 2.0f; }
+    uint32_t m = (uint32_t)std::round(delta * (float)(1 << 11)) - (1 << 11);
+    s.mant = m < (1u << 11) ? m : 0x7FFu;
+    return s;
+}
+}  // namespace
+
+void generate_qcd(CodingParams &cp) {
+    const uint32_t nd = cp.numres - 1;
+    uint32_t s = 0;
+    if (!cp.irrev) {
+        // set_rev_quant (HTParams.cpp:187-207); the RCT bit is never added
+        // because j2k_setup_encoder calls generate() before tcp->mct is set
+        // (j2k.cpp:1839 vs :1861).
+        const int B = (int)cp.prec[0];
+        float l = kBibo53L[nd];
+        cp.ss[s++] = {(uint32_t)(B + rev_bits(l * l * 1.1f)), 0};
+        for (int d = (int)nd - 1; d >= 0; --d) {
+            float bl = kBibo53L[d + 1], bh = kBibo53H[d];
+            uint32_t e = (uint32_t)(B + rev_bits(bh * bl * 1.1f));
+            cp.ss[s++] = {e, 0};
+            cp.ss[s++] = {e, 0};
+            cp.ss[s++] = {(uint32_t)(B + rev_bits(bh * bh * 1.1f)), 0};
+        }
+    } else {
+        // set_irrev_quant (HTParams.cpp:210-253), base_delta = 2^-(prec+sgnd)
+        const float base = 1.0f / (float)(1u << (cp.prec[0] + (uint32_t)cp.sgnd[0]));
+        float gl = kGain97L[nd];
+        cp.ss[s++] = irrev_step(base / (gl * gl));
+        for (int d = (int)nd - 1; d >= 0; --d) {
+            float l = kGain97L[d + 1], h = kGain97H[d];
+            StepSize t = irrev_step(base / (l * h));
+            cp.ss[s++] = t;
+            cp.ss[s++] = t;
+            cp.ss[s++] = irrev_step(base / (h * h));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// geometry (TileComponent.cpp:165-507, Quantizer.cpp:65-104, Tier1.cpp:49-62)
+// ---------------------------------------------------------------------------
+Rect tile_rect(const CodingParams &cp, uint32_t tileno) {
+    uint32_t p = tileno % cp.tw, q = tileno / cp.tw;
+    uint32_t x0 = cp.tx0 + p * cp.tdx, y0 = cp.ty0 + q * cp.tdy;
+    Rect r;
+    r.x0 = std::max(x0, cp.image.x0);
+    r.y0 = std::max(y0, cp.image.y0);
+    r.x1 = (uint32_t)std::min<uint64_t>((uint64_t)x0 + cp.tdx, cp.image.x1);
+    r.y1 = (uint32_t)std::min<uint64_t>((uint64_t)y0 + cp.tdy, cp.image.y1);
+    return r;
+}
+
+void TagTree::init(uint32_t nh, uint32_t nv) {
+    uint32_t nplh[40], nplv[40], lv = 0, n, total = 0;
+    nplh[0] = nh; nplv[0] = nv;
+    do {
+        n = nplh[lv] * nplv[lv];
+        nplh[lv + 1] = (nplh[lv] + 1) / 2;
+        nplv[lv + 1] = (nplv[lv] + 1) / 2;
+        total += n;
+        ++lv;
+    } while (n > 1);
+    nodes.assign(total ? total : 1, Node{INT64_MAX, 0, -1, 0});
+    uint32_t base = 0, pbase = nh * nv;
+    for (uint32_t l = 0; l + 1 < lv; ++l) {
+        for (uint32_t j = 0; j < nplv[l]; ++j)
+            for (uint32_t i = 0; i < nplh[l]; ++i)
+                nodes[base + j * nplh[l] + i].parent = (int32_t)(pbase + (j >> 1) * nplh[l + 1] + (i >> 1));
+        base = pbase;
+        pbase += nplh[l + 1] * nplv[l + 1];
+    }
+    nodes.back().parent = -1;
+}
+
+void TagTree::reset() {
+    for (auto &n : nodes) { n.value = INT64_MAX; n.low = 0; n.known = 0; }
+}
+
+void TagTree::setvalue(uint32_t leaf, int64_t v) {
+    int32_t n = (int32_t)leaf;
+    while (n >= 0 && nodes[n].value > v) { nodes[n].value = v; n = nodes[n].parent; }
+}
+
+void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32_t compno, bool encoder) {
+    tc.r = tr;
+    tc.numres = cp.numres;
+    tc.res.assign(cp.numres, Resolution());
+    for (uint32_t resno = 0; resno < cp.numres; ++resno) {
+        Resolution &res = tc.res[resno];
+        const uint32_t lev = cp.numres - 1 - resno;
+        res.r = {ceildivpow2(tr.x0, lev), ceildivpow2(tr.y0, lev), ceildivpow2(tr.x1, lev), ceildivpow2(tr.y1, lev)};
+        const uint32_t pdx = 15, pdy = 15;  // default precinct 2^15
+        uint32_t tpx0 = (res.r.x0 >> pdx) << pdx, tpy0 = (res.r.y0 >> pdy) << pdy;
+        uint32_t bpx1 = ceildivpow2(res.r.x1, pdx) << pdx, bpy1 = ceildivpow2(res.r.y1, pdy) << pdy;
+        res.pw = (res.r.x0 == res.r.x1) ? 0 : ((bpx1 - tpx0) >> pdx);
+        res.ph = (res.r.y0 == res.r.y1) ? 0 : ((bpy1 - tpy0) >> pdy);
+        uint32_t tlcbgx, tlcbgy, cbgw, cbgh;
+        if (resno == 0) { tlcbgx = tpx0; tlcbgy = tpy0; cbgw = pdx; cbgh = pdy; res.numbands = 1; }
+        else { tlcbgx = ceildivpow2(tpx0, 1); tlcbgy = ceildivpow2(tpy0, 1); cbgw = pdx - 1; cbgh = pdy - 1; res.numbands = 3; }
+        const uint32_t cbw = std::min(cp.cblkw, cbgw), cbh = std::min(cp.cblkh, cbgh);
+        for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+            Band &b = res.bands[bandno];
+            if (resno == 0) {
+                b.bandno = 0;
+                b.r = {ceildivpow2(tr.x0, lev), ceildivpow2(tr.y0, lev), ceildivpow2(tr.x1, lev), ceildivpow2(tr.y1, lev)};
+            } else {
+                b.bandno = bandno + 1;
+                uint64_t x0b = b.bandno & 1, y0b = b.bandno >> 1, d = (uint64_t)1 << (lev + 1);
+                b.r.x0 = (uint32_t)(((uint64_t)tr.x0 - (x0b << lev) + d - 1) >> (lev + 1));
+                b.r.y0 = (uint32_t)(((uint64_t)tr.y0 - (y0b << lev) + d - 1) >> (lev + 1));
+                b.r.x1 = (uint32_t)(((uint64_t)tr.x1 - (x0b << lev) + d - 1) >> (lev + 1));
+                b.r.y1 = (uint32_t)(((uint64_t)tr.y1 - (y0b << lev) + d - 1) >> (lev + 1));
+            }
+            // Quantizer::setBandStepSizeAndBps (Quantizer.cpp:65-104)
+            uint32_t gain = cp.irrev ? 0 : (b.bandno == 0 ? 0 : (b.bandno < 3 ? 1 : 2));
+            uint32_t numbps = cp.prec[compno] + gain;
+            uint32_t off = resno == 0 ? 0 : 3 * resno - 2;
+            const StepSize &st = cp.ss[off + bandno];
+            b.stepsize = (float)((1.0 + st.mant / 2048.0) * std::pow(2.0, (int32_t)(numbps - st.expn))) *
+                         (encoder ? 1.0f : 0.5f);
+            b.numbps = st.expn + 2 - 1;  // guard bits 2 (j2k.cpp:1834)
+            b.inv_step = (uint32_t)((8192.0 / b.stepsize) + 0.5f);
+            uint32_t np = res.pw * res.ph;
+            b.precs.assign(np, Precinct());
+            for (uint32_t precno = 0; precno < np; ++precno) {
+                Precinct &pr = b.precs[precno];
+                uint32_t cbgx0 = tlcbgx + (precno % res.pw) * (1u << cbgw);
+                uint32_t cbgy0 = tlcbgy + (precno / res.pw) * (1u << cbgh);
+                pr.r = {std::max(cbgx0, b.r.x0), std::max(cbgy0, b.r.y0), std::min(cbgx0 + (1u << cbgw), b.r.x1),
+                        std::min(cbgy0 + (1u << cbgh), b.r.y1)};
+                if (pr.r.x1 <= pr.r.x0 || pr.r.y1 <= pr.r.y0) { pr.cw = pr.ch = 0; continue; }
+                uint32_t tlx = (pr.r.x0 >> cbw) << cbw, tly = (pr.r.y0 >> cbh) << cbh;
+                uint32_t brx = ceildivpow2(pr.r.x1, cbw) << cbw, bry = ceildivpow2(pr.r.y1, cbh) << cbh;
+                pr.cw = (brx - tlx) >> cbw;
+                pr.ch = (bry - tly) >> cbh;
+                pr.cblks.assign(pr.cw * pr.ch, Cblk());
+                for (uint32_t cb = 0; cb < pr.cw * pr.ch; ++cb) {
+                    Cblk &c = pr.cblks[cb];
+                    uint32_t cx0 = tlx + (cb % pr.cw) * (1u << cbw), cy0 = tly + (cb / pr.cw) * (1u << cbh);
+                    c.r = {std::max(cx0, pr.r.x0), std::max(cy0, pr.r.y0), std::min(cx0 + (1u << cbw), pr.r.x1),
+                           std::min(cy0 + (1u << cbh), pr.r.y1)};
+                    c.bx = c.r.x0 - b.r.x0;
+                    c.by = c.r.y0 - b.r.y0;
+                    if (b.bandno & 1) c.bx += tc.res[resno - 1].r.w();
+                    if (b.bandno & 2) c.by += tc.res[resno - 1].r.h();
+                }
+                pr.incl.init(pr.cw, pr.ch);
+                pr.imsb.init(pr.cw, pr.ch);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// headers (codestream/j2k.cpp marker writers :3117-5540)
+// ---------------------------------------------------------------------------
+void write_main_header(ByteBuf &cs, const CodingParams &cp) {
+    const uint32_t nc = cp.numcomps, nd = cp.numres - 1, nb = 3 * nd + 1;
+    cs.put16(0xFF4F);  // SOC
+    cs.put16(0xFF51); cs.put16(38 + 3 * nc); cs.put16(0);  // SIZ, Rsiz = 0
+    cs.put32(cp.image.x1); cs.put32(cp.image.y1); cs.put32(cp.image.x0); cs.put32(cp.image.y0);
+    cs.put32(cp.tdx); cs.put32(cp.tdy); cs.put32(cp.tx0); cs.put32(cp.ty0);
+    cs.put16(nc);
+    for (uint32_t k = 0; k < nc; ++k) { cs.put8((cp.prec[k] - 1) + ((uint32_t)cp.sgnd[k] << 7)); cs.put8(1); cs.put8(1); }
+    cs.put16(0xFF52); cs.put16(12);  // COD
+    cs.put8(0); cs.put8(cp.prog); cs.put16(cp.numlayers); cs.put8((uint32_t)cp.mct);
+    cs.put8(nd); cs.put8(cp.cblkw - 2); cs.put8(cp.cblkh - 2); cs.put8(cp.cblksty); cs.put8(cp.irrev ? 0 : 1);
+    cs.put16(0xFF5C); cs.put16(3 + nb * (cp.irrev ? 2 : 1));  // QCD
+    cs.put8((2u << 5) | (cp.irrev ? 2u : 0u));
+    for (uint32_t i = 0; i < nb; ++i) {
+        if (cp.irrev) cs.put16((cp.ss[i].expn << 11) | cp.ss[i].mant);
+        else cs.put8(cp.ss[i].expn << 3);
+    }
+    static const char kCom[] = "Created by Grok     version 5.1.0";  // j2k.cpp:1798
+    cs.put16(0xFF64); cs.put16(4 + (uint32_t)strlen(kCom)); cs.put16(1);
+    cs.putn((const uint8_t *)kCom, strlen(kCom));
+}
+
+// ---------------------------------------------------------------------------
+// packet header bit writer (codestream/BitIO.cpp)
+// ---------------------------------------------------------------------------
+namespace {
+struct BitWriter {
+    ByteBuf &out;
+    uint32_t buf = 0, ct = 8;
+    explicit BitWriter(ByteBuf &o) : out(o) {}
+    void byteout() { out.put8(buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
+    void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
+    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    void flush() { byteout(); if (ct == 7) byteout(); }
+    void numpasses(uint32_t n) {
+        if (n == 1) write(0, 1);
+        else if (n == 2) write(2, 2);
+        else if (n <= 5) write(0xc | (n - 3), 4);
+        else if (n <= 36) write(0x1e0 | (n - 6), 9);
+        else write(0xff80 | (n - 37), 16);
+    }
+    void comma(int32_t n) { while (--n >= 0) write(1, 1); write(0, 1); }
+    // TagTree::encode (TagTree.cpp:251-287)
+    void tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
+        int32_t stk[64], sp = 0, node = (int32_t)leaf;
+        while (t.nodes[node].parent >= 0) { stk[sp++] = node; node = t.nodes[node].parent; }
+        int64_t low = 0;
+        for (;;) {
+            TagTree::Node &n = t.nodes[node];
+            if (low > n.low) n.low = low; else low = n.low;
+            while (low < threshold) {
+                if (low >= n.value) {
+                    if (!n.known) { write(1, 1); n.known = 1; }
+                    break;
+                }
+                write(0, 1);
+                ++low;
+            }
+            n.low = low;
+            if (sp == 0) break;
+            node = stk[--sp];
+        }
+    }
+};
+
+struct BitReader {
+    const uint8_t *p;
+    size_t n, off = 0;
+    uint32_t buf = 0, ct = 0;
+    bool err = false;
+    BitReader(const uint8_t *pp, size_t nn) : p(pp), n(nn) {}
+    void bytein() {
+        ct = (buf == 0xff) ? 7 : 8;
+        if (off >= n) { err = true; buf = 0; return; }
+        buf = p[off++];
+    }
+    uint32_t bit() { if (ct == 0) bytein(); ct--; return (buf >> ct) & 1; }
+    uint32_t read(uint32_t k) { uint32_t v = 0; for (uint32_t i = 0; i < k; ++i) v = (v << 1) | bit(); return v; }
+    void align() { if (buf == 0xff) bytein(); ct = 0; }
+    uint32_t numpasses() {
+        if (!read(1)) return 1;
+        if (!read(1)) return 2;
+        uint32_t v = read(2);
+        if (v != 3) return v + 3;
+        v = read(5);
+        if (v != 31) return v + 6;
+        return read(7) + 37;
+    }
+    uint32_t comma() { uint32_t k = 0; while (bit() && !err) ++k; return k; }
+    // TagTree::decodeValue (TagTree.cpp:295-321)
+    int64_t tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
+        int32_t stk[64], sp = 0, node = (int32_t)leaf;
+        while (t.nodes[node].parent >= 0) { stk[sp++] = node; node = t.nodes[node].parent; }
+        int64_t low = 0;
+        for (;;) {
+            TagTree::Node &nd = t.nodes[node];
+            if (low > nd.low) nd.low = low; else low = nd.low;
+            while (low < threshold && low < nd.value) {
+                if (bit()) nd.value = low; else ++low;
+                if (err) return INT64_MAX;
+            }
+            nd.low = low;
+            if (sp == 0) break;
+            node = stk[--sp];
+        }
+        return t.nodes[node].value;
+    }
+};
+}  // namespace
+
+void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk,
+                   const uint8_t *packed, ByteBuf &out) {
+    Resolution &res = tc.res[resno];
+    const uint32_t layno = 0;
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        Precinct &pr = b.precs[precno];
+        if (b.empty() || pr.cblks.empty()) continue;
+        pr.incl.reset(); pr.imsb.reset();
+        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+            pr.cblks[cb].included = false;
+            pr.imsb.setvalue(cb, (int64_t)b.numbps - (int64_t)blk[pr.cblks[cb].gidx].numbps);
+        }
+    }
+    BitWriter w(out);
+    w.write(1, 1);  // Grok always signals a non-empty packet (T2.cpp:924-927)
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        Precinct &pr = b.precs[precno];
+        if (b.empty() || pr.cblks.empty()) continue;
+        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb)
+            if (!pr.cblks[cb].included && blk[pr.cblks[cb].gidx].numpasses) pr.incl.setvalue(cb, layno);
+        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+            Cblk &c = pr.cblks[cb];
+            const BlockT2 &bt = blk[c.gidx];
+            const uint32_t np = bt.numpasses;
+            if (!c.included) w.tagtree(pr.incl, cb, layno + 1);
+            else w.write(np != 0, 1);
+            if (!np) continue;
+            if (!c.included) { c.numlenbits = 3; w.tagtree(pr.imsb, cb, INT64_MAX); }
+            w.numpasses(np);
+            // cblksty 0: only the last pass is terminated -> one segment
+            const uint32_t len = bt.rate[np - 1];
+            int32_t inc = floorlog2((int32_t)len) + 1 - ((int32_t)c.numlenbits + floorlog2((int32_t)np));
+            if (inc < 0) inc = 0;
+            w.comma(inc);
+            c.numlenbits += (uint32_t)inc;
+            w.write(len, c.numlenbits + (uint32_t)floorlog2((int32_t)np));
+        }
+    }
+    w.flush();
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        Precinct &pr = b.precs[precno];
+        if (b.empty() || pr.cblks.empty()) continue;
+        for (auto &c : pr.cblks) {
+            const BlockT2 &bt = blk[c.gidx];
+            if (!bt.numpasses) continue;
+            out.putn(packed + bt.packed_off, bt.rate[bt.numpasses - 1]);
+            c.included = true;
+        }
+    }
+}
+
+int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
+                      uint64_t base_off) {
+    Resolution &res = tc.res[resno];
+    if (layno == 0) {
+        for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+            Band &b = res.bands[bandno];
+            Precinct &pr = b.precs[precno];
+            if (b.empty() || pr.cblks.empty()) continue;
+            pr.incl.reset(); pr.imsb.reset();
+            for (auto &c : pr.cblks) { c.included = false; c.numpasses = 0; c.chunks.clear(); c.seglen = 0; }
+        }
+    }
+    BitReader r(p, n);
+    struct Seg { Cblk *c; uint32_t len; };
+    std::vector<Seg> segs;
+    if (r.read(1)) {
+        for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+            Band &b = res.bands[bandno];
+            Precinct &pr = b.precs[precno];
+            if (b.empty() || pr.cblks.empty()) continue;
+            for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+                Cblk &c = pr.cblks[cb];
+                uint32_t inc = c.included ? r.read(1) : (r.tagtree(pr.incl, cb, layno + 1) <= (int64_t)layno);
+                if (r.err) return -1;
+                if (!inc) continue;
+                if (!c.included) {
+                    int64_t k = r.tagtree(pr.imsb, cb, INT64_MAX);
+                    c.numbps = (uint32_t)((int64_t)b.numbps - k);
+                    c.numlenbits = 3;
+                    c.included = true;
+                }
+                uint32_t np = r.numpasses();
+                c.numlenbits += r.comma();
+                uint32_t L = r.read(c.numlenbits + (uint32_t)floorlog2((int32_t)np));
+                c.numpasses += np;
+                segs.push_back({&c, L});
+                if (r.err) return -1;
+            }
+        }
+    }
+    r.align();
+    if (r.err) return -1;
+    size_t off = r.off;
+    for (auto &s : segs) {
+        if (off + s.len > n) return -1;
+        if (s.len) s.c->chunks.push_back({base_off + off, s.len});
+        s.c->seglen += s.len;
+        off += s.len;
+    }
+    return (int64_t)off;
+}
+
+// ---------------------------------------------------------------------------
+// main header parsing (j2k.cpp j2k_read_siz / cod / qcd)
+// ---------------------------------------------------------------------------
+static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
+
+bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err) {
+    if (len < 4 || rd16(cs) != 0xFF4F) { err = "missing SOC"; return false; }
+    size_t pos = 2;
+    bool have_siz = false, have_cod = false, have_qcd = false;
+    while (pos + 4 <= len) {
+        uint32_t m = rd16(cs + pos);
+        if (m == 0xFF90) { first_sot = pos; break; }
+        uint32_t L = rd16(cs + pos + 2);
+        if (pos + 2 + L > len || L < 2) { err = "truncated marker"; return false; }
+        const uint8_t *p = cs + pos + 4;
+        if (m == 0xFF51) {
+            cp.image = {rd32(p + 10), rd32(p + 14), rd32(p + 2), rd32(p + 6)};
+            cp.tdx = rd32(p + 18); cp.tdy = rd32(p + 22); cp.tx0 = rd32(p + 26); cp.ty0 = rd32(p + 30);
+            cp.numcomps = rd16(p + 34);
+            if (cp.numcomps == 0 || cp.numcomps > 16) { err = "unsupported component count"; return false; }
+            for (uint32_t k = 0; k < cp.numcomps; ++k) {
+                cp.prec[k] = (p[36 + 3 * k] & 0x7f) + 1u;
+                cp.sgnd[k] = p[36 + 3 * k] >> 7;
+                if (p[37 + 3 * k] != 1 || p[38 + 3 * k] != 1) { err = "subsampled components not supported"; return false; }
+            }
+            if (cp.tdx == 0 || cp.tdy == 0) { err = "bad tile size"; return false; }
+            cp.tw = ceildiv(cp.image.x1 - cp.tx0, cp.tdx);
+            cp.th = ceildiv(cp.image.y1 - cp.ty0, cp.tdy);
+            have_siz = true;
+        } else if (m == 0xFF52) {
+            if (p[0] != 0) { err = "precincts/SOP/EPH (Scod != 0) not supported"; return false; }
+            cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
+            cp.numres = p[5] + 1u; cp.cblkw = p[6] + 2u; cp.cblkh = p[7] + 2u; cp.cblksty = p[8];
+            cp.irrev = p[9] == 0;
+            have_cod = true;
+        } else if (m == 0xFF5C) {
+            uint32_t sq = p[0] & 0x1f;
+            if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
+            uint32_t nb = sq == 0 ? (L - 3) : (L - 3) / 2;
+            for (uint32_t i = 0; i < nb && i < 3 * 33 + 1; ++i) {
+                if (sq == 0) cp.ss[i] = {(uint32_t)(p[1 + i] >> 3), 0};
+                else { uint32_t v = rd16(p + 1 + 2 * i); cp.ss[i] = {v >> 11, v & 0x7ff}; }
+            }
+            have_qcd = true;
+        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF5F || m == 0xFF5E || m == 0xFF60) {
+            err = "COC/QCC/POC/RGN/PPM markers not supported";
+            return false;
+        }
+        pos += 2 + L;
+    }
+    if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
+    if (cp.prog != 0) { err = "only LRCP progression supported"; return false; }
+    if (cp.cblksty != 0) { err = "code-block mode switches not supported"; return false; }
+    if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
+    for (uint32_t k = 0; k < cp.numcomps; ++k) cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
+    return true;
+}
+
+}  // namespace grkgpu

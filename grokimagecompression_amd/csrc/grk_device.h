@@ -1,0 +1,60 @@
+// grk_device.h -- device-visible descriptors shared by kernels.hip and codec.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "t1_core.h"
+
+namespace grkgpu {
+
+constexpr int GRK_MAX_COMPS = 16;
+constexpr int GRK_MAX_PASSES = 96;  // 3 * 31 - 2 = 91 passes max for cblksty 0
+
+struct PlanePtrs { int32_t *p[GRK_MAX_COMPS]; };
+struct ShiftArr { int32_t v[GRK_MAX_COMPS]; };
+
+// One code-block to encode (T1Part1::preEncode + t1_encode_cblk inputs,
+// t1/Tier1.cpp:24-96 encodeBlockInfo).
+struct EncBlock {
+    uint64_t coef_off;  // element offset of the block's top-left in the coefficient arena
+    uint64_t out_off;   // byte offset of the block's output in the MQ slab (out[-1] == 0)
+    uint32_t stride, w, h, orient;
+    int32_t qmfbid, inv_step;
+};
+
+struct EncResult {
+    uint32_t numbps, numpasses, len, pad;
+    uint32_t rate[GRK_MAX_PASSES];  // cumulative, after Grok's fix-ups
+};
+
+// One code-block to decode (t1/Tier1.cpp:98-175 decodeBlockInfo).
+struct DecBlock {
+    uint64_t data_off;  // byte offset of the (single) segment in the data buffer
+    uint64_t dst_off;   // element offset of the block's top-left in the tile arena
+    uint32_t len, numpasses, numbps, w, h, orient, dstride;
+    int32_t irrev;
+    float step;
+    uint32_t pad;
+};
+
+struct GatherItem { uint64_t src, dst; uint32_t len, pad; };
+
+hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const PlanePtrs &dst, uint32_t tw,
+                                  uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct, int32_t irrev,
+                                  hipStream_t s);
+hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t tw, uint32_t th, const PlanePtrs &dst,
+                                  uint32_t dstride, uint32_t ncomp, const ShiftArr &shift, const ShiftArr &mn,
+                                  const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s);
+hipError_t launch_dwt_fwd_level(const int32_t *src, uint32_t sstride, int32_t *ll, uint32_t llstride, int32_t *coef,
+                                uint32_t cstride, int rw, int rh, int casx, int casy, int snx, int sny, int irrev,
+                                hipStream_t s);
+hipError_t launch_dwt_inv_level(const int32_t *ll, uint32_t llstride, const int32_t *coef, uint32_t cstride,
+                                int32_t *dst, uint32_t dstride, int rw, int rh, int casx, int casy, int snx, int sny,
+                                int irrev, hipStream_t s);
+hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, BlockRows *scratch,
+                            uint8_t *out, EncResult *res, hipStream_t s);
+hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, BlockRows *scratch,
+                            int32_t *tiles, hipStream_t s);
+hipError_t launch_gather(const uint8_t *src, const GatherItem *items, uint32_t n, uint8_t *dst, hipStream_t s);
+
+}  // namespace grkgpu

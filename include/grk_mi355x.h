@@ -1,0 +1,165 @@
+/*
+ * grk_mi355x.h -- C ABI of the MI355X-native JPEG 2000 hot path
+ * (libgrk_mi355x.so).  Plain C types only: no HIP/torch types cross this
+ * boundary (streams are passed as void*).
+ *
+ * What each entry point replaces in the reference (Grok v5.1.0; paths under
+ * /root/reference/src/lib/jp2/):
+ *
+ *   grkgpu_compress        grk_compress's in-library path  grk_setup_encoder +
+ *                          grk_start_compress + grk_encode + grk_end_compress
+ *                          (grok.h:1660-1748, grok.cpp:545-600 ->
+ *                          codestream/j2k.cpp:1609 j2k_setup_encoder,
+ *                          :2059 j2k_encode) for the default coding options
+ *                          (1 layer, LRCP, 2^15 precincts, cblksty 0).
+ *   grkgpu_decompress      grk_read_header + grk_decode (grok.h:1571-1600,
+ *                          grok.cpp:381 -> j2k.cpp:1136 j2k_decode_tiles).
+ *   grkgpu_read_header     grk_read_header (grok.h:1571, j2k.cpp:406).
+ *   grkgpu_encode_tile_*   the tile hot path inside
+ *                          TileProcessor::encode_tile (TileProcessor.cpp:
+ *                          994-1012: dc_level_shift_encode :1449, mct_encode
+ *                          :1473, dwt_encode :1520, t1_encode :1535).
+ *   grkgpu_dwt_fwd/_inv    Wavelet::encode / Wavelet::decode
+ *                          (transform/Wavelet.cpp:35-56, WaveletForward.h:40,
+ *                          dwt.cpp:1208 decode_53, :2154 decode_97).
+ *   grkgpu_dcshift_mct_fwd mct::encode_rev / encode_irrev + DC shift
+ *                          (mct/mct.cpp:85, :195; TileProcessor.cpp:1449).
+ *   grkgpu_mct_inv_dcshift mct::decode_rev / decode_irrev + DC shift + clamp
+ *                          (mct/mct.cpp:143, :352; TileProcessor.cpp:1377).
+ *   grkgpu_t1_encode_blocks  Tier1::encodeCodeblocks -> T1Encoder::encode ->
+ *                          T1Part1::preEncode/encode (t1/Tier1.cpp:24,
+ *                          T1Encoder.cpp:40-85, t1_part1/T1Part1.cpp:58-127,
+ *                          t1.cpp:1182 t1_encode_cblk).
+ *   grkgpu_t1_decode_blocks  Tier1::decodeCodeblocks -> T1Part1::decode +
+ *                          postDecode (t1/Tier1.cpp:177, T1Decoder.cpp:43,
+ *                          T1Part1.cpp:129-330, t1.cpp:1038 t1_decode_cblk).
+ *
+ * Error behaviour mirrors the reference: functions return 0 on success and a
+ * negative code on failure (the reference returns bool false / nullptr and
+ * logs through its error handler); grkgpu_last_error() returns the message.
+ * Every function fails loudly (GRKGPU_ENODEV) when no gfx950 device is
+ * usable -- there is no CPU fallback.
+ */
+#ifndef GRK_MI355X_H
+#define GRK_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRKGPU_MAX_COMPS 16
+
+enum {
+    GRKGPU_OK = 0,
+    GRKGPU_EINVAL = -1,
+    GRKGPU_ENODEV = -2,
+    GRKGPU_EHIP = -3,
+    GRKGPU_EUNSUPPORTED = -4,
+    GRKGPU_ECORRUPT = -5
+};
+
+/* grk_image subset (grok.h:851-918): planar int32 components, dx = dy = 1 */
+typedef struct {
+    uint32_t x0, y0, x1, y1;
+    uint32_t numcomps;
+    uint32_t prec[GRKGPU_MAX_COMPS];
+    int32_t sgnd[GRKGPU_MAX_COMPS];
+} grkgpu_image_desc;
+
+/* grk_cparameters subset (grok.h:447-570) */
+typedef struct {
+    uint32_t numresolution;                /* default 6 */
+    uint32_t cblockw_init, cblockh_init;   /* default 64, 64 (powers of 2, <= 64) */
+    int32_t irreversible;                  /* 0: 5/3, 1: 9/7 (-I) */
+    int32_t tcp_mct;                       /* -1: auto (RGB->YCC iff >= 3 comps), 0, 1 */
+    int32_t tile_size_on;
+    uint32_t cp_tdx, cp_tdy, cp_tx0, cp_ty0;
+} grkgpu_cparams;
+
+typedef struct grkgpu_ctx grkgpu_ctx;
+
+/* Per-stage timings of the last call (device time from HIP events, ms). */
+typedef struct {
+    float h2d_ms, dcshift_mct_ms, dwt_ms, t1_ms, gather_ms, d2h_ms, host_t2_ms, total_ms;
+    uint64_t num_cblks, cs_bytes;
+} grkgpu_stats;
+
+const char *grkgpu_version(void);
+const char *grkgpu_last_error(void);
+int grkgpu_device_count(void);
+
+int grkgpu_create(int device, grkgpu_ctx **out);
+void grkgpu_destroy(grkgpu_ctx *ctx);
+/* Order all work of ctx after/with this HIP stream (hipStream_t as void*). */
+int grkgpu_set_stream(grkgpu_ctx *ctx, void *stream);
+int grkgpu_get_stats(grkgpu_ctx *ctx, grkgpu_stats *out);
+void grkgpu_default_cparams(grkgpu_cparams *p);
+
+/* Whole-codestream encode.  planes[c] = (y1-y0)*(x1-x0) int32 samples, on
+ * the device when planes_on_device != 0, else host memory.  The .j2k
+ * codestream is returned in *out (free with grkgpu_free). */
+int grkgpu_compress(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                    const int32_t *const *planes, int planes_on_device, uint8_t **out, size_t *outlen);
+
+/* Parse the main header only. */
+int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
+
+/* Whole-codestream decode into caller-provided planes (device or host). */
+int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_image_desc *img,
+                      int32_t *const *planes, int planes_on_device);
+
+void grkgpu_free(void *p);
+
+/* ---- stage entry points (device pointers, asynchronous on `stream`) ---- */
+
+int grkgpu_dcshift_mct_fwd(int32_t *const *planes, uint32_t numcomps, uint32_t w, uint32_t h,
+                           uint32_t stride, const int32_t *shift, int32_t mct, int32_t irreversible,
+                           void *stream);
+int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps, uint32_t w, uint32_t h,
+                           uint32_t stride, const uint32_t *prec, const int32_t *sgnd, int32_t mct,
+                           int32_t irreversible, void *stream);
+/* In-place (Mallat layout) forward / inverse DWT of one tile-component with
+ * origin (x0,y0), size (x1-x0) x (y1-y0), row stride x1-x0.  scratch must
+ * hold 2 * (x1-x0) * (y1-y0) + 256 int32 (device).  For 9/7 inverse the buffer holds
+ * float bit patterns. */
+int grkgpu_dwt_fwd(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                   uint32_t numres, int32_t irreversible, void *stream);
+int grkgpu_dwt_inv(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                   uint32_t numres, int32_t irreversible, void *stream);
+
+/* Code-block descriptors for the T1 entry points (all device memory). */
+typedef struct {
+    uint64_t coef_off;    /* element offset of the block's top-left in `coef` */
+    uint64_t out_off;     /* byte offset in `out`; out[out_off - 1] must be 0 */
+    uint32_t stride, w, h, orient; /* orient = band number 0:LL 1:HL 2:LH 3:HH */
+    int32_t qmfbid, inv_step;      /* qmfbid 1 = 5/3, 0 = 9/7 (13-bit inv step) */
+} grkgpu_enc_block;
+
+typedef struct {
+    uint32_t numbps, numpasses, len, pad;
+    uint32_t rate[96];    /* cumulative pass rates after Grok's fix-ups */
+} grkgpu_enc_result;
+
+typedef struct {
+    uint64_t data_off;    /* byte offset of the block's single segment in `data` */
+    uint64_t dst_off;     /* element offset of the block's top-left in `dst` */
+    uint32_t len, numpasses, numbps, w, h, orient, dstride;
+    int32_t irreversible;
+    float stepsize;       /* decode step size (Quantizer.cpp:65-104, fraction 0.5) */
+    uint32_t pad;
+} grkgpu_dec_block;
+
+/* scratch: >= nblocks * grkgpu_t1_scratch_bytes() device bytes */
+size_t grkgpu_t1_scratch_bytes(void);
+int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
+                            void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream);
+int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t nblocks, const uint8_t *data,
+                            void *scratch, int32_t *dst, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1015,7 +1015,7 @@ static void free_tilecomp(tilecomp_t *tc) {
                     free(pr->cblks[cb].seg);
                 }
                 free(pr->cblks);
-                if (pr->cw * pr->ch) { free(pr->incl.nodes); free(pr->imsb.nodes); }
+                if (pr->cw * pr->ch != 0) { free(pr->incl.nodes); free(pr->imsb.nodes); }
             }
             free(b->precs);
         }
@@ -1224,9 +1224,13 @@ static int64_t t2_decode_packet(tilecomp_t *tc, uint32_t resno, uint32_t precno,
     }
     bio_r r = {p, n, 0, 0, 0, 0};
     uint32_t present = br_read(&r, 1);
-    uint32_t seglen[4096];
-    cblk_t *segcb[4096];
+    uint32_t ncb_total = 0;
+    for (uint32_t bandno = 0; bandno < res->numbands; ++bandno)
+        ncb_total += res->bands[bandno].precs[precno].cw * res->bands[bandno].precs[precno].ch;
+    uint32_t *seglen = (uint32_t *)malloc(sizeof(uint32_t) * (ncb_total + 1));
+    cblk_t **segcb = (cblk_t **)malloc(sizeof(cblk_t *) * (ncb_total + 1));
     uint32_t nseg = 0;
+    int64_t ret = -1;
     if (present) {
         for (uint32_t bandno = 0; bandno < res->numbands; ++bandno) {
             band_t *b = &res->bands[bandno];
@@ -1250,17 +1254,17 @@ static int64_t t2_decode_packet(tilecomp_t *tc, uint32_t resno, uint32_t precno,
                 /* cblksty 0: one segment of up to 109 passes */
                 uint32_t L = br_read(&r, c->numlenbits + floorlog2_u(np));
                 c->dec_passes += np;
-                if (nseg < 4096) { seglen[nseg] = L; segcb[nseg] = c; nseg++; }
-                if (r.err) return -1;
+                seglen[nseg] = L; segcb[nseg] = c; nseg++;
+                if (r.err) goto done;
             }
         }
     }
     br_align(&r);
-    if (r.err) return -1;
+    if (r.err) goto done;
     size_t off = r.off;
     for (uint32_t i = 0; i < nseg; ++i) {
         cblk_t *c = segcb[i];
-        if (off + seglen[i] > n) return -1;
+        if (off + seglen[i] > n) goto done;
         if (c->seglen + seglen[i] + 2 > c->segcap) {
             c->segcap = (c->seglen + seglen[i] + 2) * 2;
             c->seg = (uint8_t *)realloc(c->seg, c->segcap);
@@ -1269,7 +1273,10 @@ static int64_t t2_decode_packet(tilecomp_t *tc, uint32_t resno, uint32_t precno,
         c->seglen += seglen[i];
         off += seglen[i];
     }
-    return (int64_t)off;
+    ret = (int64_t)off;
+done:
+    free(seglen); free(segcb);
+    return ret;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -1514,7 +1521,7 @@ int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads)
     }
     if (!tdata || prog != 0 || cblksty != 0 || numlayers == 0) { free(tdata); return -2; }
     uint32_t iw = out->x1 - out->x0, ih = out->y1 - out->y0;
-    for (uint32_t k = 0; k < nc; ++k) out->data[k] = (int32_t *)calloc((size_t)iw * ih ? (size_t)iw * ih : 1, sizeof(int32_t));
+    for (uint32_t k = 0; k < nc; ++k) out->data[k] = (int32_t *)calloc(((size_t)iw * ih) != 0 ? (size_t)iw * ih : 1, sizeof(int32_t));
     int rc = 0;
     for (uint32_t tileno = 0; tileno < ntiles && rc == 0; ++tileno) {
         rect_t tr;

@@ -7,7 +7,7 @@
  * product never links it.  It is a plain-C restatement written from ISO/IEC
  * 15444-1 plus the observed behaviour of the reference (file:line citations at
  * each function in grk_oracle.c), and it is pinned against the reference's own
- * output: tests/golden/*.j2k were produced by the reference grk_compress and
+ * output: the tests/golden j2k files were produced by the reference grk_compress and
  * must be reproduced byte-for-byte (tests/test_oracle_golden.py).
  *
  * Scope: DC shift, RCT/ICT, forward/inverse 5/3 + 9/7 DWT,

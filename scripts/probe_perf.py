@@ -1,0 +1,38 @@
+"""Quick per-stage timing probe on the GPU box (not the bench)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden")]
+import numpy as np
+import torch
+import grokimagecompression_amd as grk
+import synth
+
+configs = [a for a in sys.argv[1:]] or ["4k", "8k"]
+codec = grk.Codec(0)
+for cfg in configs:
+    if cfg == "4k":
+        h, w, c, bits, modes = 2160, 3840, 3, 8, [False]
+    else:
+        h, w, c, bits, modes = 4320, 7680, 3, 12, [True, False]
+    img = synth.synth_image(h, w, c, bits, 3)
+    t = torch.from_numpy(img).cuda()
+    for irrev in modes:
+        p = grk.CParams.make(irreversible=irrev)
+        for it in range(3):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            b = codec.compress(t, bits, p)
+            t1 = time.time()
+            se = codec.stats()
+            out = codec.decompress(b, device_out=True)
+            torch.cuda.synchronize()
+            t2 = time.time()
+            sd = codec.stats()
+        ok = irrev or torch.equal(out, t)
+        print(f"{cfg} irrev={irrev} bytes={len(b)} enc {1e3*(t1-t0):.1f} ms dec {1e3*(t2-t1):.1f} ms "
+              f"Mpix/s={h*w/1e6/(t2-t0):.1f} lossless_ok={ok}", flush=True)
+        print("  enc", {k: round(v, 3) if isinstance(v, float) else v for k, v in se.items()}, flush=True)
+        print("  dec", {k: round(v, 3) if isinstance(v, float) else v for k, v in sd.items()}, flush=True)
