@@ -1,0 +1,158 @@
+"""bench.py -- Mpixels/s encode+decode of 8K RGB frames, 5/3 lossless & 9/7 lossy.
+
+Workload (BASELINE.json configs[2], the metric's 8K RGB case): one synthetic
+7680x4320 12-bit RGB frame per GPU (tests/golden/synth.py "smooth", seed 3 on
+rank 0 -- the same image whose reference codestream hashes are pinned in
+tests/golden/manifest_large.json).  One step = encode + decode of the frame
+with the 9/7 irreversible path (grk_compress -I) + encode + decode with the
+5/3 lossless path (default options), i.e. 2 frames' worth of pixels through
+both directions.  The frame is HBM-resident when timing starts; decoded planes
+are written back to HBM.  The codestream crosses PCIe once each way because
+Tier-2 / headers run on the host.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each encodes/decodes
+its own frame -- a frame batch, no data-path collective;
+"scaling": "weak".  value = frames*pixels of all ranks / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden"), os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+H, W, C, BITS = 4320, 7680, 3, 12
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def dwt_bytes(h, w, c, numres=6):
+    """B_DWT: sum over levels of 8 B x |R_l| (read + write int32)."""
+    tot = 0
+    rh, rw = h, w
+    for _ in range(numres - 1):
+        tot += 8 * rh * rw
+        rh, rw = (rh + 1) // 2, (rw + 1) // 2
+    return tot * c
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    import grokimagecompression_amd as grk
+    import synth
+
+    img = synth.synth_image(H, W, C, BITS, 3 + rank)
+    frame = torch.from_numpy(img).to("cuda:%d" % local)
+    codec = grk.Codec(local)
+    p97 = grk.CParams.make(irreversible=True)
+    p53 = grk.CParams.make(irreversible=False)
+    out97 = torch.empty_like(frame)
+    out53 = torch.empty_like(frame)
+    st = {}
+
+    def step():
+        b97 = codec.compress(frame, BITS, p97, view=True)
+        st["enc97"] = codec.stats()
+        codec.decompress(b97, out=out97)
+        st["dec97"] = codec.stats()
+        b53 = codec.compress(frame, BITS, p53, view=True)
+        st["enc53"] = codec.stats()
+        codec.decompress(b53, out=out53)
+        st["dec53"] = codec.stats()
+        st["bytes"] = (len(b97), len(b53))
+
+    for _ in range(args.warmup):
+        step()
+    assert torch.equal(out53, frame), "5/3 round trip is not lossless"
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pix_per_step = 2 * H * W  # one frame through 9/7 + one through 5/3
+    value = world * pix_per_step * args.steps / elapsed / 1e6
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline: the forward DWT (encode), B_DWT / measured kernel time (HIP
+    # events around the DWT launches on the codec's stream)
+    bdwt = dwt_bytes(H, W, C)
+    dwt_ms = st["enc97"]["dwt_ms"]
+    achieved = bdwt / (dwt_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "kernel": "k_dwt_fwd_level<9/7> (all 5 levels x 3 comps)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes": bdwt, "kernel_ms": round(dwt_ms, 4)}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        import pyoracle
+        pyoracle.build()
+        ncpu = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        b = pyoracle.encode(img, BITS, pyoracle.params(irreversible=True, nthreads=ncpu))
+        pyoracle.decode(b, nthreads=ncpu)
+        b = pyoracle.encode(img, BITS, pyoracle.params(irreversible=False, nthreads=ncpu))
+        pyoracle.decode(b, nthreads=ncpu)
+        ct = time.perf_counter() - t0
+        cpu = {"value": round(pix_per_step / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "port",
+               "sample": "1 step (8K 12-bit RGB frame: 9/7 enc+dec + 5/3 enc+dec) through the C oracle "
+                         "(oracle/grk_oracle.c, byte-identical to Grok 5.1.0), %d threads" % ncpu,
+               "seconds": round(ct, 2)}
+
+    if rank == 0:
+        def r(d):
+            return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
+        line = {
+            "metric": "Mpixels/sec encode+decode, 8K RGB 5/3 lossless & 9/7 lossy",
+            "value": round(value, 2), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32/f32 (integer encode, f32 9/7 decode)",
+            "data": "synthetic (tests/golden/synth.py smooth+2% noise, seed 3+rank)",
+            "config": {"workload": "8K 7680x4320 12-bit RGB frame per GPU; 9/7 (-I) + 5/3 lossless, enc+dec; "
+                                   "6 resolutions, 64x64 code-blocks, 1 layer LRCP",
+                       "frames_per_step_per_gpu": 2, "parallelism": "frame-batch x%d (no collectives)" % world},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "codestream_bytes": {"9/7": st["bytes"][0], "5/3": st["bytes"][1]},
+            "stage_ms": {k: r(st[k]) for k in ("enc97", "dec97", "enc53", "dec53")},
+        }
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

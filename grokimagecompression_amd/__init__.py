@@ -105,6 +105,12 @@ def build():
 def lib():
     global _lib
     if _lib is None:
+        # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's); load
+        # it first so the process has ONE HIP runtime shared by torch and us.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise GrkGpuError("libgrk_mi355x.so not built (run grokimagecompression_amd.build()); "
                               "there is no CPU fallback")
@@ -119,8 +125,10 @@ def lib():
         L.grkgpu_default_cparams.argtypes = [P(CParams)]
         L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
                                       P(ctypes.c_size_t)]
-        L.grkgpu_read_header.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P(ImageDesc)]
-        L.grkgpu_decompress.argtypes = [VP, ctypes.c_char_p, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
+        L.grkgpu_compress_view.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int,
+                                           P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
+        L.grkgpu_read_header.argtypes = [VP, ctypes.c_size_t, P(ImageDesc)]
+        L.grkgpu_decompress.argtypes = [VP, VP, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_free.argtypes = [VP]
         L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
@@ -138,9 +146,25 @@ def _check(rc):
         raise GrkGpuError("grkgpu error %d: %s" % (rc, lib().grkgpu_last_error().decode()))
 
 
+def _buf_ptr(buf):
+    """(pointer, length, keepalive) of a codestream held in bytes / bytearray /
+    numpy uint8 array, without copying."""
+    if isinstance(buf, np.ndarray):
+        assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+        return ctypes.c_void_p(buf.ctypes.data), buf.size, buf
+    if isinstance(buf, bytearray):
+        arr = (ctypes.c_char * len(buf)).from_buffer(buf)
+        return ctypes.cast(arr, ctypes.c_void_p), len(buf), arr
+    if not isinstance(buf, bytes):
+        buf = bytes(buf)
+    cp = ctypes.c_char_p(buf)
+    return ctypes.cast(cp, ctypes.c_void_p), len(buf), (cp, buf)
+
+
 def read_header(buf):
     d = ImageDesc()
-    _check(lib().grkgpu_read_header(bytes(buf), len(buf), ctypes.byref(d)))
+    ptr, n, keep = _buf_ptr(buf)
+    _check(lib().grkgpu_read_header(ptr, n, ctypes.byref(d)))
     return d
 
 
@@ -178,9 +202,11 @@ class Codec:
         _check(lib().grkgpu_get_stats(self._ctx, ctypes.byref(s)))
         return s.as_dict()
 
-    def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False):
+    def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False, view=False):
         """img: (c,h,w) int32 numpy array (host) or torch tensor on cuda:<device>.
-        Returns the .j2k codestream as bytes."""
+        Returns the .j2k codestream as bytes, or (view=True) as a zero-copy numpy
+        uint8 view of the context's pinned output buffer, valid until the next
+        call on this Codec."""
         params = params or CParams.make()
         c, h, w = img.shape
         d = ImageDesc()
@@ -201,6 +227,10 @@ class Codec:
             ptrs = (ctypes.c_void_p * c)(*[img[k].ctypes.data for k in range(c)])
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
+        if view:
+            _check(lib().grkgpu_compress_view(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs,
+                                              1 if on_dev else 0, ctypes.byref(out), ctypes.byref(n)))
+            return np.ctypeslib.as_array(out, shape=(n.value,))
         _check(lib().grkgpu_compress(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0,
                                      ctypes.byref(out), ctypes.byref(n)))
         b = ctypes.string_at(out, n.value)
@@ -210,7 +240,6 @@ class Codec:
     def decompress(self, buf, device_out=False, out=None):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
         device_out / out is a cuda tensor)."""
-        buf = bytes(buf)
         d = read_header(buf)
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
         on_dev = device_out or (out is not None and not isinstance(out, np.ndarray))
@@ -224,7 +253,8 @@ class Codec:
             if out is None:
                 out = np.empty((c, h, w), dtype=np.int32)
             ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
-        _check(lib().grkgpu_decompress(self._ctx, buf, len(buf), None, ptrs, 1 if on_dev else 0))
+        bp, bn, keep = _buf_ptr(buf)
+        _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
         return out
 
 

@@ -79,7 +79,7 @@ struct grkgpu_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs;
-    HostBuf h_results, h_packed, h_gather, h_blocks;
+    HostBuf h_results, h_packed, h_gather, h_blocks, h_out;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
 };
@@ -276,9 +276,9 @@ static void for_each_cblk(TileComp &tc, F f) {
 // ---------------------------------------------------------------------------
 // encode
 // ---------------------------------------------------------------------------
-extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
-                               const int32_t *const *planes, int planes_on_device, uint8_t **out, size_t *outlen) {
-    if (!c || !planes || !out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                         const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen) {
+    if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
     if (rc) return rc;
@@ -378,11 +378,12 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     HIPCHK(hipStreamSynchronize(s));
     const EncResult *res = c->h_results.as<EncResult>();
 
-    // pack block bytes: layer 0 takes every pass -> passes[last].rate bytes
+    // Tier-2 + headers on the host (j2k_encode :2059, j2k_write_sot :5065,
+    // T2::encode_packets): only header BITS are produced here; the code-block
+    // bytes never visit the host -- a gather kernel assembles the codestream
+    // in HBM and one D2H copies it into the pinned output buffer.
+    double t_t2 = now_ms();
     std::vector<BlockT2> bt(nblk);
-    std::vector<GatherItem> gi;
-    gi.reserve(nblk);
-    uint64_t packed = 0;
     for (uint32_t i = 0; i < nblk; ++i) {
         const EncResult &r = res[i];
         if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
@@ -390,52 +391,62 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
         bt[i].numpasses = r.numpasses;
         bt[i].rate = r.rate;
         bt[i].datalen = r.numpasses ? r.rate[r.numpasses - 1] : 0;
-        bt[i].packed_off = packed;
-        if (bt[i].datalen) {
-            if (bt[i].datalen > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
-            gi.push_back({eb[i].out_off, packed, bt[i].datalen, 0});
-        }
-        packed += bt[i].datalen;
+        bt[i].dev_off = eb[i].out_off;
+        if (bt[i].datalen > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
     }
-    HIPCHK(c->gather.ensure(gi.size() * sizeof(GatherItem) + 256));
-    HIPCHK(c->h_gather.ensure(gi.size() * sizeof(GatherItem) + 256));
-    HIPCHK(c->packed.ensure(packed + 256));
-    HIPCHK(c->h_packed.ensure(packed + 256));
-    memcpy(c->h_gather.p, gi.data(), gi.size() * sizeof(GatherItem));
-    HIPCHK(hipEventRecord(c->ev[5], s));
-    HIPCHK(hipMemcpyAsync(c->gather.p, c->h_gather.p, gi.size() * sizeof(GatherItem), hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather(c->mqout.as<uint8_t>(), c->gather.as<GatherItem>(), (uint32_t)gi.size(),
-                         c->packed.as<uint8_t>(), s));
-    HIPCHK(hipEventRecord(c->ev[6], s));
-    HIPCHK(hipMemcpyAsync(c->h_packed.p, c->packed.p, packed, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipEventRecord(c->ev[7], s));
-    HIPCHK(hipStreamSynchronize(s));
-    double t_t2 = now_ms();
-
-    // host Tier-2 + headers (j2k_encode :2059, j2k_write_sot :5065, T2::encode_packets)
-    ByteBuf cs;
-    cs.v.reserve(packed + packed / 16 + 4096);
-    write_main_header(cs, cp);
-    const uint8_t *pk = c->h_packed.as<uint8_t>();
+    ByteBuf hdr;
+    hdr.v.reserve(1 << 20);
+    std::vector<PlanItem> plan;
+    plan.reserve(nblk + 64);
+    write_main_header(hdr, cp);
+    plan.push_back({0, (uint32_t)hdr.size(), 0});
     for (auto &tile : tiles) {
-        size_t sot = cs.size();
-        cs.put16(0xFF90); cs.put16(10); cs.put16(tile.index); cs.put32(0); cs.put8(0); cs.put8(1);
-        cs.put16(0xFF93);
+        size_t sot = hdr.size();
+        hdr.put16(0xFF90); hdr.put16(10); hdr.put16(tile.index); hdr.put32(0); hdr.put8(0); hdr.put8(1);
+        hdr.put16(0xFF93);
+        plan.push_back({sot, 14, 0});
+        size_t first = plan.size() - 1;
         for (uint32_t resno = 0; resno < cp.numres; ++resno)  // LRCP, one layer
             for (uint32_t k = 0; k < nc; ++k) {
                 TileComp &tc = tile.comps[k];
                 Resolution &r = tc.res[resno];
-                for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) encode_packet(tc, resno, precno, bt, pk, cs);
+                for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) encode_packet(tc, resno, precno, bt, hdr, plan);
             }
-        cs.set32(sot + 6, (uint32_t)(cs.size() - sot));
+        uint64_t psot = 0;
+        for (size_t i = first; i < plan.size(); ++i) psot += plan[i].len;
+        hdr.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
     }
-    cs.put16(0xFFD9);
+    size_t eoc = hdr.size();
+    hdr.put16(0xFFD9);
+    plan.push_back({eoc, 2, 0});
+    // gather list: dst offsets = prefix sum of run lengths
+    std::vector<GatherItem> gi;
+    gi.reserve(plan.size());
+    uint64_t total = 0;
+    for (auto &pi : plan) {
+        if (pi.len) gi.push_back({pi.src, total, pi.len, pi.kind});
+        total += pi.len;
+    }
+    double t_t2_end = now_ms();
+    HIPCHK(c->gather.ensure(gi.size() * sizeof(GatherItem) + hdr.size() + 512));
+    HIPCHK(c->h_gather.ensure(gi.size() * sizeof(GatherItem) + hdr.size() + 512));
+    HIPCHK(c->packed.ensure(total + 256));
+    HIPCHK(c->h_out.ensure(total + 256));
+    const size_t gbytes = gi.size() * sizeof(GatherItem);
+    const size_t hoff = (gbytes + 255) & ~(size_t)255;
+    memcpy(c->h_gather.p, gi.data(), gbytes);
+    memcpy(c->h_gather.as<uint8_t>() + hoff, hdr.v.data(), hdr.size());
+    HIPCHK(hipEventRecord(c->ev[5], s));
+    HIPCHK(hipMemcpyAsync(c->gather.p, c->h_gather.p, hoff + hdr.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather(c->gather.as<uint8_t>() + hoff, c->mqout.as<uint8_t>(), c->gather.as<GatherItem>(),
+                         (uint32_t)gi.size(), c->packed.as<uint8_t>(), s));
+    HIPCHK(hipEventRecord(c->ev[6], s));
+    HIPCHK(hipMemcpyAsync(c->h_out.p, c->packed.p, total, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->ev[7], s));
+    HIPCHK(hipStreamSynchronize(s));
     double t_end = now_ms();
-    uint8_t *o = (uint8_t *)malloc(cs.size());
-    if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
-    memcpy(o, cs.v.data(), cs.size());
-    *out = o;
-    *outlen = cs.size();
+    *view = c->h_out.as<uint8_t>();
+    *outlen = total;
 
     grkgpu_stats &st = c->stats;
     memset(&st, 0, sizeof(st));
@@ -445,10 +456,32 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     hipEventElapsedTime(&st.t1_ms, c->ev[3], c->ev[4]);
     hipEventElapsedTime(&st.gather_ms, c->ev[5], c->ev[6]);
     hipEventElapsedTime(&st.d2h_ms, c->ev[6], c->ev[7]);
-    st.host_t2_ms = (float)(t_end - t_t2);
+    st.host_t2_ms = (float)(t_t2_end - t_t2);
     st.total_ms = (float)(t_end - t_start);
     st.num_cblks = nblk;
-    st.cs_bytes = cs.size();
+    st.cs_bytes = total;
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_compress_view(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                                    const int32_t *const *planes, int planes_on_device, const uint8_t **out,
+                                    size_t *outlen) {
+    if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    return compress_impl(c, img, p, planes, planes_on_device, out, outlen);
+}
+
+extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                               const int32_t *const *planes, int planes_on_device, uint8_t **out, size_t *outlen) {
+    if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    const uint8_t *v = nullptr;
+    size_t n = 0;
+    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n);
+    if (rc) return rc;
+    uint8_t *o = (uint8_t *)malloc(n ? n : 1);
+    if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
+    memcpy(o, v, n);
+    *out = o;
+    *outlen = n;
     return GRKGPU_OK;
 }
 
@@ -597,13 +630,15 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(BlockRows) + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
-    HIPCHK(c->h_packed.ensure(len + extra.size() + 256));
-    memcpy(c->h_packed.p, csb, len);
-    if (!extra.empty()) memcpy(c->h_packed.as<uint8_t>() + len, extra.data(), extra.size());
     memcpy(c->h_blocks.p, db.data(), (size_t)nblk * sizeof(DecBlock));
 
     HIPCHK(hipEventRecord(c->ev[0], s));
-    HIPCHK(hipMemcpyAsync(c->cs.p, c->h_packed.p, len + extra.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->cs.p, csb, len, hipMemcpyHostToDevice, s));
+    if (!extra.empty()) {
+        HIPCHK(c->h_packed.ensure(extra.size() + 256));
+        memcpy(c->h_packed.p, extra.data(), extra.size());
+        HIPCHK(hipMemcpyAsync(c->cs.as<uint8_t>() + len, c->h_packed.p, extra.size(), hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<BlockRows>(),

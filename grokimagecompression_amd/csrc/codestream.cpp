@@ -305,8 +305,9 @@ struct BitReader {
 };
 }  // namespace
 
-void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk,
-                   const uint8_t *packed, ByteBuf &out) {
+void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk, ByteBuf &out,
+                   std::vector<PlanItem> &plan) {
+    const size_t hstart = out.size();
     Resolution &res = tc.res[resno];
     const uint32_t layno = 0;
     for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
@@ -346,6 +347,7 @@ void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vec
         }
     }
     w.flush();
+    plan.push_back({hstart, (uint32_t)(out.size() - hstart), 0});
     for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
         Band &b = res.bands[bandno];
         Precinct &pr = b.precs[precno];
@@ -353,7 +355,8 @@ void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vec
         for (auto &c : pr.cblks) {
             const BlockT2 &bt = blk[c.gidx];
             if (!bt.numpasses) continue;
-            out.putn(packed + bt.packed_off, bt.rate[bt.numpasses - 1]);
+            uint32_t L = bt.rate[bt.numpasses - 1];
+            if (L) plan.push_back({bt.dev_off, L, 1});
             c.included = true;
         }
     }

@@ -119,13 +119,23 @@ struct ByteBuf {
 struct BlockT2 {
     uint32_t numbps, numpasses, datalen;
     const uint32_t *rate;     // cumulative rates (numpasses)
-    uint64_t packed_off;      // offset of the block's bytes in the packed buffer
+    uint64_t dev_off;         // offset of the block's MQ bytes in the device slab
+};
+
+// The codestream is assembled on the device: the host writes headers into a
+// small blob and a plan of (source, length) runs; a gather kernel copies the
+// runs (header bytes or code-block bytes) into their final positions.
+struct PlanItem {
+    uint64_t src;   // kind 0: offset in the header blob; kind 1: offset in the MQ slab
+    uint32_t len;
+    uint32_t kind;
 };
 
 void write_main_header(ByteBuf &cs, const CodingParams &cp);
-// one packet (T2.cpp:859-1110), layer 0 containing all passes
-void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk,
-                   const uint8_t *packed, ByteBuf &out);
+// one packet (T2.cpp:859-1110), layer 0 containing all passes: header bits go
+// to `hdr`, the packet's runs are appended to `plan`
+void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk, ByteBuf &hdr,
+                   std::vector<PlanItem> &plan);
 
 // decoder
 bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err);

@@ -37,7 +37,7 @@ struct DecBlock {
     uint32_t pad;
 };
 
-struct GatherItem { uint64_t src, dst; uint32_t len, pad; };
+struct GatherItem { uint64_t src, dst; uint32_t len, pad; };  // pad: 0 = header blob, 1 = MQ slab
 
 hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const PlanePtrs &dst, uint32_t tw,
                                   uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct, int32_t irrev,
@@ -55,6 +55,7 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
                             uint8_t *out, EncResult *res, hipStream_t s);
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, BlockRows *scratch,
                             int32_t *tiles, hipStream_t s);
-hipError_t launch_gather(const uint8_t *src, const GatherItem *items, uint32_t n, uint8_t *dst, hipStream_t s);
+hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,
+                         hipStream_t s);
 
 }  // namespace grkgpu

@@ -344,13 +344,15 @@ __global__ __launch_bounds__(64) void k_t1_decode(const DecBlock *__restrict__ b
                          c_mq_tab, dst, b.dstride, pd);
 }
 
-// copy each block's MQ bytes to its packed position
-__global__ void k_gather(const uint8_t *__restrict__ src, const GatherItem *__restrict__ items, uint32_t n,
-                         uint8_t *__restrict__ dst) {
+// Codestream assembly: copy each run (header bytes from the host-written blob,
+// or a code-block's MQ bytes from the T1 slab) to its final offset.
+__global__ void k_gather(const uint8_t *__restrict__ hdr, const uint8_t *__restrict__ slab,
+                         const GatherItem *__restrict__ items, uint32_t n, uint8_t *__restrict__ dst) {
     uint32_t i = blockIdx.x;
     if (i >= n) return;
     GatherItem it = items[i];
-    for (uint32_t k = threadIdx.x; k < it.len; k += blockDim.x) dst[it.dst + k] = src[it.src + k];
+    const uint8_t *src = (it.pad ? slab : hdr) + it.src;
+    for (uint32_t k = threadIdx.x; k < it.len; k += blockDim.x) dst[it.dst + k] = src[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -413,9 +415,10 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     return hipGetLastError();
 }
 
-hipError_t launch_gather(const uint8_t *src, const GatherItem *items, uint32_t n, uint8_t *dst, hipStream_t s) {
+hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,
+                         hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, s, src, items, n, dst);
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, s, hdr, slab, items, n, dst);
     return hipGetLastError();
 }
 

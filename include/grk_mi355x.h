@@ -104,6 +104,11 @@ void grkgpu_default_cparams(grkgpu_cparams *p);
 int grkgpu_compress(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                     const int32_t *const *planes, int planes_on_device, uint8_t **out, size_t *outlen);
 
+/* Same, zero-copy: *out points into the context's pinned output buffer and
+ * stays valid until the next call on ctx (like the reference's memory stream). */
+int grkgpu_compress_view(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                         const int32_t *const *planes, int planes_on_device, const uint8_t **out, size_t *outlen);
+
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
 
