@@ -78,8 +78,8 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs;
-    HostBuf h_results, h_packed, h_gather, h_blocks, h_out;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff;
+    HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
 };
@@ -156,7 +156,7 @@ int grkgpu_get_stats(grkgpu_ctx *c, grkgpu_stats *out) {
 
 void grkgpu_free(void *p) { free(p); }
 
-size_t grkgpu_t1_scratch_bytes(void) { return sizeof(BlockRows); }
+size_t grkgpu_t1_scratch_bytes(void) { return sizeof(T1Scratch) + 32 * (size_t)sym_slot_bytes(64, 64); }
 
 }  // extern "C"
 
@@ -293,6 +293,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     std::vector<Tile> tiles(ntiles);
     uint64_t arena = 0, max_tc = 0;
     std::vector<EncBlock> eb;
+    std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
+    uint64_t sym_total = 0;
+    uint32_t maxdepth = 1;
     for (uint32_t t = 0; t < ntiles; ++t) {
         Tile &tile = tiles[t];
         tile.index = t;
@@ -317,6 +320,10 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 b.qmfbid = cp.irrev ? 0 : 1;
                 b.inv_step = (int32_t)band.inv_step;
                 eb.push_back(b);
+                const uint32_t bound = std::min<uint32_t>(band.numbps, 32);
+                symoff.push_back(sym_total);
+                sym_total += (uint64_t)bound * sym_slot_bytes(b.w, b.h);
+                maxdepth = std::max(maxdepth, bound);
             });
         }
     }
@@ -330,12 +337,16 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
-    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(BlockRows) + 256));
+    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     HIPCHK(c->results.ensure((size_t)nblk * sizeof(EncResult) + 256));
     HIPCHK(c->h_results.ensure((size_t)nblk * sizeof(EncResult) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
+    symoff.push_back(sym_total);
+    HIPCHK(c->sym.ensure(sym_total + 256));
+    HIPCHK(c->symoff.ensure(symoff.size() * 8 + 256));
+    HIPCHK(c->h_symoff.ensure(symoff.size() * 8 + 256));
 
     HIPCHK(hipEventRecord(c->ev[0], s));
     // input planes on the device
@@ -371,8 +382,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipEventRecord(c->ev[3], s));
     memcpy(c->h_blocks.p, eb.data(), (size_t)nblk * sizeof(EncBlock));
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(EncBlock), hipMemcpyHostToDevice, s));
-    HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<BlockRows>(),
-                            c->mqout.as<uint8_t>(), c->results.as<EncResult>(), s));
+    memcpy(c->h_symoff.p, symoff.data(), symoff.size() * 8);
+    HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
+                            c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
+                            c->results.as<EncResult>(), s));
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipMemcpyAsync(c->h_results.p, c->results.p, (size_t)nblk * sizeof(EncResult), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -386,6 +400,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     std::vector<BlockT2> bt(nblk);
     for (uint32_t i = 0; i < nblk; ++i) {
         const EncResult &r = res[i];
+        if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
         if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
         bt[i].numbps = r.numbps;
         bt[i].numpasses = r.numpasses;
@@ -627,7 +642,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
-    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(BlockRows) + 256));
+    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     memcpy(c->h_blocks.p, db.data(), (size_t)nblk * sizeof(DecBlock));
@@ -641,7 +656,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
-    HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<BlockRows>(),
+    HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
                             c->coef.as<int32_t>(), s));
     HIPCHK(hipEventRecord(c->ev[2], s));
     int32_t *llA = c->ll.as<int32_t>(), *llB = llA + (max_tc / 2 + 64);
@@ -773,7 +788,9 @@ extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t 
     if (!blocks || !coef || !scratch || !out || !results) return set_err(GRKGPU_EINVAL, "null argument");
     int rc = check_device(0);
     if (rc) return rc;
-    HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, (BlockRows *)scratch, out,
+    // scratch layout: nblocks T1Scratch records, then 32 fixed symbol slots per block
+    uint8_t *sym = (uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch);
+    HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, (T1Scratch *)scratch, sym, nullptr, 32, out,
                             (EncResult *)results, (hipStream_t)stream));
     return GRKGPU_OK;
 }
@@ -783,7 +800,7 @@ extern "C" int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t 
     if (!blocks || !data || !scratch || !dst) return set_err(GRKGPU_EINVAL, "null argument");
     int rc = check_device(0);
     if (rc) return rc;
-    HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (BlockRows *)scratch, dst,
+    HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (T1Scratch *)scratch, dst,
                             (hipStream_t)stream));
     return GRKGPU_OK;
 }

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "t1_core.h"
+#include "t1_lane.h"
 
 namespace grkgpu {
 
@@ -51,9 +51,13 @@ hipError_t launch_dwt_fwd_level(const int32_t *src, uint32_t sstride, int32_t *l
 hipError_t launch_dwt_inv_level(const int32_t *ll, uint32_t llstride, const int32_t *coef, uint32_t cstride,
                                 int32_t *dst, uint32_t dstride, int rw, int rh, int casx, int casy, int snx, int sny,
                                 int irrev, hipStream_t s);
-hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, BlockRows *scratch,
-                            uint8_t *out, EncResult *res, hipStream_t s);
-hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, BlockRows *scratch,
+// sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
+// capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
+// for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.
+hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
+                            uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
+                            hipStream_t s);
+hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s);
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,
                          hipStream_t s);

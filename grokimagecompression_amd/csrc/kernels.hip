@@ -8,13 +8,15 @@
 //     (inverse) lifting steps in LDS and scatters the four sub-bands (forward)
 //     or the reconstructed samples (inverse).  HBM traffic = one read + one
 //     write of the resolution per level (SURVEY.md 8(d) B_DWT).
-//   * T1: EBCOT encode / decode per code-block (t1_core.h).
+//   * T1: EBCOT encode / decode, one lane per code-block (t1_lane.h).
 //   * gather: compacts per-code-block MQ output into one contiguous buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "grk_device.h"
-#include "t1_core.h"
+#include "t1_lane.h"
+#include <stdlib.h>
+#include <string.h>
 
 namespace grkgpu {
 
@@ -305,43 +307,210 @@ __global__ __launch_bounds__(DWT_THREADS) void k_dwt_inv_level(const int32_t *__
 }
 
 // ---------------------------------------------------------------------------
-// T1
+// T1 (t1_lane.h).  Encode = prep (wave per block: quantise, sign rows, numbps,
+// magnitude bit-planes via ballots) + lane coder (one lane per block).
+// Decode = lane decoder (one lane per block, write-only bit-plane rows) +
+// rebuild (workgroup per block: values + post-decode scaling, coalesced).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_t1_encode(const EncBlock *__restrict__ blocks, uint32_t nblocks,
-                                                  const int32_t *__restrict__ coef, BlockRows *scratch,
-                                                  uint8_t *__restrict__ out, EncResult *__restrict__ res) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nblocks) return;
-    const EncBlock b = blocks[i];
-    EncResult &r = res[i];
-    out[b.out_off - 1] = 0;  // the MQ coder starts at bp = start - 1 (mqc_enc.cpp:240-260)
-    PassInfo passes[GRK_MAX_PASSES];
-    uint32_t numbps, len;
-    uint32_t np = t1_encode_block(coef + b.coef_off, b.stride, b.w, b.h, b.orient, b.qmfbid, b.inv_step,
-                                  scratch[i], c_mq_tab, out + b.out_off, passes, &numbps, &len);
-    r.numbps = numbps;
-    r.numpasses = np;
-    r.len = len;
-    for (uint32_t p = 0; p < np; ++p) r.rate[p] = passes[p].rate;
+template <int LANES>
+__device__ __forceinline__ void t1_tables_init(uint8_t *zc, uint8_t *sc, uint32_t *mq) {
+    for (uint32_t k = threadIdx.x; k < 2048; k += LANES) zc[k] = zc_lut_entry(k >> 9, k & 511);
+    for (uint32_t k = threadIdx.x; k < 256; k += LANES) sc[k] = sc_lut_entry(k);
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES) mq[k] = c_mq_tab[k];
+    __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_t1_decode(const DecBlock *__restrict__ blocks, uint32_t nblocks,
-                                                  const uint8_t *__restrict__ data, BlockRows *scratch,
-                                                  int32_t *__restrict__ tiles) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nblocks) return;
-    const DecBlock b = blocks[i];
-    int32_t *dst = tiles + b.dst_off;
-    if (b.len == 0 || b.numpasses == 0) {
-        for (uint32_t y = 0; y < b.h; ++y)
-            for (uint32_t x = 0; x < b.w; ++x) dst[(size_t)y * b.dstride + x] = 0;
+__global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blocks, const int32_t *__restrict__ coef,
+                                                T1Scratch *__restrict__ scr, EncResult *__restrict__ res) {
+    const uint32_t i = blockIdx.x, x = threadIdx.x;
+    const EncBlock b = blocks[i];
+    const int32_t *src = coef + b.coef_off;
+    uint32_t m[64];
+    uint64_t negrow = 0;
+    uint32_t orv = 0;
+#pragma unroll
+    for (int y = 0; y < 64; ++y) {
+        uint32_t mv = 0, ng = 0;
+        if ((uint32_t)y < b.h && x < b.w) mv = quant_mag(src[(size_t)y * b.stride + x], b.qmfbid, b.inv_step, &ng);
+        m[y] = mv;
+        orv |= mv;
+        uint64_t bal = __ballot(ng);
+        if (x == (uint32_t)y) negrow = bal;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) orv |= __shfl_xor(orv, off);
+    uint32_t numbps = 0;
+    if (orv) {
+        uint32_t t = 32u - (uint32_t)__clz(orv);
+        numbps = t <= 6 ? 0 : t - 6;
+    }
+    T1Scratch &S = scr[i];
+    S.st.neg[x + 1] = x < b.h ? negrow : 0;
+    if (x == 0) S.st.neg[0] = 0;
+    if (x == 63) S.st.neg[65] = 0;
+    uint64_t acc = 0;  // significance before plane p = OR of the planes above
+    for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
+        uint64_t mine = 0;
+#pragma unroll
+        for (int y = 0; y < 64; ++y) {
+            uint64_t bal = __ballot((m[y] >> (p + 6)) & 1u);
+            if (x == (uint32_t)y) mine = bal;
+        }
+        if (x < b.h) {
+            S.pa[p * 64 + x] = mine;
+            S.pb[p * 64 + x] = acc;
+        }
+        acc |= mine;
+    }
+    if (x == 0) {
+        res[i].numbps = numbps;
+        res[i].pad = 0;
+    }
+}
+
+// Context modelling, one lane per (block, bit-plane): lanes are laid out
+// depth-major (depth = numbps-1-p) so a wavefront holds the same depth of 64
+// neighbouring blocks -- similar statistics, little divergence.
+__device__ __forceinline__ uint64_t sym_block_off(const uint64_t *sym_off, uint32_t i, uint32_t *cap) {
+    if (!sym_off) {
+        *cap = 32;
+        return (uint64_t)i * 32 * sym_slot_bytes(64, 64);
+    }
+    return sym_off[i];
+}
+
+__global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth,
+                                                 T1Scratch *__restrict__ scr, uint8_t *__restrict__ sym,
+                                                 const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res) {
+    __shared__ uint8_t s_sc[256];
+    for (uint32_t k = threadIdx.x; k < 256; k += 64) s_sc[k] = sc_lut_entry(k);
+    __syncthreads();
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= n * maxdepth) return;
+    const uint32_t i = t % n, d = t / n;
+    const uint32_t numbps = res[i].numbps;
+    if (d >= numbps) return;
+    const EncBlock b = blocks[i];
+    const uint32_t slot = sym_slot_bytes(b.w, b.h);
+    uint32_t cap = 0;
+    const uint64_t off = sym_block_off(sym_off, i, &cap);
+    if (sym_off) cap = (uint32_t)((sym_off[i + 1] - off) / slot);
+    if (numbps > cap) {
+        if (d == 0) res[i].pad = 1;  // numbps above the band's bound: reported by the host
         return;
     }
-    PostDecode pd;
-    pd.irreversible = b.irrev;
-    pd.step = b.step;
-    t1_decode_block_impl(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, b.orient, scratch[i],
-                         c_mq_tab, dst, b.dstride, pd);
+    const uint32_t p = numbps - 1 - d;
+    T1Scratch &S = scr[i];
+    uint8_t *base = sym + off + (uint64_t)p * slot;
+    t1_model_plane(b.w, b.h, b.orient, S.pa + p * 64, S.pb + p * 64, p + 1 < numbps ? S.pb + (p + 1) * 64 : nullptr,
+                   S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4);
+}
+
+// MQ coding, one lane per block.
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
+                                                 const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
+                                                 const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
+                                                 EncResult *__restrict__ res) {
+    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_cx[LANES * 33];  // 19 contexts + read-ahead slack; odd stride: no bank conflicts
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (i >= n) return;
+    const EncBlock b = blocks[i];
+    EncResult &r = res[i];
+    if (r.pad) return;
+    uint32_t cap;
+    const uint64_t off = sym_block_off(sym_off, i, &cap);
+    uint32_t len;
+    uint32_t np = t1_mq_block(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
+                              s_cx + threadIdx.x * 33, (uint32_t *)(out + b.out_off), r.rate, &len);
+    r.numpasses = np;
+    r.len = len;
+}
+
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_encode_lane(const EncBlock *__restrict__ blocks, uint32_t n,
+                                                          T1Scratch *__restrict__ scr, uint8_t *__restrict__ out,
+                                                          EncResult *__restrict__ res) {
+    __shared__ uint8_t s_zc[2048];
+    __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_cx[LANES * 21];
+    t1_tables_init<LANES>(s_zc, s_sc, s_mq);
+    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (i >= n) return;
+    const EncBlock b = blocks[i];
+    EncResult &r = res[i];
+    const T1Tables T{s_zc, s_sc, s_mq};
+    uint32_t len;
+    uint32_t np = t1_encode_lane(b.w, b.h, r.numbps, scr[i].pa, scr[i].st, T, b.orient, s_cx + threadIdx.x * 21,
+                                 (uint32_t *)(out + b.out_off), r.rate, &len);
+    r.numpasses = np;
+    r.len = len;
+}
+
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_decode_lane(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                          const uint8_t *__restrict__ data,
+                                                          T1Scratch *__restrict__ scr) {
+    __shared__ uint8_t s_zc[2048];
+    __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_cx[LANES * 21];
+    t1_tables_init<LANES>(s_zc, s_sc, s_mq);
+    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    const T1Tables T{s_zc, s_sc, s_mq};
+    T1Scratch &S = scr[i];
+    t1_decode_lane(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, b.orient, S.st, T,
+                   s_cx + threadIdx.x * 21, S.pa, S.pb);
+}
+
+// One workgroup per block, lane = column: values from the bit-plane rows
+// (staged in LDS, broadcast reads), then T1Part1::postDecode scaling
+// (5/3: v/2, 9/7: float(v) * step) and a coalesced row store.
+__global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ blocks,
+                                                   const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles) {
+    __shared__ uint64_t s_sig[32 * 64];
+    __shared__ uint64_t s_ref[32 * 64];
+    __shared__ uint64_t s_neg[64];
+    const uint32_t i = blockIdx.x, x = threadIdx.x;
+    const DecBlock b = blocks[i];
+    const DecodedPlanes dp = decoded_planes(b.len ? b.numpasses : 0, b.numbps);
+    const T1Scratch &S = scr[i];
+    const uint32_t h = b.h;
+    for (int32_t q = dp.low; q <= dp.top; ++q)
+        if (x < h) s_sig[q * 64 + x] = S.pa[q * 64 + x];
+    for (int32_t q = dp.qlow; q < dp.top; ++q)
+        if (x < h) s_ref[q * 64 + x] = S.pb[q * 64 + x];
+    if (dp.top >= 0 && x < h) s_neg[x] = S.st.neg[x + 1];
+    __syncthreads();
+    if (x >= b.w) return;
+    int32_t *dst = tiles + b.dst_off + x;
+    for (uint32_t y = 0; y < h; ++y) {
+        int32_t v = 0;
+        if (dp.top >= 0) {
+            uint32_t cs = 0;  // bit (q - low): significant after plane q
+            for (int32_t q = dp.top; q >= dp.low; --q) cs = (cs << 1) | (uint32_t)((s_sig[q * 64 + y] >> x) & 1u);
+            if (cs) {
+                int32_t p = dp.low + 31 - (int32_t)__clz(cs);
+                int32_t ql = p < dp.qlow ? p : dp.qlow;
+                uint32_t cr = 0;  // bit (q - ql): refinement bit at plane q, q in [ql, p)
+                for (int32_t q = p - 1; q >= ql; --q) cr = (cr << 1) | (uint32_t)((s_ref[q * 64 + y] >> x) & 1u);
+                uint32_t bits = (1u << (p - ql)) | cr;
+                int32_t mag = (int32_t)((bits << (ql + 1)) | (1u << ql));
+                v = ((s_neg[y] >> x) & 1u) ? -mag : mag;
+            }
+        }
+        int32_t o;
+        if (!b.irrev) o = v / 2;
+        else o = __float_as_int(__fmul_rn((float)v, b.step));
+        dst[(size_t)y * b.dstride] = o;
+    }
 }
 
 // Codestream assembly: copy each run (header bytes from the host-written blob,
@@ -401,17 +570,78 @@ hipError_t launch_dwt_inv_level(const int32_t *ll, uint32_t llstride, const int3
     return hipGetLastError();
 }
 
-hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, BlockRows *scratch,
-                            uint8_t *out, EncResult *res, hipStream_t s) {
+static int t1_mq_lanes() {
+    static int lanes = [] {
+        const char *e = getenv("GRKGPU_MQ_LANES");
+        int v = e ? atoi(e) : 32;
+        return (v == 16 || v == 32 || v == 64) ? v : 32;
+    }();
+    return lanes;
+}
+
+static int t1_lanes() {
+    static int lanes = [] {
+        const char *e = getenv("GRKGPU_T1_LANES");
+        int v = e ? atoi(e) : 16;
+        return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
+    }();
+    return lanes;
+}
+
+template <int L>
+static void launch_enc_lane(const EncBlock *blocks, uint32_t n, T1Scratch *scr, uint8_t *out, EncResult *res,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_t1_encode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, scr, out, res);
+}
+
+template <int L>
+static void launch_dec_lane(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scr, hipStream_t s) {
+    hipLaunchKernelGGL(k_t1_decode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
+}
+
+template <int L>
+static void launch_mq(const EncBlock *blocks, uint32_t n, const T1Scratch *scr, const uint8_t *sym,
+                      const uint64_t *sym_off, uint8_t *out, EncResult *res, hipStream_t s) {
+    hipLaunchKernelGGL(k_t1_mq<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res);
+}
+
+hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
+                            uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
+                            hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_encode, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, coef, scratch, out, res);
+    hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
+    static const bool lane = getenv("GRKGPU_T1_ENC") && !strcmp(getenv("GRKGPU_T1_ENC"), "lane");
+    if (lane) {
+        switch (t1_lanes()) {
+            case 8: launch_enc_lane<8>(blocks, n, scratch, out, res, s); break;
+            case 32: launch_enc_lane<32>(blocks, n, scratch, out, res, s); break;
+            case 64: launch_enc_lane<64>(blocks, n, scratch, out, res, s); break;
+            default: launch_enc_lane<16>(blocks, n, scratch, out, res, s); break;
+        }
+        return hipGetLastError();
+    }
+    if (maxdepth > 32) maxdepth = 32;
+    uint64_t threads = (uint64_t)n * maxdepth;
+    hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
+                       scratch, sym, sym_off, res);
+    switch (t1_mq_lanes()) {
+        case 16: launch_mq<16>(blocks, n, scratch, sym, sym_off, out, res, s); break;
+        case 64: launch_mq<64>(blocks, n, scratch, sym, sym_off, out, res, s); break;
+        default: launch_mq<32>(blocks, n, scratch, sym, sym_off, out, res, s); break;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, BlockRows *scratch,
+hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_decode, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, scratch, tiles);
+    switch (t1_lanes()) {
+        case 8: launch_dec_lane<8>(blocks, n, data, scratch, s); break;
+        case 32: launch_dec_lane<32>(blocks, n, data, scratch, s); break;
+        case 64: launch_dec_lane<64>(blocks, n, data, scratch, s); break;
+        default: launch_dec_lane<16>(blocks, n, data, scratch, s); break;
+    }
+    hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
     return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #define GRK_HD __host__ __device__ __forceinline__
 #else
 #define GRK_HD inline
+struct uint4 { uint32_t x, y, z, w; };  // host build of the shared coder
 #endif
 
 namespace grkgpu {

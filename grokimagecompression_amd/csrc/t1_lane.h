@@ -1,0 +1,969 @@
+// t1_lane.h -- lane-per-code-block EBCOT Tier-1 coder, v2 (MI355X layout).
+//
+// One GPU lane owns one code-block (w, h <= 64).  All per-block state lives in
+// HBM as 64-bit ROW MASKS (bit x = column x) and is streamed through
+// registers one 4-row stripe at a time (Stripe), so the serial MQ loop only
+// touches registers and three small LDS tables (zero-coding LUT, sign LUT,
+// MQ state table).  Decoded magnitudes are never read back: the decoder
+// writes write-only bit-plane rows (significance after each plane, refinement
+// bits per plane) and a separate, fully parallel kernel rebuilds the values
+// (t1_rebuild).  Same source compiles for the host (tests/cpp) and gfx950.
+//
+// Semantics: Grok v5.1.0 t1/t1_part1/t1.cpp (t1_encode_cblk :1182,
+// t1_decode_cblk :1038), mqc_enc.cpp, mqc_dec_inl.h; cblksty 0.
+#pragma once
+#include "t1_core.h"
+
+namespace grkgpu {
+
+// ---- LUTs (built once per workgroup into LDS; host: static arrays) ----
+// zero coding: index orient*512 + 9-bit neighbourhood (NW,N,NE,W,-,E,SW,S,SE)
+GRK_HD uint8_t zc_lut_entry(uint32_t orient, uint32_t nb) {
+    int h = (int)(((nb >> 3) & 1) + ((nb >> 5) & 1));
+    int v = (int)(((nb >> 1) & 1) + ((nb >> 7) & 1));
+    int d = (int)((nb & 1) + ((nb >> 2) & 1) + ((nb >> 6) & 1) + ((nb >> 8) & 1));
+    return (uint8_t)zc_ctx(h, v, d, orient);
+}
+// sign coding: index bit0 sigW, 1 negW, 2 sigE, 3 negE, 4 sigN, 5 negN, 6 sigS, 7 negS
+// entry: context number | xorbit << 7
+GRK_HD uint8_t sc_lut_entry(uint32_t i) {
+    uint32_t xr;
+    int cx = sc_ctx(i & 1, (i >> 2) & 1, (i >> 4) & 1, (i >> 6) & 1, (i >> 1) & 1, (i >> 3) & 1, (i >> 5) & 1,
+                    (i >> 7) & 1, &xr);
+    return (uint8_t)(cx | (xr << 7));
+}
+
+struct T1Tables {
+    const uint8_t *zc;    // 2048
+    const uint8_t *sc;    // 256
+    const uint32_t *mq;   // 47
+};
+
+// 3 bits (x-1, x, x+1) of a row mask
+GRK_HD uint32_t b3(uint64_t row, uint32_t x) {
+    uint32_t left = x ? (uint32_t)(row >> (x - 1)) & 1u : 0u;
+    return left | (((uint32_t)(row >> x) & 3u) << 1);
+}
+
+GRK_HD uint32_t nb9(uint64_t up, uint64_t mid, uint64_t dn, uint32_t x) {
+    return b3(up, x) | ((b3(mid, x) & 5u) << 3) | (b3(dn, x) << 6);
+}
+
+GRK_HD uint32_t sc_index(uint64_t sup, uint64_t smid, uint64_t sdn, uint64_t nup, uint64_t nmid, uint64_t ndn,
+                         uint32_t x) {
+    uint32_t sm = b3(smid, x), nm = b3(nmid, x);
+    uint32_t i = (sm & 1) | ((nm & 1) << 1) | (((sm >> 2) & 1) << 2) | (((nm >> 2) & 1) << 3);
+    i |= (uint32_t)((sup >> x) & 1) << 4 | (uint32_t)((nup >> x) & 1) << 5;
+    i |= (uint32_t)((sdn >> x) & 1) << 6 | (uint32_t)((ndn >> x) & 1) << 7;
+    return i;
+}
+
+// ---- per-block HBM state (rows y = -1..h stored at index y+1) ----
+struct BlockState {
+    uint64_t sig[66];
+    uint64_t neg[66];
+    uint64_t vis[66];
+    uint64_t ref[66];
+};
+
+// pass index -> (plane, type): pass 0 = cleanup of plane numbps-1, then
+// (sig, ref, cln) per lower plane.
+GRK_HD void pass_info(uint32_t passno, uint32_t numbps, int32_t *plane, int *type) {
+    if (passno == 0) { *plane = (int32_t)numbps - 1; *type = 2; return; }
+    *plane = (int32_t)numbps - 2 - (int32_t)((passno - 1) / 3);
+    *type = (int)((passno - 1) % 3);
+}
+
+// explicit s_waitcnt vmcnt(0): placed where the data is known to have landed
+// long ago, so the compiler does not scatter conservative waits in hot loops
+GRK_HD void vm_wait_all() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+GRK_HD uint32_t clz32(uint32_t v) { return (uint32_t)__builtin_clz(v); }
+GRK_HD uint32_t ctz64(uint64_t v) { return (uint32_t)__builtin_ctzll(v); }
+GRK_HD uint64_t dil(uint64_t m) { return m | (m << 1) | (m >> 1); }
+
+// MQ context registers are 32-bit words: the packed table entry of the
+// current state (Qe | NMPS<<16 | NLPS<<22 | SWITCH<<28) | MPS<<31, so one LDS
+// read per symbol yields Qe; the next-state lookup is off the critical path.
+// mqc_resetstates (mqc_dec.cpp:207-215): UNI -> 46, AGG -> 3, ZC0 -> 4.
+GRK_HD void mq_reset_words(uint32_t *cxw, const uint32_t *tab) {
+    for (int i = 0; i < NUM_CX; ++i) cxw[i] = tab[0];
+    cxw[CX_UNI] = tab[46];
+    cxw[CX_AGG] = tab[3];
+    cxw[CX_ZC] = tab[4];
+}
+
+// ---------------------------------------------------------------------------
+// MQ encoder (mqc_enc.cpp) with a register byte sink: only the byte at bp can
+// still change (carry); everything before it is final and leaves as dwords.
+// ---------------------------------------------------------------------------
+struct MqEncLane {
+    uint32_t a, c, ct;
+    int32_t bp;        // index of `cur` (starts at -1: Grok's bp = start - 1)
+    uint32_t cur;      // byte at bp (still subject to carry)
+    uint32_t acc;      // committed bytes of the current dword
+    uint32_t *out;     // 4-byte aligned
+};
+
+GRK_HD void sink_commit(MqEncLane &e, int32_t pos, uint32_t byte) {
+    if (pos < 0) return;  // the zero pad byte before the block
+    uint32_t sh = ((uint32_t)pos & 3u) * 8u;
+    e.acc = (e.acc & ~(0xFFu << sh)) | (byte << sh);
+    if ((pos & 3) == 3) { e.out[pos >> 2] = e.acc; e.acc = 0; }
+}
+
+GRK_HD void mqel_emit(MqEncLane &e, uint32_t byte) {  // new byte at bp + 1
+    sink_commit(e, e.bp, e.cur);
+    e.bp++;
+    e.cur = byte & 0xFF;
+}
+
+// BYTEOUT (mqc_enc.cpp:168-199)
+GRK_HD void mqel_byteout(MqEncLane &e) {
+    if (e.cur == 0xff) {
+        mqel_emit(e, e.c >> 20); e.c &= 0xfffff; e.ct = 7;
+    } else if ((e.c & 0x8000000) == 0) {
+        mqel_emit(e, e.c >> 19); e.c &= 0x7ffff; e.ct = 8;
+    } else {
+        e.cur++;
+        if (e.cur == 0xff) {
+            e.c &= 0x7ffffff;
+            mqel_emit(e, e.c >> 20); e.c &= 0xfffff; e.ct = 7;
+        } else {
+            mqel_emit(e, e.c >> 19); e.c &= 0x7ffff; e.ct = 8;
+        }
+    }
+}
+
+// encode (mqc_enc.cpp:50-110); RENORME's one-bit loop becomes clz-sized
+// shifts between byte boundaries (identical state sequence).
+GRK_HD void mqel_encode(MqEncLane &e, uint32_t *cxw, const uint32_t *tab, uint32_t cx, uint32_t d) {
+    const uint32_t w = cxw[cx];
+    const uint32_t qe = w & 0xffff, mps = w >> 31;
+    e.a -= qe;
+    if (d == mps) {
+        if (e.a & 0x8000) { e.c += qe; return; }
+        if (e.a < qe) e.a = qe; else e.c += qe;
+        cxw[cx] = tab[(w >> 16) & 63] | (mps << 31);
+    } else {
+        if (e.a < qe) e.c += qe; else e.a = qe;
+        cxw[cx] = tab[(w >> 22) & 63] | ((mps ^ ((w >> 28) & 1)) << 31);
+    }
+    uint32_t n = clz32(e.a) - 16;
+    while (n) {
+        uint32_t sh = n < e.ct ? n : e.ct;
+        e.a <<= sh; e.c <<= sh; e.ct -= sh; n -= sh;
+        if (e.ct == 0) mqel_byteout(e);
+    }
+}
+
+GRK_HD void mqel_flush(MqEncLane &e) {
+    uint32_t tempc = e.c + e.a;
+    e.c |= 0xffff;
+    if (e.c >= tempc) e.c -= 0x8000;
+    e.c <<= e.ct; mqel_byteout(e);
+    e.c <<= e.ct; mqel_byteout(e);
+    if (e.cur != 0xff) mqel_emit(e, 0);  // "if (*bp != 0xff) bp++"
+}
+
+GRK_HD void mqel_finish(MqEncLane &e, uint32_t len) {
+    if (e.bp >= 0 && (uint32_t)e.bp < len) sink_commit(e, e.bp, e.cur);
+    if (len & 3) e.out[len >> 2] = e.acc;
+}
+
+// ---------------------------------------------------------------------------
+// MQ decoder (mqc_dec_inl.h) with a register byte window over an 8-byte
+// aligned stream; bytes past the segment read as 0xFF.
+// ---------------------------------------------------------------------------
+struct MqDecLane {
+    uint32_t a, c, ct;
+    uint32_t bp, len;
+    uint32_t cur, nxt;     // bytes at bp and bp+1
+    const uint64_t *src;   // aligned base
+    uint32_t s0;           // byte offset of the segment start within src
+    uint64_t w0, w1;       // window: chunks wk and wk+1
+    uint32_t wk;
+};
+
+GRK_HD uint32_t mqdl_fetch(MqDecLane &d, uint32_t i) {  // byte i; requests are non-decreasing
+    if (i >= d.len) return 0xFF;
+    uint32_t a = d.s0 + i, k = a >> 3;
+    while (k > d.wk) { d.w0 = d.w1; d.w1 = d.src[d.wk + 2]; d.wk++; }
+    return (uint32_t)(d.w0 >> ((a & 7) * 8)) & 0xFF;
+}
+
+GRK_HD void mqdl_bytein(MqDecLane &d) {
+    if (d.cur == 0xff) {
+        if (d.nxt > 0x8f) { d.c += 0xff00; d.ct = 8; return; }
+        d.bp++; d.c += d.nxt << 9; d.ct = 7;
+    } else {
+        d.bp++; d.c += d.nxt << 8; d.ct = 8;
+    }
+    d.cur = d.nxt;
+    d.nxt = mqdl_fetch(d, d.bp + 1);
+}
+
+GRK_HD void mqdl_init(MqDecLane &d, const uint8_t *data, uint32_t len) {
+    uintptr_t p = (uintptr_t)data;
+    d.src = (const uint64_t *)(p & ~(uintptr_t)7);
+    d.s0 = (uint32_t)(p & 7);
+    d.len = len;
+    d.wk = 0;
+    d.w0 = d.src[0];
+    d.w1 = d.src[1];
+    d.bp = 0;
+    d.cur = mqdl_fetch(d, 0);
+    d.nxt = mqdl_fetch(d, 1);
+    d.c = (len == 0 ? 0xffu : d.cur) << 16;
+    mqdl_bytein(d);
+    d.c <<= 7; d.ct -= 7; d.a = 0x8000;
+}
+
+GRK_HD uint32_t mqdl_decode(MqDecLane &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
+    const uint32_t w = cxw[cx];
+    const uint32_t qe = w & 0xffff, mps = w >> 31;
+    uint32_t r;
+    bool lps_state;
+    d.a -= qe;
+    if (d.c < (qe << 16)) {
+        lps_state = d.a >= qe;
+        d.a = qe;
+    } else {
+        d.c -= qe << 16;
+        if (d.a & 0x8000) return mps;
+        lps_state = d.a < qe;
+    }
+    if (lps_state) {
+        r = mps ^ 1;
+        cxw[cx] = tab[(w >> 22) & 63] | ((mps ^ ((w >> 28) & 1)) << 31);
+    } else {
+        r = mps;
+        cxw[cx] = tab[(w >> 16) & 63] | (mps << 31);
+    }
+    uint32_t n = clz32(d.a) - 16;
+    while (n) {
+        if (d.ct == 0) mqdl_bytein(d);
+        uint32_t sh = n < d.ct ? n : d.ct;
+        d.a <<= sh; d.c <<= sh; d.ct -= sh; n -= sh;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Coding passes, shared by encoder and decoder.  A 4-row stripe of the block
+// state is held in registers; each lane walks only the columns that hold
+// work for the pass (bit-scan over candidate masks), which keeps SIMT
+// divergence between the blocks of a wavefront low.
+// ---------------------------------------------------------------------------
+struct Stripe {
+    uint64_t sig[6], neg[6];  // rows k-1 .. k+4
+    uint64_t vis[4], ref[4];  // rows k .. k+3
+    uint64_t bit[4];          // encoder: magnitude bits of the plane; decoder: refinement bits out
+};
+
+GRK_HD uint64_t spp_candidates(const Stripe &s, uint32_t nr) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if ((uint32_t)r >= nr) break;
+        uint64_t nb = dil(s.sig[r]) | dil(s.sig[r + 2]) | (s.sig[r + 1] << 1) | (s.sig[r + 1] >> 1);
+        c |= nb & ~(s.sig[r + 1] | s.vis[r]);
+    }
+    return c;
+}
+
+// Coder: code(cx, v) encodes v / decodes and returns the bit.
+template <class Coder>
+GRK_HD void t1_passes(Coder &cd, uint32_t w, uint32_t h, uint32_t numbps, uint32_t maxpasses, BlockState &st,
+                      const uint8_t *zc, const uint8_t *sc) {
+    const uint64_t wmask = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
+    int32_t bpno = (int32_t)numbps - 1;
+    int passtype = 2;
+    for (uint32_t passno = 0; passno < maxpasses && bpno >= 0; ++passno) {
+        cd.begin_pass(bpno);
+        for (uint32_t k = 0; k < h; k += 4) {
+            Stripe s;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { s.sig[i] = st.sig[k + i]; s.neg[i] = st.neg[k + i]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                s.vis[i] = st.vis[k + 1 + i];
+                s.ref[i] = st.ref[k + 1 + i];
+                s.bit[i] = cd.stripe_bits(k + i, h);
+            }
+            const uint32_t nr = h - k < 4 ? h - k : 4;
+            if (passtype == 0) {  // significance propagation (t1.cpp:197-338)
+                uint64_t cand = spp_candidates(s, nr) & wmask;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    const uint64_t bx = (uint64_t)1 << x;
+                    const uint64_t done = bx | (bx - 1);
+                    bool grew = false;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((uint32_t)r >= nr) break;
+                        if ((s.sig[r + 1] | s.vis[r]) & bx) continue;
+                        uint32_t nb = nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x);
+                        if (!nb) continue;
+                        if (cd.code(zc[nb], (uint32_t)(s.bit[r] >> x) & 1u)) {
+                            uint32_t si = sc[sc_index(s.sig[r], s.sig[r + 1], s.sig[r + 2], s.neg[r], s.neg[r + 1],
+                                                      s.neg[r + 2], x)];
+                            uint32_t xr = si >> 7;
+                            uint32_t sg = cd.code(si & 0x7f, ((uint32_t)(s.neg[r + 1] >> x) & 1u) ^ xr) ^ xr;
+                            s.sig[r + 1] |= bx;
+                            if (sg) s.neg[r + 1] |= bx;
+                            grew = true;
+                        }
+                        s.vis[r] |= bx;
+                    }
+                    cand &= ~done;
+                    if (grew) cand = spp_candidates(s, nr) & wmask & ~done;
+                }
+            } else if (passtype == 1) {  // magnitude refinement (t1.cpp:443-555)
+                uint64_t mem = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((uint32_t)r < nr) mem |= s.sig[r + 1] & ~s.vis[r];
+                while (mem) {
+                    const uint32_t x = ctz64(mem);
+                    const uint64_t bx = (uint64_t)1 << x;
+                    mem &= mem - 1;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((uint32_t)r >= nr) break;
+                        if (!(s.sig[r + 1] & bx) || (s.vis[r] & bx)) continue;
+                        uint32_t cx;
+                        if (s.ref[r] & bx) cx = CX_MAG + 2;
+                        else cx = CX_MAG + (nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x) ? 1 : 0);
+                        if (cd.code(cx, (uint32_t)(s.bit[r] >> x) & 1u)) s.bit[r] |= bx;
+                        s.ref[r] |= bx;
+                    }
+                }
+            } else {  // cleanup + run-length (t1.cpp:639-782)
+                uint64_t cand = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((uint32_t)r < nr) cand |= ~(s.sig[r + 1] | s.vis[r]);
+                cand &= wmask;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    const uint64_t bx = (uint64_t)1 << x;
+                    cand &= cand - 1;
+                    int r0 = 0;
+                    bool partial = false;
+                    if (nr == 4) {
+                        uint64_t wn = s.sig[0] | s.sig[1] | s.sig[2] | s.sig[3] | s.sig[4] | s.sig[5];
+                        uint64_t vs = s.vis[0] | s.vis[1] | s.vis[2] | s.vis[3];
+                        if (b3(wn, x) == 0 && !(vs & bx)) {
+                            uint32_t rl = 4;  // encoder: first row with a 1 bit
+#pragma unroll
+                            for (int r = 3; r >= 0; --r)
+                                if ((s.bit[r] >> x) & 1u) rl = (uint32_t)r;
+                            if (!cd.code(CX_AGG, rl != 4)) continue;
+                            uint32_t r1 = cd.code(CX_UNI, rl >> 1);
+                            uint32_t r2 = cd.code(CX_UNI, rl & 1);
+                            r0 = (int)(r1 * 2 + r2);
+                            partial = true;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((uint32_t)r >= nr || r < r0) continue;
+                        uint32_t code_sign = 0;
+                        if (partial && r == r0) code_sign = 1;
+                        else if (!((s.sig[r + 1] | s.vis[r]) & bx))
+                            code_sign = cd.code(zc[nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x)],
+                                                (uint32_t)(s.bit[r] >> x) & 1u);
+                        if (code_sign) {
+                            uint32_t si = sc[sc_index(s.sig[r], s.sig[r + 1], s.sig[r + 2], s.neg[r], s.neg[r + 1],
+                                                      s.neg[r + 2], x)];
+                            uint32_t xr = si >> 7;
+                            uint32_t sg = cd.code(si & 0x7f, ((uint32_t)(s.neg[r + 1] >> x) & 1u) ^ xr) ^ xr;
+                            s.sig[r + 1] |= bx;
+                            if (sg) s.neg[r + 1] |= bx;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s.vis[r] = 0;  // the cleanup pass clears every PI flag
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                st.sig[k + 1 + i] = s.sig[i + 1];
+                if (Coder::kDecoder) st.neg[k + 1 + i] = s.neg[i + 1];
+                st.vis[k + 1 + i] = s.vis[i];
+                st.ref[k + 1 + i] = s.ref[i];
+            }
+            cd.end_stripe(k, nr, passtype, s);
+        }
+        cd.end_pass(passno, passtype, bpno);
+        if (++passtype == 3) { passtype = 0; bpno--; }
+    }
+}
+
+struct LaneEncoder {
+    static constexpr bool kDecoder = false;
+    MqEncLane e;
+    uint32_t *cxw;
+    const uint32_t *tab;
+    const uint64_t *planes, *pl;
+    uint32_t *rate;
+    GRK_HD void begin_pass(int32_t bpno) { pl = planes + (uint32_t)bpno * 64; }
+    GRK_HD uint64_t stripe_bits(uint32_t y, uint32_t h) const { return y < h ? pl[y] : 0; }
+    GRK_HD uint32_t code(uint32_t cx, uint32_t v) { mqel_encode(e, cxw, tab, cx, v); return v; }
+    GRK_HD void end_stripe(uint32_t, uint32_t, int, const Stripe &) {}
+    GRK_HD void end_pass(uint32_t passno, int passtype, int32_t bpno) {
+        if (passtype == 2 && bpno == 0) {  // the last cleanup pass is terminated
+            mqel_flush(e);
+            rate[passno] = (uint32_t)e.bp;
+        } else {  // rate_extra_bytes (t1.cpp:1278-1288)
+            rate[passno] = (uint32_t)e.bp + 5 + (e.ct < 5 ? 1 : 0);
+        }
+    }
+};
+
+struct LaneDecoder {
+    static constexpr bool kDecoder = true;
+    MqDecLane d;
+    uint32_t *cxw;
+    const uint32_t *tab;
+    uint64_t *sigafter, *refbit, *sa, *rb;
+    GRK_HD void begin_pass(int32_t bpno) {
+        sa = sigafter + (uint32_t)bpno * 64;
+        rb = refbit + (uint32_t)bpno * 64;
+    }
+    GRK_HD uint64_t stripe_bits(uint32_t, uint32_t) const { return 0; }
+    GRK_HD uint32_t code(uint32_t cx, uint32_t) { return mqdl_decode(d, cxw, tab, cx); }
+    GRK_HD void end_stripe(uint32_t k, uint32_t nr, int passtype, const Stripe &s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((uint32_t)i < nr) {
+                if (passtype == 1) rb[k + i] = s.bit[i];
+                else sa[k + i] = s.sig[i + 1];
+            }
+    }
+    GRK_HD void end_pass(uint32_t, int, int32_t) {}
+};
+
+// ENCODER: magnitude bit-plane rows planes[p*64 + y] and sign rows st.neg
+// come from the prep step.  Output bytes to out (4-byte aligned), cumulative
+// pass rates (after Grok's fix-ups) to rate[].  Returns the pass count.
+GRK_HD uint32_t t1_encode_lane(uint32_t w, uint32_t h, uint32_t numbps, const uint64_t *planes, BlockState &st,
+                               const T1Tables &T, uint32_t orient, uint32_t *cxw, uint32_t *out, uint32_t *rate,
+                               uint32_t *len_out) {
+    *len_out = 0;
+    if (numbps == 0) return 0;
+    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
+    LaneEncoder cd;
+    mq_reset_words(cxw, T.mq);
+    cd.e.a = 0x8000; cd.e.c = 0; cd.e.ct = 12; cd.e.bp = -1; cd.e.cur = 0; cd.e.acc = 0; cd.e.out = out;
+    cd.cxw = cxw; cd.tab = T.mq; cd.planes = planes; cd.pl = planes; cd.rate = rate;
+    const uint32_t total = 3 * numbps - 2;
+    t1_passes(cd, w, h, numbps, total, st, T.zc + orient * 512, T.sc);
+    const uint32_t len = (uint32_t)cd.e.bp;
+    mqel_finish(cd.e, len);
+    // non-increasing rates + no pass ends on 0xFF (t1.cpp:1303-1324)
+    uint32_t last = len;
+    for (uint32_t i = total; i > 0;) {
+        --i;
+        uint32_t r = rate[i];
+        if (r > last) r = last; else last = r;
+        rate[i] = r;
+    }
+    const uint8_t *ob = (const uint8_t *)out;
+    for (uint32_t i = 0; i < total; ++i)
+        if (rate[i] > 0 && ob[rate[i] - 1] == 0xFF) rate[i]--;
+    *len_out = len;
+    return total;
+}
+
+// DECODER: outputs per plane p: sigafter[p*64+y] = significance rows after
+// the last decoded pass of plane p; refbit[p*64+y] = refinement bits decoded
+// at plane p.  Final sign rows stay in st.neg.
+GRK_HD void t1_decode_lane(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
+                           uint32_t h, uint32_t orient, BlockState &st, const T1Tables &T, uint32_t *cxw,
+                           uint64_t *sigafter, uint64_t *refbit) {
+    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
+    LaneDecoder cd;
+    mq_reset_words(cxw, T.mq);
+    mqdl_init(cd.d, data, len);
+    cd.cxw = cxw; cd.tab = T.mq; cd.sigafter = sigafter; cd.refbit = refbit; cd.sa = sigafter; cd.rb = refbit;
+    t1_passes(cd, w, h, numbps, numpasses, st, T.zc + orient * 512, T.sc);
+}
+
+// ===========================================================================
+// Encoder, split form.  Because the encoder knows every magnitude up front,
+// the significance state before bit-plane p is simply "magnitude >= 2^(p+1)"
+// (the `above` rows), so each bit-plane's three passes can be modelled
+// independently of the others and of the MQ coder:
+//   t1_model_plane  one lane per (block, plane): bit-parallel row-mask
+//                   modelling (64 columns per op), emits the plane's symbol
+//                   stream (SPP, MRP, CUP) as bytes  ctx | decision << 5
+//   t1_mq_block     one lane per block: MQ-codes the streams plane by plane,
+//                   recording Grok's pass rates.
+// ===========================================================================
+GRK_HD uint32_t sym_stream_bytes(uint32_t w, uint32_t h) {
+    // per plane: <= 1 ZC/MAG + 1 sign per sample, <= 2 extra (AGG/UNI) per stripe column
+    return (w * h * 2 + ((h + 3) / 4) * w * 2 + 15) & ~15u;
+}
+GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h) + 2 * 64 * 8; }
+
+struct SymOut {
+    uint32_t *out;
+    uint32_t acc, n;
+    GRK_HD void put(uint32_t b) {
+        acc |= b << ((n & 3) * 8);
+        ++n;
+        if ((n & 3) == 0) { out[(n >> 2) - 1] = acc; acc = 0; }
+    }
+    GRK_HD void flush() { if (n & 3) out[n >> 2] = acc; }
+};
+
+// Bit-sliced zero-coding context (t1_generate_luts.cpp:63-140) for 64
+// samples at once from the 8 neighbour significance masks (bit x = sample x).
+struct Ctx4 { uint64_t c0, c1, c2, c3; };
+
+GRK_HD Ctx4 zc_slices(uint64_t NW, uint64_t N, uint64_t NE, uint64_t W, uint64_t E, uint64_t SW, uint64_t S,
+                      uint64_t SE, uint32_t orient) {
+    uint64_t hA = orient == 1 ? N : W, hB = orient == 1 ? S : E;
+    uint64_t vA = orient == 1 ? W : N, vB = orient == 1 ? E : S;
+    const uint64_t h1 = hA ^ hB, h2 = hA & hB, hz = ~(hA | hB);
+    const uint64_t v1 = vA ^ vB, v2 = vA & vB, vz = ~(vA | vB);
+    const uint64_t a = NW ^ NE, b = NW & NE, c = SW ^ SE, e = SW & SE;
+    const uint64_t s0 = a ^ c, cr = a & c;
+    const uint64_t s1 = b ^ e ^ cr;
+    const uint64_t s2 = (b & e) | ((b ^ e) & cr);
+    const uint64_t dz = ~(NW | NE | SW | SE);
+    const uint64_t d1 = s0 & ~s1 & ~s2;
+    const uint64_t dge2 = ~dz & ~d1;
+    const uint64_t dge3 = s2 | (s1 & s0);
+    uint64_t x1, x2, x3, x4, x5, x6, x7, x8;
+    if (orient != 3) {
+        x8 = h2; x7 = h1 & ~vz; x6 = h1 & vz & ~dz; x5 = h1 & vz & dz;
+        x4 = hz & v2; x3 = hz & v1; x2 = hz & vz & dge2; x1 = hz & vz & d1;
+    } else {
+        const uint64_t hv0 = hz & vz, hv1 = (h1 & vz) | (hz & v1), hv2 = ~hv0 & ~hv1;
+        const uint64_t d2 = dge2 & ~dge3;
+        x8 = dge3; x7 = d2 & ~hv0; x6 = d2 & hv0; x5 = d1 & hv2; x4 = d1 & hv1; x3 = d1 & hv0;
+        x2 = dz & hv2; x1 = dz & hv1;
+    }
+    Ctx4 r;
+    r.c0 = x1 | x3 | x5 | x7;
+    r.c1 = x2 | x3 | x6 | x7;
+    r.c2 = x4 | x5 | x6 | x7;
+    r.c3 = x8;
+    return r;
+}
+
+GRK_HD uint32_t ctx_at(const Ctx4 &c, uint32_t x) {
+    return (uint32_t)((c.c0 >> x) & 1) | (uint32_t)((c.c1 >> x) & 1) << 1 | (uint32_t)((c.c2 >> x) & 1) << 2 |
+           (uint32_t)((c.c3 >> x) & 1) << 3;
+}
+
+// sign symbol for sample x: W/E/N/S significance masks already aligned to x
+GRK_HD uint32_t sc_symbol(const uint8_t *sc, uint64_t sW, uint64_t nW, uint64_t sE, uint64_t nE, uint64_t sN,
+                          uint64_t nN, uint64_t sS, uint64_t nS, uint64_t neg, uint32_t x) {
+    uint32_t i = (uint32_t)((sW >> x) & 1) | (uint32_t)((nW >> x) & 1) << 1 | (uint32_t)((sE >> x) & 1) << 2 |
+                 (uint32_t)((nE >> x) & 1) << 3 | (uint32_t)((sN >> x) & 1) << 4 | (uint32_t)((nN >> x) & 1) << 5 |
+                 (uint32_t)((sS >> x) & 1) << 6 | (uint32_t)((nS >> x) & 1) << 7;
+    uint32_t si = sc[i];
+    return (si & 0x7f) | ((((uint32_t)(neg >> x) & 1u) ^ (si >> 7)) << 5);
+}
+
+GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0 && (uint32_t)y < h) ? a[y] : 0; }
+
+// Model bit-plane p of one block.  above = significance before plane p,
+// ref = significance before plane p+1 (refined-before flags), negr = sign
+// rows (index y+1), tmp = 128 rows of scratch.  Writes the plane's stream and
+// cnt[0..2] = symbols of its SPP / MRP / CUP (SPP and MRP are empty for the
+// top plane).  Semantics: t1.cpp:197-338 (SPP), 443-555 (MRP), 639-782 (CUP).
+GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64_t *bitp, const uint64_t *above,
+                           const uint64_t *ref, const uint64_t *negr, uint64_t *tmp, const uint8_t *sc,
+                           uint32_t *out, uint32_t *cnt) {
+    const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
+    uint64_t *postS = tmp, *visS = tmp + 64;
+    SymOut so{out, 0, 0};
+    // ---- significance propagation ----
+    uint64_t U = 0;  // post-SPP significance of row k-1
+    for (uint32_t k = 0; k < h; k += 4) {
+        const uint32_t nr = h - k < 4 ? h - k : 4;
+        uint64_t pre[4], bit[4], C[4], post[4], ng[6];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            pre[r] = ldrow(above, (int32_t)(k + r), h);
+            bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+            C[r] = (uint32_t)r < nr ? ~pre[r] & wm : 0;
+            post[r] = pre[r];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
+        const uint64_t D = ldrow(above, (int32_t)(k + 4), h);
+        // fixed point of the causal significance recurrence; the W->E chain
+        // inside a row is resolved with one carry-propagating add
+        for (int it = 0; it < 300; ++it) {
+            uint64_t changed = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t up = r == 0 ? U : post[r - 1], ne = r == 0 ? U : pre[r - 1];
+                const uint64_t dnp = r == 3 ? D : post[r + 1], dn = r == 3 ? D : pre[r + 1];
+                const uint64_t B = (up << 1) | up | (ne >> 1) | (pre[r] << 1) | (pre[r] >> 1) | (dnp << 1) | dn |
+                                   (dn >> 1);
+                const uint64_t P = C[r] & bit[r], sd = P & B;
+                const uint64_t ns = (((P + sd) ^ P) | sd) & P;
+                const uint64_t np = pre[r] | ns;
+                changed |= np ^ post[r];
+                post[r] = np;
+            }
+            if (!changed) break;
+        }
+        uint64_t coded[4];
+        Ctx4 cz[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t up = r == 0 ? U : post[r - 1], ne = r == 0 ? U : pre[r - 1];
+            const uint64_t dnp = r == 3 ? D : post[r + 1], dn = r == 3 ? D : pre[r + 1];
+            const uint64_t NW = up << 1, N = up, NE = ne >> 1, W = post[r] << 1, E = pre[r] >> 1, SW = dnp << 1,
+                           S = dn, SE = dn >> 1;
+            coded[r] = C[r] & (NW | N | NE | W | E | SW | S | SE);
+            cz[r] = zc_slices(NW, N, NE, W, E, SW, S, SE, orient);
+            if ((uint32_t)r < nr) { postS[k + r] = post[r]; visS[k + r] = coded[r]; }
+        }
+        uint64_t cols = coded[0] | coded[1] | coded[2] | coded[3];
+        while (cols) {
+            const uint32_t x = ctz64(cols);
+            cols &= cols - 1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (!((coded[r] >> x) & 1)) continue;
+                const uint32_t s = (uint32_t)((post[r] >> x) & 1);
+                so.put(ctx_at(cz[r], x) | s << 5);
+                if (s) {
+                    const uint64_t up = r == 0 ? U : post[r - 1], dn = r == 3 ? D : pre[r + 1];
+                    so.put(sc_symbol(sc, post[r] << 1, ng[r + 1] << 1, pre[r] >> 1, ng[r + 1] >> 1, up, ng[r], dn,
+                                     ng[r + 2], ng[r + 1], x));
+                }
+            }
+        }
+        U = post[3];
+    }
+    cnt[0] = so.n;
+    // ---- magnitude refinement: members = significant before this plane ----
+    for (uint32_t k = 0; k < h; k += 4) {
+        uint64_t m[4], rf[4], bit[4], sS[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sS[i] = ldrow(postS, (int32_t)(k + i) - 1, h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            m[r] = ldrow(above, (int32_t)(k + r), h);
+            rf[r] = ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
+            bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+        }
+        uint64_t cols = m[0] | m[1] | m[2] | m[3];
+        while (cols) {
+            const uint32_t x = ctz64(cols);
+            cols &= cols - 1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (!((m[r] >> x) & 1)) continue;
+                const uint64_t nb = dil(sS[r]) | dil(sS[r + 2]) | (sS[r + 1] << 1) | (sS[r + 1] >> 1);
+                uint32_t cx = ((rf[r] >> x) & 1) ? CX_MAG + 2 : CX_MAG + (uint32_t)((nb >> x) & 1);
+                so.put(cx | (uint32_t)((bit[r] >> x) & 1) << 5);
+            }
+        }
+    }
+    cnt[1] = so.n - cnt[0];
+    // ---- cleanup (+ run-length) ----
+    U = 0;  // post-CUP significance of row k-1
+    for (uint32_t k = 0; k < h; k += 4) {
+        const uint32_t nr = h - k < 4 ? h - k : 4;
+        uint64_t sS[4], cand[4], bit[4], pc[4], ng[6];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            sS[r] = ldrow(postS, (int32_t)(k + r), h);
+            bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+            cand[r] = (uint32_t)r < nr ? ~(sS[r] | ldrow(visS, (int32_t)(k + r), h)) & wm : 0;
+            pc[r] = sS[r] | (cand[r] & bit[r]);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
+        const uint64_t D = ldrow(postS, (int32_t)(k + 4), h);
+        uint64_t agg = 0;
+        if (nr == 4) {
+            agg = cand[0] & cand[1] & cand[2] & cand[3];
+            agg &= ~((pc[0] | pc[1] | pc[2] | pc[3]) << 1);
+            agg &= ~((sS[0] | sS[1] | sS[2] | sS[3]) >> 1);
+            agg &= ~(dil(U) | dil(D));
+        }
+        Ctx4 cz[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t up = r == 0 ? U : pc[r - 1], ne = r == 0 ? U : sS[r - 1];
+            const uint64_t dnc = r == 3 ? D : pc[r + 1], dn = r == 3 ? D : sS[r + 1];
+            cz[r] = zc_slices(up << 1, up, ne >> 1, pc[r] << 1, sS[r] >> 1, dnc << 1, dn, dn >> 1, orient);
+        }
+        uint64_t cols = cand[0] | cand[1] | cand[2] | cand[3];
+        while (cols) {
+            const uint32_t x = ctz64(cols);
+            cols &= cols - 1;
+            int r0 = 0;
+            bool rl = false;
+            if ((agg >> x) & 1) {
+                uint32_t colbits = (uint32_t)((bit[0] >> x) & 1) | (uint32_t)((bit[1] >> x) & 1) << 1 |
+                                   (uint32_t)((bit[2] >> x) & 1) << 2 | (uint32_t)((bit[3] >> x) & 1) << 3;
+                so.put(CX_AGG | (colbits ? 1u : 0u) << 5);
+                if (!colbits) continue;
+                uint32_t run = (uint32_t)__builtin_ctz(colbits);
+                so.put(CX_UNI | (run >> 1) << 5);
+                so.put(CX_UNI | (run & 1) << 5);
+                r0 = (int)run;
+                rl = true;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (r < r0 || !((cand[r] >> x) & 1)) continue;
+                const uint32_t s = (uint32_t)((bit[r] >> x) & 1);
+                if (!(rl && r == r0)) so.put(ctx_at(cz[r], x) | s << 5);
+                if (s) {
+                    const uint64_t up = r == 0 ? U : pc[r - 1], dn = r == 3 ? D : sS[r + 1];
+                    so.put(sc_symbol(sc, pc[r] << 1, ng[r + 1] << 1, sS[r] >> 1, ng[r + 1] >> 1, up, ng[r], dn,
+                                     ng[r + 2], ng[r + 1], x));
+                }
+            }
+        }
+        U = pc[3];
+    }
+    cnt[2] = so.n - cnt[0] - cnt[1];
+    so.flush();
+}
+
+// MQ-code one block from its per-plane symbol streams (slot p at
+// sym + p * slot_words).  Same outputs as t1_encode_lane.  The serial loop is
+// built for a lone lane: symbols are consumed in 16-byte chunks while the
+// chunk two ahead is in flight (the only wait on it sits at the chunk end),
+// the next symbol's context word is read from LDS before the current one is
+// written back (same-context bypass), and the coding step is select-based.
+
+// BYTEOUT without data-dependent branches (mqc_enc.cpp:168-199): the carry
+// into a non-0xFF byte, then 7 or 8 bits out depending on whether the byte
+// before is 0xFF.  Clearing bit 27 before the 8-bit case is harmless: that bit
+// lands in bit 8 of the emitted value, which the byte store drops.
+GRK_HD void mqel_byteout_bf(MqEncLane &e) {
+    const uint32_t carry = e.cur == 0xff ? 0u : (e.c >> 27) & 1u;
+    e.cur += carry;
+    e.c &= ~(carry << 27);
+    const bool big = e.cur == 0xff;
+    const uint32_t byte = big ? (e.c >> 20) : (e.c >> 19);
+    e.c &= big ? 0xfffffu : 0x7ffffu;
+    e.ct = big ? 7u : 8u;
+    mqel_emit(e, byte);
+}
+
+// one MQ coding step with the context word already in hand; returns the
+// context's new word (mqc_enc.cpp:50-110).  Select-based: the MPS/LPS and
+// exchange cases share one instruction stream, the next-state table read is
+// unconditional (its latency overlaps the renormalisation) and only a renorm
+// that crosses a byte boundary branches.
+GRK_HD uint32_t mqel_step(MqEncLane &e, const uint32_t *tab, uint32_t w, uint32_t d) {
+    const uint32_t qe = w & 0xffff, mps = w >> 31;
+    const uint32_t a = e.a - qe;
+    const bool is_mps = d == mps;
+    const bool addc = is_mps != (a < qe);
+    e.c += addc ? qe : 0u;
+    uint32_t na = addc ? a : qe;
+    const bool keep = is_mps && (a & 0x8000);  // no renormalisation, no state change
+    const uint32_t nidx = (w >> (is_mps ? 16 : 22)) & 63;
+    const uint32_t nmps = mps ^ (is_mps ? 0u : (w >> 28) & 1u);
+    const uint32_t tw = tab[nidx];
+    uint32_t n = clz32(na) - 16;
+    if (n < e.ct) {
+        na <<= n; e.c <<= n; e.ct -= n;
+    } else {
+        do {
+            const uint32_t sh = n < e.ct ? n : e.ct;
+            na <<= sh; e.c <<= sh; e.ct -= sh; n -= sh;
+            if (e.ct == 0) mqel_byteout_bf(e);
+        } while (n);
+    }
+    e.a = na;
+    return keep ? w : (tw | (nmps << 31));
+}
+
+GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_words, const uint32_t *cnt,
+                            const uint32_t *tab, uint32_t *cxw, uint32_t *out, uint32_t *rate, uint32_t *len_out) {
+    *len_out = 0;
+    if (numbps == 0) return 0;
+    LaneEncoder cd;
+    mq_reset_words(cxw, tab);
+    cd.e.a = 0x8000; cd.e.c = 0; cd.e.ct = 12; cd.e.bp = -1; cd.e.cur = 0; cd.e.acc = 0; cd.e.out = out;
+    cd.cxw = cxw; cd.tab = tab; cd.rate = rate;
+    uint32_t passno = 0;
+    for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
+        const uint32_t *c = cnt + p * 4;
+        int t = (p == (int32_t)numbps - 1) ? 2 : 0;
+        const uint32_t b0 = t == 2 ? 0 : c[0], b1 = t == 2 ? 0 : c[0] + c[1];
+        const uint32_t total = b1 + c[2];
+        uint32_t bnd = t == 0 ? b0 : t == 1 ? b1 : total;  // end of the current pass
+        const uint4 *src = (const uint4 *)(sym + (size_t)p * slot_words);
+        uint4 c0 = src[0], c1 = src[1];
+        src += 2;
+        uint32_t i = 0;
+        while (t < 3 && i == bnd) {  // leading empty passes
+            cd.end_pass(passno++, t, p);
+            ++t;
+            bnd = t == 1 ? b1 : total;
+        }
+        uint32_t w = cxw[c0.x & 31];
+        uint4 c2 = *src++;
+        // one symbol; the next symbol's context word is read before this one's
+        // is written back (the LDS pipe keeps the order), bypassed if equal
+#define GRK_MQ_SYMBOL()                                                   \
+    {                                                                     \
+        const uint32_t b = cur & 0xff;                                    \
+        cur >>= 8;                                                        \
+        ++i;                                                              \
+        const uint32_t wn = cxw[cur & 31];                                \
+        const uint32_t nw = mqel_step(cd.e, tab, w, b >> 5);              \
+        cxw[b & 31] = nw;                                                 \
+        w = (((cur ^ b) & 31) == 0) ? nw : wn;                            \
+        if (i == bnd) {                                                   \
+            do {                                                          \
+                cd.end_pass(passno++, t, p);                              \
+                ++t;                                                      \
+                bnd = t == 1 ? b1 : total;                                \
+            } while (t < 3 && i == bnd);                                  \
+        }                                                                 \
+    }
+        while (total - i >= 16) {  // full chunks
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t cur = q == 0 ? c0.x : q == 1 ? c0.y : q == 2 ? c0.z : c0.w;
+                const uint32_t nxt = q == 0 ? c0.y : q == 1 ? c0.z : q == 2 ? c0.w : c1.x;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k == 3) cur |= nxt << 8;  // read-ahead byte for the last symbol of the word
+                    GRK_MQ_SYMBOL();
+                }
+            }
+            c0 = c1; c1 = c2; c2 = *src++;
+        }
+        while (i < total) {  // tail: < 16 symbols, all in c0
+            uint32_t cur = c0.x;
+            for (int k = 0; k < 4 && i < total; ++k) {
+                if (k == 3) cur |= c0.y << 8;
+                GRK_MQ_SYMBOL();
+            }
+            c0.x = c0.y; c0.y = c0.z; c0.z = c0.w;
+        }
+#undef GRK_MQ_SYMBOL
+    }
+    const uint32_t total = passno;
+    const uint32_t len = (uint32_t)cd.e.bp;
+    mqel_finish(cd.e, len);
+    uint32_t last = len;
+    for (uint32_t i = total; i > 0;) {
+        --i;
+        uint32_t r = rate[i];
+        if (r > last) r = last; else last = r;
+        rate[i] = r;
+    }
+    const uint8_t *ob = (const uint8_t *)out;
+    for (uint32_t i = 0; i < total; ++i)
+        if (rate[i] > 0 && ob[rate[i] - 1] == 0xFF) rate[i]--;
+    *len_out = len;
+    return total;
+}
+
+// Which bit-planes a decode produced: sigafter rows are valid for planes
+// [low, top], refinement rows for planes [qlow, top-1] (qlow = 32: none).
+struct DecodedPlanes { int32_t top, low, qlow; };
+
+GRK_HD DecodedPlanes decoded_planes(uint32_t numpasses, uint32_t numbps) {
+    DecodedPlanes d{-1, 0, 32};
+    if (numbps == 0 || numpasses == 0) return d;
+    uint32_t maxp = 3 * numbps - 2;
+    uint32_t last = (numpasses < maxp ? numpasses : maxp) - 1;
+    int32_t plane; int type;
+    pass_info(last, numbps, &plane, &type);
+    d.top = (int32_t)numbps - 1;
+    d.low = plane;
+    if (last >= 2) {
+        uint32_t im = last - (last - 2) % 3;  // last decoded refinement pass
+        d.qlow = (int32_t)numbps - 2 - (int32_t)((im - 1) / 3);
+    }
+    return d;
+}
+
+// Grok's decoded value (t1->data incl. the extra half-LSB) of sample (x, y):
+// significant at plane p (highest plane whose sigafter bit is set), refined at
+// planes p-1..qlow:  M = (1 v_{p-1} .. v_ql)b << (ql+1) | 1 << ql, ql = min(p, qlow).
+GRK_HD int32_t t1_rebuild(uint32_t x, uint32_t y, const DecodedPlanes &dp, const uint64_t *sigafter,
+                          const uint64_t *refbit, uint64_t negrow) {
+    int32_t p = -1;
+    for (int32_t q = dp.top; q >= dp.low; --q)
+        if ((sigafter[(uint32_t)q * 64 + y] >> x) & 1u) { p = q; break; }
+    if (p < 0) return 0;
+    uint32_t bits = 1;
+    int32_t ql = p;
+    for (int32_t q = p - 1; q >= dp.qlow; --q) {
+        bits = (bits << 1) | (uint32_t)((refbit[(uint32_t)q * 64 + y] >> x) & 1u);
+        ql = q;
+    }
+    int32_t m = (int32_t)((bits << (ql + 1)) | (1u << ql));
+    return ((negrow >> x) & 1u) ? -m : m;
+}
+
+// Per-block HBM scratch: state rows + two 32-plane x 64-row bit-plane sets
+// (encoder: pa = magnitude bit-planes; decoder: pa = sigafter, pb = refbit).
+struct T1Scratch {
+    BlockState st;
+    uint64_t pa[32 * 64];
+    uint64_t pb[32 * 64];
+    uint32_t cnt[32 * 4];  // encoder: symbols per (plane, pass type)
+};
+
+// Serial restatement of the encoder prep kernel (quantise, sign rows,
+// numbps, magnitude bit-planes): T1Part1::preEncode (T1Part1.cpp:58-94).
+GRK_HD uint32_t t1_prep_serial(const int32_t *coef, uint32_t stride, uint32_t w, uint32_t h, int32_t qmfbid,
+                               int32_t inv_step, BlockState &st, uint64_t *planes) {
+    uint32_t maxv = 0;
+    for (uint32_t y = 0; y < 66; ++y) st.neg[y] = 0;
+    for (uint32_t y = 0; y < h; ++y)
+        for (uint32_t x = 0; x < w; ++x) {
+            uint32_t ng;
+            uint32_t m = quant_mag(coef[(size_t)y * stride + x], qmfbid, inv_step, &ng);
+            if (ng) st.neg[y + 1] |= (uint64_t)1 << x;
+            maxv |= m;
+        }
+    uint32_t numbps = 0;
+    if (maxv) {
+        uint32_t t = 32u - (uint32_t)__builtin_clz(maxv);
+        numbps = t <= 6 ? 0 : t - 6;
+    }
+    for (uint32_t p = 0; p < numbps; ++p)
+        for (uint32_t y = 0; y < h; ++y) {
+            uint64_t row = 0;
+            for (uint32_t x = 0; x < w; ++x) {
+                uint32_t ng;
+                uint32_t m = quant_mag(coef[(size_t)y * stride + x], qmfbid, inv_step, &ng);
+                row |= (uint64_t)((m >> (p + 6)) & 1u) << x;
+            }
+            planes[p * 64 + y] = row;
+        }
+    return numbps;
+}
+
+// above[p*64+y] = OR of magnitude planes q > p (significance before plane p)
+GRK_HD void t1_prep_above(uint32_t h, uint32_t numbps, const uint64_t *planes, uint64_t *above) {
+    for (uint32_t y = 0; y < h; ++y) {
+        uint64_t acc = 0;
+        for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
+            above[(uint32_t)p * 64 + y] = acc;
+            acc |= planes[(uint32_t)p * 64 + y];
+        }
+    }
+}
+
+}  // namespace grkgpu

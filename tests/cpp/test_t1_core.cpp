@@ -5,7 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
-#include "../../grokimagecompression_amd/csrc/t1_core.h"
+#include "../../grokimagecompression_amd/csrc/t1_lane.h"
 #include "../../oracle/grk_oracle.h"
 
 using namespace grkgpu;
@@ -14,9 +14,15 @@ static const uint32_t kTab[47] = GRK_MQ_TABLE_INIT;
 static uint64_t rng = 88172645463325252ull;
 static uint32_t rnd() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return (uint32_t)rng; }
 
+static T1Scratch scr;
+
 int main(int argc, char **argv) {
     int iters = argc > 1 ? atoi(argv[1]) : 400;
     int fails = 0;
+    static uint8_t zc[2048], sc[256];
+    for (uint32_t i = 0; i < 2048; ++i) zc[i] = zc_lut_entry(i >> 9, i & 511);
+    for (uint32_t i = 0; i < 256; ++i) sc[i] = sc_lut_entry(i);
+    const T1Tables T{zc, sc, kTab};
     for (int it = 0; it < iters; ++it) {
         uint32_t w = 1 + rnd() % 64, h = 1 + rnd() % 64;
         if (it % 3 == 0) { w = 64; h = 64; }
@@ -52,6 +58,40 @@ int main(int argc, char **argv) {
             fails++;
             continue;
         }
+        // lane coder v2 (t1_lane.h): prep + encode must give the same bytes and rates
+        {
+            uint32_t lnb = t1_prep_serial(coef.data(), w, w, h, qmfbid, inv_step, scr.st, scr.pa);
+            std::vector<uint32_t> lout(w * h * 2 + 64, 0);
+            uint32_t lrate[100], llen = 0;
+            uint32_t cx[32];
+            uint32_t lnp = t1_encode_lane(w, h, lnb, scr.pa, scr.st, T, orient, cx, lout.data(), lrate, &llen);
+            bool lok = (int)lnp == onp && lnb == onb && llen == olen && memcmp(lout.data(), obuf.data() + 1, olen) == 0;
+            for (int p = 0; lok && p < onp; ++p) lok = lrate[p] == op[p].rate;
+            // split encoder: per-plane modelling + MQ
+            t1_prep_above(h, lnb, scr.pa, scr.pb);
+            const uint32_t slot = sym_slot_bytes(w, h), sb = sym_stream_bytes(w, h);
+            std::vector<uint32_t> sym((size_t)(lnb ? lnb : 1) * slot / 4 + 16, 0);
+            for (uint32_t p = 0; p < lnb; ++p) {
+                uint32_t *base = sym.data() + (size_t)p * slot / 4;
+                t1_model_plane(w, h, orient, scr.pa + p * 64, scr.pb + p * 64, p + 1 < lnb ? scr.pb + (p + 1) * 64 : nullptr,
+                               scr.st.neg, (uint64_t *)(base + sb / 4), sc, base, scr.cnt + p * 4);
+            }
+            std::vector<uint32_t> sout(w * h * 2 + 64, 0);
+            uint32_t srate[100], slen = 0;
+            uint32_t snp = t1_mq_block(lnb, sym.data(), slot / 4, scr.cnt, kTab, cx, sout.data(), srate, &slen);
+            bool sok = (int)snp == onp && slen == olen && memcmp(sout.data(), obuf.data() + 1, olen) == 0;
+            for (int p = 0; sok && p < onp; ++p) sok = srate[p] == op[p].rate;
+            if (!sok) {
+                printf("SPLIT ENC MISMATCH it=%d w=%u h=%u orient=%u q=%d np %u/%d len %u/%u\n", it, w, h, orient, qmfbid,
+                       snp, onp, slen, olen);
+                fails++;
+            }
+            if (!lok) {
+                printf("LANE ENC MISMATCH it=%d w=%u h=%u orient=%u q=%d np %u/%d nb %u/%u len %u/%u\n", it, w, h,
+                       orient, qmfbid, lnp, onp, lnb, onb, llen, olen);
+                fails++;
+            }
+        }
         if (onp == 0) continue;
         // decode round trip: all passes, and a truncated prefix
         for (int trunc = 0; trunc < 2; ++trunc) {
@@ -65,6 +105,20 @@ int main(int argc, char **argv) {
             t1_decode_block_impl(data.data(), len, np, onb, w, h, orient, rows, kTab, gd.data(), w, Id());
             if (od != gd) {
                 printf("DEC MISMATCH it=%d w=%u h=%u np=%u\n", it, w, h, np);
+                fails++;
+            }
+            // lane decoder v2 + rebuild, from an arbitrarily aligned copy
+            std::vector<uint8_t> pad(len + 64, 0);
+            uint8_t *lp = pad.data() + 16 + (it & 7);
+            memcpy(lp, gbuf.data() + 1, len);
+            uint32_t cx[20];
+            t1_decode_lane(lp, len, np, onb, w, h, orient, scr.st, T, cx, scr.pa, scr.pb);
+            DecodedPlanes dp = decoded_planes(np, onb);
+            std::vector<int32_t> ld(w * h);
+            for (uint32_t y = 0; y < h; ++y)
+                for (uint32_t x = 0; x < w; ++x) ld[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
+            if (od != ld) {
+                printf("LANE DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u\n", it, w, h, np, onb);
                 fails++;
             }
         }

@@ -48,7 +48,7 @@ def test_no_cpu_fallback_without_gpu():
 def test_t1_core_host_matches_oracle(oracle, tmp_path):
     exe = tmp_path / "test_t1_core"
     ob = os.path.join(ROOT, "oracle", "build")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), os.path.join(ROOT, "tests/cpp/test_t1_core.cpp"),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-o", str(exe), os.path.join(ROOT, "tests/cpp/test_t1_core.cpp"),
                     "-L" + ob, "-lgrk_oracle", "-Wl,-rpath," + ob], check=True)
     r = subprocess.run([str(exe), "800"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:]
