@@ -14,7 +14,7 @@
 #include <stdint.h>
 
 #include "grk_device.h"
-#include "t1_lane.h"
+#include "t1_dec.h"
 #include <stdlib.h>
 #include <string.h>
 
@@ -470,6 +470,28 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_lane(const DecBlock *__rest
                    s_cx + threadIdx.x * 21, S.pa, S.pb);
 }
 
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_decode_v3(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                        const uint8_t *__restrict__ data,
+                                                        T1Scratch *__restrict__ scr) {
+    __shared__ uint8_t s_zc[2048];
+    __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_cx[LANES * 21];
+    for (uint32_t k = threadIdx.x; k < 2048; k += LANES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
+    for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
+    T1Scratch &S = scr[i];
+    t1_decode_v3(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, S.st, T, s_cx + threadIdx.x * 21, S.pa,
+                 S.pb);
+}
+
 // One workgroup per block, lane = column: values from the bit-plane rows
 // (staged in LDS, broadcast reads), then T1Part1::postDecode scaling
 // (5/3: v/2, 9/7: float(v) * step) and a coalesced row store.
@@ -596,7 +618,11 @@ static void launch_enc_lane(const EncBlock *blocks, uint32_t n, T1Scratch *scr, 
 
 template <int L>
 static void launch_dec_lane(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scr, hipStream_t s) {
-    hipLaunchKernelGGL(k_t1_decode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
+    static const bool v2 = getenv("GRKGPU_T1_DEC") && !strcmp(getenv("GRKGPU_T1_DEC"), "v2");
+    if (v2)
+        hipLaunchKernelGGL(k_t1_decode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
+    else
+        hipLaunchKernelGGL(k_t1_decode_v3<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
 }
 
 template <int L>

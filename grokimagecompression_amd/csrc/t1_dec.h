@@ -1,0 +1,310 @@
+// t1_dec.h -- EBCOT Tier-1 decoder, v3: one lane per code-block, built for a
+// lone serial lane on CDNA4.
+//
+//   * block state = 64-bit row masks in HBM, one 4-row stripe held in
+//     registers (Stripe); each lane visits only the columns of a stripe that
+//     hold work for the pass (bit-scan of candidate masks)
+//   * per column, the 3x6 significance neighbourhood (rows k-1..k+4, columns
+//     x-1..x+1) is packed into an 18-bit window P; the zero-coding context of
+//     row r is the LUT entry for (P >> 3r) & 0x1FF and the sign context comes
+//     from the N/W/E/S bits of P and of the matching sign window Q
+//   * the symbols of a column go through ONE decode site (a small state
+//     machine: ZC -> SC, AGG -> UNI -> UNI -> SC), so lanes of a wavefront
+//     that sit in different rows / symbol kinds still share the MQ code
+//   * the MQ decoder is select-based; only a renormalisation that needs a new
+//     byte branches.  Bytes arrive through a 16-byte-chunk ring refilled one
+//     chunk ahead.
+//   * outputs are write-only bit-plane rows (sigafter / refbit, t1_lane.h)
+//     rebuilt into coefficients by k_t1_rebuild.
+//
+// Semantics: Grok v5.1.0 t1/t1_part1/t1.cpp t1_decode_cblk (:1038) with
+// dec_sigpass / dec_refpass / dec_clnpass, mqc_dec_inl.h; cblksty 0.
+#pragma once
+#include "t1_lane.h"
+
+namespace grkgpu {
+
+// sign LUT in window order: bit0 sigN, 1 negN, 2 sigW, 3 negW, 4 sigE, 5 negE,
+// 6 sigS, 7 negS  ->  context | xorbit << 7
+GRK_HD uint8_t sc_win_entry(uint32_t i) {
+    uint32_t xr;
+    int cx = sc_ctx((i >> 2) & 1, (i >> 4) & 1, i & 1, (i >> 6) & 1, (i >> 3) & 1, (i >> 5) & 1, (i >> 1) & 1,
+                    (i >> 7) & 1, &xr);
+    return (uint8_t)(cx | (xr << 7));
+}
+
+struct Dec3 {
+    uint32_t a, c, ct;
+    uint32_t cur, nxt;  // code bytes at bp and bp + 1
+    const uint4 *p;     // next chunk to load
+    uint4 c0, c1, c2;   // c0.x = current word (consumed low byte first)
+    uint32_t wleft, wq; // bytes left in c0.x, words left in c0
+    uint32_t idx, len;  // bytes handed out so far, segment length
+};
+
+GRK_HD uint32_t d3_byte(Dec3 &d) {
+    const uint32_t b = d.c0.x & 0xff;
+    d.c0.x >>= 8;
+    if (--d.wleft == 0) {
+        d.wleft = 4;
+        if (--d.wq == 0) {
+            d.wq = 4;
+            d.c0 = d.c1; d.c1 = d.c2; d.c2 = *d.p++;
+        } else {
+            d.c0.x = d.c0.y; d.c0.y = d.c0.z; d.c0.z = d.c0.w;
+        }
+    }
+    return d.idx++ < d.len ? b : 0xffu;
+}
+
+// BYTEIN (mqc_dec_inl.h): a 0xFF followed by a byte > 0x8F is a marker and
+// feeds 1-bits from then on
+GRK_HD void d3_bytein(Dec3 &d) {
+    const bool ff = d.cur == 0xff;
+    const bool marker = ff && d.nxt > 0x8f;
+    d.c += marker ? 0xff00u : (d.nxt << (ff ? 9 : 8));
+    d.ct = (ff && !marker) ? 7u : 8u;
+    if (!marker) {
+        d.cur = d.nxt;
+        d.nxt = d3_byte(d);
+    }
+}
+
+GRK_HD void d3_init(Dec3 &d, const uint8_t *data, uint32_t len) {
+    const uintptr_t pa = (uintptr_t)data;
+    d.p = (const uint4 *)(pa & ~(uintptr_t)15);
+    d.c0 = d.p[0]; d.c1 = d.p[1]; d.c2 = d.p[2];
+    d.p += 3;
+    d.wleft = 4; d.wq = 4;
+    d.idx = 0; d.len = 0;  // skip the bytes before the segment start
+    for (uint32_t s = (uint32_t)(pa & 15); s > 0; --s) { d3_byte(d); }
+    d.idx = 0; d.len = len;
+    d.cur = d3_byte(d);
+    d.nxt = d3_byte(d);
+    d.c = d.cur << 16;  // len == 0 reads 0xFF, as Grok's padded buffer does
+    d3_bytein(d);
+    d.c <<= 7; d.ct -= 7; d.a = 0x8000;
+}
+
+// MQ decode of one symbol in context cx (mqc_dec_inl.h DECODE_SYMBOL).
+GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
+    const uint32_t w = cxw[cx];
+    const uint32_t qe = w & 0xffff, mps = w >> 31;
+    uint32_t a = d.a - qe;
+    const uint32_t qe16 = qe << 16;
+    const bool lo = d.c < qe16;
+    const bool lps = lo ? (a >= qe) : (a < qe);
+    const bool keep = !lo && (a & 0x8000);
+    d.c = lo ? d.c : d.c - qe16;
+    a = lo ? qe : a;
+    const uint32_t nidx = (w >> (lps ? 22 : 16)) & 63;
+    const uint32_t nmps = mps ^ (lps ? (w >> 28) & 1u : 0u);
+    const uint32_t tw = tab[nidx];
+    uint32_t n = clz32(a) - 16;
+    if (n <= d.ct) {
+        a <<= n; d.c <<= n; d.ct -= n;
+    } else {
+        do {
+            if (d.ct == 0) d3_bytein(d);
+            const uint32_t sh = n < d.ct ? n : d.ct;
+            a <<= sh; d.c <<= sh; d.ct -= sh; n -= sh;
+        } while (n);
+    }
+    d.a = a;
+    if (!keep) cxw[cx] = tw | (nmps << 31);
+    return mps ^ (uint32_t)lps;
+}
+
+// 18-bit 3x6 window of column x: bits 3i..3i+2 = row i (k-1+i), columns x-1..x+1
+GRK_HD uint32_t win18(const uint64_t *r6, uint32_t x) {
+    const uint32_t s1 = x ? x - 1 : 0, m = x ? 7u : 3u, s2 = x ? 0u : 1u;
+    uint32_t P = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) P |= ((((uint32_t)(r6[i] >> s1)) & m) << s2) << (3 * i);
+    return P;
+}
+
+GRK_HD uint32_t col4(const uint64_t *r4, uint32_t x) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v |= (uint32_t)((r4[i] >> x) & 1) << i;
+    return v;
+}
+
+GRK_HD void setcol4(uint64_t *r4, uint32_t x, uint32_t bits) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r4[i] |= (uint64_t)((bits >> i) & 1) << x;
+}
+
+// self bits of the window (rows k..k+3 of column x)
+GRK_HD uint32_t win_self4(uint32_t P) { return ((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 8) & 4) | ((P >> 10) & 8); }
+
+struct DecTables {
+    const uint8_t *zc;   // 512 entries for this block's orientation
+    const uint8_t *sc;   // 256, window order
+    const uint32_t *mq;  // 47
+};
+
+// significance propagation (CUP = false) or cleanup (CUP = true) of one
+// column; returns true if a sample became significant.
+template <bool CUP>
+GRK_HD bool d3_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+    uint32_t P = win18(s.sig, x);
+    const uint32_t vis4 = col4(s.vis, x);
+    const uint32_t rows = (1u << nr) - 1;
+    const uint32_t sig4 = win_self4(P);
+    uint32_t todo;
+    if (!CUP) {
+        uint32_t nz = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nz |= (((P >> (3 * r)) & 0x1EF) != 0 ? 1u : 0u) << r;
+        todo = nz & ~sig4 & ~vis4 & rows;
+    } else {
+        todo = ~sig4 & ~vis4 & rows;
+    }
+    uint32_t kind = 0, r = 0;  // 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo)
+    if (CUP && nr == 4 && P == 0 && vis4 == 0) {
+        kind = 2;
+    } else {
+        if (!todo) return false;
+        r = (uint32_t)__builtin_ctz(todo);
+    }
+    uint32_t Q = 0, newsig = 0, newneg = 0, newvis = 0, si = 0;
+    bool haveQ = false;
+    for (;;) {
+        uint32_t cx;
+        if (kind == 0) cx = T.zc[(P >> (3 * r)) & 0x1FF];
+        else if (kind == 1) cx = si & 0x7f;
+        else cx = kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
+        const uint32_t bit = d3_decode(d, cxw, T.mq, cx);
+        bool advance = true;
+        if (kind == 0) {
+            if (!CUP) newvis |= 1u << r;
+            if (bit) { kind = 1; advance = false; }
+        } else if (kind == 1) {
+            const uint32_t sg = bit ^ (si >> 7);
+            P |= 1u << (3 * r + 4);
+            Q |= sg << (3 * r + 4);
+            newsig |= 1u << r;
+            newneg |= sg << r;
+            // the sample below now has a significant neighbour (SPP)
+            if (!CUP) todo |= (rows & ~(sig4 | vis4)) & (2u << r);
+            kind = 0;
+        } else if (kind == 2) {
+            if (!bit) break;
+            kind = 3; advance = false;
+        } else if (kind == 3) {
+            r = bit << 1; kind = 4; advance = false;
+        } else {
+            r |= bit;
+            todo = rows & ~((2u << r) - 1);  // the rows after the run are plain ZC
+            kind = 1; advance = false;
+        }
+        if (kind == 1 && !advance) {
+            if (!haveQ) { Q = win18(s.neg, x); haveQ = true; }
+            si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
+        }
+        if (advance) {
+            todo &= ~((2u << r) - 1);
+            if (!todo) break;
+            r = (uint32_t)__builtin_ctz(todo);
+        }
+    }
+    if (!CUP && newvis) setcol4(s.vis, x, newvis);
+    if (newsig) {
+        setcol4(s.sig + 1, x, newsig);
+        setcol4(s.neg + 1, x, newneg);
+        return true;
+    }
+    return false;
+}
+
+// magnitude refinement of one column
+GRK_HD void d3_mrp_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+    const uint32_t P = win18(s.sig, x);
+    const uint32_t rows = (1u << nr) - 1;
+    uint32_t m4 = win_self4(P) & ~col4(s.vis, x) & rows;
+    const uint32_t ref4 = col4(s.ref, x);
+    const uint32_t mem = m4;
+    uint32_t bits = 0;
+    while (m4) {
+        const uint32_t r = (uint32_t)__builtin_ctz(m4);
+        m4 &= m4 - 1;
+        const uint32_t cx = ((ref4 >> r) & 1) ? CX_MAG + 2 : CX_MAG + (((P >> (3 * r)) & 0x1EF) ? 1u : 0u);
+        bits |= d3_decode(d, cxw, T.mq, cx) << r;
+    }
+    setcol4(s.ref, x, mem);
+    setcol4(s.bit, x, bits);
+}
+
+// Decode one block into write-only bit-plane rows (see t1_decode_lane).
+GRK_HD void t1_decode_v3(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
+                         uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw, uint64_t *sigafter,
+                         uint64_t *refbit) {
+    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
+    mq_reset_words(cxw, T.mq);
+    Dec3 d;
+    d3_init(d, data, len);
+    const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
+    int32_t bpno = (int32_t)numbps - 1;
+    int passtype = 2;
+    for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
+        uint64_t *sa = sigafter + (uint32_t)bpno * 64;
+        uint64_t *rb = refbit + (uint32_t)bpno * 64;
+        for (uint32_t k = 0; k < h; k += 4) {
+            Stripe s;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { s.sig[i] = st.sig[k + i]; s.neg[i] = st.neg[k + i]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { s.vis[i] = st.vis[k + 1 + i]; s.ref[i] = st.ref[k + 1 + i]; s.bit[i] = 0; }
+            const uint32_t nr = h - k < 4 ? h - k : 4;
+            if (passtype == 0) {
+                uint64_t cand = spp_candidates(s, nr) & wm;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
+                    const bool grew = d3_column<false>(d, cxw, T, s, x, nr);
+                    cand &= ~done;
+                    if (grew) cand = spp_candidates(s, nr) & wm & ~done;
+                }
+            } else if (passtype == 1) {
+                uint64_t mem = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((uint32_t)r < nr) mem |= s.sig[r + 1] & ~s.vis[r];
+                while (mem) {
+                    const uint32_t x = ctz64(mem);
+                    mem &= mem - 1;
+                    d3_mrp_column(d, cxw, T, s, x, nr);
+                }
+            } else {
+                uint64_t cand = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((uint32_t)r < nr) cand |= ~(s.sig[r + 1] | s.vis[r]);
+                cand &= wm;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    cand &= cand - 1;
+                    d3_column<true>(d, cxw, T, s, x, nr);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s.vis[r] = 0;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                st.sig[k + 1 + i] = s.sig[i + 1];
+                st.neg[k + 1 + i] = s.neg[i + 1];
+                st.vis[k + 1 + i] = s.vis[i];
+                st.ref[k + 1 + i] = s.ref[i];
+                if ((uint32_t)i < nr) {
+                    if (passtype == 1) rb[k + i] = s.bit[i];
+                    else sa[k + i] = s.sig[i + 1];
+                }
+            }
+        }
+        if (++passtype == 3) { passtype = 0; bpno--; }
+    }
+}
+
+}  // namespace grkgpu

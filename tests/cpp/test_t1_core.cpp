@@ -5,7 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
-#include "../../grokimagecompression_amd/csrc/t1_lane.h"
+#include <algorithm>
+#include "../../grokimagecompression_amd/csrc/t1_dec.h"
 #include "../../oracle/grk_oracle.h"
 
 using namespace grkgpu;
@@ -23,6 +24,8 @@ int main(int argc, char **argv) {
     for (uint32_t i = 0; i < 2048; ++i) zc[i] = zc_lut_entry(i >> 9, i & 511);
     for (uint32_t i = 0; i < 256; ++i) sc[i] = sc_lut_entry(i);
     const T1Tables T{zc, sc, kTab};
+    static uint8_t scw[256];
+    for (uint32_t i = 0; i < 256; ++i) scw[i] = sc_win_entry(i);
     for (int it = 0; it < iters; ++it) {
         uint32_t w = 1 + rnd() % 64, h = 1 + rnd() % 64;
         if (it % 3 == 0) { w = 64; h = 64; }
@@ -108,7 +111,7 @@ int main(int argc, char **argv) {
                 fails++;
             }
             // lane decoder v2 + rebuild, from an arbitrarily aligned copy
-            std::vector<uint8_t> pad(len + 64, 0);
+            std::vector<uint8_t> pad(len + 160, 0);
             uint8_t *lp = pad.data() + 16 + (it & 7);
             memcpy(lp, gbuf.data() + 1, len);
             uint32_t cx[20];
@@ -120,6 +123,21 @@ int main(int argc, char **argv) {
             if (od != ld) {
                 printf("LANE DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u\n", it, w, h, np, onb);
                 fails++;
+            }
+            // decoder v3 (t1_dec.h)
+            {
+                const DecTables DT{zc + orient * 512, scw, kTab};
+                uint32_t cx3[32];
+                std::fill(scr.pa, scr.pa + 32 * 64, ~0ull);
+                std::fill(scr.pb, scr.pb + 32 * 64, ~0ull);
+                t1_decode_v3(lp, len, np, onb, w, h, scr.st, DT, cx3, scr.pa, scr.pb);
+                std::vector<int32_t> vd(w * h);
+                for (uint32_t y = 0; y < h; ++y)
+                    for (uint32_t x = 0; x < w; ++x) vd[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
+                if (od != vd) {
+                    printf("V3 DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u orient=%u\n", it, w, h, np, onb, orient);
+                    fails++;
+                }
             }
         }
     }
