@@ -15,10 +15,11 @@
  *   grkgpu_decompress      grk_read_header + grk_decode (grok.h:1571-1600,
  *                          grok.cpp:381 -> j2k.cpp:1136 j2k_decode_tiles).
  *   grkgpu_read_header     grk_read_header (grok.h:1571, j2k.cpp:406).
- *   grkgpu_encode_tile_*   the tile hot path inside
+ *   (stage entry points below = the tile hot path inside
  *                          TileProcessor::encode_tile (TileProcessor.cpp:
  *                          994-1012: dc_level_shift_encode :1449, mct_encode
- *                          :1473, dwt_encode :1520, t1_encode :1535).
+ *                          :1473, dwt_encode :1520, t1_encode :1535) and
+ *                          decode_tile (:1127-1176).)
  *   grkgpu_dwt_fwd/_inv    Wavelet::encode / Wavelet::decode
  *                          (transform/Wavelet.cpp:35-56, WaveletForward.h:40,
  *                          dwt.cpp:1208 decode_53, :2154 decode_97).
