@@ -105,15 +105,26 @@ def main():
     value = world * pix_per_step * args.steps / elapsed / 1e6
     ms_per_step = 1e3 * elapsed / args.steps
 
-    # roofline: the forward DWT (encode), B_DWT / measured kernel time (HIP
-    # events around the DWT launches on the codec's stream)
+    # roofline: the forward 9/7 DWT of the frame = 5 level launches (one per
+    # decomposition level, all 3 components in each), B_DWT / the HIP-event
+    # time around those launches on the codec's stream (= per-launch bytes /
+    # mean launch duration).  traffic: HBM bytes per launch from the committed
+    # rocprofv3 PMC summary (scripts/pmc_bench.sh), when present.
     bdwt = dwt_bytes(H, W, C)
+    nlaunch = 5
     dwt_ms = st["enc97"]["dwt_ms"]
     achieved = bdwt / (dwt_ms * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "kernel": "k_dwt_fwd_level<9/7> (all 5 levels x 3 comps)",
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
+    if os.path.exists(pmc):
+        d = json.load(open(pmc))
+        tot = sum(e["bytes"] for k, v in d["kernels"].items() if "k_dwt_fwd<true" in k for e in v)
+        traffic = round(tot / nlaunch)
+    roofline = {"bound": "hbm", "kernel": "k_dwt_fwd<9/7> (5 level launches x 3 comps, dwt.hip)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "algorithmic_bytes": bdwt, "kernel_ms": round(dwt_ms, 4)}
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": bdwt // nlaunch, "launches": nlaunch,
+                "kernel_ms_per_launch": round(dwt_ms / nlaunch, 4)}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:

@@ -134,6 +134,8 @@ def lib():
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
         L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
         L.grkgpu_dwt_inv.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
+        L.grkgpu_dwt_scratch_bytes.restype = ctypes.c_size_t
+        L.grkgpu_dwt_scratch_bytes.argtypes = [U32, U32, U32, U32, U32]
         L.grkgpu_t1_scratch_bytes.restype = ctypes.c_size_t
         L.grkgpu_t1_encode_blocks.argtypes = [VP, U32, VP, VP, VP, VP, VP]
         L.grkgpu_t1_decode_blocks.argtypes = [VP, U32, VP, VP, VP, VP]
@@ -264,7 +266,7 @@ def dwt_fwd(t, x0, y0, numres, irreversible):
     """In-place forward DWT of a (h,w) int32 cuda tensor (Mallat layout)."""
     torch = _torch()
     h, w = t.shape
-    scratch = torch.empty(2 * h * w + 256, dtype=torch.int32, device=t.device)
+    scratch = torch.empty(lib().grkgpu_dwt_scratch_bytes(x0, y0, x0 + w, y0 + h, numres) // 4 + 64, dtype=torch.int32, device=t.device)
     _check(lib().grkgpu_dwt_fwd(t.data_ptr(), scratch.data_ptr(), x0, y0, x0 + w, y0 + h, numres,
                                 1 if irreversible else 0, _stream_handle(t.device)))
     return t
@@ -273,7 +275,7 @@ def dwt_fwd(t, x0, y0, numres, irreversible):
 def dwt_inv(t, x0, y0, numres, irreversible):
     torch = _torch()
     h, w = t.shape
-    scratch = torch.empty(2 * h * w + 256, dtype=torch.int32, device=t.device)
+    scratch = torch.empty(lib().grkgpu_dwt_scratch_bytes(x0, y0, x0 + w, y0 + h, numres) // 4 + 64, dtype=torch.int32, device=t.device)
     _check(lib().grkgpu_dwt_inv(t.data_ptr(), scratch.data_ptr(), x0, y0, x0 + w, y0 + h, numres,
                                 1 if irreversible else 0, _stream_handle(t.device)))
     return t

@@ -78,8 +78,8 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff;
-    HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs;
+    HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
 };
@@ -203,60 +203,131 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *p, C
     return GRKGPU_OK;
 }
 
-// Forward DWT of one tile-component: src -> coef (Mallat), ll scratch ping-pong.
-static hipError_t run_dwt_fwd(const int32_t *src, int32_t *coef, int32_t *llA, int32_t *llB, const TileComp &tc,
-                              int irrev, hipStream_t s) {
-    const uint32_t stride = tc.r.w();
-    const int32_t *in = src;
-    uint32_t instride = stride;
-    int32_t *bufs[2] = {llA, llB};
-    int flip = 0;
-    for (int lvl = 0; lvl + 1 < (int)tc.numres; ++lvl) {
-        const Rect &cur = tc.res[tc.numres - 1 - lvl].r;
-        const Rect &nxt = tc.res[tc.numres - 2 - lvl].r;
-        bool last = lvl + 2 == (int)tc.numres;
-        int32_t *llout = last ? coef : bufs[flip];
-        uint32_t llstride = last ? stride : nxt.w();
-        if (cur.w() && cur.h()) {
-            hipError_t e = launch_dwt_fwd_level(in, instride, llout, llstride, coef, stride, (int)cur.w(),
-                                                (int)cur.h(), (int)(cur.x0 & 1), (int)(cur.y0 & 1), (int)nxt.w(),
-                                                (int)nxt.h(), irrev, s);
-            if (e != hipSuccess) return e;
-        }
-        in = llout;
-        instride = llstride;
-        flip ^= 1;
-    }
-    if (tc.numres == 1)
-        return hipMemcpyAsync(coef, src, sizeof(int32_t) * (size_t)tc.r.w() * tc.r.h(), hipMemcpyDeviceToDevice, s);
-    return hipSuccess;
+// ---------------------------------------------------------------------------
+// DWT job tables (dwt.hip).  Every tile-component owns two LL ping-pong
+// buffers (A: the largest LL, R_{numres-2}; B: the next one), with rows padded
+// to 16 elements.  Forward level l writes its LL into buffer l % 2 (the last
+// level straight into the Mallat buffer); inverse level r writes into
+// (numres - 2 - r) % 2 (the last into the output buffer).
+// ---------------------------------------------------------------------------
+static uint32_t pad16(uint32_t v) { return (v + 15) & ~15u; }
+
+struct LLGeom { uint32_t strideA = 0, rowsA = 0, strideB = 0, rowsB = 0; uint64_t elems = 0; };
+
+static LLGeom ll_geom(const TileComp &tc) {
+    LLGeom g;
+    if (tc.numres >= 2) { g.strideA = pad16(tc.res[tc.numres - 2].r.w()); g.rowsA = tc.res[tc.numres - 2].r.h(); }
+    if (tc.numres >= 3) { g.strideB = pad16(tc.res[tc.numres - 3].r.w()); g.rowsB = tc.res[tc.numres - 3].r.h(); }
+    g.elems = ((uint64_t)g.strideA * g.rowsA + 63) / 64 * 64 + ((uint64_t)g.strideB * g.rowsB + 63) / 64 * 64;
+    return g;
 }
 
-// Inverse DWT: coef (Mallat) -> dst, ll scratch ping-pong.
-static hipError_t run_dwt_inv(const int32_t *coef, int32_t *dst, int32_t *llA, int32_t *llB, const TileComp &tc,
-                              int irrev, hipStream_t s) {
-    const uint32_t stride = tc.r.w();
-    if (tc.numres == 1)
-        return hipMemcpyAsync(dst, coef, sizeof(int32_t) * (size_t)tc.r.w() * tc.r.h(), hipMemcpyDeviceToDevice, s);
-    const int32_t *ll = coef;
-    uint32_t llstride = stride;
-    int32_t *bufs[2] = {llA, llB};
-    int flip = 0;
-    for (uint32_t r = 1; r < tc.numres; ++r) {
-        const Rect &lo = tc.res[r - 1].r;
-        const Rect &cur = tc.res[r].r;
-        bool last = r + 1 == tc.numres;
-        int32_t *out = last ? dst : bufs[flip];
-        uint32_t ostride = last ? stride : cur.w();
-        if (cur.w() && cur.h()) {
-            hipError_t e = launch_dwt_inv_level(ll, llstride, coef, stride, out, ostride, (int)cur.w(), (int)cur.h(),
-                                                (int)(cur.x0 & 1), (int)(cur.y0 & 1), (int)lo.w(), (int)lo.h(),
-                                                irrev, s);
-            if (e != hipSuccess) return e;
+struct DwtPlan {
+    std::vector<std::vector<DwtJob>> levels;  // [level][job]
+    std::vector<int> th;                      // window rows per level (dwt_finalize)
+    std::vector<std::pair<int32_t *, const int32_t *>> copies;  // numres == 1: dst <- src
+    uint64_t copy_elems = 0;
+};
+
+static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *coef, int32_t *llbase, int irrev,
+                        bool inverse) {
+    const uint32_t stride = tc.r.w(), rows = tc.r.h();
+    if (tc.numres == 1) {
+        if (inverse) P.copies.push_back({work, coef});
+        else P.copies.push_back({coef, work});
+        P.copy_elems = (uint64_t)stride * rows;
+        return;
+    }
+    const LLGeom g = ll_geom(tc);
+    int32_t *buf[2] = {llbase, llbase + ((uint64_t)g.strideA * g.rowsA + 63) / 64 * 64};
+    const uint32_t bstride[2] = {g.strideA, g.strideB}, brows[2] = {g.rowsA, g.rowsB};
+    const uint32_t full_bytes = (uint32_t)std::min<uint64_t>((uint64_t)stride * rows * 4, 0xffffffffu);
+    if (P.levels.size() < tc.numres - 1) P.levels.resize(tc.numres - 1);
+    for (uint32_t lvl = 0; lvl + 1 < tc.numres; ++lvl) {
+        DwtJob j{};
+        const bool last = lvl + 2 == tc.numres;
+        Rect cur, lo;
+        uint32_t slot;
+        if (!inverse) {
+            cur = tc.res[tc.numres - 1 - lvl].r;
+            lo = tc.res[tc.numres - 2 - lvl].r;
+            slot = lvl & 1;
+            const uint32_t pslot = (lvl - 1) & 1;
+            j.in = lvl == 0 ? work : buf[pslot];
+            j.in_stride = lvl == 0 ? stride : bstride[pslot];
+            j.in_bytes = lvl == 0 ? full_bytes : bstride[pslot] * brows[pslot] * 4;
+            j.out = last ? coef : buf[slot];
+            j.out_stride = last ? stride : bstride[slot];
+            j.out_bytes = last ? full_bytes : bstride[slot] * brows[slot] * 4;
+            j.bands = coef;
+            j.bands_stride = stride;
+            j.bands_bytes = full_bytes;
+        } else {
+            const uint32_t r = lvl + 1;
+            cur = tc.res[r].r;
+            lo = tc.res[r - 1].r;
+            slot = (tc.numres - 2 - r) & 1;
+            const uint32_t pslot = slot ^ 1;
+            j.in = r == 1 ? coef : buf[pslot];
+            j.in_stride = r == 1 ? stride : bstride[pslot];
+            j.in_bytes = r == 1 ? full_bytes : bstride[pslot] * brows[pslot] * 4;
+            j.coef = coef;
+            j.coef_stride = stride;
+            j.coef_bytes = full_bytes;
+            j.out = last ? work : buf[slot];
+            j.out_stride = last ? stride : bstride[slot];
+            j.out_bytes = last ? full_bytes : bstride[slot] * brows[slot] * 4;
         }
-        ll = out;
-        llstride = ostride;
-        flip ^= 1;
+        if (!cur.w() || !cur.h()) continue;
+        j.rw = (int32_t)cur.w(); j.rh = (int32_t)cur.h();
+        j.casx = (int32_t)(cur.x0 & 1); j.casy = (int32_t)(cur.y0 & 1);
+        j.snx = (int32_t)lo.w(); j.sny = (int32_t)lo.h();
+        P.levels[lvl].push_back(j);
+    }
+}
+
+// Pick each level's window height from the level's total size; tile counts.
+static void dwt_finalize(DwtPlan &P, int irrev) {
+    P.th.assign(P.levels.size(), 8);
+    for (size_t l = 0; l < P.levels.size(); ++l) {
+        uint64_t samples = 0;
+        for (auto &j : P.levels[l]) samples += (uint64_t)j.rw * j.rh;
+        P.th[l] = dwt_pick_th(irrev, samples);
+        for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j.rw, j.rh, j.casx, j.casy, &j.tiles_x, &j.ntiles);
+    }
+}
+
+// Upload the job table (one H2D from pinned memory).
+static hipError_t dwt_upload(DwtPlan &P, DevBuf &djobs, HostBuf &hjobs, int irrev, hipStream_t s) {
+    dwt_finalize(P, irrev);
+    size_t n = 0;
+    for (auto &l : P.levels) n += l.size();
+    if (!n) return hipSuccess;
+    hipError_t e = djobs.ensure(n * sizeof(DwtJob) + 256);
+    if (e == hipSuccess) e = hjobs.ensure(n * sizeof(DwtJob) + 256);
+    if (e != hipSuccess) return e;
+    DwtJob *h = hjobs.as<DwtJob>();
+    size_t k = 0;
+    for (auto &l : P.levels)
+        for (auto &j : l) h[k++] = j;
+    return hipMemcpyAsync(djobs.p, hjobs.p, n * sizeof(DwtJob), hipMemcpyHostToDevice, s);
+}
+
+// Run the levels (job table already uploaded by dwt_upload on the same stream).
+static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse, hipStream_t s) {
+    for (auto &cp : P.copies) {
+        hipError_t e = hipMemcpyAsync(cp.first, cp.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    size_t k = 0;
+    for (size_t li = 0; li < P.levels.size(); ++li) {
+        const auto &l = P.levels[li];
+        uint32_t maxt = 0;
+        for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
+        e = launch_dwt_jobs(djobs.as<DwtJob>() + k, (uint32_t)l.size(), maxt, P.th[li], irrev, inverse ? 1 : 0, s);
+        if (e != hipSuccess) return e;
+        k += l.size();
     }
     return hipSuccess;
 }
@@ -291,7 +362,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     // geometry for every tile, arena offsets, block table
     const uint32_t ntiles = cp.tw * cp.th;
     std::vector<Tile> tiles(ntiles);
-    uint64_t arena = 0, max_tc = 0;
+    uint64_t arena = 0, llarena = 0;
+    std::vector<uint64_t> lloff(ntiles * nc);
     std::vector<EncBlock> eb;
     std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
     uint64_t sym_total = 0;
@@ -307,7 +379,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             tc.arena_off = arena;
             uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
             arena += (area + 63) & ~63ull;
-            max_tc = std::max(max_tc, area);
+            lloff[t * nc + k] = llarena;
+            llarena += ll_geom(tc).elems;
             for_each_cblk(tc, [&](Band &band, Cblk &cb) {
                 cb.gidx = (uint32_t)eb.size();
                 EncBlock b;
@@ -336,7 +409,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     }
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
-    HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
+    HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
@@ -363,7 +436,14 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipEventRecord(c->ev[1], s));
     ShiftArr sh{};
     for (uint32_t k = 0; k < nc; ++k) sh.v[k] = cp.shift[k];
-    int32_t *llA = c->ll.as<int32_t>(), *llB = llA + (max_tc / 2 + 64);
+    DwtPlan dplan;
+    for (auto &tile : tiles)
+        for (uint32_t k = 0; k < nc; ++k) {
+            const TileComp &tc = tile.comps[k];
+            dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
+                        c->ll.as<int32_t>() + lloff[tile.index * nc + k], cp.irrev, false);
+        }
+    HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
         PlanePtrs tsrc{}, tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
@@ -373,12 +453,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         HIPCHK(launch_dcshift_mct_fwd(tsrc, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
-    for (auto &tile : tiles)
-        for (uint32_t k = 0; k < nc; ++k) {
-            const TileComp &tc = tile.comps[k];
-            HIPCHK(run_dwt_fwd(c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off, llA, llB,
-                               tc, cp.irrev, s));
-        }
+    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, false, s));
     HIPCHK(hipEventRecord(c->ev[3], s));
     memcpy(c->h_blocks.p, eb.data(), (size_t)nblk * sizeof(EncBlock));
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(EncBlock), hipMemcpyHostToDevice, s));
@@ -562,7 +637,8 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
 
     // host Tier-2 over every tile; code-block segments -> DecBlock table
     std::vector<Tile> tiles(ntiles);
-    uint64_t arena = 0, max_tc = 0;
+    uint64_t arena = 0, llarena = 0;
+    std::vector<uint64_t> lloff(ntiles * nc);
     std::vector<DecBlock> db;
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     std::vector<uint8_t> tilebuf;
@@ -576,7 +652,8 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
             tile.comps[k].arena_off = arena;
             uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
             arena += (area + 63) & ~63ull;
-            max_tc = std::max(max_tc, area);
+            lloff[t * nc + k] = llarena;
+            llarena += ll_geom(tile.comps[k]).elems;
         }
         // tile data: single tile-part -> decode in place; else concatenate
         const uint8_t *td;
@@ -641,7 +718,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->work.ensure(arena * 4 + 256));
-    HIPCHK(c->ll.ensure((max_tc / 2 + 64) * 4 * 2 + 256));
+    HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
@@ -655,17 +732,19 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
         HIPCHK(hipMemcpyAsync(c->cs.as<uint8_t>() + len, c->h_packed.p, extra.size(), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
+    DwtPlan dplan;
+    for (auto &tile : tiles)
+        for (uint32_t k = 0; k < nc; ++k) {
+            const TileComp &tc = tile.comps[k];
+            dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
+                        c->ll.as<int32_t>() + lloff[tile.index * nc + k], cp.irrev, true);
+        }
+    HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
                             c->coef.as<int32_t>(), s));
     HIPCHK(hipEventRecord(c->ev[2], s));
-    int32_t *llA = c->ll.as<int32_t>(), *llB = llA + (max_tc / 2 + 64);
-    for (auto &tile : tiles)
-        for (uint32_t k = 0; k < nc; ++k) {
-            const TileComp &tc = tile.comps[k];
-            HIPCHK(run_dwt_inv(c->coef.as<int32_t>() + tc.arena_off, c->work.as<int32_t>() + tc.arena_off, llA, llB,
-                               tc, cp.irrev, s));
-        }
+    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
     HIPCHK(hipEventRecord(c->ev[3], s));
     PlanePtrs dst{};
     if (planes_on_device) {
@@ -744,12 +823,8 @@ extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps,
     return GRKGPU_OK;
 }
 
-static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
-                      uint32_t numres, int32_t irrev, void *stream, bool inverse) {
-    if (!buf || !scratch || x1 <= x0 || y1 <= y0 || numres < 1 || numres > 33)
-        return set_err(GRKGPU_EINVAL, "bad arguments");
-    int rc = check_device(0);
-    if (rc) return rc;
+static void dwt_stage_geom(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t numres, int32_t irrev,
+                           bool inverse, TileComp &tc) {
     CodingParams cp;
     cp.numcomps = 1;
     cp.image = {x0, y0, x1, y1};
@@ -757,15 +832,50 @@ static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, 
     cp.numres = numres;
     cp.irrev = irrev;
     generate_qcd(cp);
-    TileComp tc;
     build_tilecomp(tc, cp.image, cp, 0, !inverse);
-    uint64_t area = (uint64_t)(x1 - x0) * (y1 - y0);
-    // scratch: [0, area) = temporary full buffer, [area, 2*area) = LL ping-pong
-    int32_t *tmp = scratch, *llA = scratch + area, *llB = llA + (area / 2 + 32);
+}
+
+// scratch layout: [temporary copy of buf | LL ping-pong | job table]
+extern "C" size_t grkgpu_dwt_scratch_bytes(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t numres) {
+    if (x1 <= x0 || y1 <= y0 || numres < 1 || numres > 33) return 0;
+    TileComp tc;
+    dwt_stage_geom(x0, y0, x1, y1, numres, 0, false, tc);
+    const uint64_t area = ((uint64_t)(x1 - x0) * (y1 - y0) + 63) / 64 * 64;
+    return (size_t)(area + ll_geom(tc).elems) * 4 + 64 * sizeof(DwtJob) + 512;
+}
+
+static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
+                      uint32_t numres, int32_t irrev, void *stream, bool inverse) {
+    if (!buf || !scratch || x1 <= x0 || y1 <= y0 || numres < 1 || numres > 33)
+        return set_err(GRKGPU_EINVAL, "bad arguments");
+    int rc = check_device(0);
+    if (rc) return rc;
+    TileComp tc;
+    dwt_stage_geom(x0, y0, x1, y1, numres, irrev, inverse, tc);
+    const uint64_t area = ((uint64_t)(x1 - x0) * (y1 - y0) + 63) / 64 * 64;
+    int32_t *tmp = scratch, *ll = scratch + area;
+    DwtJob *djobs = (DwtJob *)(((uintptr_t)(ll + ll_geom(tc).elems) + 255) & ~(uintptr_t)255);
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipMemcpyAsync(tmp, buf, area * 4, hipMemcpyDeviceToDevice, s));
-    if (!inverse) { HIPCHK(run_dwt_fwd(tmp, buf, llA, llB, tc, irrev, s)); }
-    else { HIPCHK(run_dwt_inv(tmp, buf, llA, llB, tc, irrev, s)); }
+    HIPCHK(hipMemcpyAsync(tmp, buf, (uint64_t)(x1 - x0) * (y1 - y0) * 4, hipMemcpyDeviceToDevice, s));
+    DwtPlan P;
+    if (!inverse) dwt_plan_tc(P, tc, tmp, buf, ll, irrev, false);
+    else dwt_plan_tc(P, tc, buf, tmp, ll, irrev, true);
+    dwt_finalize(P, irrev);
+    std::vector<DwtJob> flat;
+    for (auto &l : P.levels) flat.insert(flat.end(), l.begin(), l.end());
+    if (!flat.empty()) {
+        HIPCHK(hipMemcpyAsync(djobs, flat.data(), flat.size() * sizeof(DwtJob), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    for (auto &cpy : P.copies) HIPCHK(hipMemcpyAsync(cpy.first, cpy.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s));
+    size_t k = 0;
+    for (size_t li = 0; li < P.levels.size(); ++li) {
+        const auto &l = P.levels[li];
+        uint32_t maxt = 0;
+        for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
+        HIPCHK(launch_dwt_jobs(djobs + k, (uint32_t)l.size(), maxt, P.th[li], irrev, inverse ? 1 : 0, s));
+        k += l.size();
+    }
     return GRKGPU_OK;
 }
 

@@ -45,12 +45,22 @@ hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const 
 hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t tw, uint32_t th, const PlanePtrs &dst,
                                   uint32_t dstride, uint32_t ncomp, const ShiftArr &shift, const ShiftArr &mn,
                                   const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s);
-hipError_t launch_dwt_fwd_level(const int32_t *src, uint32_t sstride, int32_t *ll, uint32_t llstride, int32_t *coef,
-                                uint32_t cstride, int rw, int rh, int casx, int casy, int snx, int sny, int irrev,
-                                hipStream_t s);
-hipError_t launch_dwt_inv_level(const int32_t *ll, uint32_t llstride, const int32_t *coef, uint32_t cstride,
-                                int32_t *dst, uint32_t dstride, int rw, int rh, int casx, int casy, int snx, int sny,
-                                int irrev, hipStream_t s);
+// One DWT level of one tile-component (dwt.hip).  A launch runs one level of
+// every job in a table (grid.y = job).
+struct DwtJob {
+    const int32_t *in;     // fwd: resolution samples;     inv: LL band
+    const int32_t *coef;   // inv: HL/LH/HH (Mallat)
+    int32_t *out;          // fwd: LL band output;         inv: reconstructed resolution
+    int32_t *bands;        // fwd: HL/LH/HH output (Mallat)
+    uint32_t in_stride, coef_stride, out_stride, bands_stride;  // elements
+    uint32_t in_bytes, coef_bytes, out_bytes, bands_bytes;      // buffer extents
+    int32_t rw, rh, casx, casy, snx, sny;
+    int32_t tiles_x, ntiles;
+};
+int dwt_pick_th(int irrev, uint64_t level_samples);  // window rows for a level of that many samples
+void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
+hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
+                           int inverse, hipStream_t s);
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.

@@ -2,12 +2,7 @@
 //
 //   * pointwise: DC level shift + RCT/ICT (forward), inverse RCT/ICT + DC
 //     shift + clamp (TileProcessor.cpp:1449-1518 / 1303-1432, mct/mct.cpp)
-//   * DWT: one launch per decomposition level; a 256-thread workgroup owns a
-//     64x64 tile of the resolution, stages it (+ lifting halo) in LDS, runs
-//     the vertical then horizontal (forward) / horizontal then vertical
-//     (inverse) lifting steps in LDS and scatters the four sub-bands (forward)
-//     or the reconstructed samples (inverse).  HBM traffic = one read + one
-//     write of the resolution per level (SURVEY.md 8(d) B_DWT).
+//   * DWT: see dwt.hip
 //   * T1: EBCOT encode / decode, one lane per code-block (t1_lane.h).
 //   * gather: compacts per-code-block MQ output into one contiguous buffer.
 #include <hip/hip_runtime.h>
@@ -95,214 +90,6 @@ __global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t tw, uint32_t th, Plane
         if (irrev) v = (int32_t)rintf(__int_as_float(v));
         v += shift.v[c];
         dst.p[c][di] = v < minv.v[c] ? minv.v[c] : (v > maxv.v[c] ? maxv.v[c] : v);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// DWT (one level).  Lifting on an interleaved line with whole-sample
-// symmetric extension at the resolution edge: every reference formulation
-// (dwt53.cpp:150-169, dwt97.cpp:90-123, dwt.cpp:256-363, 1392-1537) clamps
-// the neighbour index at each step, which is exactly reflection about the
-// edge sample; interior tile edges get a halo instead.
-// ---------------------------------------------------------------------------
-constexpr int DWT_T = 64;                 // output tile (resolution samples)
-constexpr int DWT_THREADS = 256;
-
-template <bool IRREV>
-struct DwtCfg {
-    static constexpr int H = IRREV ? 4 : 2;  // lifting steps = halo
-    static constexpr int W = DWT_T + 2 * H;
-    static constexpr int P = W + 1;          // padded LDS row
-};
-
-__device__ __forceinline__ int reflect(int p, int n) {
-    if (p < 0) return -p;
-    if (p > n - 1) return 2 * (n - 1) - p;
-    return p;
-}
-
-// forward lifting step on the window: targets positions with ((g ^ cas)&1) ==
-// tpar (tpar 1 = high-pass), g = window origin + local index.
-enum StepOp { FWD53_H, FWD53_L, FWD97_1, FWD97_2, FWD97_3, FWD97_4, INV53_L, INV53_H, INV97_D, INV97_G, INV97_B, INV97_A };
-
-template <int OP>
-__device__ __forceinline__ void lift_apply(int32_t &t, int32_t l, int32_t r) {
-    if constexpr (OP == FWD53_H) t -= (l + r) >> 1;
-    else if constexpr (OP == FWD53_L) t += (l + r + 2) >> 2;
-    else if constexpr (OP == FWD97_1) t -= fix_mul13(l + r, 12994);
-    else if constexpr (OP == FWD97_2) t -= fix_mul13(l + r, 434);
-    else if constexpr (OP == FWD97_3) t += fix_mul13(l + r, 7233);
-    else if constexpr (OP == FWD97_4) t += fix_mul13(l + r, 3633);
-    else if constexpr (OP == INV53_L) t -= (l + r + 2) >> 2;
-    else if constexpr (OP == INV53_H) t += (l + r) >> 1;
-    else {
-        constexpr float c = OP == INV97_D ? -0.443506852f
-                          : OP == INV97_G ? -0.882911075f
-                          : OP == INV97_B ? 0.052980118f
-                                          : 1.586134342f;
-        float ft = __int_as_float(t), fl = __int_as_float(l), fr = __int_as_float(r);
-        t = __float_as_int(__fadd_rn(ft, __fmul_rn(__fadd_rn(fl, fr), c)));
-    }
-}
-
-// Apply one lifting step along one axis of the LDS window.
-//  axis 0: vertical (lines are columns), axis 1: horizontal (lines are rows)
-template <int OP, bool IRREV>
-__device__ void lift_step(int32_t *win, int axis, int tpar, int cas, int org, int n, int nlines, int wlen) {
-    using C = DwtCfg<IRREV>;
-    const int half = (wlen + 1) / 2;
-    for (int idx = threadIdx.x; idx < nlines * half; idx += DWT_THREADS) {
-        int line = idx % nlines;
-        int k = idx / nlines;
-        // local positions with global parity tpar
-        int first = ((org ^ cas ^ tpar) & 1);  // local index of first target
-        int lp = first + 2 * k;
-        if (lp >= wlen) continue;
-        int g = org + lp;
-        if (g < 0 || g >= n) continue;
-        int gl = reflect(g - 1, n) - org, gr = reflect(g + 1, n) - org;
-        gl = gl < 0 ? 0 : (gl >= wlen ? wlen - 1 : gl);
-        gr = gr < 0 ? 0 : (gr >= wlen ? wlen - 1 : gr);
-        int32_t *base = axis == 0 ? (win + line) : (win + line * C::P);
-        int st = axis == 0 ? C::P : 1;
-        int32_t t = base[lp * st];
-        lift_apply<OP>(t, base[gl * st], base[gr * st]);
-        base[lp * st] = t;
-    }
-}
-
-template <bool IRREV>
-__device__ void scale_fwd97(int32_t *win, int axis, int cas, int org, int n, int nlines, int wlen) {
-    using C = DwtCfg<IRREV>;
-    for (int idx = threadIdx.x; idx < nlines * wlen; idx += DWT_THREADS) {
-        int line = idx % nlines, lp = idx / nlines;
-        int g = org + lp;
-        if (g < 0 || g >= n) continue;
-        int32_t *p = axis == 0 ? (win + lp * C::P + line) : (win + line * C::P + lp);
-        bool high = ((g ^ cas) & 1) != 0;
-        *p = fix_mul13(*p, high ? 5039 : 6659);
-    }
-}
-
-template <bool IRREV>
-__device__ void scale_inv97(int32_t *win, int axis, int cas, int org, int n, int nlines, int wlen) {
-    using C = DwtCfg<IRREV>;
-    for (int idx = threadIdx.x; idx < nlines * wlen; idx += DWT_THREADS) {
-        int line = idx % nlines, lp = idx / nlines;
-        int g = org + lp;
-        if (g < 0 || g >= n) continue;
-        int32_t *p = axis == 0 ? (win + lp * C::P + line) : (win + line * C::P + lp);
-        bool high = ((g ^ cas) & 1) != 0;
-        *p = __float_as_int(__fmul_rn(__int_as_float(*p), high ? 1.625732422f : 1.230174105f));
-    }
-}
-
-// single-sample lines (dwt53.cpp:161, dwt.cpp:341)
-template <bool IRREV, bool INV>
-__device__ void single_sample(int32_t *win, int axis, int cas, int nlines, int wlen) {
-    using C = DwtCfg<IRREV>;
-    if (IRREV || !cas) return;
-    for (int idx = threadIdx.x; idx < nlines * wlen; idx += DWT_THREADS) {
-        int line = idx % nlines, lp = idx / nlines;
-        int32_t *p = axis == 0 ? (win + lp * C::P + line) : (win + line * C::P + lp);
-        *p = INV ? (*p / 2) : (int32_t)((uint32_t)*p << 1);
-    }
-}
-
-template <bool IRREV>
-__device__ void lift_fwd_axis(int32_t *win, int axis, int cas, int org, int n, int nlines, int wlen) {
-    if (n == 1) { single_sample<IRREV, false>(win, axis, cas, nlines, wlen); __syncthreads(); return; }
-    if constexpr (!IRREV) {
-        lift_step<FWD53_H, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<FWD53_L, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-    } else {
-        lift_step<FWD97_1, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<FWD97_2, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<FWD97_3, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<FWD97_4, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-        scale_fwd97<IRREV>(win, axis, cas, org, n, nlines, wlen); __syncthreads();
-    }
-}
-
-template <bool IRREV>
-__device__ void lift_inv_axis(int32_t *win, int axis, int cas, int org, int n, int nlines, int wlen) {
-    if (n == 1) { single_sample<IRREV, true>(win, axis, cas, nlines, wlen); __syncthreads(); return; }
-    if constexpr (!IRREV) {
-        lift_step<INV53_L, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<INV53_H, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-    } else {
-        scale_inv97<IRREV>(win, axis, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<INV97_D, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<INV97_G, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<INV97_B, IRREV>(win, axis, 0, cas, org, n, nlines, wlen); __syncthreads();
-        lift_step<INV97_A, IRREV>(win, axis, 1, cas, org, n, nlines, wlen); __syncthreads();
-    }
-}
-
-// Forward level: src (rw x rh, stride sstride) -> LL into ll (stride llstride),
-// HL/LH/HH into coef (Mallat positions, stride cstride).
-template <bool IRREV>
-__global__ __launch_bounds__(DWT_THREADS) void k_dwt_fwd_level(const int32_t *__restrict__ src, uint32_t sstride,
-                                                               int32_t *__restrict__ ll, uint32_t llstride,
-                                                               int32_t *__restrict__ coef, uint32_t cstride,
-                                                               int rw, int rh, int casx, int casy, int snx, int sny) {
-    using C = DwtCfg<IRREV>;
-    __shared__ int32_t win[C::W * C::P];
-    const int ox = blockIdx.x * DWT_T - C::H, oy = blockIdx.y * DWT_T - C::H;  // window origin
-    const int wx = min(C::W, rw - ox), wy = min(C::W, rh - oy);
-    for (int i = threadIdx.x; i < C::W * C::W; i += DWT_THREADS) {
-        int ly = i / C::W, lx = i % C::W;
-        int gx = ox + lx, gy = oy + ly;
-        if (gx >= 0 && gy >= 0 && gx < rw && gy < rh) win[ly * C::P + lx] = src[(size_t)gy * sstride + gx];
-    }
-    __syncthreads();
-    lift_fwd_axis<IRREV>(win, 0, casy, oy, rh, wx, wy);
-    lift_fwd_axis<IRREV>(win, 1, casx, ox, rw, wy, wx);
-    for (int i = threadIdx.x; i < DWT_T * DWT_T; i += DWT_THREADS) {
-        int ly = C::H + i / DWT_T, lx = C::H + i % DWT_T;
-        int gx = ox + lx, gy = oy + ly;
-        if (gx >= rw || gy >= rh) continue;
-        int32_t v = win[ly * C::P + lx];
-        bool hx = ((gx ^ casx) & 1) != 0, hy = ((gy ^ casy) & 1) != 0;
-        int ix = hx ? (gx - (1 - casx)) >> 1 : (gx - casx) >> 1;
-        int iy = hy ? (gy - (1 - casy)) >> 1 : (gy - casy) >> 1;
-        if (!hx && !hy) ll[(size_t)iy * llstride + ix] = v;
-        else coef[(size_t)(iy + (hy ? sny : 0)) * cstride + ix + (hx ? snx : 0)] = v;
-    }
-}
-
-// Inverse level: LL from ll (stride llstride) + HL/LH/HH from coef ->
-// reconstructed resolution into dst (stride dstride).
-template <bool IRREV>
-__global__ __launch_bounds__(DWT_THREADS) void k_dwt_inv_level(const int32_t *__restrict__ ll, uint32_t llstride,
-                                                               const int32_t *__restrict__ coef, uint32_t cstride,
-                                                               int32_t *__restrict__ dst, uint32_t dstride,
-                                                               int rw, int rh, int casx, int casy, int snx, int sny) {
-    using C = DwtCfg<IRREV>;
-    __shared__ int32_t win[C::W * C::P];
-    const int ox = blockIdx.x * DWT_T - C::H, oy = blockIdx.y * DWT_T - C::H;
-    const int wx = min(C::W, rw - ox), wy = min(C::W, rh - oy);
-    for (int i = threadIdx.x; i < C::W * C::W; i += DWT_THREADS) {
-        int ly = i / C::W, lx = i % C::W;
-        int gx = ox + lx, gy = oy + ly;
-        if (gx < 0 || gy < 0 || gx >= rw || gy >= rh) continue;
-        bool hx = ((gx ^ casx) & 1) != 0, hy = ((gy ^ casy) & 1) != 0;
-        int ix = hx ? (gx - (1 - casx)) >> 1 : (gx - casx) >> 1;
-        int iy = hy ? (gy - (1 - casy)) >> 1 : (gy - casy) >> 1;
-        int32_t v;
-        if (!hx && !hy) v = ll[(size_t)iy * llstride + ix];
-        else v = coef[(size_t)(iy + (hy ? sny : 0)) * cstride + ix + (hx ? snx : 0)];
-        win[ly * C::P + lx] = v;
-    }
-    __syncthreads();
-    // decode order: horizontal then vertical (dwt.cpp:1560-1738, :724-858)
-    lift_inv_axis<IRREV>(win, 1, casx, ox, rw, wy, wx);
-    lift_inv_axis<IRREV>(win, 0, casy, oy, rh, wx, wy);
-    for (int i = threadIdx.x; i < DWT_T * DWT_T; i += DWT_THREADS) {
-        int ly = C::H + i / DWT_T, lx = C::H + i % DWT_T;
-        int gx = ox + lx, gy = oy + ly;
-        if (gx >= rw || gy >= rh) continue;
-        dst[(size_t)gy * dstride + gx] = win[ly * C::P + lx];
     }
 }
 
@@ -563,32 +350,6 @@ hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t tw, uint32_t th
     dim3 grid((tw + 255) / 256, th);
     hipLaunchKernelGGL(k_mct_inv_dcshift, grid, dim3(256), 0, s, src, tw, th, dst, dstride, ncomp, shift, mn, mx,
                        mct, irrev);
-    return hipGetLastError();
-}
-
-hipError_t launch_dwt_fwd_level(const int32_t *src, uint32_t sstride, int32_t *ll, uint32_t llstride, int32_t *coef,
-                                uint32_t cstride, int rw, int rh, int casx, int casy, int snx, int sny, int irrev,
-                                hipStream_t s) {
-    dim3 grid((rw + DWT_T - 1) / DWT_T, (rh + DWT_T - 1) / DWT_T);
-    if (irrev)
-        hipLaunchKernelGGL(k_dwt_fwd_level<true>, grid, dim3(DWT_THREADS), 0, s, src, sstride, ll, llstride, coef,
-                           cstride, rw, rh, casx, casy, snx, sny);
-    else
-        hipLaunchKernelGGL(k_dwt_fwd_level<false>, grid, dim3(DWT_THREADS), 0, s, src, sstride, ll, llstride, coef,
-                           cstride, rw, rh, casx, casy, snx, sny);
-    return hipGetLastError();
-}
-
-hipError_t launch_dwt_inv_level(const int32_t *ll, uint32_t llstride, const int32_t *coef, uint32_t cstride,
-                                int32_t *dst, uint32_t dstride, int rw, int rh, int casx, int casy, int snx, int sny,
-                                int irrev, hipStream_t s) {
-    dim3 grid((rw + DWT_T - 1) / DWT_T, (rh + DWT_T - 1) / DWT_T);
-    if (irrev)
-        hipLaunchKernelGGL(k_dwt_inv_level<true>, grid, dim3(DWT_THREADS), 0, s, ll, llstride, coef, cstride, dst,
-                           dstride, rw, rh, casx, casy, snx, sny);
-    else
-        hipLaunchKernelGGL(k_dwt_inv_level<false>, grid, dim3(DWT_THREADS), 0, s, ll, llstride, coef, cstride, dst,
-                           dstride, rw, rh, casx, casy, snx, sny);
     return hipGetLastError();
 }
 

@@ -129,8 +129,9 @@ int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps, uint32_t w
                            int32_t irreversible, void *stream);
 /* In-place (Mallat layout) forward / inverse DWT of one tile-component with
  * origin (x0,y0), size (x1-x0) x (y1-y0), row stride x1-x0.  scratch must
- * hold 2 * (x1-x0) * (y1-y0) + 256 int32 (device).  For 9/7 inverse the buffer holds
- * float bit patterns. */
+ * hold grkgpu_dwt_scratch_bytes(...) device bytes.  For 9/7 inverse the buffer
+ * holds float bit patterns. */
+size_t grkgpu_dwt_scratch_bytes(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t numres);
 int grkgpu_dwt_fwd(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
                    uint32_t numres, int32_t irreversible, void *stream);
 int grkgpu_dwt_inv(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,

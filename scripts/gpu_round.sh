@@ -11,5 +11,5 @@ tail -3 $OUT/pytest_gpu.txt
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 > $OUT/bench_prof.json 2> $OUT/prof.err || { echo "rocprof failed"; tail -30 $OUT/prof.err; exit 1; }
-find $OUT/prof -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv
-head -30 $OUT/kernel_stats.csv
+python3 scripts/prof_summary.py $OUT/prof $OUT/kernel_stats.csv > /dev/null
+head -14 $OUT/kernel_stats.csv

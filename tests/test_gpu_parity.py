@@ -64,7 +64,9 @@ def test_device_resident_roundtrip(codec):
 
 @pytest.mark.parametrize("irrev", [False, True])
 @pytest.mark.parametrize("shape_off", [((64, 64), (0, 0)), ((77, 100), (3, 5)), ((1, 37), (0, 1)),
-                                       ((45, 1), (1, 0)), ((129, 200), (1, 1)), ((513, 257), (0, 3))])
+                                       ((45, 1), (1, 0)), ((129, 200), (1, 1)), ((513, 257), (0, 3)),
+                                       ((2, 3), (1, 1)), ((3, 130), (1, 0)), ((4, 5), (0, 1)), ((250, 121), (0, 0)),
+                                       ((37, 260), (1, 1)), ((300, 497), (2, 2))])
 @pytest.mark.parametrize("numres", [1, 2, 6, 9])
 def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
     import torch
