@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--concurrency", type=int, default=4, help="frames in flight per GPU: 1, 2 (one 9/7 + one 5/3) or 4 (two of each)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -63,23 +64,52 @@ def main():
 
     img = synth.synth_image(H, W, C, BITS, 3 + rank)
     frame = torch.from_numpy(img).to("cuda:%d" % local)
-    codec = grk.Codec(local)
+    # two codec contexts (each with its own HIP stream and host thread): the
+    # 9/7 and the 5/3 frame of a step are coded concurrently, so the T1
+    # kernels of one overlap the other's (T1 is latency-bound and leaves most
+    # SIMD issue slots free) and host Tier-2 overlaps device work.
+    ncodec = max(1, args.concurrency)
+    assert ncodec in (1, 2, 4), "--concurrency must be 1, 2 or 4"
+    codecs = [grk.Codec(local) for _ in range(ncodec)]
     p97 = grk.CParams.make(irreversible=True)
     p53 = grk.CParams.make(irreversible=False)
-    out97 = torch.empty_like(frame)
-    out53 = torch.empty_like(frame)
+    npairs = 2 if ncodec == 4 else 1          # (9/7 frame, 5/3 frame) pairs per step
+    outs = [(torch.empty_like(frame), torch.empty_like(frame)) for _ in range(npairs)]
+    out97, out53 = outs[0]
     st = {}
 
+    # one torch stream per codec (the codec runs on the caller's current
+    # stream, which torch keeps per host thread)
+    streams = [torch.cuda.Stream(device=local) for _ in range(ncodec)]
+    torch.cuda.synchronize()
+
+    def pipe(codec, p, out, tag):
+        with torch.cuda.stream(streams[codecs.index(codec)]):
+            b = codec.compress(frame, BITS, p, view=True)
+            st["enc" + tag] = codec.stats()
+            n = len(b)
+            codec.decompress(b, out=out)
+            st["dec" + tag] = codec.stats()
+            st["bytes" + tag] = n
+
+    pool = None
+
+    if ncodec > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=ncodec)
+
     def step():
-        b97 = codec.compress(frame, BITS, p97, view=True)
-        st["enc97"] = codec.stats()
-        codec.decompress(b97, out=out97)
-        st["dec97"] = codec.stats()
-        b53 = codec.compress(frame, BITS, p53, view=True)
-        st["enc53"] = codec.stats()
-        codec.decompress(b53, out=out53)
-        st["dec53"] = codec.stats()
-        st["bytes"] = (len(b97), len(b53))
+        if pool is None:
+            pipe(codecs[0], p97, out97, "97")
+            pipe(codecs[0], p53, out53, "53")
+        else:
+            f = []
+            for i in range(npairs):
+                f.append(pool.submit(pipe, codecs[2 * i], p97, outs[i][0], "97"))
+                f.append(pool.submit(pipe, codecs[2 * i + 1], p53, outs[i][1], "53"))
+            for x in f:
+                x.result()
+        st["bytes"] = (st["bytes97"], st["bytes53"])
 
     for _ in range(args.warmup):
         step()
@@ -101,7 +131,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    pix_per_step = 2 * H * W  # one frame through 9/7 + one through 5/3
+    pix_per_step = 2 * npairs * H * W  # npairs x (one frame through 9/7 + one through 5/3)
     value = world * pix_per_step * args.steps / elapsed / 1e6
     ms_per_step = 1e3 * elapsed / args.steps
 
@@ -110,9 +140,18 @@ def main():
     # time around those launches on the codec's stream (= per-launch bytes /
     # mean launch duration).  traffic: HBM bytes per launch from the committed
     # rocprofv3 PMC summary (scripts/pmc_bench.sh), when present.
+    # measured in isolation after the timed region (the timed region overlaps
+    # frames, so kernel durations there include contention): 3 x 9/7 encodes
+    # on one context, nothing else in flight, min of the HIP-event DWT times.
     bdwt = dwt_bytes(H, W, C)
     nlaunch = 5
-    dwt_ms = st["enc97"]["dwt_ms"]
+    torch.cuda.synchronize()
+    iso = []
+    with torch.cuda.stream(streams[0]):
+        for _ in range(3):
+            codecs[0].compress(frame, BITS, p97, view=True)
+            iso.append(codecs[0].stats()["dwt_ms"])
+    dwt_ms = min(iso)
     achieved = bdwt / (dwt_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
@@ -124,7 +163,8 @@ def main():
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": bdwt // nlaunch, "launches": nlaunch,
-                "kernel_ms_per_launch": round(dwt_ms / nlaunch, 4)}
+                "kernel_ms_per_launch": round(dwt_ms / nlaunch, 4),
+                "measured": "HIP events on the codec stream, 9/7 encode run alone after the timed region"}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -137,7 +177,7 @@ def main():
         b = pyoracle.encode(img, BITS, pyoracle.params(irreversible=False, nthreads=ncpu))
         pyoracle.decode(b, nthreads=ncpu)
         ct = time.perf_counter() - t0
-        cpu = {"value": round(pix_per_step / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "port",
+        cpu = {"value": round(2 * H * W / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "port",
                "sample": "1 step (8K 12-bit RGB frame: 9/7 enc+dec + 5/3 enc+dec) through the C oracle "
                          "(oracle/grk_oracle.c, byte-identical to Grok 5.1.0), %d threads" % ncpu,
                "seconds": round(ct, 2)}
@@ -153,14 +193,16 @@ def main():
             "data": "synthetic (tests/golden/synth.py smooth+2% noise, seed 3+rank)",
             "config": {"workload": "8K 7680x4320 12-bit RGB frame per GPU; 9/7 (-I) + 5/3 lossless, enc+dec; "
                                    "6 resolutions, 64x64 code-blocks, 1 layer LRCP",
-                       "frames_per_step_per_gpu": 2, "parallelism": "frame-batch x%d (no collectives)" % world},
+                       "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
+                       "parallelism": "frame-batch x%d (no collectives)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "codestream_bytes": {"9/7": st["bytes"][0], "5/3": st["bytes"][1]},
             "stage_ms": {k: r(st[k]) for k in ("enc97", "dec97", "enc53", "dec53")},
         }
         print(json.dumps(line), flush=True)
-    codec.close()
+    for c in codecs:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -78,7 +78,7 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf;
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
@@ -720,6 +720,15 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
+    // v4 decoder: per-block unstuffed-stream regions (16-byte units in pad)
+    const bool flat = t1_dec_flat_enabled();
+    uint64_t uwords = 0;
+    for (auto &d : db) {
+        d.pad = (uint32_t)(uwords / 4);
+        if (flat) uwords += t1_unstuff_region_words(d.len);
+    }
+    if (uwords / 4 > 0xffffffffull) return set_err(GRKGPU_EUNSUPPORTED, "codestream too large for one call");
+    if (flat) HIPCHK(c->ubuf.ensure(uwords * 4 + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     memcpy(c->h_blocks.p, db.data(), (size_t)nblk * sizeof(DecBlock));
@@ -742,7 +751,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
-                            c->coef.as<int32_t>(), s));
+                            c->coef.as<int32_t>(), s, flat ? c->ubuf.as<uint32_t>() : nullptr));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
     HIPCHK(hipEventRecord(c->ev[3], s));

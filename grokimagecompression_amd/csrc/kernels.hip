@@ -9,7 +9,7 @@
 #include <stdint.h>
 
 #include "grk_device.h"
-#include "t1_dec.h"
+#include "t1_flat.h"
 #include <stdlib.h>
 #include <string.h>
 
@@ -194,8 +194,8 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
 }
 
 // MQ coding, one lane per block.
-template <int LANES>
-__global__ __launch_bounds__(LANES) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
+template <int LANES, int MINW = 1>
+__global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
                                                  const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
                                                  EncResult *__restrict__ res) {
@@ -257,8 +257,8 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_lane(const DecBlock *__rest
                    s_cx + threadIdx.x * 21, S.pa, S.pb);
 }
 
-template <int LANES>
-__global__ __launch_bounds__(LANES) void k_t1_decode_v3(const DecBlock *__restrict__ blocks, uint32_t n,
+template <int LANES, int MINW = 1>
+__global__ __launch_bounds__(LANES, MINW) void k_t1_decode_v3(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint8_t *__restrict__ data,
                                                         T1Scratch *__restrict__ scr) {
     __shared__ uint8_t s_zc[2048];
@@ -277,6 +277,68 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_v3(const DecBlock *__restri
     T1Scratch &S = scr[i];
     t1_decode_v3(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, S.st, T, s_cx + threadIdx.x * 21, S.pa,
                  S.pb);
+}
+
+// Decoder v4 (t1_flat.h).  Pass 1, lane per block: remove the MQ byte
+// stuffing into a plain bit stream + carry events (region at blocks[i].pad *
+// 16 bytes: header {nwords, ncarry}, words, carries).  Pass 2, lane per block:
+// one MQ decision per loop iteration.
+__global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                   const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    uint32_t *region = ubuf + (size_t)b.pad * 4;
+    uint32_t *words = region + 4, *carries = words + unstuff_word_cap(b.len);
+    const uintptr_t pa = (uintptr_t)(data + b.data_off);
+    const uint4 *src = (const uint4 *)(pa & ~(uintptr_t)15);
+    const uint32_t skip = (uint32_t)(pa & 15), end = skip + b.len;
+    const uint32_t nch = (end + 15) >> 4;
+    Unstuff u;
+    uint32_t nw = 0, nc = 0;
+    uint4 nxt = src[0];
+    for (uint32_t ch = 0; ch < nch; ++ch) {
+        const uint4 cur = nxt;
+        if (ch + 1 < nch) nxt = src[ch + 1];
+        const uint32_t wv4[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t pos = ch * 16 + j;
+            if (pos < skip || pos >= end) continue;
+            uint32_t wv, cv;
+            if (u.push((wv4[j >> 2] >> (8 * (j & 3))) & 0xffu, &wv, &cv)) words[nw++] = wv;
+            if (cv != 0xffffffffu) carries[nc++] = cv;
+        }
+    }
+    words[nw++] = u.tail();
+    words[nw++] = 0xffffffffu;
+    carries[nc] = 0xffffffffu;
+    region[0] = nw;
+    region[1] = nc;
+}
+
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_decode_flat(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                          const uint32_t *__restrict__ ubuf,
+                                                          T1Scratch *__restrict__ scr) {
+    __shared__ uint8_t s_zc[2048];
+    __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_cx[LANES * 21];
+    for (uint32_t k = threadIdx.x; k < 2048; k += LANES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
+    for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
+    T1Scratch &S = scr[i];
+    const uint32_t *region = ubuf + (size_t)b.pad * 4;
+    t1_decode_flat(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, S.st,
+                   T, s_cx + threadIdx.x * 21, S.pa, S.pb);
 }
 
 // One workgroup per block, lane = column: values from the bit-plane rows
@@ -357,7 +419,7 @@ static int t1_mq_lanes() {
     static int lanes = [] {
         const char *e = getenv("GRKGPU_MQ_LANES");
         int v = e ? atoi(e) : 32;
-        return (v == 16 || v == 32 || v == 64) ? v : 32;
+        return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 32;
     }();
     return lanes;
 }
@@ -366,7 +428,7 @@ static int t1_lanes() {
     static int lanes = [] {
         const char *e = getenv("GRKGPU_T1_LANES");
         int v = e ? atoi(e) : 16;
-        return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
+        return (v == 4 || v == 8 || v == 16 || v == 32) ? v : 16;
     }();
     return lanes;
 }
@@ -377,19 +439,49 @@ static void launch_enc_lane(const EncBlock *blocks, uint32_t n, T1Scratch *scr, 
     hipLaunchKernelGGL(k_t1_encode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, scr, out, res);
 }
 
+static int t1_minw() {
+    static int v = [] {
+        const char *e = getenv("GRKGPU_T1_MINW");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 template <int L>
 static void launch_dec_lane(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scr, hipStream_t s) {
     static const bool v2 = getenv("GRKGPU_T1_DEC") && !strcmp(getenv("GRKGPU_T1_DEC"), "v2");
-    if (v2)
-        hipLaunchKernelGGL(k_t1_decode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
-    else
-        hipLaunchKernelGGL(k_t1_decode_v3<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, data, scr);
+    const dim3 g((n + L - 1) / L);
+    if (v2) { hipLaunchKernelGGL(k_t1_decode_lane<L>, g, dim3(L), 0, s, blocks, n, data, scr); return; }
+    switch (t1_minw()) {
+        case 2: hipLaunchKernelGGL((k_t1_decode_v3<L, 2>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        case 3: hipLaunchKernelGGL((k_t1_decode_v3<L, 3>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        case 4: hipLaunchKernelGGL((k_t1_decode_v3<L, 4>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        case 5: hipLaunchKernelGGL((k_t1_decode_v3<L, 5>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        case 6: hipLaunchKernelGGL((k_t1_decode_v3<L, 6>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        case 8: hipLaunchKernelGGL((k_t1_decode_v3<L, 8>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+        default: hipLaunchKernelGGL((k_t1_decode_v3<L, 1>), g, dim3(L), 0, s, blocks, n, data, scr); break;
+    }
+}
+
+static int mq_minw() {
+    static int v = [] {
+        const char *e = getenv("GRKGPU_MQ_MINW");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
 }
 
 template <int L>
 static void launch_mq(const EncBlock *blocks, uint32_t n, const T1Scratch *scr, const uint8_t *sym,
                       const uint64_t *sym_off, uint8_t *out, EncResult *res, hipStream_t s) {
-    hipLaunchKernelGGL(k_t1_mq<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res);
+    const dim3 g((n + L - 1) / L);
+    switch (mq_minw()) {
+        case 2: hipLaunchKernelGGL((k_t1_mq<L, 2>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+        case 4: hipLaunchKernelGGL((k_t1_mq<L, 4>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+        case 6: hipLaunchKernelGGL((k_t1_mq<L, 6>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+        case 8: hipLaunchKernelGGL((k_t1_mq<L, 8>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+        default: hipLaunchKernelGGL((k_t1_mq<L, 1>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+    }
 }
 
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
@@ -412,6 +504,8 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res);
     switch (t1_mq_lanes()) {
+        case 4: launch_mq<4>(blocks, n, scratch, sym, sym_off, out, res, s); break;
+        case 8: launch_mq<8>(blocks, n, scratch, sym, sym_off, out, res, s); break;
         case 16: launch_mq<16>(blocks, n, scratch, sym, sym_off, out, res, s); break;
         case 64: launch_mq<64>(blocks, n, scratch, sym, sym_off, out, res, s); break;
         default: launch_mq<32>(blocks, n, scratch, sym, sym_off, out, res, s); break;
@@ -419,14 +513,45 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     return hipGetLastError();
 }
 
+// v4 (flat) decoder: correct, but measured 2.2x slower than v3 on the 8K
+// frame (more VALU/SALU per decision); kept behind GRKGPU_T1_DEC=v4.
+bool t1_dec_flat_enabled() {
+    static const bool on = getenv("GRKGPU_T1_DEC") && !strcmp(getenv("GRKGPU_T1_DEC"), "v4");
+    return on;
+}
+
+static int t1_dec_lanes() {
+    static int lanes = [] {
+        const char *e = getenv("GRKGPU_T1_DEC_LANES");
+        int v = e ? atoi(e) : 16;
+        return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
+    }();
+    return lanes;
+}
+
+template <int L>
+static void launch_dec_flat(const DecBlock *blocks, uint32_t n, const uint32_t *ubuf, T1Scratch *scr, hipStream_t s) {
+    hipLaunchKernelGGL(k_t1_decode_flat<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
+}
+
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
-                            int32_t *tiles, hipStream_t s) {
+                            int32_t *tiles, hipStream_t s, uint32_t *ubuf) {
     if (!n) return hipSuccess;
-    switch (t1_lanes()) {
-        case 8: launch_dec_lane<8>(blocks, n, data, scratch, s); break;
-        case 32: launch_dec_lane<32>(blocks, n, data, scratch, s); break;
-        case 64: launch_dec_lane<64>(blocks, n, data, scratch, s); break;
-        default: launch_dec_lane<16>(blocks, n, data, scratch, s); break;
+    if (ubuf && t1_dec_flat_enabled()) {
+        hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf);
+        switch (t1_dec_lanes()) {
+            case 8: launch_dec_flat<8>(blocks, n, ubuf, scratch, s); break;
+            case 32: launch_dec_flat<32>(blocks, n, ubuf, scratch, s); break;
+            case 64: launch_dec_flat<64>(blocks, n, ubuf, scratch, s); break;
+            default: launch_dec_flat<16>(blocks, n, ubuf, scratch, s); break;
+        }
+    } else {
+        switch (t1_lanes()) {
+            case 4: launch_dec_lane<4>(blocks, n, data, scratch, s); break;
+            case 8: launch_dec_lane<8>(blocks, n, data, scratch, s); break;
+            case 32: launch_dec_lane<32>(blocks, n, data, scratch, s); break;
+            default: launch_dec_lane<16>(blocks, n, data, scratch, s); break;
+        }
     }
     hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
     return hipGetLastError();

@@ -112,6 +112,9 @@ GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t 
     }
     d.a = a;
     if (!keep) cxw[cx] = tw | (nmps << 31);
+#ifdef T1_TRACE
+    T1_TRACE(cx, mps ^ (uint32_t)lps, d.a, d.c >> 16);
+#endif
     return mps ^ (uint32_t)lps;
 }
 

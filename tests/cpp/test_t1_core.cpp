@@ -6,7 +6,7 @@
 #include <string.h>
 #include <vector>
 #include <algorithm>
-#include "../../grokimagecompression_amd/csrc/t1_dec.h"
+#include "../../grokimagecompression_amd/csrc/t1_flat.h"
 #include "../../oracle/grk_oracle.h"
 
 using namespace grkgpu;
@@ -136,6 +136,28 @@ int main(int argc, char **argv) {
                     for (uint32_t x = 0; x < w; ++x) vd[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
                 if (od != vd) {
                     printf("V3 DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u orient=%u\n", it, w, h, np, onb, orient);
+                    fails++;
+                }
+            }
+            // decoder v4 (t1_flat.h): unstuffed bit stream, one decision per step
+            {
+                const DecTables DT{zc + orient * 512, scw, kTab};
+                uint32_t cx4[32];
+                std::vector<uint32_t> words(unstuff_word_cap(len) + 8, 0), carr(unstuff_carry_cap(len), 0);
+                uint32_t *wp = (uint32_t *)(((uintptr_t)words.data() + 15) & ~(uintptr_t)15);
+                uint32_t ncar = 0;
+                uint32_t nw = t1_unstuff(lp, len, wp, carr.data(), &ncar);
+                std::fill(scr.pa, scr.pa + 32 * 64, ~0ull);
+                std::fill(scr.pb, scr.pb + 32 * 64, ~0ull);
+                for (int i = 0; i < 66; ++i) { scr.st.sig[i] = scr.st.neg[i] = scr.st.vis[i] = scr.st.ref[i] = ~0ull; }
+                t1_decode_flat(wp, nw, carr.data(), np, onb, w, h, scr.st, DT, cx4, scr.pa, scr.pb);
+                std::vector<int32_t> fd(w * h);
+                for (uint32_t y = 0; y < h; ++y)
+                    for (uint32_t x = 0; x < w; ++x) fd[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
+                if (od != fd) {
+                    int bad = 0;
+                    for (uint32_t i = 0; i < w * h; ++i) bad += od[i] != fd[i];
+                    printf("V4 DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u orient=%u bad=%d\n", it, w, h, np, onb, orient, bad);
                     fails++;
                 }
             }
