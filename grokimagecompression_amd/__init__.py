@@ -130,6 +130,10 @@ def lib():
         L.grkgpu_read_header.argtypes = [VP, ctypes.c_size_t, P(ImageDesc)]
         L.grkgpu_decompress.argtypes = [VP, VP, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_free.argtypes = [VP]
+        L.grkgpu_num_tiles.argtypes = [P(ImageDesc), P(CParams), P(U32)]
+        L.grkgpu_compress_tiles.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32,
+                                            P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
+        L.grkgpu_decompress_tiles.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, P(VP), ctypes.c_int]
         L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
         L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
@@ -161,6 +165,23 @@ def _buf_ptr(buf):
         buf = bytes(buf)
     cp = ctypes.c_char_p(buf)
     return ctypes.cast(cp, ctypes.c_void_p), len(buf), (cp, buf)
+
+
+PART_TILES, PART_HEADER, PART_EOC, PART_ALL = 0, 1, 2, 3
+
+
+def num_tiles(shape, prec, params, offset=(0, 0)):
+    """Tile count of a (c,h,w) image under `params` (grkgpu_num_tiles)."""
+    c, h, w = shape
+    d = ImageDesc()
+    d.x0, d.y0 = offset
+    d.x1, d.y1 = offset[0] + w, offset[1] + h
+    d.numcomps = c
+    for k in range(c):
+        d.prec[k] = prec
+    n = ctypes.c_uint32()
+    _check(lib().grkgpu_num_tiles(ctypes.byref(d), ctypes.byref(params), ctypes.byref(n)))
+    return n.value
 
 
 def read_header(buf):
@@ -204,12 +225,7 @@ class Codec:
         _check(lib().grkgpu_get_stats(self._ctx, ctypes.byref(s)))
         return s.as_dict()
 
-    def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False, view=False):
-        """img: (c,h,w) int32 numpy array (host) or torch tensor on cuda:<device>.
-        Returns the .j2k codestream as bytes, or (view=True) as a zero-copy numpy
-        uint8 view of the context's pinned output buffer, valid until the next
-        call on this Codec."""
-        params = params or CParams.make()
+    def _image(self, img, prec, offset, sgnd):
         c, h, w = img.shape
         d = ImageDesc()
         d.x0, d.y0 = offset
@@ -227,6 +243,15 @@ class Codec:
         else:
             img = np.ascontiguousarray(img, dtype=np.int32)
             ptrs = (ctypes.c_void_p * c)(*[img[k].ctypes.data for k in range(c)])
+        return d, ptrs, on_dev, img
+
+    def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False, view=False):
+        """img: (c,h,w) int32 numpy array (host) or torch tensor on cuda:<device>.
+        Returns the .j2k codestream as bytes, or (view=True) as a zero-copy numpy
+        uint8 view of the context's pinned output buffer, valid until the next
+        call on this Codec."""
+        params = params or CParams.make()
+        d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
         if view:
@@ -238,6 +263,34 @@ class Codec:
         b = ctypes.string_at(out, n.value)
         lib().grkgpu_free(out)
         return b
+
+    def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False):
+        """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
+        (plus the main header / EOC when `parts` asks for them) as bytes."""
+        d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _check(lib().grkgpu_compress_tiles(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs,
+                                           1 if on_dev else 0, tile_begin, tile_end, parts, ctypes.byref(out),
+                                           ctypes.byref(n)))
+        b = ctypes.string_at(out, n.value)
+        lib().grkgpu_free(out)
+        return b
+
+    def decompress_tiles(self, buf, tile_begin, tile_end, out):
+        """Decode tiles [tile_begin, tile_end) of a codestream into `out`
+        ((c,h,w) int32 numpy array or cuda tensor); other tiles untouched."""
+        c = out.shape[0]
+        on_dev = not isinstance(out, np.ndarray)
+        if on_dev:
+            lib().grkgpu_set_stream(self._ctx, _stream_handle(out.device))
+            ptrs = (ctypes.c_void_p * c)(*[out[k].data_ptr() for k in range(c)])
+        else:
+            assert out.dtype == np.int32 and out.flags.c_contiguous
+            ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
+        bp, bn, keep = _buf_ptr(buf)
+        _check(lib().grkgpu_decompress_tiles(self._ctx, bp, bn, tile_begin, tile_end, ptrs, 1 if on_dev else 0))
+        return out
 
     def decompress(self, buf, device_out=False, out=None):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when

@@ -347,20 +347,28 @@ static void for_each_cblk(TileComp &tc, F f) {
 // ---------------------------------------------------------------------------
 // encode
 // ---------------------------------------------------------------------------
+// Encode tiles [tb, te) (a tile shard: j2k_encode's per-tile loop,
+// j2k.cpp:2088-2111) and emit [main header][their tile-parts][EOC] per `parts`.
 static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
-                         const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen) {
+                         const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen,
+                         uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
     if (rc) return rc;
+    {
+        const uint32_t nt = cp.tw * cp.th;
+        if (te > nt) te = nt;
+        if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
+    }
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     double t_start = now_ms();
     const uint32_t nc = cp.numcomps, iw = cp.image.w(), ih = cp.image.h();
     const uint64_t plane = (uint64_t)iw * ih;
 
-    // geometry for every tile, arena offsets, block table
-    const uint32_t ntiles = cp.tw * cp.th;
+    // geometry for every tile of the shard, arena offsets, block table
+    const uint32_t ntiles = te - tb;
     std::vector<Tile> tiles(ntiles);
     uint64_t arena = 0, llarena = 0;
     std::vector<uint64_t> lloff(ntiles * nc);
@@ -370,8 +378,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     uint32_t maxdepth = 1;
     for (uint32_t t = 0; t < ntiles; ++t) {
         Tile &tile = tiles[t];
-        tile.index = t;
-        tile.r = tile_rect(cp, t);
+        tile.index = tb + t;
+        tile.r = tile_rect(cp, tile.index);
         tile.comps.resize(nc);
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
@@ -441,7 +449,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
-                        c->ll.as<int32_t>() + lloff[tile.index * nc + k], cp.irrev, false);
+                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, false);
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
@@ -488,8 +496,10 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     hdr.v.reserve(1 << 20);
     std::vector<PlanItem> plan;
     plan.reserve(nblk + 64);
-    write_main_header(hdr, cp);
-    plan.push_back({0, (uint32_t)hdr.size(), 0});
+    if (parts & GRKGPU_PART_HEADER) {
+        write_main_header(hdr, cp);
+        plan.push_back({0, (uint32_t)hdr.size(), 0});
+    }
     for (auto &tile : tiles) {
         size_t sot = hdr.size();
         hdr.put16(0xFF90); hdr.put16(10); hdr.put16(tile.index); hdr.put32(0); hdr.put8(0); hdr.put8(1);
@@ -506,9 +516,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         for (size_t i = first; i < plan.size(); ++i) psot += plan[i].len;
         hdr.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
     }
-    size_t eoc = hdr.size();
-    hdr.put16(0xFFD9);
-    plan.push_back({eoc, 2, 0});
+    if (parts & GRKGPU_PART_EOC) {
+        size_t eoc = hdr.size();
+        hdr.put16(0xFFD9);
+        plan.push_back({eoc, 2, 0});
+    }
     // gather list: dst offsets = prefix sum of run lengths
     std::vector<GatherItem> gi;
     gi.reserve(plan.size());
@@ -575,6 +587,31 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     return GRKGPU_OK;
 }
 
+extern "C" int grkgpu_num_tiles(const grkgpu_image_desc *img, const grkgpu_cparams *p, uint32_t *ntiles) {
+    if (!ntiles) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    int rc = setup_params(img, p, cp);
+    if (rc) return rc;
+    *ntiles = cp.tw * cp.th;
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_compress_tiles(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                                     const int32_t *const *planes, int planes_on_device, uint32_t tile_begin,
+                                     uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen) {
+    if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    const uint8_t *v = nullptr;
+    size_t n = 0;
+    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n, tile_begin, tile_end, parts);
+    if (rc) return rc;
+    uint8_t *o = (uint8_t *)malloc(n ? n : 1);
+    if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
+    memcpy(o, v, n);
+    *out = o;
+    *outlen = n;
+    return GRKGPU_OK;
+}
+
 // ---------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------
@@ -594,8 +631,8 @@ extern "C" int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_de
 static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
 static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
 
-extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
-                                 int32_t *const *planes, int planes_on_device) {
+static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
+                           int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te) {
     if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     double t_start = now_ms();
     CodingParams cp;
@@ -610,6 +647,9 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     hipStream_t s = c->stream;
     const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th, iw = cp.image.w(), ih = cp.image.h();
     const uint64_t plane = (uint64_t)iw * ih;
+    if (te > ntiles) te = ntiles;
+    if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
+    const bool whole = tb == 0 && te == ntiles;
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
     std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
@@ -635,15 +675,17 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
         pos = end;
     }
 
-    // host Tier-2 over every tile; code-block segments -> DecBlock table
-    std::vector<Tile> tiles(ntiles);
+    // host Tier-2 over every tile of the shard; code-block segments -> DecBlock table
+    const uint32_t nsh = te - tb;
+    std::vector<Tile> tiles(nsh);
     uint64_t arena = 0, llarena = 0;
-    std::vector<uint64_t> lloff(ntiles * nc);
+    std::vector<uint64_t> lloff(nsh * nc);
     std::vector<DecBlock> db;
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     std::vector<uint8_t> tilebuf;
-    for (uint32_t t = 0; t < ntiles; ++t) {
-        Tile &tile = tiles[t];
+    for (uint32_t lt = 0; lt < nsh; ++lt) {
+        const uint32_t t = tb + lt;
+        Tile &tile = tiles[lt];
         tile.index = t;
         tile.r = tile_rect(cp, t);
         tile.comps.resize(nc);
@@ -652,7 +694,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
             tile.comps[k].arena_off = arena;
             uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
             arena += (area + 63) & ~63ull;
-            lloff[t * nc + k] = llarena;
+            lloff[lt * nc + k] = llarena;
             llarena += ll_geom(tile.comps[k]).elems;
         }
         // tile data: single tile-part -> decode in place; else concatenate
@@ -746,7 +788,7 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
-                        c->ll.as<int32_t>() + lloff[tile.index * nc + k], cp.irrev, true);
+                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true);
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
@@ -777,9 +819,19 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
         HIPCHK(launch_mct_inv_dcshift(tsrc, tile.r.w(), tile.r.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
-    if (!planes_on_device)
-        for (uint32_t k = 0; k < nc; ++k)
-            HIPCHK(hipMemcpyAsync(planes[k], dst.p[k], plane * 4, hipMemcpyDeviceToHost, s));
+    if (!planes_on_device) {
+        if (whole) {
+            for (uint32_t k = 0; k < nc; ++k)
+                HIPCHK(hipMemcpyAsync(planes[k], dst.p[k], plane * 4, hipMemcpyDeviceToHost, s));
+        } else {  // only the shard's tiles
+            for (auto &tile : tiles)
+                for (uint32_t k = 0; k < nc; ++k) {
+                    const uint64_t o = (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+                    HIPCHK(hipMemcpy2DAsync(planes[k] + o, (size_t)iw * 4, dst.p[k] + o, (size_t)iw * 4,
+                                            (size_t)tile.r.w() * 4, tile.r.h(), hipMemcpyDeviceToHost, s));
+                }
+        }
+    }
     HIPCHK(hipEventRecord(c->ev[5], s));
     HIPCHK(hipStreamSynchronize(s));
     double t_end = now_ms();
@@ -795,6 +847,16 @@ extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, 
     st.num_cblks = nblk;
     st.cs_bytes = len;
     return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
+                                 int32_t *const *planes, int planes_on_device) {
+    return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu);
+}
+
+extern "C" int grkgpu_decompress_tiles(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t tile_begin,
+                                       uint32_t tile_end, int32_t *const *planes, int planes_on_device) {
+    return decompress_impl(c, csb, len, nullptr, planes, planes_on_device, tile_begin, tile_end);
 }
 
 // ---------------------------------------------------------------------------

@@ -110,12 +110,33 @@ int grkgpu_compress(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_
 int grkgpu_compress_view(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                          const int32_t *const *planes, int planes_on_device, const uint8_t **out, size_t *outlen);
 
+/* Tile shards (multi-GPU): tiles are independent through the
+ * whole path, and a codestream is [main header][tile-parts in tile order]
+ * [EOC] (j2k.cpp:2088-2111, 2376-2435), so each GPU encodes a contiguous
+ * tile range and the host concatenates.  grkgpu_compress_tiles encodes tiles
+ * [tile_begin, tile_end) and emits the parts selected by `parts`;
+ * grkgpu_compress == grkgpu_compress_tiles(0, n, GRKGPU_PART_ALL). */
+#define GRKGPU_PART_HEADER 1u
+#define GRKGPU_PART_TILES 0u
+#define GRKGPU_PART_EOC 2u
+#define GRKGPU_PART_ALL 3u
+int grkgpu_num_tiles(const grkgpu_image_desc *img, const grkgpu_cparams *p, uint32_t *ntiles);
+int grkgpu_compress_tiles(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                          const int32_t *const *planes, int planes_on_device, uint32_t tile_begin,
+                          uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
+
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
 
 /* Whole-codestream decode into caller-provided planes (device or host). */
 int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_image_desc *img,
                       int32_t *const *planes, int planes_on_device);
+/* Decode only tiles [tile_begin, tile_end) (a tile shard; the reference's
+ * tile-by-tile decode, grk_decode_tile_data / j2k.cpp decode_tiles); the
+ * other tiles' samples in planes are left untouched.  Host planes are written
+ * for the shard's tiles only. */
+int grkgpu_decompress_tiles(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t tile_begin,
+                            uint32_t tile_end, int32_t *const *planes, int planes_on_device);
 
 void grkgpu_free(void *p);
 
