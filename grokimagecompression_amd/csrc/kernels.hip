@@ -312,16 +312,17 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
         }
     }
     words[nw++] = u.tail();
-    words[nw++] = 0xffffffffu;
+    do { words[nw++] = 0xffffffffu; } while (nw & 3);
+    for (int k = 0; k < 8; ++k) words[nw++] = 0xffffffffu;
     carries[nc] = 0xffffffffu;
     region[0] = nw;
     region[1] = nc;
 }
 
-template <int LANES>
-__global__ __launch_bounds__(LANES) void k_t1_decode_flat(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                          const uint32_t *__restrict__ ubuf,
-                                                          T1Scratch *__restrict__ scr) {
+template <int LANES, bool FLAT>
+__global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                        const uint32_t *__restrict__ ubuf,
+                                                        T1Scratch *__restrict__ scr) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
@@ -337,8 +338,12 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_flat(const DecBlock *__rest
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
     T1Scratch &S = scr[i];
     const uint32_t *region = ubuf + (size_t)b.pad * 4;
-    t1_decode_flat(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, S.st,
-                   T, s_cx + threadIdx.x * 21, S.pa, S.pb);
+    if (FLAT)
+        t1_decode_flat(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h,
+                       S.st, T, s_cx + threadIdx.x * 21, S.pa, S.pb);
+    else
+        t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h,
+                     S.st, T, s_cx + threadIdx.x * 21, S.pa, S.pb);
 }
 
 // One workgroup per block, lane = column: values from the bit-plane rows
@@ -415,6 +420,23 @@ hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t tw, uint32_t th
     return hipGetLastError();
 }
 
+// Decoder selection (GRKGPU_T1_DEC): v5 (default) = v3's pass / stripe /
+// column walk over the unstuffed bit stream (k_t1_unstuff + branch-free MQ
+// renormalisation); v3 = byte-level MQ input; v4 = flat (one decision per
+// loop step; correct but measured 2.2x slower than v3 on the 8K frame);
+// v2 = first lane decoder.  v4 / v5 need the unstuff pass.
+static int t1_dec_mode() {
+    static const int m = [] {
+        const char *e = getenv("GRKGPU_T1_DEC");
+        if (e && !strcmp(e, "v4")) return 4;
+        if (e && !strcmp(e, "v3")) return 3;
+        if (e && !strcmp(e, "v2")) return 2;
+        return 5;
+    }();
+    return m;
+}
+bool t1_dec_flat_enabled() { return t1_dec_mode() >= 4; }
+
 static int t1_mq_lanes() {
     static int lanes = [] {
         const char *e = getenv("GRKGPU_MQ_LANES");
@@ -449,7 +471,7 @@ static int t1_minw() {
 
 template <int L>
 static void launch_dec_lane(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scr, hipStream_t s) {
-    static const bool v2 = getenv("GRKGPU_T1_DEC") && !strcmp(getenv("GRKGPU_T1_DEC"), "v2");
+    const bool v2 = t1_dec_mode() == 2;
     const dim3 g((n + L - 1) / L);
     if (v2) { hipLaunchKernelGGL(k_t1_decode_lane<L>, g, dim3(L), 0, s, blocks, n, data, scr); return; }
     switch (t1_minw()) {
@@ -513,12 +535,7 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     return hipGetLastError();
 }
 
-// v4 (flat) decoder: correct, but measured 2.2x slower than v3 on the 8K
-// frame (more VALU/SALU per decision); kept behind GRKGPU_T1_DEC=v4.
-bool t1_dec_flat_enabled() {
-    static const bool on = getenv("GRKGPU_T1_DEC") && !strcmp(getenv("GRKGPU_T1_DEC"), "v4");
-    return on;
-}
+
 
 static int t1_dec_lanes() {
     static int lanes = [] {
@@ -531,7 +548,10 @@ static int t1_dec_lanes() {
 
 template <int L>
 static void launch_dec_flat(const DecBlock *blocks, uint32_t n, const uint32_t *ubuf, T1Scratch *scr, hipStream_t s) {
-    hipLaunchKernelGGL(k_t1_decode_flat<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
+    if (t1_dec_mode() == 4)
+        hipLaunchKernelGGL((k_t1_decode_ub<L, true>), dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
+    else
+        hipLaunchKernelGGL((k_t1_decode_ub<L, false>), dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
 }
 
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,

@@ -33,6 +33,9 @@ GRK_HD uint8_t sc_win_entry(uint32_t i) {
     return (uint8_t)(cx | (xr << 7));
 }
 
+struct Dec3;
+GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx);
+
 struct Dec3 {
     uint32_t a, c, ct;
     uint32_t cur, nxt;  // code bytes at bp and bp + 1
@@ -40,6 +43,7 @@ struct Dec3 {
     uint4 c0, c1, c2;   // c0.x = current word (consumed low byte first)
     uint32_t wleft, wq; // bytes left in c0.x, words left in c0
     uint32_t idx, len;  // bytes handed out so far, segment length
+    GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) { return d3_decode(*this, cxw, tab, cx); }
 };
 
 GRK_HD uint32_t d3_byte(Dec3 &d) {
@@ -150,8 +154,8 @@ struct DecTables {
 
 // significance propagation (CUP = false) or cleanup (CUP = true) of one
 // column; returns true if a sample became significant.
-template <bool CUP>
-GRK_HD bool d3_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+template <bool CUP, class D>
+GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
     uint32_t P = win18(s.sig, x);
     const uint32_t vis4 = col4(s.vis, x);
     const uint32_t rows = (1u << nr) - 1;
@@ -179,7 +183,7 @@ GRK_HD bool d3_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uin
         if (kind == 0) cx = T.zc[(P >> (3 * r)) & 0x1FF];
         else if (kind == 1) cx = si & 0x7f;
         else cx = kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
-        const uint32_t bit = d3_decode(d, cxw, T.mq, cx);
+        const uint32_t bit = d.decode(cxw, T.mq, cx);
         bool advance = true;
         if (kind == 0) {
             if (!CUP) newvis |= 1u << r;
@@ -223,7 +227,8 @@ GRK_HD bool d3_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uin
 }
 
 // magnitude refinement of one column
-GRK_HD void d3_mrp_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+template <class D>
+GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
     const uint32_t P = win18(s.sig, x);
     const uint32_t rows = (1u << nr) - 1;
     uint32_t m4 = win_self4(P) & ~col4(s.vis, x) & rows;
@@ -234,20 +239,17 @@ GRK_HD void d3_mrp_column(Dec3 &d, uint32_t *cxw, const DecTables &T, Stripe &s,
         const uint32_t r = (uint32_t)__builtin_ctz(m4);
         m4 &= m4 - 1;
         const uint32_t cx = ((ref4 >> r) & 1) ? CX_MAG + 2 : CX_MAG + (((P >> (3 * r)) & 0x1EF) ? 1u : 0u);
-        bits |= d3_decode(d, cxw, T.mq, cx) << r;
+        bits |= d.decode(cxw, T.mq, cx) << r;
     }
     setcol4(s.ref, x, mem);
     setcol4(s.bit, x, bits);
 }
 
-// Decode one block into write-only bit-plane rows (see t1_decode_lane).
-GRK_HD void t1_decode_v3(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
-                         uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw, uint64_t *sigafter,
-                         uint64_t *refbit) {
-    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    mq_reset_words(cxw, T.mq);
-    Dec3 d;
-    d3_init(d, data, len);
+// The pass / stripe / column walk shared by v3 (byte-level MQ input, Dec3)
+// and v5 (unstuffed bit stream, BitDec in t1_flat.h).
+template <class D>
+GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, BlockState &st,
+                             const DecTables &T, uint32_t *cxw, uint64_t *sigafter, uint64_t *refbit) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     int32_t bpno = (int32_t)numbps - 1;
     int passtype = 2;
@@ -308,6 +310,17 @@ GRK_HD void t1_decode_v3(const uint8_t *data, uint32_t len, uint32_t numpasses, 
         }
         if (++passtype == 3) { passtype = 0; bpno--; }
     }
+}
+
+// Decode one block into write-only bit-plane rows (see t1_decode_lane).
+GRK_HD void t1_decode_v3(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
+                         uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw, uint64_t *sigafter,
+                         uint64_t *refbit) {
+    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
+    mq_reset_words(cxw, T.mq);
+    Dec3 d;
+    d3_init(d, data, len);
+    t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sigafter, refbit);
 }
 
 }  // namespace grkgpu

@@ -76,7 +76,8 @@ struct Unstuff {
 };
 
 // capacity (32-bit words) of the word and carry areas for a segment of len bytes
-GRK_HD uint32_t unstuff_word_cap(uint32_t len) { return ((len * 8 + 95) / 32 + 3) & ~3u; }
+// (data words + the 1-bit tail + two all-ones chunks, rounded to chunks)
+GRK_HD uint32_t unstuff_word_cap(uint32_t len) { return ((len * 8) / 32 + 1 + 1 + 8 + 3) & ~3u; }
 GRK_HD uint32_t unstuff_carry_cap(uint32_t len) { return (len / 2 + 4 + 3) & ~3u; }
 
 GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, uint32_t *carries,
@@ -88,7 +89,8 @@ GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, u
         if (cv != 0xffffffffu) carries[nc++] = cv;
     }
     words[nw++] = u.tail();
-    words[nw++] = 0xffffffffu;
+    do { words[nw++] = 0xffffffffu; } while (nw & 3);
+    for (int i = 0; i < 8; ++i) words[nw++] = 0xffffffffu;
     carries[nc] = 0xffffffffu;  // sentinel
     *ncarry = nc;
     return nw;
@@ -109,11 +111,9 @@ struct FlatBits {
     const uint4 *base;
 };
 
-GRK_HD uint4 fb_load(const FlatBits &b, uint32_t ci) {
-    if (ci < b.nchunks) return b.base[ci];
-    uint4 o; o.x = o.y = o.z = o.w = 0xffffffffu;
-    return o;
-}
+// the stream ends with two all-ones chunks, so reads past the end clamp to
+// the last chunk (no branch around the load, no select on its result)
+GRK_HD uint4 fb_load(const FlatBits &b, uint32_t ci) { return b.base[ci < b.nchunks ? ci : b.nchunks - 1]; }
 
 GRK_HD uint32_t fb_word(FlatBits &b) {
     const uint32_t v = b.wi == 0 ? b.cur.x : b.wi == 1 ? b.cur.y : b.wi == 2 ? b.cur.z : b.cur.w;
@@ -126,7 +126,77 @@ GRK_HD uint32_t fb_word(FlatBits &b) {
 }
 
 // ---------------------------------------------------------------------------
-// the decoder
+// MQ decoder over the unstuffed stream (used by the nested-loop decoder v5
+// in t1_dec.h and by t1_decode_flat): branch-free renormalisation.
+// ---------------------------------------------------------------------------
+struct BitDec {
+    FlatBits bits;
+    uint32_t A, C, consumed, cq;
+    const uint32_t *cp;
+    GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
+        bits.base = (const uint4 *)words;
+        bits.nchunks = (nwords + 3) >> 2;
+        bits.cur = fb_load(bits, 0);
+        bits.nxt = fb_load(bits, 1);
+        bits.chunk = 1;
+        bits.wi = 0;
+        const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
+        const uint64_t v = (w0 << 32) | w1;
+        C = (uint32_t)(v >> 33);  // first 31 stream bits (INITDEC: consumed 24, then 7 shifts)
+        bits.W = v << 31;
+        bits.NB = 33;
+        A = 0x8000;
+        consumed = 31;
+        cq = carries[0];
+        cp = carries + 1;
+        if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
+    }
+    GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
+        const uint32_t wd = cxw[cx];
+        const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
+        uint32_t a = A - qe;
+        const bool lo = (C >> 16) < qe;
+        const bool lps = lo ? (a >= qe) : (a < qe);
+        const bool keep = !lo && (a & 0x8000u);
+        C = lo ? C : C - (qe << 16);
+        a = lo ? qe : a;
+        const uint32_t nidx = (wd >> (lps ? 22 : 16)) & 63u;
+        const uint32_t nmps = mps ^ (lps ? (wd >> 28) & 1u : 0u);
+        const uint32_t tw = tab[nidx];
+        const uint32_t n = clz32(a) - 16;
+        C = (C << n) | (uint32_t)((bits.W >> 1) >> (63 - n));
+        bits.W <<= n;
+        bits.NB -= n;
+        A = a << n;
+        const uint32_t c1 = consumed + n;
+        if (cq < c1) { C += 1u << (16 + c1 - cq); cq = *cp++; }  // carry event (see Unstuff)
+        consumed = c1;
+        if (bits.NB < 32) {
+            bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
+            bits.NB += 32;
+        }
+        if (!keep) cxw[cx] = tw | (nmps << 31);
+#ifdef T1_TRACE
+        T1_TRACE(cx, mps ^ (uint32_t)lps, A, C >> 16);
+#endif
+        return mps ^ (uint32_t)lps;
+    }
+};
+
+// v5: the nested pass / stripe / column walk of v3 (lanes of a wavefront stay
+// converged on the pass structure) fed by the unstuffed bit stream.
+GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
+                         uint32_t numbps, uint32_t w, uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw,
+                         uint64_t *sa, uint64_t *rb) {
+    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
+    mq_reset_words(cxw, T.mq);
+    BitDec d;
+    d.init(words, nwords, carries);
+    t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sa, rb);
+}
+
+// ---------------------------------------------------------------------------
+// the flat decoder
 // ---------------------------------------------------------------------------
 enum FlatKind : uint32_t { FK_ZC = 0, FK_SC = 1, FK_MAG = 2, FK_AGG = 3, FK_UNI1 = 4, FK_UNI2 = 5 };
 
@@ -156,28 +226,8 @@ GRK_HD void t1_decode_flat(const uint32_t *words, uint32_t nwords, const uint32_
     const uint64_t wmask = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     const uint32_t nstripes = (h + 3) >> 2;
 
-    // bit reader + MQ registers
-    FlatBits bits;
-    bits.base = (const uint4 *)words;
-    bits.nchunks = (nwords + 3) >> 2;
-    bits.chunk = 0;
-    bits.cur = fb_load(bits, 0);
-    bits.nxt = fb_load(bits, 1);
-    bits.chunk = 1;
-    bits.wi = 0;
-    // C[16] holds stream bit (consumed - 17); INITDEC leaves consumed = 31
-    // (it loads the first byte at C[23:16], i.e. consumed = 24, then shifts 7)
-    uint32_t A = 0x8000, C, consumed = 31;
-    uint32_t cq = carries[0];
-    const uint32_t *cp = carries + 1;
-    {
-        const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
-        const uint64_t v = (w0 << 32) | w1;
-        C = (uint32_t)(v >> 33);  // first 31 stream bits
-        bits.W = v << 31;
-        bits.NB = 33;
-        if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
-    }
+    BitDec md;
+    md.init(words, nwords, carries);
 
     // pass / stripe / column cursor
     uint32_t ptype = 2;                 // first pass: cleanup of the top plane
@@ -273,39 +323,7 @@ GRK_HD void t1_decode_flat(const uint32_t *words, uint32_t nwords, const uint32_
             else if (kind == FK_MAG) cx = ((ref4 >> r) & 1u) ? CX_MAG + 2 : CX_MAG + ((nb9 & 0x1EFu) ? 1u : 0u);
             else cx = kind == FK_AGG ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
 
-            const uint32_t wd = cxw[cx];
-            const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
-            uint32_t a = A - qe;
-            const bool lo = (C >> 16) < qe;
-            const bool lps = lo ? (a >= qe) : (a < qe);
-            const bool keep = !lo && (a & 0x8000u);
-            C = lo ? C : C - (qe << 16);
-            a = lo ? qe : a;
-            const uint32_t nidx = (wd >> (lps ? 22 : 16)) & 63u;
-            const uint32_t nmps = mps ^ (lps ? (wd >> 28) & 1u : 0u);
-            const uint32_t tw = T.mq[nidx];
-            const uint32_t n = clz32(a) - 16;
-            C = (C << n) | (uint32_t)((bits.W >> 1) >> (63 - n));
-            bits.W <<= n;
-            bits.NB -= n;
-            A = a << n;
-            {
-                const uint32_t c1 = consumed + n;
-                if (cq < c1) { C += 1u << (16 + c1 - cq); cq = *cp++; }  // carry event (see Unstuff)
-                consumed = c1;
-            }
-            if (!keep) cxw[cx] = tw | (nmps << 31);
-            if (bits.NB < 32) {
-                bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
-                bits.NB += 32;
-            }
-            const uint32_t d = mps ^ (uint32_t)lps;
-#ifdef T1_TRACE
-            T1_TRACE(cx, d, A, C >> 16);
-#ifdef T1_TRACE2
-            T1_TRACE2(bits.chunk, bits.wi, bits.NB);
-#endif
-#endif
+            const uint32_t d = md.decode(cxw, T.mq, cx);
 
             // ---------------- apply ----------------
             bool advance = true;

@@ -154,6 +154,19 @@ int main(int argc, char **argv) {
                 std::vector<int32_t> fd(w * h);
                 for (uint32_t y = 0; y < h; ++y)
                     for (uint32_t x = 0; x < w; ++x) fd[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
+                // v5: v3's walk over the same unstuffed stream
+                {
+                    std::fill(scr.pa, scr.pa + 32 * 64, ~0ull);
+                    std::fill(scr.pb, scr.pb + 32 * 64, ~0ull);
+                    t1_decode_v5(wp, nw, carr.data(), np, onb, w, h, scr.st, DT, cx4, scr.pa, scr.pb);
+                    std::vector<int32_t> v5(w * h);
+                    for (uint32_t y = 0; y < h; ++y)
+                        for (uint32_t x = 0; x < w; ++x) v5[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
+                    if (od != v5) {
+                        printf("V5 DEC MISMATCH it=%d w=%u h=%u np=%u nb=%u orient=%u\n", it, w, h, np, onb, orient);
+                        fails++;
+                    }
+                }
                 if (od != fd) {
                     int bad = 0;
                     for (uint32_t i = 0; i < w * h; ++i) bad += od[i] != fd[i];
