@@ -319,8 +319,8 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     region[1] = nc;
 }
 
-template <int LANES, bool FLAT>
-__global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
+template <int LANES, bool FLAT, int MINW = 1>
+__global__ __launch_bounds__(LANES, MINW) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf,
                                                         T1Scratch *__restrict__ scr) {
     __shared__ uint8_t s_zc[2048];
@@ -537,10 +537,15 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
 
 
 
+// Lanes (= code-blocks) per wavefront of the v4/v5 decoder.  The decoder is
+// latency-bound per block, so throughput = resident blocks / block time:
+// 64 lanes per wavefront keep 4x more blocks resident per wave slot than 16
+// (8K frame batch, 12 frames in flight: 2.0-2.2 vs 1.25 Gpix/s); a lone
+// frame decodes ~10% faster with 16 (GRKGPU_T1_DEC_LANES=16).
 static int t1_dec_lanes() {
     static int lanes = [] {
         const char *e = getenv("GRKGPU_T1_DEC_LANES");
-        int v = e ? atoi(e) : 16;
+        int v = e ? atoi(e) : 64;
         return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
     }();
     return lanes;
@@ -548,10 +553,16 @@ static int t1_dec_lanes() {
 
 template <int L>
 static void launch_dec_flat(const DecBlock *blocks, uint32_t n, const uint32_t *ubuf, T1Scratch *scr, hipStream_t s) {
-    if (t1_dec_mode() == 4)
-        hipLaunchKernelGGL((k_t1_decode_ub<L, true>), dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
-    else
-        hipLaunchKernelGGL((k_t1_decode_ub<L, false>), dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, ubuf, scr);
+    const dim3 g((n + L - 1) / L);
+    if (t1_dec_mode() == 4) {
+        hipLaunchKernelGGL((k_t1_decode_ub<L, true>), g, dim3(L), 0, s, blocks, n, ubuf, scr);
+        return;
+    }
+    switch (t1_minw()) {
+        case 4: hipLaunchKernelGGL((k_t1_decode_ub<L, false, 4>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
+        case 5: hipLaunchKernelGGL((k_t1_decode_ub<L, false, 5>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
+        default: hipLaunchKernelGGL((k_t1_decode_ub<L, false>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
+    }
 }
 
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,

@@ -12,6 +12,6 @@ bash scripts/pmc_bench.sh $TAG/pmc > /dev/null || { echo "pmc failed"; exit 1; }
 cp $OUT/pmc/pmc_summary.json profiles/dwt_pmc_latest.json
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 --concurrency 1 > $OUT/bench_prof.json 2> $OUT/prof.err || { echo "rocprof failed"; tail -30 $OUT/prof.err; exit 1; }
+GPU_MAX_HW_QUEUES=16 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 --concurrency 1 > $OUT/bench_prof.json 2> $OUT/prof.err || { echo "rocprof failed"; tail -30 $OUT/prof.err; exit 1; }
 python3 scripts/prof_summary.py $OUT/prof $OUT/kernel_stats.csv > /dev/null
 head -16 $OUT/kernel_stats.csv
