@@ -109,21 +109,27 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=ncodec)
 
-    def step():
+    jobs = [(codecs[0], p97, out97, "97"), (codecs[0], p53, out53, "53")] if pool is None else \
+        [j for i in range(npairs) for j in ((codecs[2 * i], p97, outs[i][0], "97"),
+                                            (codecs[2 * i + 1], p53, outs[i][1], "53"))]
+
+    def run_steps(n):
+        """n steps; each frame's pipeline runs its n iterations back to back on
+        its own thread/stream (no barrier between steps, so no pipeline waits
+        for the slowest one before starting its next frame)."""
         if pool is None:
-            pipe(codecs[0], p97, out97, "97")
-            pipe(codecs[0], p53, out53, "53")
+            for _ in range(n):
+                for j in jobs:
+                    pipe(*j)
         else:
-            f = []
-            for i in range(npairs):
-                f.append(pool.submit(pipe, codecs[2 * i], p97, outs[i][0], "97"))
-                f.append(pool.submit(pipe, codecs[2 * i + 1], p53, outs[i][1], "53"))
-            for x in f:
+            def loop(j):
+                for _ in range(n):
+                    pipe(*j)
+            for x in [pool.submit(loop, j) for j in jobs]:
                 x.result()
         st["bytes"] = (st["bytes97"], st["bytes53"])
 
-    for _ in range(args.warmup):
-        step()
+    run_steps(args.warmup)
     assert torch.equal(out53, frame), "5/3 round trip is not lossless"
 
     def barrier():
@@ -133,8 +139,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:

@@ -440,8 +440,8 @@ bool t1_dec_flat_enabled() { return t1_dec_mode() >= 4; }
 static int t1_mq_lanes() {
     static int lanes = [] {
         const char *e = getenv("GRKGPU_MQ_LANES");
-        int v = e ? atoi(e) : 32;
-        return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 32;
+        int v = e ? atoi(e) : 64;  // 64 blocks per wavefront: see t1_dec_lanes
+        return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 64;
     }();
     return lanes;
 }
