@@ -291,8 +291,13 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
     P.th.assign(P.levels.size(), 8);
     for (size_t l = 0; l < P.levels.size(); ++l) {
         uint64_t samples = 0;
-        for (auto &j : P.levels[l]) samples += (uint64_t)j.rw * j.rh;
-        P.th[l] = dwt_pick_th(irrev, samples);
+        int minw = INT32_MAX, minh = INT32_MAX;
+        for (auto &j : P.levels[l]) {
+            samples += (uint64_t)j.rw * j.rh;
+            minw = std::min(minw, (int)j.rw);
+            minh = std::min(minh, (int)j.rh);
+        }
+        P.th[l] = dwt_pick_th(irrev, samples, minw, minh);
         for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j.rw, j.rh, j.casx, j.casy, &j.tiles_x, &j.ntiles);
     }
 }

@@ -57,7 +57,9 @@ struct DwtJob {
     int32_t rw, rh, casx, casy, snx, sny;
     int32_t tiles_x, ntiles;
 };
-int dwt_pick_th(int irrev, uint64_t level_samples);  // window rows for a level of that many samples
+// level geometry code (window rows | strip windows << 8) for a level of that
+// many samples whose smallest resolution is minw x minh
+int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh);
 void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
                            int inverse, hipStream_t s);

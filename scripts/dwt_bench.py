@@ -29,7 +29,7 @@ def one():
             d = codec.stats()["dwt_ms"]
             res.append((e, d))
         out["97" if irrev else "53"] = {"enc_dwt_ms": min(r[0] for r in res), "dec_dwt_ms": min(r[1] for r in res)}
-    print(json.dumps({"th": os.environ.get("GRKGPU_DWT_TH", "default"), **out}), flush=True)
+    print(json.dumps(out), flush=True)
 
 
 def stage():
@@ -53,8 +53,14 @@ if __name__ == "__main__":
     if "--stage" in sys.argv:
         stage()
     elif "--sweep" in sys.argv:
-        for th in ["8", "16", "24", "32"]:
-            env = dict(os.environ, GRKGPU_DWT_TH=th)
+        # each remaining argument: comma-separated ENV=VALUE settings of one run
+        specs = [a for a in sys.argv[1:] if a != "--sweep"] or ["GRKGPU_DWT_STRIP=0"]
+        for spec in specs:
+            env = dict(os.environ)
+            for kv in filter(None, spec.split(",")):
+                k, v = kv.split("=", 1)
+                env[k] = v
+            print("==", spec, flush=True)
             subprocess.run([sys.executable, __file__], env=env, check=True, timeout=300)
     else:
         one()

@@ -11,7 +11,7 @@ i=0
 for E in "$@"; do
   i=$((i+1))
   export $E
-  GPU_MAX_HW_QUEUES=16 timeout -s KILL 180 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/run$i -o run -- python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/run$i.log 2>&1 || { echo "pmc run $i failed"; tail -5 $OUT/run$i.log; exit 1; }
+  GPU_MAX_HW_QUEUES=16 timeout -s KILL 180 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/run$i -o run -- python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --concurrency 1 > $OUT/run$i.log 2>&1 || { echo "pmc run $i failed"; tail -5 $OUT/run$i.log; exit 1; }
   unset ${E%%=*}
   echo "run$i: $E"
 done

@@ -7,7 +7,7 @@ for d in sys.argv[1:]:
             acc[r["Kernel_Name"].split("(")[0][-40:]][r["Counter_Name"]] += float(r["Counter_Value"])
     print("==", d)
     for k, v in acc.items():
-        if "t1" not in k:
+        if "t1" not in k and "dwt" not in k:
             continue
         w = v.get("SQ_WAVES", 1) or 1
         print("%-40s waves %7d  valu/wave %9.0f salu/wave %8.0f lds/wave %8.0f cyc/wave %10.0f wait %.2f waitinst %.2f active %.2f" % (

@@ -94,6 +94,43 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
 
 
 @pytest.mark.parametrize("irrev", [False, True])
+@pytest.mark.parametrize("shape_off", [((64, 64), (0, 0)), ((77, 100), (3, 5)), ((129, 200), (1, 1)),
+                                       ((513, 257), (0, 3)), ((300, 497), (2, 2)), ((37, 260), (1, 1)),
+                                       ((16, 16), (1, 1)), ((700, 1030), (1, 0))])
+@pytest.mark.parametrize("sth_nch", [(8, 1), (16, 3), (24, 2), (32, 8)])
+def test_dwt_strip_stage_vs_oracle(oracle, monkeypatch, irrev, shape_off, sth_nch):
+    """The strip kernels (windows walking down 128-column strips with the
+    overlap rows carried in registers) forced onto every level they accept
+    (resolutions >= 16 x 16), at several window heights and strip lengths."""
+    import torch
+    import grokimagecompression_amd as grk
+    monkeypatch.setenv("GRKGPU_DWT_STRIP", "1")
+    monkeypatch.setenv("GRKGPU_DWT_STRIP_MIN", "0")
+    monkeypatch.setenv("GRKGPU_DWT_STH", str(sth_nch[0]))
+    monkeypatch.setenv("GRKGPU_DWT_NCH", str(sth_nch[1]))
+    (h, w), (x0, y0) = shape_off
+    numres = 5
+    rng = np.random.default_rng(h * 7 + w + sth_nch[0])
+    a = rng.integers(-(1 << 20) if irrev else -4096, 1 << 20 if irrev else 4096, size=(h, w)).astype(np.int32)
+    ref = oracle.dwt_fwd(a, x0, y0, numres, irrev)
+    t = torch.from_numpy(a).cuda()
+    grk.dwt_fwd(t, x0, y0, numres, irrev)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), ref)
+    if not irrev:
+        grk.dwt_inv(t, x0, y0, numres, False)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), a)
+    else:
+        f = (rng.standard_normal((h, w)) * 100).astype(np.float32).view(np.int32)
+        ref = oracle.dwt_inv(f, x0, y0, numres, True)
+        t = torch.from_numpy(f.copy()).cuda()
+        grk.dwt_inv(t, x0, y0, numres, True)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("irrev", [False, True])
 def test_mct_stage_vs_oracle(oracle, irrev):
     import torch
     import grokimagecompression_amd as grk
