@@ -227,6 +227,8 @@ struct DwtPlan {
     std::vector<int> th;                      // window rows per level (dwt_finalize)
     std::vector<std::pair<int32_t *, const int32_t *>> copies;  // numres == 1: dst <- src
     uint64_t copy_elems = 0;
+    bool fused0 = false;  // forward level 0 reads the image planes (DC shift + MCT fused, dwt.hip)
+    bool mct3 = false;    // ... and its jobs are MCT component triples (tile-major, component-minor)
 };
 
 static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *coef, int32_t *llbase, int irrev,
@@ -330,7 +332,8 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
         const auto &l = P.levels[li];
         uint32_t maxt = 0;
         for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
-        e = launch_dwt_jobs(djobs.as<DwtJob>() + k, (uint32_t)l.size(), maxt, P.th[li], irrev, inverse ? 1 : 0, s);
+        const int code = P.th[li] | (li == 0 && P.fused0 && !inverse ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) : 0);
+        e = launch_dwt_jobs(djobs.as<DwtJob>() + k, (uint32_t)l.size(), maxt, code, irrev, inverse ? 1 : 0, s);
         if (e != hipSuccess) return e;
         k += l.size();
     }
@@ -449,15 +452,46 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipEventRecord(c->ev[1], s));
     ShiftArr sh{};
     for (uint32_t k = 0; k < nc; ++k) sh.v[k] = cp.shift[k];
-    DwtPlan dplan;
+    // GRKGPU_DWT_FUSE=1 fuses the DC shift + MCT into the first DWT level
+    // (every tile-component decomposed at least once and spanning its tile).
+    // Off by default: it saves the 8 B/sample MCT round trip, but measured
+    // 1.3-1.6x SLOWER than MCT pass + level 0 on the 8K frame.
+    bool fuse = getenv("GRKGPU_DWT_FUSE") && atoi(getenv("GRKGPU_DWT_FUSE")) != 0;
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
+            fuse = fuse && tc.numres >= 2 && tc.r.w() == tile.r.w() && tc.r.h() == tile.r.h();
+        }
+    if (cp.mct && nc != 3) fuse = false;  // MCT over more than 3 components: separate pass
+    DwtPlan dplan;
+    dplan.fused0 = fuse;
+    dplan.mct3 = fuse && cp.mct && nc == 3;
+    for (auto &tile : tiles)
+        for (uint32_t k = 0; k < nc; ++k) {
+            const TileComp &tc = tile.comps[k];
+            const size_t before = dplan.levels.empty() ? 0 : dplan.levels[0].size();
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, false);
+            if (!fuse || dplan.levels.empty() || dplan.levels[0].size() == before) continue;
+            DwtJob &j = dplan.levels[0].back();
+            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+            const bool mct3 = cp.mct && nc >= 3 && k < 3;
+            for (uint32_t i = 0; i < 3; ++i) {
+                const uint32_t pk = mct3 ? i : k;
+                j.src[i] = src.p[pk] + org;
+                j.shift[i] = cp.shift[pk];
+            }
+            j.src_stride = iw;
+            j.src_bytes = (uint32_t)std::min<uint64_t>((plane - org) * 4, 0xffffffffu);
+            j.mct_mode = mct3 ? (cp.irrev ? 3 : 2) : 1;
+            j.comp = (int32_t)k;
+            bool al = (iw & 1) == 0;
+            for (uint32_t i = 0; i < 3; ++i) al = al && ((uintptr_t)j.src[i] & 7) == 0;
+            j.src_vec = al ? 1 : 0;
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
+        if (fuse) break;
         PlanePtrs tsrc{}, tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
             tsrc.p[k] = src.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
@@ -761,6 +795,21 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
+    // The decoder runs one code-block per lane, 64 per wavefront, so a
+    // wavefront lasts as long as its longest block.  Order the blocks by
+    // segment length (longest first; counting sort on len / 32) so each
+    // wavefront gets blocks of similar length.  Block order is free: every
+    // DecBlock carries its own destination (GRKGPU_T1_SORT=0 keeps T2 order).
+    if (!getenv("GRKGPU_T1_SORT") || atoi(getenv("GRKGPU_T1_SORT")) != 0) {
+        constexpr uint32_t NB = 4096;
+        std::vector<uint32_t> cnt(NB + 1, 0);
+        auto key = [](const DecBlock &d) { return NB - 1 - std::min<uint32_t>(d.len >> 5, NB - 1); };
+        for (auto &d : db) cnt[key(d) + 1]++;
+        for (uint32_t b = 0; b < NB; ++b) cnt[b + 1] += cnt[b];
+        std::vector<DecBlock> sorted(db.size());
+        for (auto &d : db) sorted[cnt[key(d)]++] = d;
+        db.swap(sorted);
+    }
     double t_t2 = now_ms();
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));

@@ -109,23 +109,32 @@ __device__ __forceinline__ void vstep(int32_t (&v)[R]) {
     for (int k = PAR == 0 ? 2 : 1; k + 1 < R; k += 2) v[k] = lift<OP>(v[k], v[k - 1], v[k + 1]);
 }
 
+// Linear workgroup id -> position in an order where each XCD (workgroups are
+// dealt round-robin to the 8 XCDs by linear id) owns one contiguous run.
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+    const int q = total >> 3, r = total & 7, x = L & 7, k = L >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
 // Window of this wavefront.  The launch is a 2-D grid (x: workgroups of one
 // job, y: job); `lay` bit 0 remaps the linear workgroup id so that each XCD
 // (workgroups are dealt round-robin to the 8 XCDs) receives a contiguous run
 // of workgroups -- neighbouring windows, whose halo rows and columns overlap,
 // then share one L2; bit 1 stacks the 4 wavefronts of a workgroup vertically
-// (same column window, 4 consecutive row windows) instead of horizontally.
+// (same column window, 4 consecutive row windows) instead of horizontally;
+// bit 2 orders the workgroups job-minor, so the same window of every job
+// (the components of a tile, which the fused level 0 reads from the same
+// image planes) is processed at the same time on the same XCD.
 // Returns false for a wavefront past the job's windows.
 __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int lay, int th, DwtJob &J, int &tx,
                                            int &ty) {
     const int gx = gridDim.x;
     int L = blockIdx.y * gx + blockIdx.x;
-    if (lay & 1) {
-        const int total = gx * gridDim.y, q = total >> 3, r = total & 7, x = L & 7, k = L >> 3;
-        L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-    }
-    const int wg = L % gx;
-    J = jobs[L / gx];
+    if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+    int wg, job;
+    if (lay & 4) { job = L % (int)gridDim.y; wg = L / (int)gridDim.y; }  // job-minor: same window of every job adjacent
+    else { wg = L % gx; job = L / gx; }
+    J = jobs[job];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nty = (J.rh + J.casy + th - 1) / th;
     if (lay & 2) {
@@ -143,14 +152,84 @@ __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int 
 // forward level
 // ---------------------------------------------------------------------------
 
-template <bool IRREV, int TH, int XM = 0, int LAUX = 0, int SAUX = 0>
+// DC shift + forward MCT of one sample (k_dcshift_mct_fwd, kernels.hip;
+// TileProcessor.cpp:1449-1471, mct.cpp:85-139 RCT, :195-350 ICT).
+template <bool IRREV>
+__device__ __forceinline__ int32_t mct_px(const DwtJob &J, int32_t a, int32_t b, int32_t c) {
+    if (J.mct_mode == 1) {
+        const int32_t v = a - J.shift[0];
+        return IRREV ? (int32_t)((uint32_t)v << 11) : v;
+    }
+    int32_t r = a - J.shift[0], g = b - J.shift[1], bl = c - J.shift[2];
+    if constexpr (!IRREV) {
+        return J.comp == 0 ? (r + (g * 2) + bl) >> 2 : J.comp == 1 ? bl - g : r - g;
+    } else {
+        r = (int32_t)((uint32_t)r << 11); g = (int32_t)((uint32_t)g << 11); bl = (int32_t)((uint32_t)bl << 11);
+        if (J.comp == 0) return fixmul13(r, 2449) + fixmul13(g, 4809) + fixmul13(bl, 934);
+        if (J.comp == 1) return -fixmul13(r, 1382) - fixmul13(g, 2714) + fixmul13(bl, 4096);
+        return fixmul13(r, 4096) - fixmul13(g, 3430) - fixmul13(bl, 666);
+    }
+}
+
+// Window rows of a fused level 0: DC shift + MCT applied as the image planes
+// are read (3 planes for an MCT component, 1 otherwise).
+template <bool IRREV, int R>
+__device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], int32_t (&hi)[R], int xw, int yw,
+                                           int gx0, int gx1) {
+    const int rw = J.rw, rh = J.rh;
+    const int st = (int)J.src_stride * 4;
+    const bool three = J.mct_mode >= 2;
+    const rsrc_t p0 = mkbuf(J.src[0], J.src_bytes);
+    const rsrc_t p1 = mkbuf(three ? J.src[1] : J.src[0], J.src_bytes);
+    const rsrc_t p2 = mkbuf(three ? J.src[2] : J.src[0], J.src_bytes);
+    const bool vec = J.src_vec && J.casx == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
+    const bool rows_in = yw >= 0 && yw + R <= rh;
+    const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int so = (rows_in ? yw + r : mirror_idx(yw + r, rh)) * st;
+        int32_t a0, a1, b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+        if (vec) {
+            const auto a = __builtin_amdgcn_raw_buffer_load_b64(p0, gx0 * 4, so, 0);
+            a0 = (int32_t)a[0]; a1 = (int32_t)a[1];
+            if (three) {
+                const auto b = __builtin_amdgcn_raw_buffer_load_b64(p1, gx0 * 4, so, 0);
+                const auto c = __builtin_amdgcn_raw_buffer_load_b64(p2, gx0 * 4, so, 0);
+                b0 = (int32_t)b[0]; b1 = (int32_t)b[1]; c0 = (int32_t)c[0]; c1 = (int32_t)c[1];
+            }
+        } else {
+            a0 = ld32(p0, o0, so); a1 = ld32(p0, o1, so);
+            if (three) { b0 = ld32(p1, o0, so); b1 = ld32(p1, o1, so); c0 = ld32(p2, o0, so); c1 = ld32(p2, o1, so); }
+        }
+        lo[r] = mct_px<IRREV>(J, a0, b0, c0);
+        hi[r] = mct_px<IRREV>(J, a1, b1, c1);
+    }
+}
+
+// FUSED: 0 = reads `in`; 1 = DC shift fused into the loads (fused_load);
+// 2 = the three MCT components of one window in one workgroup of 3
+// wavefronts (wavefront w = component w): each loads its own image plane,
+// the raw rows are exchanged through LDS, and each wavefront forms its MCT
+// component -- every image sample is read from HBM once.
+template <bool IRREV, int TH, int XM = 0, int FUSED = 0>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__restrict__ jobs, int lay) {
     constexpr bool NOCOMP = XM != 0;  // timing probes: 1 no lifting, 2 loads only, 3 stores only
     using G = DwtGeo<IRREV, TH>;
     constexpr int R = G::R;
     DwtJob J;
     int tx, ty;
-    if (!dwt_window(jobs, lay, TH, J, tx, ty)) return;
+    if constexpr (FUSED == 2) {
+        const int gx = gridDim.x;
+        int L = blockIdx.y * gx + blockIdx.x;
+        if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+        const int wg = L % gx, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        J = jobs[(L / gx) * 3 + w];
+        tx = wg % J.tiles_x;
+        ty = wg / J.tiles_x;
+        if (ty >= (J.rh + J.casy + TH - 1) / TH) return;  // same for the 3 wavefronts
+    } else {
+        if (!dwt_window(jobs, lay, TH, J, tx, ty)) return;
+    }
     const int lane = threadIdx.x & 63;
     const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
     const int xw = tx * G::CW - casx - G::HALO;  // window column origin (parity of casx)
@@ -161,16 +240,21 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
     if (XM == 3) {
 #pragma unroll
         for (int r = 0; r < R; ++r) { lo[r] = lane + r; hi[r] = lane - r; }
+    } else if (FUSED == 1) {
+        fused_load<IRREV, R>(J, lo, hi, xw, yw, gx0, gx1);
     } else {
-        const rsrc_t in = mkbuf(J.in, J.in_bytes);
-        const int st = (int)J.in_stride * 4;
-        const bool vec = (casx | (J.in_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int32_t *sp = w == 0 ? J.src[0] : w == 1 ? J.src[1] : J.src[2];  // no dynamic struct index
+        const rsrc_t in = FUSED == 2 ? mkbuf(sp, J.src_bytes) : mkbuf(J.in, J.in_bytes);
+        const int st = (int)(FUSED == 2 ? J.src_stride : J.in_stride) * 4;
+        const bool vec = (FUSED == 2 ? J.src_vec && !casx : (casx | (J.in_stride & 1)) == 0) && xw >= 0 &&
+                         xw + DWT_WIN <= rw;  // wave-uniform
         const bool rows_in = yw >= 0 && yw + R <= rh;  // no row mirroring: offsets are base + r * stride
         if (vec && rows_in) {
             const int base = yw * st;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, base + r * st, LAUX);
+                const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, base + r * st, 0);
                 lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
             }
         } else if (vec) {
@@ -186,6 +270,21 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
                 const int so = mirror_idx(yw + r, rh) * st;
                 lo[r] = ld32(in, o0, so); hi[r] = ld32(in, o1, so);
             }
+        }
+    }
+    if constexpr (FUSED == 2) {  // exchange the raw planes, form this wavefront's MCT component
+        __shared__ int32_t xs[3][R][DWT_WIN];
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            xs[w][r][2 * lane] = lo[r];
+            xs[w][r][2 * lane + 1] = hi[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            lo[r] = mct_px<IRREV>(J, xs[0][r][2 * lane], xs[1][r][2 * lane], xs[2][r][2 * lane]);
+            hi[r] = mct_px<IRREV>(J, xs[0][r][2 * lane + 1], xs[1][r][2 * lane + 1], xs[2][r][2 * lane + 1]);
         }
     }
     // vertical (position = window row; even rows are low pass)
@@ -256,12 +355,12 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
         }
         if ((r & 1) == 0) {  // low row -> LL | HL
             const int iy = lbase + r / 2;
-            st32<SAUX>(L, outb, vl, iy * ost);
-            st32<SAUX>(H, bandb, vh, iy * bst);
+            st32(L, outb, vl, iy * ost);
+            st32(H, bandb, vh, iy * bst);
         } else {             // high row -> LH | HH
             const int so = (hbase + (r - 1) / 2) * bst;
-            st32<SAUX>(L, bandb, vl, so);
-            st32<SAUX>(H, bandb, vh, so);
+            st32(L, bandb, vl, so);
+            st32(H, bandb, vh, so);
         }
     }
 }
@@ -708,7 +807,8 @@ void dwt_job_tiles(int irrev, int code, int rw, int rh, int casx, int casy, int3
 }
 
 template <int TH>
-static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int nch, hipStream_t s) {
+static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int nch, int fused,
+                      hipStream_t s) {
     const int lay = env_int("GRKGPU_DWT_LAY", 1);
     if (nch) {
         if (!inverse) {
@@ -720,18 +820,20 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         }
         return;
     }
-    if (!inverse && TH == 24 && irrev && env_int("GRKGPU_DWT_X", 0)) {  // timing probes
-        switch (env_int("GRKGPU_DWT_X", 0)) {
-            case 1: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1>), grid, block, 0, s, jobs, lay); break;
-            case 8: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 2>), grid, block, 0, s, jobs, lay); break;
-            case 9: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 3>), grid, block, 0, s, jobs, lay); break;
-            case 2: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 2, 0>), grid, block, 0, s, jobs, lay); break;
-            case 3: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 0, 2>), grid, block, 0, s, jobs, lay); break;
-            case 4: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 2, 2>), grid, block, 0, s, jobs, lay); break;
-            case 5: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1, 2, 2>), grid, block, 0, s, jobs, lay); break;
-            case 6: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 1, 1>), grid, block, 0, s, jobs, lay); break;
-            default: hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 3, 3>), grid, block, 0, s, jobs, lay); break;
-        }
+    if (!inverse && TH == 24 && irrev && env_int("GRKGPU_DWT_X", 0)) {  // timing probes: 1 no lifting, 2 loads only
+        if (env_int("GRKGPU_DWT_X", 0) == 1) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1>), grid, block, 0, s, jobs, lay);
+        else hipLaunchKernelGGL((k_dwt_fwd<true, TH, 2>), grid, block, 0, s, jobs, lay);
+        return;
+    }
+    if (fused == 2) {  // forward level 0, MCT triples: workgroup = the 3 components of one window
+        const dim3 g3(grid.x * DWT_WAVES, grid.y / 3), b3(192);
+        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 2>), g3, b3, 0, s, jobs, lay);
+        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 2>), g3, b3, 0, s, jobs, lay);
+        return;
+    }
+    if (fused == 1) {  // forward level 0 with the DC shift in the loads
+        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 1>), grid, block, 0, s, jobs, lay);
+        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 1>), grid, block, 0, s, jobs, lay);
         return;
     }
     if (!inverse) {
@@ -747,12 +849,13 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
                            int inverse, hipStream_t s) {
     if (!njobs || !max_tiles) return hipSuccess;
     dim3 grid((max_tiles + DWT_WAVES - 1) / DWT_WAVES, njobs), block(64 * DWT_WAVES);
-    const int nch = code >> 8;
+    const int nch = (code >> 8) & 0xff;
+    const int fused = inverse || nch ? 0 : (code & DWT_FUSED_MCT3) ? 2 : (code & DWT_FUSED) ? 1 : 0;
     switch (code & 0xff) {
-        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, s); break;
-        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, s); break;
-        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, nch, s); break;
-        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, nch, s); break;
+        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
+        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
+        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
+        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

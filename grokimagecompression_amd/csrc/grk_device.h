@@ -56,10 +56,21 @@ struct DwtJob {
     uint32_t in_bytes, coef_bytes, out_bytes, bands_bytes;      // buffer extents
     int32_t rw, rh, casx, casy, snx, sny;
     int32_t tiles_x, ntiles;
+    // Forward level 0 with the DC shift + MCT fused into its loads
+    // (TileProcessor.cpp:1449-1471, mct.cpp:85-139 / 195-350): the window is
+    // read from the image planes instead of `in`.  mct_mode 0: not fused;
+    // 1: DC shift of src[0]; 2: RCT output component `comp` of src[0..2];
+    // 3: ICT output component `comp`.
+    const int32_t *src[3];      // image planes at the tile origin
+    uint32_t src_stride, src_bytes;  // elements; bytes from src[i] to its plane's end (min)
+    int32_t shift[3];
+    int32_t mct_mode, comp, src_vec;  // src_vec: 8-byte loads allowed (aligned base, even stride)
 };
 // level geometry code (window rows | strip windows << 8) for a level of that
 // many samples whose smallest resolution is minw x minh
 int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh);
+constexpr int DWT_FUSED = 1 << 16;       // geometry-code flag: forward level with fused DC shift loads
+constexpr int DWT_FUSED_MCT3 = 1 << 17;  // ... with fused DC shift + MCT (jobs in component triples)
 void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
                            int inverse, hipStream_t s);

@@ -47,6 +47,19 @@ def test_decode_matches_reference(codec, name):
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
 
+@pytest.mark.parametrize("name", ["g8_off35", "rgb12_I", "rgb8_128x96", "rgb12_tiles_I", "g16_I", "rgb8_nomct",
+                                  "g8_off_tiles"])
+def test_encode_fused_mct_dwt(codec, monkeypatch, name):
+    """Opt-in fused level 0 (DC shift + MCT in the first DWT level's loads,
+    GRKGPU_DWT_FUSE=1): same bytes as the reference."""
+    import grokimagecompression_amd as grk
+    monkeypatch.setenv("GRKGPU_DWT_FUSE", "1")
+    m = MAN[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    assert codec.compress(img, bits, p, offset=off) == open(f"{GOLD}/{name}.j2k", "rb").read()
+
+
 def test_device_resident_roundtrip(codec):
     import torch
     import grokimagecompression_amd as grk
