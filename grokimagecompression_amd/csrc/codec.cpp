@@ -78,7 +78,7 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf, mqsort;
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
@@ -430,6 +430,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     HIPCHK(c->results.ensure((size_t)nblk * sizeof(EncResult) + 256));
+    HIPCHK(c->mqsort.ensure(t1_mq_sort_words(nblk) * 4 + 256));
     HIPCHK(c->h_results.ensure((size_t)nblk * sizeof(EncResult) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     symoff.push_back(sym_total);
@@ -508,7 +509,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
-                            c->results.as<EncResult>(), s));
+                            c->results.as<EncResult>(), s, c->mqsort.as<uint32_t>()));
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipMemcpyAsync(c->h_results.p, c->results.p, (size_t)nblk * sizeof(EncResult), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -795,12 +796,12 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
-    // The decoder runs one code-block per lane, 64 per wavefront, so a
-    // wavefront lasts as long as its longest block.  Order the blocks by
-    // segment length (longest first; counting sort on len / 32) so each
-    // wavefront gets blocks of similar length.  Block order is free: every
-    // DecBlock carries its own destination (GRKGPU_T1_SORT=0 keeps T2 order).
-    if (!getenv("GRKGPU_T1_SORT") || atoi(getenv("GRKGPU_T1_SORT")) != 0) {
+    // GRKGPU_T1_SORT=1: deal the blocks to decoder lanes longest segment
+    // first (counting sort on len / 32), so the 64 blocks of a wavefront end
+    // together.  Block order is free (every DecBlock carries its destination).
+    // Off by default: no gain measured with 12 frames in flight (2390-2450
+    // Mpix/s either way over 6-step runs) and 2 % slower for a lone frame.
+    if (getenv("GRKGPU_T1_SORT") && atoi(getenv("GRKGPU_T1_SORT")) != 0) {
         constexpr uint32_t NB = 4096;
         std::vector<uint32_t> cnt(NB + 1, 0);
         auto key = [](const DecBlock &d) { return NB - 1 - std::min<uint32_t>(d.len >> 5, NB - 1); };

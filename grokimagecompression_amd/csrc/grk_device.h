@@ -79,7 +79,9 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s);
+                            hipStream_t s, uint32_t *sortbuf = nullptr);
+// words of launch_t1_encode's sortbuf for n blocks (MQ lane order)
+inline size_t t1_mq_sort_words(uint32_t n) { return 1024 + 2 * (size_t)n; }
 // ubuf (optional): unstuffed-stream arena for the v4 decoder, block i's region
 // at blocks[i].pad * 16 bytes (t1_unstuff_region_words); null selects v3.
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,

@@ -193,18 +193,59 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
                    S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4);
 }
 
-// MQ coding, one lane per block.
+// MQ lane order.  A wavefront of the MQ kernel codes 64 blocks, one per lane,
+// and lasts as long as its longest block, so the blocks are dealt to lanes
+// longest first (symbol count from the modelling pass): a bucketed counting
+// sort in three small kernels -- keys + histogram, exclusive scan, scatter.
+constexpr uint32_t MQ_BUCKETS = 1024;
+
+__global__ __launch_bounds__(256) void k_mq_keys(const T1Scratch *__restrict__ scr, const EncResult *__restrict__ res,
+                                                 uint32_t n, uint32_t *__restrict__ key, uint32_t *__restrict__ hist) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t nb = min(res[i].numbps, 32u);
+    const uint32_t *c = scr[i].cnt;
+    uint32_t tot = 0;
+    for (uint32_t p = 0; p < nb; ++p) tot += c[p * 4] + c[p * 4 + 1] + c[p * 4 + 2];
+    const uint32_t b = MQ_BUCKETS - 1 - min(tot >> 6, MQ_BUCKETS - 1);  // longest first
+    key[i] = b;
+    atomicAdd(&hist[b], 1u);
+}
+
+__global__ __launch_bounds__(MQ_BUCKETS) void k_mq_scan(uint32_t *__restrict__ hist) {
+    __shared__ uint32_t s[MQ_BUCKETS];
+    const uint32_t t = threadIdx.x, own = hist[t];
+    s[t] = own;
+    __syncthreads();
+    for (uint32_t off = 1; off < MQ_BUCKETS; off <<= 1) {
+        const uint32_t v = t >= off ? s[t - off] : 0u;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    hist[t] = s[t] - own;  // exclusive prefix = first slot of bucket t
+}
+
+__global__ __launch_bounds__(256) void k_mq_scatter(const uint32_t *__restrict__ key, uint32_t *__restrict__ slot,
+                                                    uint32_t n, uint32_t *__restrict__ perm) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    perm[atomicAdd(&slot[key[i]], 1u)] = i;
+}
+
+// MQ coding, one lane per block (lane j codes block perm[j], or j).
 template <int LANES, int MINW = 1>
 __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
                                                  const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
-                                                 EncResult *__restrict__ res) {
+                                                 EncResult *__restrict__ res, const uint32_t *__restrict__ perm) {
     __shared__ uint32_t s_mq[48];
     __shared__ uint32_t s_cx[LANES * 33];  // 19 contexts + read-ahead slack; odd stride: no bank conflicts
     for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
-    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t j = blockIdx.x * LANES + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = perm ? perm[j] : j;
     const EncBlock b = blocks[i];
     EncResult &r = res[i];
     if (r.pad) return;
@@ -495,20 +536,20 @@ static int mq_minw() {
 
 template <int L>
 static void launch_mq(const EncBlock *blocks, uint32_t n, const T1Scratch *scr, const uint8_t *sym,
-                      const uint64_t *sym_off, uint8_t *out, EncResult *res, hipStream_t s) {
+                      const uint64_t *sym_off, uint8_t *out, EncResult *res, const uint32_t *perm, hipStream_t s) {
     const dim3 g((n + L - 1) / L);
     switch (mq_minw()) {
-        case 2: hipLaunchKernelGGL((k_t1_mq<L, 2>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
-        case 4: hipLaunchKernelGGL((k_t1_mq<L, 4>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
-        case 6: hipLaunchKernelGGL((k_t1_mq<L, 6>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
-        case 8: hipLaunchKernelGGL((k_t1_mq<L, 8>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
-        default: hipLaunchKernelGGL((k_t1_mq<L, 1>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res); break;
+        case 2: hipLaunchKernelGGL((k_t1_mq<L, 2>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
+        case 4: hipLaunchKernelGGL((k_t1_mq<L, 4>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
+        case 6: hipLaunchKernelGGL((k_t1_mq<L, 6>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
+        case 8: hipLaunchKernelGGL((k_t1_mq<L, 8>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
+        default: hipLaunchKernelGGL((k_t1_mq<L, 1>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
     }
 }
 
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t *sortbuf) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
     static const bool lane = getenv("GRKGPU_T1_ENC") && !strcmp(getenv("GRKGPU_T1_ENC"), "lane");
@@ -525,12 +566,26 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res);
+    // sortbuf (MQ_BUCKETS + 2n words): histogram / bucket slots, keys, permutation
+    const uint32_t *perm = nullptr;
+    // GRKGPU_MQ_SORT=1 (off by default: no measured gain, see codec.cpp T1_SORT)
+    static const bool sort = getenv("GRKGPU_MQ_SORT") && atoi(getenv("GRKGPU_MQ_SORT")) != 0;
+    if (sortbuf && sort) {
+        uint32_t *hist = sortbuf, *key = sortbuf + MQ_BUCKETS, *pm = key + n;
+        hipError_t e = hipMemsetAsync(hist, 0, MQ_BUCKETS * 4, s);
+        if (e != hipSuccess) return e;
+        const dim3 g((n + 255) / 256);
+        hipLaunchKernelGGL(k_mq_keys, g, dim3(256), 0, s, scratch, res, n, key, hist);
+        hipLaunchKernelGGL(k_mq_scan, dim3(1), dim3(MQ_BUCKETS), 0, s, hist);
+        hipLaunchKernelGGL(k_mq_scatter, g, dim3(256), 0, s, key, hist, n, pm);
+        perm = pm;
+    }
     switch (t1_mq_lanes()) {
-        case 4: launch_mq<4>(blocks, n, scratch, sym, sym_off, out, res, s); break;
-        case 8: launch_mq<8>(blocks, n, scratch, sym, sym_off, out, res, s); break;
-        case 16: launch_mq<16>(blocks, n, scratch, sym, sym_off, out, res, s); break;
-        case 64: launch_mq<64>(blocks, n, scratch, sym, sym_off, out, res, s); break;
-        default: launch_mq<32>(blocks, n, scratch, sym, sym_off, out, res, s); break;
+        case 4: launch_mq<4>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
+        case 8: launch_mq<8>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
+        case 16: launch_mq<16>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
+        case 64: launch_mq<64>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
+        default: launch_mq<32>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
     }
     return hipGetLastError();
 }
