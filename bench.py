@@ -29,7 +29,16 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden"), os.path.join(ROOT, 
 # reads the value when the process starts, so with fewer than 16 the bench
 # reruns itself as a child process with 16 (nothing has touched the GPU yet)
 # and exits with the child's status.
-HW_QUEUES = 16
+def _concurrency_arg():
+    for i, a in enumerate(sys.argv):
+        if a.startswith("--concurrency"):
+            v = a.split("=", 1)[1] if "=" in a else (sys.argv[i + 1] if i + 1 < len(sys.argv) else "12")
+            return int(v)
+    return 12
+
+
+# one hardware queue per codec stream plus torch's own (gpurun caps the knob at 32)
+HW_QUEUES = min(32, max(16, _concurrency_arg() + 4))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < HW_QUEUES:
     import subprocess
     sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, GPU_MAX_HW_QUEUES=str(HW_QUEUES))))

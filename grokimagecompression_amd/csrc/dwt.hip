@@ -211,7 +211,7 @@ __device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], in
 // wavefronts (wavefront w = component w): each loads its own image plane,
 // the raw rows are exchanged through LDS, and each wavefront forms its MCT
 // component -- every image sample is read from HBM once.
-template <bool IRREV, int TH, int XM = 0, int FUSED = 0>
+template <bool IRREV, int TH, int XM = 0, int FUSED = 0, int BAUX = 0>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__restrict__ jobs, int lay) {
     constexpr bool NOCOMP = XM != 0;  // timing probes: 1 no lifting, 2 loads only, 3 stores only
     using G = DwtGeo<IRREV, TH>;
@@ -356,11 +356,11 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
         if ((r & 1) == 0) {  // low row -> LL | HL
             const int iy = lbase + r / 2;
             st32(L, outb, vl, iy * ost);
-            st32(H, bandb, vh, iy * bst);
+            st32<BAUX>(H, bandb, vh, iy * bst);
         } else {             // high row -> LH | HH
             const int so = (hbase + (r - 1) / 2) * bst;
-            st32(L, bandb, vl, so);
-            st32(H, bandb, vh, so);
+            st32<BAUX>(L, bandb, vl, so);
+            st32<BAUX>(H, bandb, vh, so);
         }
     }
 }
@@ -837,6 +837,11 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         return;
     }
     if (!inverse) {
+        if (env_int("GRKGPU_DWT_BNT", 0)) {  // probe: band stores non-temporal (LL stays cached)
+            if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 0, 2>), grid, block, 0, s, jobs, lay);
+            else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 0, 2>), grid, block, 0, s, jobs, lay);
+            return;
+        }
         if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH>), grid, block, 0, s, jobs, lay);
         else hipLaunchKernelGGL((k_dwt_fwd<false, TH>), grid, block, 0, s, jobs, lay);
     } else {

@@ -27,6 +27,15 @@ __device__ __forceinline__ int32_t fix_mul13(int32_t a, int32_t b) {
 
 // src: image planes (row stride sstride), dst: tile-component buffers
 // (row stride tw).  One thread per sample of the tile.
+template <bool NT>
+__device__ __forceinline__ void put(int32_t *p, int32_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// NT: non-temporal stores (the output is streamed to HBM instead of lingering
+// dirty in the caches for the next kernel to evict).
+template <bool NT>
 __global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst, uint32_t tw, uint32_t th,
                                   uint32_t ncomp, ShiftArr shift, int32_t mct, int32_t irrev) {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,12 +56,12 @@ __global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst
             o1 = -fix_mul13(r, 1382) - fix_mul13(g, 2714) + fix_mul13(b, 4096);
             o2 = fix_mul13(r, 4096) - fix_mul13(g, 3430) - fix_mul13(b, 666);
         }
-        dst.p[0][di] = o0; dst.p[1][di] = o1; dst.p[2][di] = o2;
+        put<NT>(&dst.p[0][di], o0); put<NT>(&dst.p[1][di], o1); put<NT>(&dst.p[2][di], o2);
         c0 = 3;
     }
     for (uint32_t c = c0; c < ncomp; ++c) {
         int32_t v = src.p[c][si] - shift.v[c];
-        dst.p[c][di] = irrev ? (int32_t)((uint32_t)v << 11) : v;
+        put<NT>(&dst.p[c][di], irrev ? (int32_t)((uint32_t)v << 11) : v);
     }
 }
 
@@ -448,7 +457,17 @@ hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const 
                                   uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct, int32_t irrev,
                                   hipStream_t s) {
     dim3 grid((tw + 255) / 256, th);
-    hipLaunchKernelGGL(k_dcshift_mct_fwd, grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, shift, mct, irrev);
+    // Non-temporal output stores by default (GRKGPU_MCT_NT=0: plain stores):
+    // with plain stores the 8 B/sample this pass writes sit dirty in L2 / MALL
+    // and are written back while the first DWT level runs, which then reads
+    // at ~4 TB/s instead of ~6 (scripts/probe/read_pattern.hip "dirty 1").
+    // Measured on the 8K frame: MCT 0.137 -> 0.150 ms, 9/7 DWT 0.255 -> 0.239.
+    if (!getenv("GRKGPU_MCT_NT") || atoi(getenv("GRKGPU_MCT_NT")))
+        hipLaunchKernelGGL(k_dcshift_mct_fwd<true>, grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, shift, mct,
+                           irrev);
+    else
+        hipLaunchKernelGGL(k_dcshift_mct_fwd<false>, grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, shift,
+                           mct, irrev);
     return hipGetLastError();
 }
 
@@ -569,7 +588,7 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     // sortbuf (MQ_BUCKETS + 2n words): histogram / bucket slots, keys, permutation
     const uint32_t *perm = nullptr;
     // GRKGPU_MQ_SORT=1 (off by default: no measured gain, see codec.cpp T1_SORT)
-    static const bool sort = getenv("GRKGPU_MQ_SORT") && atoi(getenv("GRKGPU_MQ_SORT")) != 0;
+    const bool sort = getenv("GRKGPU_MQ_SORT") && atoi(getenv("GRKGPU_MQ_SORT")) != 0;  // read per call (tests)
     if (sortbuf && sort) {
         uint32_t *hist = sortbuf, *key = sortbuf + MQ_BUCKETS, *pm = key + n;
         hipError_t e = hipMemsetAsync(hist, 0, MQ_BUCKETS * 4, s);
