@@ -207,6 +207,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
 // longest first (symbol count from the modelling pass): a bucketed counting
 // sort in three small kernels -- keys + histogram, exclusive scan, scatter.
 constexpr uint32_t MQ_BUCKETS = 1024;
+constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
 
 __global__ __launch_bounds__(256) void k_mq_keys(const T1Scratch *__restrict__ scr, const EncResult *__restrict__ res,
                                                  uint32_t n, uint32_t *__restrict__ key, uint32_t *__restrict__ hist) {
@@ -249,7 +250,12 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
                                                  EncResult *__restrict__ res, const uint32_t *__restrict__ perm) {
     __shared__ uint32_t s_mq[48];
-    __shared__ uint32_t s_cx[LANES * 33];  // 19 contexts + read-ahead slack; odd stride: no bank conflicts
+    // 19 context words per lane at an odd stride (no bank conflicts).  The
+    // read-ahead of the symbol after a pass's last one may index up to 31
+    // (its value is never used): a lane's slots plus the tail slack keep it
+    // inside the array.  21 words per lane (not 32) keeps LDS from limiting
+    // the occupancy: 5.6 KB per 64-lane workgroup -> 7 wavefronts per SIMD.
+    __shared__ uint32_t s_cx[LANES * MQ_CX_STRIDE + 32];
     for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
     const uint32_t j = blockIdx.x * LANES + threadIdx.x;
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     const uint64_t off = sym_block_off(sym_off, i, &cap);
     uint32_t len;
     uint32_t np = t1_mq_block(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
-                              s_cx + threadIdx.x * 33, (uint32_t *)(out + b.out_off), r.rate, &len);
+                              s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len);
     r.numpasses = np;
     r.len = len;
 }

@@ -256,23 +256,20 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
     for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
         uint64_t *sa = sigafter + (uint32_t)bpno * 64;
         uint64_t *rb = refbit + (uint32_t)bpno * 64;
+        // Each pass type loads and stores only the state rows it reads or
+        // changes (SPP / CUP: sig, neg, vis; MRP: sig, vis, ref + the
+        // refinement bits), so no row is live across the three branches:
+        // fewer VGPRs for the lane decoder and fewer state round trips.
         for (uint32_t k = 0; k < h; k += 4) {
+            const uint32_t nr = h - k < 4 ? h - k : 4;
             Stripe s;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) { s.sig[i] = st.sig[k + i]; s.neg[i] = st.neg[k + i]; }
+            for (int i = 0; i < 6; ++i) s.sig[i] = st.sig[k + i];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { s.vis[i] = st.vis[k + 1 + i]; s.ref[i] = st.ref[k + 1 + i]; s.bit[i] = 0; }
-            const uint32_t nr = h - k < 4 ? h - k : 4;
-            if (passtype == 0) {
-                uint64_t cand = spp_candidates(s, nr) & wm;
-                while (cand) {
-                    const uint32_t x = ctz64(cand);
-                    const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
-                    const bool grew = d3_column<false>(d, cxw, T, s, x, nr);
-                    cand &= ~done;
-                    if (grew) cand = spp_candidates(s, nr) & wm & ~done;
-                }
-            } else if (passtype == 1) {
+            for (int i = 0; i < 4; ++i) s.vis[i] = st.vis[k + 1 + i];
+            if (passtype == 1) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { s.ref[i] = st.ref[k + 1 + i]; s.bit[i] = 0; }
                 uint64_t mem = 0;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
@@ -281,6 +278,24 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                     const uint32_t x = ctz64(mem);
                     mem &= mem - 1;
                     d3_mrp_column(d, cxw, T, s, x, nr);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    st.ref[k + 1 + i] = s.ref[i];
+                    if ((uint32_t)i < nr) rb[k + i] = s.bit[i];
+                }
+                continue;
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) s.neg[i] = st.neg[k + i];
+            if (passtype == 0) {
+                uint64_t cand = spp_candidates(s, nr) & wm;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
+                    const bool grew = d3_column<false>(d, cxw, T, s, x, nr);
+                    cand &= ~done;
+                    if (grew) cand = spp_candidates(s, nr) & wm & ~done;
                 }
             } else {
                 uint64_t cand = 0;
@@ -301,11 +316,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                 st.sig[k + 1 + i] = s.sig[i + 1];
                 st.neg[k + 1 + i] = s.neg[i + 1];
                 st.vis[k + 1 + i] = s.vis[i];
-                st.ref[k + 1 + i] = s.ref[i];
-                if ((uint32_t)i < nr) {
-                    if (passtype == 1) rb[k + i] = s.bit[i];
-                    else sa[k + i] = s.sig[i + 1];
-                }
+                if ((uint32_t)i < nr) sa[k + i] = s.sig[i + 1];
             }
         }
         if (++passtype == 3) { passtype = 0; bpno--; }
