@@ -13,14 +13,21 @@ import synth
 configs = [a for a in sys.argv[1:]] or ["4k", "8k"]
 codec = grk.Codec(0)
 for cfg in configs:
-    if cfg == "4k":
-        h, w, c, bits, modes = 2160, 3840, 3, 8, [False]
-    else:
-        h, w, c, bits, modes = 4320, 7680, 3, 12, [True, False]
-    img = synth.synth_image(h, w, c, bits, 3)
+    kw = {}
+    if cfg == "512":  # BASELINE configs[0]
+        h, w, c, bits, modes, seed = 512, 512, 1, 8, [False], 1
+    elif cfg == "4k":  # configs[1]
+        h, w, c, bits, modes, seed = 2160, 3840, 3, 8, [False], 2
+    elif cfg == "16k":  # configs[3]: 1024^2 tiles, 7 resolutions (6 DWT levels)
+        h, w, c, bits, modes, seed = 16384, 16384, 1, 16, [False], 4
+        kw = dict(numresolution=7, tiles=(1024, 1024))
+    else:  # configs[2]
+        h, w, c, bits, modes, seed = 4320, 7680, 3, 12, [True, False], 3
+    img = synth.synth_image(h, w, c, bits, seed)
     t = torch.from_numpy(img).cuda()
+    del img
     for irrev in modes:
-        p = grk.CParams.make(irreversible=irrev)
+        p = grk.CParams.make(irreversible=irrev, **kw)
         for it in range(3):
             torch.cuda.synchronize()
             t0 = time.time()
