@@ -792,7 +792,8 @@ int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh) {
         nch = nch < 1 ? 1 : (nch > 255 ? 255 : nch);
         return th | (nch << 8);
     }
-    return level_samples >= (1u << 22) ? dwt_th_big(irrev) : 8;
+    // tall windows only where they still fill the chip (GRKGPU_DWT_BIGMIN samples)
+    return level_samples >= (uint64_t)env_int("GRKGPU_DWT_BIGMIN", 1 << 23) ? dwt_th_big(irrev) : 8;
 }
 
 void dwt_job_tiles(int irrev, int code, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles) {
