@@ -295,7 +295,9 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                     const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
                     const bool grew = d3_column<false>(d, cxw, T, s, x, nr);
                     cand &= ~done;
-                    if (grew) cand = spp_candidates(s, nr) & wm & ~done;
+                    // a new significant sample in column x can only make
+                    // column x + 1 a candidate (x - 1 is behind the scan)
+                    if (grew) cand |= ((uint64_t)2 << x) & wm;
                 }
             } else {
                 uint64_t cand = 0;

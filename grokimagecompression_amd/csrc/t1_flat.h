@@ -99,14 +99,15 @@ GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, u
 // ---------------------------------------------------------------------------
 // Bit reader over the unstuffed words: 64-bit MSB-aligned window W holding
 // NB >= 32 valid bits after every refill; 4-word chunks (uint4) are fetched
-// one chunk ahead.  Past the end it returns 1-bits.
+// when the current one is used up (no prefetch register: the decoder's VGPR
+// budget sets its occupancy).  Past the end it returns 1-bits.
 // ---------------------------------------------------------------------------
 struct FlatBits {
     uint64_t W;
     uint32_t NB;
-    uint4 cur, nxt;
+    uint4 cur;
     uint32_t wi;            // next word of `cur` (0..3)
-    uint32_t chunk;         // index of the chunk held in `nxt`
+    uint32_t chunk;         // index of the chunk held in `cur`
     uint32_t nchunks;
     const uint4 *base;
 };
@@ -119,8 +120,7 @@ GRK_HD uint32_t fb_word(FlatBits &b) {
     const uint32_t v = b.wi == 0 ? b.cur.x : b.wi == 1 ? b.cur.y : b.wi == 2 ? b.cur.z : b.cur.w;
     if (++b.wi == 4) {
         b.wi = 0;
-        b.cur = b.nxt;
-        b.nxt = fb_load(b, ++b.chunk);
+        b.cur = fb_load(b, ++b.chunk);  // no chunk prefetch: 4 VGPRs fewer (decoder occupancy)
     }
     return v;
 }
@@ -137,8 +137,7 @@ struct BitDec {
         bits.base = (const uint4 *)words;
         bits.nchunks = (nwords + 3) >> 2;
         bits.cur = fb_load(bits, 0);
-        bits.nxt = fb_load(bits, 1);
-        bits.chunk = 1;
+        bits.chunk = 0;
         bits.wi = 0;
         const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
         const uint64_t v = (w0 << 32) | w1;
