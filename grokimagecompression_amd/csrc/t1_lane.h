@@ -837,8 +837,8 @@ GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_
         }                                                                 \
     }
         while (total - i >= 16) {  // full chunks
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
+#pragma unroll 1
+            for (int q = 0; q < 4; ++q) {  // not unrolled: keeps the kernel's code small (I-cache)
                 uint32_t cur = q == 0 ? c0.x : q == 1 ? c0.y : q == 2 ? c0.z : c0.w;
                 const uint32_t nxt = q == 0 ? c0.y : q == 1 ? c0.z : q == 2 ? c0.w : c1.x;
 #pragma unroll
