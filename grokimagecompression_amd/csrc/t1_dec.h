@@ -178,44 +178,37 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     }
     uint32_t Q = 0, newsig = 0, newneg = 0, newvis = 0, si = 0;
     bool haveQ = false;
+    // The symbol-kind transitions are selects, not branches: the 64 lanes of
+    // a wavefront sit in different kinds, and every branch taken by any lane
+    // costs the whole wavefront its exec-mask bookkeeping.
     for (;;) {
-        uint32_t cx;
-        if (kind == 0) cx = T.zc[(P >> (3 * r)) & 0x1FF];
-        else if (kind == 1) cx = si & 0x7f;
-        else cx = kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
+        const uint32_t sh = 3 * r;
+        const uint32_t zcx = T.zc[(P >> sh) & 0x1FF];  // read for every kind (LDS, in bounds)
+        const uint32_t cx = kind == 0 ? zcx : kind == 1 ? (si & 0x7f) : kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
         const uint32_t bit = d.decode(cxw, T.mq, cx);
-        bool advance = true;
-        if (kind == 0) {
-            if (!CUP) newvis |= 1u << r;
-            if (bit) { kind = 1; advance = false; }
-        } else if (kind == 1) {
-            const uint32_t sg = bit ^ (si >> 7);
-            P |= 1u << (3 * r + 4);
-            Q |= sg << (3 * r + 4);
-            newsig |= 1u << r;
-            newneg |= sg << r;
-            // the sample below now has a significant neighbour (SPP)
-            if (!CUP) todo |= (rows & ~(sig4 | vis4)) & (2u << r);
-            kind = 0;
-        } else if (kind == 2) {
-            if (!bit) break;
-            kind = 3; advance = false;
-        } else if (kind == 3) {
-            r = bit << 1; kind = 4; advance = false;
-        } else {
-            r |= bit;
-            todo = rows & ~((2u << r) - 1);  // the rows after the run are plain ZC
-            kind = 1; advance = false;
-        }
+        if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
+        const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;
+        if (!CUP) newvis |= k0 ? 1u << r : 0u;
+        // SC: the sample is significant with sign sg
+        const uint32_t sg = bit ^ (si >> 7);
+        P |= k1 ? 1u << (sh + 4) : 0u;
+        Q |= k1 ? sg << (sh + 4) : 0u;
+        newsig |= k1 ? 1u << r : 0u;
+        newneg |= k1 ? sg << r : 0u;
+        // the sample below now has a significant neighbour (SPP)
+        if (!CUP) todo |= k1 ? (rows & ~(sig4 | vis4)) & (2u << r) : 0u;
+        // UNI, UNI: the run position; the rows after it are plain ZC
+        r = k3 ? bit << 1 : k4 ? (r | bit) : r;
+        todo = k4 ? rows & ~((2u << r) - 1) : todo;
+        const bool advance = k1 || (k0 && !bit);
+        kind = k0 ? bit : k1 ? 0u : kind == 2 ? 3u : k3 ? 4u : 1u;
         if (kind == 1 && !advance) {
             if (!haveQ) { Q = win18(s.neg, x); haveQ = true; }
             si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
         }
-        if (advance) {
-            todo &= ~((2u << r) - 1);
-            if (!todo) break;
-            r = (uint32_t)__builtin_ctz(todo);
-        }
+        todo = advance ? todo & ~((2u << r) - 1) : todo;
+        if (advance && !todo) break;
+        r = advance ? (uint32_t)__builtin_ctz(todo | 0x10u) : r;
     }
     if (!CUP && newvis) setcol4(s.vis, x, newvis);
     if (newsig) {
