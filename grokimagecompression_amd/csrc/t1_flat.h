@@ -174,7 +174,7 @@ struct BitDec {
             bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
             bits.NB += 32;
         }
-        if (!keep) cxw[cx] = tw | (nmps << 31);
+        cxw[cx] = keep ? wd : (tw | (nmps << 31));  // unconditional LDS write: no branch
 #ifdef T1_TRACE
         T1_TRACE(cx, mps ^ (uint32_t)lps, A, C >> 16);
 #endif
