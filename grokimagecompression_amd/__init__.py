@@ -134,6 +134,7 @@ def lib():
         L.grkgpu_compress_tiles.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32,
                                             P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
         L.grkgpu_decompress_tiles.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, P(VP), ctypes.c_int]
+        L.grkgpu_decompress_reduced.argtypes = [VP, VP, ctypes.c_size_t, U32, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
         L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
@@ -292,10 +293,15 @@ class Codec:
         _check(lib().grkgpu_decompress_tiles(self._ctx, bp, bn, tile_begin, tile_end, ptrs, 1 if on_dev else 0))
         return out
 
-    def decompress(self, buf, device_out=False, out=None):
+    def decompress(self, buf, device_out=False, out=None, reduce=0):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
-        device_out / out is a cuda tensor)."""
+        device_out / out is a cuda tensor).  reduce > 0: the image at
+        resolution numres-1-reduce (grk_decompress -r), ceil(x / 2^reduce)
+        in every coordinate."""
         d = read_header(buf)
+        if reduce:
+            cd = lambda v: -(-v >> reduce)  # noqa: E731
+            d.x0, d.y0, d.x1, d.y1 = cd(d.x0), cd(d.y0), cd(d.x1), cd(d.y1)
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
         on_dev = device_out or (out is not None and not isinstance(out, np.ndarray))
         if on_dev:
@@ -309,7 +315,10 @@ class Codec:
                 out = np.empty((c, h, w), dtype=np.int32)
             ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
         bp, bn, keep = _buf_ptr(buf)
-        _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
+        if reduce:
+            _check(lib().grkgpu_decompress_reduced(self._ctx, bp, bn, reduce, None, ptrs, 1 if on_dev else 0))
+        else:
+            _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
         return out
 
 

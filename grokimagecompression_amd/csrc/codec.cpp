@@ -227,13 +227,24 @@ struct DwtPlan {
     std::vector<int> th;                      // window rows per level (dwt_finalize)
     std::vector<std::pair<int32_t *, const int32_t *>> copies;  // numres == 1: dst <- src
     uint64_t copy_elems = 0;
+    struct Copy2D { int32_t *dst; const int32_t *src; uint32_t dpitch, spitch, w, h; };  // elements
+    std::vector<Copy2D> copies2d;  // reduced decode at resolution 0: LL band -> compact output
     bool fused0 = false;  // forward level 0 reads the image planes (DC shift + MCT fused, dwt.hip)
     bool mct3 = false;    // ... and its jobs are MCT component triples (tile-major, component-minor)
 };
 
+// inverse with numres_dec < tc.numres (reduced-resolution decode): only the
+// levels up to resolution numres_dec - 1; the last writes that resolution
+// compactly (stride = its width) into `work`.
 static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *coef, int32_t *llbase, int irrev,
-                        bool inverse) {
+                        bool inverse, uint32_t numres_dec = 0) {
     const uint32_t stride = tc.r.w(), rows = tc.r.h();
+    if (!inverse || numres_dec == 0 || numres_dec > tc.numres) numres_dec = tc.numres;
+    if (inverse && numres_dec == 1 && tc.numres > 1) {
+        const Rect &r0 = tc.res[0].r;
+        if (r0.w() && r0.h()) P.copies2d.push_back({work, coef, r0.w(), stride, r0.w(), r0.h()});
+        return;
+    }
     if (tc.numres == 1) {
         if (inverse) P.copies.push_back({work, coef});
         else P.copies.push_back({coef, work});
@@ -244,10 +255,11 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
     int32_t *buf[2] = {llbase, llbase + ((uint64_t)g.strideA * g.rowsA + 63) / 64 * 64};
     const uint32_t bstride[2] = {g.strideA, g.strideB}, brows[2] = {g.rowsA, g.rowsB};
     const uint32_t full_bytes = (uint32_t)std::min<uint64_t>((uint64_t)stride * rows * 4, 0xffffffffu);
-    if (P.levels.size() < tc.numres - 1) P.levels.resize(tc.numres - 1);
-    for (uint32_t lvl = 0; lvl + 1 < tc.numres; ++lvl) {
+    const uint32_t nlev = inverse ? numres_dec : tc.numres;
+    if (P.levels.size() < nlev - 1) P.levels.resize(nlev - 1);
+    for (uint32_t lvl = 0; lvl + 1 < nlev; ++lvl) {
         DwtJob j{};
-        const bool last = lvl + 2 == tc.numres;
+        const bool last = lvl + 2 == nlev;
         Rect cur, lo;
         uint32_t slot;
         if (!inverse) {
@@ -276,8 +288,9 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
             j.coef = coef;
             j.coef_stride = stride;
             j.coef_bytes = full_bytes;
+            const bool compact = numres_dec < tc.numres;  // reduced: the last level's output is compact
             j.out = last ? work : buf[slot];
-            j.out_stride = last ? stride : bstride[slot];
+            j.out_stride = last ? (compact ? cur.w() : stride) : bstride[slot];
             j.out_bytes = last ? full_bytes : bstride[slot] * brows[slot] * 4;
         }
         if (!cur.w() || !cur.h()) continue;
@@ -326,6 +339,11 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
         hipError_t e = hipMemcpyAsync(cp.first, cp.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
+    for (auto &cp : P.copies2d) {
+        hipError_t e = hipMemcpy2DAsync(cp.dst, (size_t)cp.dpitch * 4, cp.src, (size_t)cp.spitch * 4, (size_t)cp.w * 4,
+                                        cp.h, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+    }
     hipError_t e = hipSuccess;
     size_t k = 0;
     for (size_t li = 0; li < P.levels.size(); ++li) {
@@ -341,8 +359,8 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
 }
 
 template <typename F>
-static void for_each_cblk(TileComp &tc, F f) {
-    for (uint32_t resno = 0; resno < tc.numres; ++resno) {
+static void for_each_cblk(TileComp &tc, F f, uint32_t maxres = 0xffffffffu) {
+    for (uint32_t resno = 0; resno < tc.numres && resno < maxres; ++resno) {
         Resolution &res = tc.res[resno];
         for (uint32_t b = 0; b < res.numbands; ++b) {
             Band &band = res.bands[b];
@@ -671,8 +689,17 @@ extern "C" int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_de
 static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
 static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
 
+static uint32_t ceil_pow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + ((1ull << r) - 1)) >> r); }
+
+// reduce > 0 (whole-image decode only): the image at resolution
+// numres - 1 - reduce (grk_decompress -r, cp_reduce, grok.h:698-702): every
+// packet is still parsed, code-blocks of the dropped resolutions are not
+// decoded, the inverse DWT stops `reduce` levels early (TileProcessor.cpp:1165,
+// TileComponent.cpp:199-204) and MCT + DC shift run on the reduced tiles; the
+// image is ceil(coordinate / 2^reduce) (j2k.cpp:1464-1476).
 static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
-                           int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te) {
+                           int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te,
+                           uint32_t reduce = 0) {
     if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     double t_start = now_ms();
     CodingParams cp;
@@ -683,13 +710,24 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         int rc = grkgpu_read_header(csb, len, img);
         if (rc) return rc;
     }
+    if (reduce >= cp.numres)  // j2k.cpp:6994
+        return set_err(GRKGPU_EINVAL, "reduce must be smaller than the number of resolutions");
+    const uint32_t numres_dec = cp.numres - reduce;
+    // output image geometry (reduced when reduce > 0)
+    const uint32_t ix0 = ceil_pow2(cp.image.x0, reduce), iy0 = ceil_pow2(cp.image.y0, reduce);
+    if (img && reduce) {
+        img->x0 = ix0; img->y0 = iy0;
+        img->x1 = ceil_pow2(cp.image.x1, reduce); img->y1 = ceil_pow2(cp.image.y1, reduce);
+    }
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th, iw = cp.image.w(), ih = cp.image.h();
+    const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th;
+    const uint32_t iw = ceil_pow2(cp.image.x1, reduce) - ix0, ih = ceil_pow2(cp.image.y1, reduce) - iy0;
     const uint64_t plane = (uint64_t)iw * ih;
     if (te > ntiles) te = ntiles;
     if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
     const bool whole = tb == 0 && te == ntiles;
+    if (reduce && !whole) return set_err(GRKGPU_EINVAL, "reduced decode of a tile range is not supported");
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
     std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
@@ -792,7 +830,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     d.len = 0;
                 }
                 db.push_back(d);
-            });
+            }, numres_dec);
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
@@ -843,7 +881,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
-                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true);
+                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true, numres_dec);
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
@@ -867,11 +905,13 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     }
     for (auto &tile : tiles) {
         PlanePtrs tsrc{}, tdst{};
+        const Rect tr = tile.comps[0].res[numres_dec - 1].r;  // the tile at the decoded resolution
+        if (!tr.w() || !tr.h()) continue;
         for (uint32_t k = 0; k < nc; ++k) {
             tsrc.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
-            tdst.p[k] = dst.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+            tdst.p[k] = dst.p[k] + (uint64_t)(tr.y0 - iy0) * iw + (tr.x0 - ix0);
         }
-        HIPCHK(launch_mct_inv_dcshift(tsrc, tile.r.w(), tile.r.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev, s));
+        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), tr.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
     if (!planes_on_device) {
@@ -907,6 +947,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
 extern "C" int grkgpu_decompress(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
                                  int32_t *const *planes, int planes_on_device) {
     return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu);
+}
+
+extern "C" int grkgpu_decompress_reduced(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t reduce,
+                                         grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device) {
+    return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, reduce);
 }
 
 extern "C" int grkgpu_decompress_tiles(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t tile_begin,

@@ -131,6 +131,13 @@ int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
 /* Whole-codestream decode into caller-provided planes (device or host). */
 int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_image_desc *img,
                       int32_t *const *planes, int planes_on_device);
+/* Reduced-resolution decode (grk_decompress -r; grk_decompress_parameters
+ * cp_reduce, grok.h:698-702, applied in j2k.cpp:1464-1476 and
+ * TileComponent.cpp:199-204): the image at resolution numres-1-reduce, every
+ * coordinate ceil(x / 2^reduce); img (if given) receives the reduced
+ * geometry.  reduce must be < the number of resolutions (GRKGPU_EINVAL). */
+int grkgpu_decompress_reduced(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t reduce,
+                              grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
 /* Decode only tiles [tile_begin, tile_end) (a tile shard; the reference's
  * tile-by-tile decode, grk_decode_tile_data / j2k.cpp decode_tiles); the
  * other tiles' samples in planes are left untouched.  Host planes are written

@@ -737,10 +737,22 @@ int orc_dwt_fwd(int32_t *buf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1
 
 /* decode_tile_53 / decode_tile_97 (transform/dwt.cpp:724, :1544): per level
  * from the lowest resolution up, horizontal then vertical. */
+/* Inverse levels for resolutions 1 .. numres_dec-1 only (reduced-resolution
+ * decode: Wavelet::decode(tilec, resno_decoded + 1), TileProcessor.cpp:1165,
+ * with minimum_num_resolutions = numres - reduce, TileComponent.cpp:199-204).
+ * The resolution geometry is the full tile's; the buffer keeps its stride. */
+static int dwt_inv_levels(int32_t *buf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t numres,
+                          uint32_t numres_dec, int32_t irreversible, int32_t nthreads);
+
 int orc_dwt_inv(int32_t *buf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1,
                 uint32_t numres, int32_t irreversible, int32_t nthreads) {
+    return dwt_inv_levels(buf, x0, y0, x1, y1, numres, numres, irreversible, nthreads);
+}
+
+static int dwt_inv_levels(int32_t *buf, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t numres,
+                          uint32_t numres_dec, int32_t irreversible, int32_t nthreads) {
     uint32_t stride = x1 - x0;
-    for (uint32_t r = 1; r < numres; ++r) {
+    for (uint32_t r = 1; r < numres_dec; ++r) {
         rect_t lo, cur;
         res_rect(&lo, x0, y0, x1, y1, numres, r - 1);
         res_rect(&cur, x0, y0, x1, y1, numres, r);
@@ -1466,6 +1478,16 @@ void orc_image_free(orc_image *img) {
 }
 
 int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads) {
+    return orc_decode_reduce(buf, len, out, nthreads, 0);
+}
+
+static uint32_t ceildivpow2_u32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + ((1ull << b) - 1)) >> b); }
+
+/* reduce > 0: decode at resolution numres-1-reduce (grk_decompress -r,
+ * cp_reduce, grok.h:698-702): every packet is parsed, the inverse DWT stops
+ * reduce levels early, MCT + DC shift run on the reduced tile-components, and
+ * the image is ceil(x / 2^reduce) in every coordinate (j2k.cpp:1464-1476). */
+int orc_decode_reduce(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads, uint32_t reduce) {
     memset(out, 0, sizeof(*out));
     if (len < 4 || rd16(buf) != 0xFF4F) return -1;
     size_t pos = 2;
@@ -1520,14 +1542,22 @@ int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads)
         pos += 2 + L;
     }
     if (!tdata || prog != 0 || cblksty != 0 || numlayers == 0) { free(tdata); return -2; }
+    if (reduce >= numres) { free(tdata); return -5; } /* j2k.cpp:6994: reduce must be < numresolutions */
+    const uint32_t numres_dec = numres - reduce;
+    const orc_image full = *out;  /* full-resolution geometry (tiles) */
+    out->x0 = ceildivpow2_u32(out->x0, reduce); out->y0 = ceildivpow2_u32(out->y0, reduce);
+    out->x1 = ceildivpow2_u32(out->x1, reduce); out->y1 = ceildivpow2_u32(out->y1, reduce);
     uint32_t iw = out->x1 - out->x0, ih = out->y1 - out->y0;
     for (uint32_t k = 0; k < nc; ++k) out->data[k] = (int32_t *)calloc(((size_t)iw * ih) != 0 ? (size_t)iw * ih : 1, sizeof(int32_t));
     int rc = 0;
     for (uint32_t tileno = 0; tileno < ntiles && rc == 0; ++tileno) {
         rect_t tr;
-        tile_rect(out, tdx, tdy, tx0, ty0, tw, tileno, &tr);
+        tile_rect(&full, tdx, tdy, tx0, ty0, tw, tileno, &tr);
         tilecomp_t *tcs = (tilecomp_t *)calloc(nc, sizeof(tilecomp_t));
-        uint64_t n = (uint64_t)(tr.x1 - tr.x0) * (tr.y1 - tr.y0);
+        rect_t rr; /* the tile at the decoded resolution; samples keep the full tile's stride */
+        res_rect(&rr, tr.x0, tr.y0, tr.x1, tr.y1, numres, numres_dec - 1);
+        const uint32_t fw = tr.x1 - tr.x0;
+        const uint64_t n = (uint64_t)fw * (tr.y1 - tr.y0);
         for (uint32_t k = 0; k < nc; ++k) {
             build_tilecomp(&tcs[k], tr, numres, cblkw, cblkh, ss, out->prec[k], (int)irrev, 0);
             tcs[k].data = (int32_t *)calloc(n ? n : 1, sizeof(int32_t));
@@ -1553,12 +1583,13 @@ int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads)
             ctx.irrev = (int)irrev;
             parallel_for(cnt, nthreads, t1_dec_job, &ctx);
             free(ctx.refs);
-            orc_dwt_inv(tcs[k].data, tr.x0, tr.y0, tr.x1, tr.y1, numres, (int32_t)irrev, nthreads);
+            dwt_inv_levels(tcs[k].data, tr.x0, tr.y0, tr.x1, tr.y1, numres, numres_dec, (int32_t)irrev, nthreads);
         }
         /* mct_decode (TileProcessor.cpp:1303-1375) */
         if (rc == 0 && mct == 1 && nc >= 3) {
             int32_t *c0 = tcs[0].data, *c1 = tcs[1].data, *c2 = tcs[2].data;
-            for (uint64_t i = 0; i < n; ++i) {
+            for (uint64_t j = 0; j < (uint64_t)(rr.x1 - rr.x0) * (rr.y1 - rr.y0); ++j) {
+                const uint64_t i = (j / (rr.x1 - rr.x0)) * fw + j % (rr.x1 - rr.x0);
                 if (!irrev) {
                     int32_t y = c0[i], u = c1[i], v = c2[i];
                     int32_t g = y - ((u + v) >> 2);
@@ -1580,10 +1611,9 @@ int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads)
             int32_t mn, mx, sh = out->sgnd[k] ? 0 : (1 << (out->prec[k] - 1));
             if (out->sgnd[k]) { mn = -(1 << (out->prec[k] - 1)); mx = (1 << (out->prec[k] - 1)) - 1; }
             else { mn = 0; mx = (1 << out->prec[k]) - 1; }
-            uint32_t w = tr.x1 - tr.x0;
-            for (uint32_t y = tr.y0; y < tr.y1; ++y)
-                for (uint32_t x = tr.x0; x < tr.x1; ++x) {
-                    int32_t v = tcs[k].data[(size_t)(y - tr.y0) * w + (x - tr.x0)];
+            for (uint32_t y = rr.y0; y < rr.y1; ++y)
+                for (uint32_t x = rr.x0; x < rr.x1; ++x) {
+                    int32_t v = tcs[k].data[(size_t)(y - rr.y0) * fw + (x - rr.x0)];
                     if (irrev) { float f; memcpy(&f, &v, 4); v = (int32_t)lrintf(f); }
                     v += sh;
                     v = v < mn ? mn : (v > mx ? mx : v);

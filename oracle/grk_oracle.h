@@ -57,6 +57,8 @@ void orc_default_params(orc_params *p);
 /* Whole-codestream encode/decode (reference: grk_compress / grk_decompress). */
 int orc_encode(const orc_image *img, const orc_params *p, uint8_t **out, size_t *outlen);
 int orc_decode(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads);
+/* Reduced-resolution decode (grk_decompress -r / cp_reduce): -5 if reduce >= numresolutions. */
+int orc_decode_reduce(const uint8_t *buf, size_t len, orc_image *out, int32_t nthreads, uint32_t reduce);
 void orc_free(void *ptr);
 void orc_image_free(orc_image *img);
 

@@ -47,6 +47,8 @@ def lib():
         _lib.orc_encode.argtypes = [ctypes.POINTER(OrcImage), ctypes.POINTER(OrcParams),
                                     ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t)]
         _lib.orc_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(OrcImage), ctypes.c_int32]
+        _lib.orc_decode_reduce.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(OrcImage), ctypes.c_int32,
+                                           ctypes.c_uint32]
         _lib.orc_free.argtypes = [ctypes.c_void_p]
         _lib.orc_image_free.argtypes = [ctypes.POINTER(OrcImage)]
         _lib.orc_dwt_fwd.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 5 + [ctypes.c_int32, ctypes.c_int32]
@@ -134,11 +136,11 @@ def encode(img, prec, p, offset=(0, 0), sgnd=False):
     return b
 
 
-def decode(buf, nthreads=0):
-    """bytes -> (c,h,w) int32"""
+def decode(buf, nthreads=0, reduce=0):
+    """bytes -> (c,h,w) int32; reduce > 0: the image at resolution numres-1-reduce"""
     oi = OrcImage()
     src = ctypes.create_string_buffer(bytes(buf), len(buf))
-    rc = lib().orc_decode(src, len(buf), ctypes.byref(oi), nthreads)
+    rc = lib().orc_decode_reduce(src, len(buf), ctypes.byref(oi), nthreads, reduce)
     if rc != 0:
         raise RuntimeError("orc_decode failed %d" % rc)
     w, h = oi.x1 - oi.x0, oi.y1 - oi.y0

@@ -201,3 +201,36 @@ def test_large_tiled_16k(codec):
     assert hashlib.sha256(b).hexdigest() == m["j2k_sha256"]
     d = codec.decompress(b, device_out=True)
     assert torch.equal(d, t)
+
+
+@pytest.mark.parametrize("name", sorted(MAN))
+def test_reduced_decode_matches_oracle(codec, oracle, name):
+    """grk_decompress -r: every reduce level of every golden codestream, GPU
+    vs the oracle's reduced decode (bit-exact, 9/7 included).  The oracle's
+    reduced decode is pinned for 5/3 by the forward-LL property
+    (tests/test_oracle_golden.py::test_oracle_reduce_is_forward_ll); no
+    reference fixture exists for -r."""
+    import grokimagecompression_amd as grk
+    gold = open(f"{GOLD}/{name}.j2k", "rb").read()
+    args = MAN[name]["args"]
+    numres = int(args[args.index("-n") + 1]) if "-n" in args else 6
+    for r in range(1, numres):
+        ref = oracle.decode(gold, reduce=r)
+        d = codec.decompress(gold, reduce=r)
+        assert d.shape == ref.shape, (name, r)
+        assert np.array_equal(d, ref), (name, r)
+    with pytest.raises(grk.GrkGpuError):
+        codec.decompress(gold, reduce=numres)
+
+
+def test_reduced_decode_device_out_4k(codec):
+    """Reduced decode of the 4K lossless config straight into HBM: the LL
+    image equals the oracle's reduced decode."""
+    import synth as sy
+    import grokimagecompression_amd as grk
+    img = sy.synth_image(2160, 3840, 3, 8, 2)
+    b = codec.compress(img, 8, grk.CParams.make())
+    d = codec.decompress(b, device_out=True, reduce=2)
+    assert tuple(d.shape) == (3, 540, 960)
+    import pyoracle
+    assert np.array_equal(d.cpu().numpy(), pyoracle.decode(b, nthreads=8, reduce=2))
