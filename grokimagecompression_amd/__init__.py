@@ -135,6 +135,8 @@ def lib():
                                             P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
         L.grkgpu_decompress_tiles.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, P(VP), ctypes.c_int]
         L.grkgpu_decompress_reduced.argtypes = [VP, VP, ctypes.c_size_t, U32, P(ImageDesc), P(VP), ctypes.c_int]
+        L.grkgpu_decompress_window.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, U32, U32, P(ImageDesc), P(VP),
+                                               ctypes.c_int]
         L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
         L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
@@ -293,15 +295,21 @@ class Codec:
         _check(lib().grkgpu_decompress_tiles(self._ctx, bp, bn, tile_begin, tile_end, ptrs, 1 if on_dev else 0))
         return out
 
-    def decompress(self, buf, device_out=False, out=None, reduce=0):
+    def decompress(self, buf, device_out=False, out=None, reduce=0, window=None):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
         device_out / out is a cuda tensor).  reduce > 0: the image at
         resolution numres-1-reduce (grk_decompress -r), ceil(x / 2^reduce)
-        in every coordinate."""
+        in every coordinate.  window = (x0, y0, x1, y1) in image coordinates:
+        only that region (grk_set_decode_area), clipped to the image."""
         d = read_header(buf)
         if reduce:
             cd = lambda v: -(-v >> reduce)  # noqa: E731
             d.x0, d.y0, d.x1, d.y1 = cd(d.x0), cd(d.y0), cd(d.x1), cd(d.y1)
+        if window is not None:
+            wx0, wy0, wx1, wy1 = window
+            d.x0, d.y0, d.x1, d.y1 = max(d.x0, wx0), max(d.y0, wy0), min(d.x1, wx1), min(d.y1, wy1)
+            if d.x1 <= d.x0 or d.y1 <= d.y0:
+                raise GrkGpuError("decode window outside the image")
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
         on_dev = device_out or (out is not None and not isinstance(out, np.ndarray))
         if on_dev:
@@ -315,7 +323,10 @@ class Codec:
                 out = np.empty((c, h, w), dtype=np.int32)
             ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
         bp, bn, keep = _buf_ptr(buf)
-        if reduce:
+        if window is not None:
+            _check(lib().grkgpu_decompress_window(self._ctx, bp, bn, *[int(v) for v in window], None, ptrs,
+                                                  1 if on_dev else 0))
+        elif reduce:
             _check(lib().grkgpu_decompress_reduced(self._ctx, bp, bn, reduce, None, ptrs, 1 if on_dev else 0))
         else:
             _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))

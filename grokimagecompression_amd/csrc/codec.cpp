@@ -13,6 +13,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <array>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -358,16 +360,55 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
     return hipSuccess;
 }
 
+static bool overlap(const Rect &a, const Rect &b) { return a.x0 < b.x1 && b.x0 < a.x1 && a.y0 < b.y1 && b.y0 < a.y1; }
+static Rect intersect(const Rect &a, const Rect &b) {
+    Rect r{std::max(a.x0, b.x0), std::max(a.y0, b.y0), std::min(a.x1, b.x1), std::min(a.y1, b.y1)};
+    if (r.x1 < r.x0) r.x1 = r.x0;
+    if (r.y1 < r.y0) r.y1 = r.y0;
+    return r;
+}
+
+using BandNeed = std::vector<std::array<Rect, 3>>;  // [resno][band] region a window needs
+
+// need: (window decode) only code-blocks overlapping need[resno][band].
 template <typename F>
-static void for_each_cblk(TileComp &tc, F f, uint32_t maxres = 0xffffffffu) {
+static void for_each_cblk(TileComp &tc, F f, uint32_t maxres = 0xffffffffu, const BandNeed *need = nullptr) {
     for (uint32_t resno = 0; resno < tc.numres && resno < maxres; ++resno) {
         Resolution &res = tc.res[resno];
         for (uint32_t b = 0; b < res.numbands; ++b) {
             Band &band = res.bands[b];
             for (auto &pr : band.precs)
-                for (auto &c : pr.cblks) f(band, c);
+                for (auto &c : pr.cblks)
+                    if (!need || overlap(c.r, (*need)[resno][b])) f(band, c);
         }
     }
+}
+
+// Window decode: the sub-band regions whose coefficients reach the samples
+// of `win` (tile-component coordinates).  Going down from the full
+// resolution, a region of resolution r needs, in each of its bands and in the
+// resolution r-1 below, the half-size region widened by M samples on every
+// side -- more than the synthesis supports (5/3: 2 taps, 9/7: 4 taps at the
+// full scale, i.e. <= 2 at the band scale), so every coefficient that
+// influences the window is decoded and the window's samples come out exactly
+// as in a full decode (dwt.cpp decode_tile_53 / _97 compute each output from
+// its support only).
+static BandNeed window_need(const TileComp &tc, const Rect &win) {
+    constexpr uint32_t M = 4;
+    BandNeed need(tc.numres);
+    Rect n = intersect(win, tc.res[tc.numres - 1].r);
+    for (int32_t r = (int32_t)tc.numres - 1; r >= 0; --r) {
+        const Resolution &res = tc.res[r];
+        if (r == 0) {
+            need[0][0] = intersect(n, res.bands[0].r);
+            break;
+        }
+        const Rect half{n.x0 / 2 > M ? n.x0 / 2 - M : 0, n.y0 / 2 > M ? n.y0 / 2 - M : 0, (n.x1 + 1) / 2 + M,
+                        (n.y1 + 1) / 2 + M};
+        for (uint32_t b = 0; b < res.numbands; ++b) need[r][b] = intersect(half, res.bands[b].r);
+        n = intersect(half, tc.res[r - 1].r);
+    }
+    return need;
 }
 
 // ---------------------------------------------------------------------------
@@ -697,9 +738,15 @@ static uint32_t ceil_pow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t
 // decoded, the inverse DWT stops `reduce` levels early (TileProcessor.cpp:1165,
 // TileComponent.cpp:199-204) and MCT + DC shift run on the reduced tiles; the
 // image is ceil(coordinate / 2^reduce) (j2k.cpp:1464-1476).
+//
+// win (image coordinates; whole-image decode only): the window decode of
+// grk_set_decode_area (grok.h:1587, j2k.cpp j2k_set_decode_area): only tiles
+// meeting the window are parsed, only code-blocks whose coefficients reach it
+// are decoded (window_need), the inverse DWT runs on those tiles and MCT +
+// DC shift on the window; the output planes are the window.
 static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
                            int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te,
-                           uint32_t reduce = 0) {
+                           uint32_t reduce = 0, const Rect *win = nullptr) {
     if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     double t_start = now_ms();
     CodingParams cp;
@@ -713,16 +760,23 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (reduce >= cp.numres)  // j2k.cpp:6994
         return set_err(GRKGPU_EINVAL, "reduce must be smaller than the number of resolutions");
     const uint32_t numres_dec = cp.numres - reduce;
-    // output image geometry (reduced when reduce > 0)
-    const uint32_t ix0 = ceil_pow2(cp.image.x0, reduce), iy0 = ceil_pow2(cp.image.y0, reduce);
-    if (img && reduce) {
+    Rect wr{};  // window, clipped to the image
+    if (win) {
+        if (reduce) return set_err(GRKGPU_EINVAL, "window decode at a reduced resolution is not supported");
+        wr = intersect(*win, cp.image);
+        if (wr.empty()) return set_err(GRKGPU_EINVAL, "decode window outside the image");
+    }
+    // output image geometry (reduced when reduce > 0, the window when win)
+    const uint32_t ix0 = win ? wr.x0 : ceil_pow2(cp.image.x0, reduce), iy0 = win ? wr.y0 : ceil_pow2(cp.image.y0, reduce);
+    const uint32_t ix1 = win ? wr.x1 : ceil_pow2(cp.image.x1, reduce), iy1 = win ? wr.y1 : ceil_pow2(cp.image.y1, reduce);
+    if (img && (reduce || win)) {
         img->x0 = ix0; img->y0 = iy0;
-        img->x1 = ceil_pow2(cp.image.x1, reduce); img->y1 = ceil_pow2(cp.image.y1, reduce);
+        img->x1 = ix1; img->y1 = iy1;
     }
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th;
-    const uint32_t iw = ceil_pow2(cp.image.x1, reduce) - ix0, ih = ceil_pow2(cp.image.y1, reduce) - iy0;
+    const uint32_t iw = ix1 - ix0, ih = iy1 - iy0;
     const uint64_t plane = (uint64_t)iw * ih;
     if (te > ntiles) te = ntiles;
     if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
@@ -766,6 +820,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         Tile &tile = tiles[lt];
         tile.index = t;
         tile.r = tile_rect(cp, t);
+        if (win && !overlap(tile.r, wr)) continue;  // left without components: skipped below
         tile.comps.resize(nc);
         for (uint32_t k = 0; k < nc; ++k) {
             build_tilecomp(tile.comps[k], tile.r, cp, k, false);
@@ -806,6 +861,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 }
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
+            const BandNeed need = win ? window_need(tc, wr) : BandNeed();
             for_each_cblk(tc, [&](Band &band, Cblk &cb) {
                 DecBlock d{};
                 d.dst_off = tc.arena_off + (uint64_t)cb.by * tile.r.w() + cb.bx;
@@ -830,7 +886,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     d.len = 0;
                 }
                 db.push_back(d);
-            }, numres_dec);
+            }, numres_dec, win ? &need : nullptr);
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
@@ -878,12 +934,16 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
     DwtPlan dplan;
     for (auto &tile : tiles)
-        for (uint32_t k = 0; k < nc; ++k) {
+        for (uint32_t k = 0; k < tile.comps.size(); ++k) {
             const TileComp &tc = tile.comps[k];
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true, numres_dec);
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
+    // window decode: the coefficients of the code-blocks left undecoded are
+    // zero (they lie outside every window sample's support; zero keeps the
+    // 9/7 float lifting free of stale NaNs)
+    if (win && arena) HIPCHK(hipMemsetAsync(c->coef.p, 0, arena * 4, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
                             c->coef.as<int32_t>(), s, flat ? c->ubuf.as<uint32_t>() : nullptr));
@@ -904,14 +964,18 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         else { mn.v[k] = 0; mx.v[k] = (1 << cp.prec[k]) - 1; }
     }
     for (auto &tile : tiles) {
+        if (tile.comps.empty()) continue;  // outside the window
         PlanePtrs tsrc{}, tdst{};
         const Rect tr = tile.comps[0].res[numres_dec - 1].r;  // the tile at the decoded resolution
-        if (!tr.w() || !tr.h()) continue;
+        const Rect out = win ? intersect(tr, wr) : tr;        // its part of the output
+        if (out.empty()) continue;
         for (uint32_t k = 0; k < nc; ++k) {
-            tsrc.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
-            tdst.p[k] = dst.p[k] + (uint64_t)(tr.y0 - iy0) * iw + (tr.x0 - ix0);
+            tsrc.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off + (uint64_t)(out.y0 - tr.y0) * tr.w() +
+                        (out.x0 - tr.x0);
+            tdst.p[k] = dst.p[k] + (uint64_t)(out.y0 - iy0) * iw + (out.x0 - ix0);
         }
-        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), tr.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev, s));
+        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev,
+                                      s));
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
     if (!planes_on_device) {
@@ -954,6 +1018,13 @@ extern "C" int grkgpu_decompress_reduced(grkgpu_ctx *c, const uint8_t *csb, size
     return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, reduce);
 }
 
+extern "C" int grkgpu_decompress_window(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t x0, uint32_t y0,
+                                        uint32_t x1, uint32_t y1, grkgpu_image_desc *img, int32_t *const *planes,
+                                        int planes_on_device) {
+    const Rect w{x0, y0, x1, y1};
+    return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, 0, &w);
+}
+
 extern "C" int grkgpu_decompress_tiles(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t tile_begin,
                                        uint32_t tile_end, int32_t *const *planes, int planes_on_device) {
     return decompress_impl(c, csb, len, nullptr, planes, planes_on_device, tile_begin, tile_end);
@@ -978,8 +1049,8 @@ extern "C" int grkgpu_dcshift_mct_fwd(int32_t *const *planes, uint32_t numcomps,
 extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps, uint32_t w, uint32_t h,
                                       uint32_t stride, const uint32_t *prec, const int32_t *sgnd, int32_t mct,
                                       int32_t irreversible, void *stream) {
-    if (!planes || !prec || !sgnd || numcomps < 1 || numcomps > 16 || stride != w)
-        return set_err(GRKGPU_EINVAL, "bad arguments (stride must equal w)");
+    if (!planes || !prec || !sgnd || numcomps < 1 || numcomps > 16 || stride < w)
+        return set_err(GRKGPU_EINVAL, "bad arguments (stride must be >= w)");
     int rc = check_device(0);
     if (rc) return rc;
     PlanePtrs p{};
@@ -990,7 +1061,7 @@ extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps,
         if (sgnd[k]) { mn.v[k] = -(1 << (prec[k] - 1)); mx.v[k] = (1 << (prec[k] - 1)) - 1; }
         else { mn.v[k] = 0; mx.v[k] = (1 << prec[k]) - 1; }
     }
-    HIPCHK(launch_mct_inv_dcshift(p, w, h, p, w, numcomps, sh, mn, mx, mct, irreversible, (hipStream_t)stream));
+    HIPCHK(launch_mct_inv_dcshift(p, stride, w, h, p, stride, numcomps, sh, mn, mx, mct, irreversible, (hipStream_t)stream));
     return GRKGPU_OK;
 }
 

@@ -66,13 +66,13 @@ __global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst
 }
 
 // Inverse MCT + DC shift + clamp, tile buffers -> image planes.
-__global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t tw, uint32_t th, PlanePtrs dst, uint32_t dstride,
-                                  uint32_t ncomp, ShiftArr shift, ShiftArr minv, ShiftArr maxv, int32_t mct,
-                                  int32_t irrev) {
+__global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t sstride, uint32_t tw, uint32_t th, PlanePtrs dst,
+                                  uint32_t dstride, uint32_t ncomp, ShiftArr shift, ShiftArr minv, ShiftArr maxv,
+                                  int32_t mct, int32_t irrev) {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
     if (x >= tw || y >= th) return;
-    size_t si = (size_t)y * tw + x, di = (size_t)y * dstride + x;
+    size_t si = (size_t)y * sstride + x, di = (size_t)y * dstride + x;
     uint32_t c0 = 0;
     if (mct && ncomp >= 3) {
         int32_t o[3];
@@ -477,12 +477,12 @@ hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const 
     return hipGetLastError();
 }
 
-hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t tw, uint32_t th, const PlanePtrs &dst,
-                                  uint32_t dstride, uint32_t ncomp, const ShiftArr &shift, const ShiftArr &mn,
-                                  const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s) {
+hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32_t tw, uint32_t th,
+                                  const PlanePtrs &dst, uint32_t dstride, uint32_t ncomp, const ShiftArr &shift,
+                                  const ShiftArr &mn, const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s) {
     dim3 grid((tw + 255) / 256, th);
-    hipLaunchKernelGGL(k_mct_inv_dcshift, grid, dim3(256), 0, s, src, tw, th, dst, dstride, ncomp, shift, mn, mx,
-                       mct, irrev);
+    hipLaunchKernelGGL(k_mct_inv_dcshift, grid, dim3(256), 0, s, src, sstride, tw, th, dst, dstride, ncomp, shift, mn,
+                       mx, mct, irrev);
     return hipGetLastError();
 }
 

@@ -138,6 +138,13 @@ int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_ima
  * geometry.  reduce must be < the number of resolutions (GRKGPU_EINVAL). */
 int grkgpu_decompress_reduced(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t reduce,
                               grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
+/* Window decode (grk_set_decode_area, grok.h:1587; grk_decompress -d):
+ * decode only the samples of [x0, x1) x [y0, y1) (image coordinates, clipped
+ * to the image) into planes of the window's size; img (if given) receives the
+ * window geometry.  Same samples as a full decode, cropped.  Only the tiles
+ * meeting the window and the code-blocks reaching it are decoded. */
+int grkgpu_decompress_window(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t x0, uint32_t y0, uint32_t x1,
+                             uint32_t y1, grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
 /* Decode only tiles [tile_begin, tile_end) (a tile shard; the reference's
  * tile-by-tile decode, grk_decode_tile_data / j2k.cpp decode_tiles); the
  * other tiles' samples in planes are left untouched.  Host planes are written
