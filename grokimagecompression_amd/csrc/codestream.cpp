@@ -389,6 +389,9 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                 if (!inc) continue;
                 if (!c.included) {
                     int64_t k = r.tagtree(pr.imsb, cb, INT64_MAX);
+                    // corrupt streams: a missing-MSB count above the band's
+                    // bit-planes has no code-block to decode (T2.cpp:1188-1200)
+                    if (r.err || k < 0 || k > (int64_t)b.numbps) return -1;
                     c.numbps = (uint32_t)((int64_t)b.numbps - k);
                     c.numlenbits = 3;
                     c.included = true;
@@ -397,6 +400,9 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                 c.numlenbits += r.comma();
                 uint32_t L = r.read(c.numlenbits + (uint32_t)floorlog2((int32_t)np));
                 c.numpasses += np;
+                // cblksty 0: at most 3 * numbps - 2 passes; more can only come
+                // from a corrupt header and would overrun the decoder's pass tables
+                if (c.numpasses > (c.numbps ? 3 * c.numbps - 2 : 0) || c.numpasses > 3u * 31 - 2) return -1;
                 segs.push_back({&c, L});
                 if (r.err) return -1;
             }
@@ -423,6 +429,7 @@ static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
 bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err) {
     if (len < 4 || rd16(cs) != 0xFF4F) { err = "missing SOC"; return false; }
     size_t pos = 2;
+    first_sot = 0;
     bool have_siz = false, have_cod = false, have_qcd = false;
     while (pos + 4 <= len) {
         uint32_t m = rd16(cs + pos);
@@ -434,23 +441,38 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             cp.image = {rd32(p + 10), rd32(p + 14), rd32(p + 2), rd32(p + 6)};
             cp.tdx = rd32(p + 18); cp.tdy = rd32(p + 22); cp.tx0 = rd32(p + 26); cp.ty0 = rd32(p + 30);
             cp.numcomps = rd16(p + 34);
+            // read_siz checks, j2k.cpp:3380-3480: marker length vs Csiz, non-empty
+            // image, tile size, tile origin at or before the image origin
+            if (L < 38) { err = "Error with SIZ marker size"; return false; }
             if (cp.numcomps == 0 || cp.numcomps > 16) { err = "unsupported component count"; return false; }
+            if (L != 38 + 3 * cp.numcomps) { err = "Error with SIZ marker: number of components vs marker length"; return false; }
+            if (cp.image.x0 >= cp.image.x1 || cp.image.y0 >= cp.image.y1) { err = "Error with SIZ marker: negative or zero image size"; return false; }
             for (uint32_t k = 0; k < cp.numcomps; ++k) {
                 cp.prec[k] = (p[36 + 3 * k] & 0x7f) + 1u;
                 cp.sgnd[k] = p[36 + 3 * k] >> 7;
+                if (cp.prec[k] > 16) { err = "precision above 16 bits not supported"; return false; }
                 if (p[37 + 3 * k] != 1 || p[38 + 3 * k] != 1) { err = "subsampled components not supported"; return false; }
             }
             if (cp.tdx == 0 || cp.tdy == 0) { err = "bad tile size"; return false; }
+            if (cp.tx0 > cp.image.x0 || cp.ty0 > cp.image.y0 || (uint64_t)cp.tx0 + cp.tdx <= cp.image.x0 ||
+                (uint64_t)cp.ty0 + cp.tdy <= cp.image.y0) { err = "Error with SIZ marker: illegal tile offset"; return false; }
             cp.tw = ceildiv(cp.image.x1 - cp.tx0, cp.tdx);
             cp.th = ceildiv(cp.image.y1 - cp.ty0, cp.tdy);
             have_siz = true;
         } else if (m == 0xFF52) {
+            if (L < 12) { err = "Error reading COD marker"; return false; }
             if (p[0] != 0) { err = "precincts/SOP/EPH (Scod != 0) not supported"; return false; }
             cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
             cp.numres = p[5] + 1u; cp.cblkw = p[6] + 2u; cp.cblkh = p[7] + 2u; cp.cblksty = p[8];
             cp.irrev = p[9] == 0;
+            // read_SPCod_SPCoc, j2k.cpp:6978-7025 / COD layers j2k.cpp:3855
+            if (cp.numlayers == 0) { err = "Invalid number of layers in COD marker"; return false; }
+            if (cp.numres > 33) { err = "Number of resolutions is greater than GRK_J2K_MAXRLVLS"; return false; }
+            if (p[6] > 8 || p[7] > 8 || p[6] + p[7] > 8) { err = "Error reading SPCod SPCoc element, invalid code-block size"; return false; }
+            if (p[9] > 1) { err = "Invalid qmfbid"; return false; }
             have_cod = true;
         } else if (m == 0xFF5C) {
+            if (L < 4) { err = "Error reading QCD marker"; return false; }  // j2k.cpp:4075
             uint32_t sq = p[0] & 0x1f;
             if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
             uint32_t nb = sq == 0 ? (L - 3) : (L - 3) / 2;
@@ -466,6 +488,8 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
         pos += 2 + L;
     }
     if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
+    // j2k_read_header stops at the first SOT; a stream that ends before it is truncated
+    if (first_sot == 0) { err = "truncated main header (no SOT)"; return false; }
     if (cp.prog != 0) { err = "only LRCP progression supported"; return false; }
     if (cp.cblksty != 0) { err = "code-block mode switches not supported"; return false; }
     if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }

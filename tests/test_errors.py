@@ -1,0 +1,164 @@
+"""Error behaviour on malformed input (the reference's fuzz-regression cases,
+j2k.cpp:3380-3480 read_siz, :3829-3884 read_cod, :4075 read_qcd,
+:6978-7025 read_SPCod_SPCoc): a malformed or unsupported codestream makes
+the call fail with a GrkGpuError (grkgpu status != 0) -- never a crash, a
+hang or a GPU fault -- and the codec keeps working afterwards.
+
+CPU tests exercise the host header parser (grkgpu_read_header needs no GPU);
+the gpu tests push truncated / corrupted tile data through the whole decoder.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_manifest
+
+MAN = load_manifest()
+NAMES = sorted(MAN)
+
+
+def _cs(name):
+    return open("%s/%s.j2k" % (GOLD, name), "rb").read()
+
+
+def _marker(cs, code):
+    """Offset of the first main-header marker `code` (SOC .. first SOT)."""
+    pos = 2
+    while pos + 4 <= len(cs):
+        m, L = struct.unpack(">HH", cs[pos:pos + 4])
+        if m == code:
+            return pos
+        if m == 0xFF90:  # first SOT: end of the main header
+            break
+        pos += 2 + L
+    raise KeyError(hex(code))
+
+
+def _patch(cs, off, fmt, value):
+    b = bytearray(cs)
+    struct.pack_into(fmt, b, off, value)
+    return bytes(b)
+
+
+def _grk():
+    import grokimagecompression_amd as grk
+    return grk
+
+
+def _rejects(cs):
+    grk = _grk()
+    with pytest.raises(grk.GrkGpuError):
+        grk.read_header(cs)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_goldens_parse(name):
+    d = _grk().read_header(_cs(name))
+    h, w, c, bits = MAN[name]["shape"]
+    assert (d.numcomps, d.x1 - d.x0, d.y1 - d.y0) == (c, w, h)
+
+
+def test_truncated_main_header_rejected():
+    for name in ("rgb12_I", "g8_off_tiles", "g16_128"):
+        cs = _cs(name)
+        sot = _marker(cs, 0xFF90)
+        for n in range(sot):
+            _rejects(cs[:n])
+
+
+def test_siz_field_checks():
+    cs = _cs("rgb8_128x96")
+    siz = _marker(cs, 0xFF51)
+    x1, y1, x0, y0 = struct.unpack(">IIII", cs[siz + 6:siz + 22])
+    _rejects(_patch(cs, siz + 14, ">I", x1))          # x0 == x1: zero image size
+    _rejects(_patch(cs, siz + 18, ">I", y1 + 5))      # y0 > y1
+    _rejects(_patch(cs, siz + 22, ">I", 0))           # tdx == 0
+    _rejects(_patch(cs, siz + 34, ">I", x0 + 1))      # tile origin right of the image origin
+    _rejects(_patch(cs, siz + 38, ">H", 4))           # Csiz does not match the marker length
+    _rejects(_patch(cs, siz + 38, ">H", 0))           # no components
+    _rejects(_patch(cs, siz + 40, ">B", 16))          # 17-bit precision: unsupported
+    _rejects(_patch(cs, siz + 41, ">B", 2))           # subsampled component
+    _rejects(_patch(cs, siz + 2, ">H", 20))           # marker too short
+
+
+def test_cod_qcd_field_checks():
+    cs = _cs("g8_256")
+    cod = _marker(cs, 0xFF52)
+    p = cod + 4
+    _rejects(_patch(cs, p + 1, ">B", 1))              # RLCP progression
+    _rejects(_patch(cs, p + 2, ">H", 0))              # zero layers
+    _rejects(_patch(cs, p + 5, ">B", 33))             # 34 resolutions
+    _rejects(_patch(cs, p + 6, ">B", 9))              # 2^11-wide code-blocks
+    _rejects(_patch(cs, p + 8, ">B", 1))              # BYPASS mode switch
+    _rejects(_patch(cs, p + 9, ">B", 2))              # qmfbid 2
+    _rejects(_patch(cs, p, ">B", 1))                  # Scod: user precincts
+    _rejects(_patch(cs, cod + 2, ">H", 4))            # COD too short
+    qcd = _marker(cs, 0xFF5C)
+    _rejects(_patch(cs, qcd + 4, ">B", 1))            # scalar-derived quantisation
+    _rejects(_patch(cs, qcd + 2, ">H", 2))            # QCD too short
+
+
+def test_random_main_header_corruption_never_crashes():
+    grk = _grk()
+    rng = np.random.default_rng(7)
+    for name in ("rgb12_I", "g8_off_tiles", "g8_n1"):
+        cs = _cs(name)
+        sot = _marker(cs, 0xFF90)
+        for _ in range(3000):
+            b = bytearray(cs)
+            for pos in rng.integers(0, sot, size=int(rng.integers(1, 4))):
+                b[pos] = int(rng.integers(0, 256))
+            try:
+                d = grk.read_header(bytes(b))
+            except grk.GrkGpuError:
+                continue
+            assert 1 <= d.numcomps <= 16 and d.x1 > d.x0 and d.y1 > d.y0
+
+
+# ---------------------------------------------------------------- GPU decode
+
+def _decode_or_error(codec, cs):
+    grk = _grk()
+    try:
+        out = codec.decompress(cs)
+    except grk.GrkGpuError:
+        return None
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rgb12_I", "g8_256", "g8_off_tiles", "g16_128"])
+def test_truncated_tile_data(codec, name):
+    """Cut the codestream anywhere inside the tile-parts: the decoder either
+    reports the corruption or decodes what is there; never faults."""
+    cs = _cs(name)
+    sot = _marker(cs, 0xFF90)
+    ref = np.load("%s/%s.dec.npy" % (GOLD, name))
+    rng = np.random.default_rng(11)
+    cuts = sorted(set([sot + 1, sot + 12, sot + 14, len(cs) - 2, len(cs) - 1] +
+                      [int(v) for v in rng.integers(sot, len(cs), size=24)]))
+    for n in cuts:
+        out = _decode_or_error(codec, cs[:n])
+        if out is not None:
+            assert out.shape == ref.shape
+    assert np.array_equal(codec.decompress(cs), ref)   # still healthy
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rgb12_I", "g8_256", "g16_uniform_64"])
+def test_corrupted_tile_data(codec, name):
+    """Random byte damage in packet headers and code-block bytes (the MQ
+    decoder runs on garbage): an error or an image of the right shape."""
+    cs = _cs(name)
+    sot = _marker(cs, 0xFF90) + 14
+    ref = np.load("%s/%s.dec.npy" % (GOLD, name))
+    rng = np.random.default_rng(5)
+    for _ in range(40):
+        b = bytearray(cs)
+        for pos in rng.integers(sot, len(cs) - 2, size=int(rng.integers(1, 8))):
+            b[pos] = int(rng.integers(0, 256))
+        out = _decode_or_error(codec, bytes(b))
+        if out is not None:
+            assert out.shape == ref.shape
+    assert np.array_equal(codec.decompress(cs), ref)
