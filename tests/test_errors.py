@@ -162,3 +162,36 @@ def test_corrupted_tile_data(codec, name):
         if out is not None:
             assert out.shape == ref.shape
     assert np.array_equal(codec.decompress(cs), ref)
+
+
+def test_encoder_parameter_checks():
+    """grk_setup_encoder-style validation (j2k.cpp:1637-1660: resolutions in
+    [1, 33], precision, code-block sizes; tile origin j2k.cpp:3466-3471), run
+    through grkgpu_num_tiles, which shares the encoder's parameter setup."""
+    grk = _grk()
+    ok = grk.num_tiles((3, 64, 80), 8, grk.CParams.make())
+    assert ok == 1
+    assert grk.num_tiles((1, 100, 130), 8, grk.CParams.make(tiles=(32, 32))) == 4 * 5
+    bad = [
+        ((3, 64, 80), 8, grk.CParams.make(numresolution=0), (0, 0)),
+        ((3, 64, 80), 8, grk.CParams.make(numresolution=34), (0, 0)),
+        ((3, 64, 80), 8, grk.CParams.make(cblk=(128, 32)), (0, 0)),
+        ((3, 64, 80), 8, grk.CParams.make(cblk=(48, 32)), (0, 0)),
+        ((3, 64, 80), 8, grk.CParams.make(cblk=(2, 64)), (0, 0)),
+        ((3, 64, 80), 17, grk.CParams.make(), (0, 0)),
+        ((3, 64, 80), 0, grk.CParams.make(), (0, 0)),
+        ((1, 0, 8), 8, grk.CParams.make(), (0, 0)),
+        ((1, 64, 64), 8, grk.CParams.make(tiles=(16, 16), tile_offset=(5, 0)), (3, 0)),   # tx0 > x0
+        ((1, 64, 64), 8, grk.CParams.make(tiles=(16, 16), tile_offset=(0, 0)), (20, 0)),  # x0 >= tx0 + tdx
+        ((1, 4096, 4096), 8, grk.CParams.make(tiles=(8, 8)), (0, 0)),                    # 262144 tiles > 65535
+    ]
+    for shape, prec, params, off in bad:
+        with pytest.raises(grk.GrkGpuError):
+            grk.num_tiles(shape, prec, params, offset=off)
+    import ctypes
+    d = grk.ImageDesc()
+    d.x1, d.y1, d.numcomps = 8, 8, 17                 # more components than the ABI carries
+    for k in range(16):
+        d.prec[k] = 8
+    n = ctypes.c_uint32()
+    assert grk.lib().grkgpu_num_tiles(ctypes.byref(d), ctypes.byref(grk.CParams.make()), ctypes.byref(n)) != 0
