@@ -97,7 +97,8 @@ _EXPORTS = None
 
 
 def build():
-    """Compile libgrk_mi355x.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    """Compile libgrk_mi355x.so for gfx950 (hipcc cross-compiles without a GPU) and the
+    minpf plugin libgrok_plugin.so, in-tree."""
     import subprocess
     subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")], check=True)
 
