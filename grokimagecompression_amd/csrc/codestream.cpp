@@ -412,7 +412,10 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
     if (r.err) return -1;
     size_t off = r.off;
     for (auto &s : segs) {
-        if (off + s.len > n) return -1;
+        // T2::read_packet_data (T2.cpp:686-698): a segment running past the
+        // tile data is truncated to what is there (the decoder reads the
+        // missing tail as the 0xFF fill), not an error
+        if (off + s.len > n) s.len = (uint32_t)(n - off);
         if (s.len) s.c->chunks.push_back({base_off + off, s.len});
         s.c->seglen += s.len;
         off += s.len;
