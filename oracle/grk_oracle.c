@@ -1276,7 +1276,8 @@ static int64_t t2_decode_packet(tilecomp_t *tc, uint32_t resno, uint32_t precno,
     size_t off = r.off;
     for (uint32_t i = 0; i < nseg; ++i) {
         cblk_t *c = segcb[i];
-        if (off + seglen[i] > n) goto done;
+        /* T2::read_packet_data (T2.cpp:686-698): truncate to the bytes present */
+        if (off + seglen[i] > n) seglen[i] = (uint32_t)(n - off);
         if (c->seglen + seglen[i] + 2 > c->segcap) {
             c->segcap = (c->seglen + seglen[i] + 2) * 2;
             c->seg = (uint8_t *)realloc(c->seg, c->segcap);
@@ -1508,7 +1509,8 @@ int orc_decode_reduce(const uint8_t *buf, size_t len, orc_image *out, int32_t nt
             while (pos + 2 <= len && rd16(buf + pos) != 0xFF93) pos += 2 + rd16(buf + pos + 2);
             pos += 2;
             size_t end = psot ? sot + psot : len - 2;
-            if (end > len || isot >= ntiles) return -1;
+            if (end > len) end = len; /* a stream cut inside a tile-part: keep what is there */
+            if (isot >= ntiles || pos > end) return -1;
             bb_putn(&tdata[isot], buf + pos, end - pos);
             pos = end;
             continue;
