@@ -1,12 +1,13 @@
-"""Generate the golden fixtures under tests/golden/ from the REFERENCE codec.
+"""Generate (or check) the golden fixtures under tests/golden/ with the REFERENCE codec.
 
-Runs ONLY in the build container (never on the GPU box; nothing at test/bench
-time imports this file).  It feeds images from tests/golden/synth.py to the
-reference CLI (grk_compress / grk_decompress of Grok v5.1.0, built out of tree
-from /root/reference by the survey step -- binaries located via $GRK_REF_BIN,
-default /tmp/grkbuild/bin; this repo ships no recipe for that build, see
-DESIGN.md "Oracle") and stores:
+Test infrastructure; runs only in the build container (the GPU box has no
+/root/reference).  The reference is Grok v5.1.0's own libgrok, compiled
+straight from /root/reference/src/lib/jp2 by the committed recipe
+oracle/ref.mk (no CMake, no stand-ins), driven through its grk_* C API by
+oracle/ref_driver.cpp (the grk_compress / grk_decompress option mapping for
+the options below).  Images come from tests/golden/synth.py.
 
+Stores:
   tests/golden/<case>.j2k        reference codestream (byte-exact parity target)
   tests/golden/<case>.dec.npy    reference decode of that codestream, int32 (c,h,w)
   tests/golden/manifest.json     per case: image spec, grk_compress args,
@@ -14,7 +15,9 @@ DESIGN.md "Oracle") and stores:
   tests/golden/manifest_large.json  same hashes for the BASELINE.json configs
                                  (full-size streams are too big to commit)
 
-Usage:  python oracle/make_golden.py [--large]
+Usage:  python oracle/make_golden.py [--large] [--check] [--only NAME ...]
+  --check  regenerate into a temporary directory and compare with the
+           committed files instead of overwriting them (exit 1 on a mismatch)
 """
 import argparse
 import hashlib
@@ -27,11 +30,12 @@ import tempfile
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-GOLD = os.path.join(HERE, "..", "tests", "golden")
+ROOT = os.path.dirname(HERE)
+GOLD = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, GOLD)
 import synth  # noqa: E402
 
-REF = os.environ.get("GRK_REF_BIN", "/tmp/grkbuild/bin")
+DRIVER = os.path.join(HERE, "_ref", "ref_driver")
 
 # name, (h, w, c, bits), kind, seed, extra grk_compress args
 CASES = [
@@ -76,7 +80,7 @@ CASES = [
     ("g8_1x37_I", (37, 1, 1, 8), "smooth", 50, ["-I"]),
 ]
 
-# BASELINE.json configs (hash-only; C5 cinema needs PCRD rate control -> next)
+# BASELINE.json configs (hash-only)
 LARGE = [
     ("C1_512_gray8", (512, 512, 1, 8), "smooth", 1, []),
     ("C2_4k_rgb8", (2160, 3840, 3, 8), "smooth", 2, []),
@@ -90,23 +94,39 @@ def sha(b):
     return hashlib.sha256(b).hexdigest()
 
 
-def run_case(name, shape, kind, seed, args, tmp, keep_files):
+def build_ref():
+    """Compile oracle/_ref from /root/reference (no-op when up to date)."""
+    subprocess.run(["make", "-s", "-f", "oracle/ref.mk", "-j8"], cwd=ROOT, check=True)
+
+
+def ref_encode(img, bits, args, tmp, signed=False):
+    c, h, w = img.shape
+    src = os.path.join(tmp, "in.i32")
+    out = os.path.join(tmp, "out.j2k")
+    np.ascontiguousarray(img, dtype="<i4").tofile(src)
+    subprocess.run([DRIVER, "enc", src, out, str(w), str(h), str(c), str(bits), str(int(signed))] + list(args),
+                   check=True, stdout=subprocess.DEVNULL)
+    with open(out, "rb") as f:
+        return f.read()
+
+
+def ref_decode(j2k, tmp, extra=()):
+    """Reference decode -> (int32 array (c,h,w), header tuple)."""
+    src = os.path.join(tmp, "in.j2k")
+    out = os.path.join(tmp, "out.i32")
+    with open(src, "wb") as f:
+        f.write(j2k)
+    r = subprocess.run([DRIVER, "dec", src, out] + list(extra), check=True, capture_output=True, text=True)
+    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.split())
+    dec = np.fromfile(out, dtype="<i4").reshape(nc, ch, cw)
+    return dec, (x0, y0, x1, y1, prec, sgnd)
+
+
+def run_case(name, shape, kind, seed, args, tmp, keep_dir=None):
     h, w, c, bits = shape
     img = synth.synth_image(h, w, c, bits, seed, kind)
-    ext = "ppm" if c == 3 else "pgm"
-    src = os.path.join(tmp, f"{name}.{ext}")
-    synth.write_pnm(src, img, bits)
-    j2k = os.path.join(tmp, f"{name}.j2k")
-    env = dict(os.environ, LD_LIBRARY_PATH=REF)
-    subprocess.run([os.path.join(REF, "grk_compress"), "-i", src, "-o", j2k] + args,
-                   check=True, env=env, stdout=subprocess.DEVNULL)
-    raw = os.path.join(tmp, f"{name}.raw")
-    subprocess.run([os.path.join(REF, "grk_decompress"), "-i", j2k, "-o", raw],
-                   check=True, env=env, stdout=subprocess.DEVNULL)
-    d = open(raw, "rb").read()
-    dt = np.uint8 if bits <= 8 else np.dtype(">u2")
-    dec = np.frombuffer(d, dtype=dt).reshape(c, h, w).astype(np.int32)
-    jb = open(j2k, "rb").read()
+    jb = ref_encode(img, bits, args, tmp)
+    dec, _ = ref_decode(jb, tmp)
     diff = (dec.astype(np.int64) - img).ravel()
     mse = float((diff.astype(np.float64) ** 2).mean())
     rec = dict(shape=[h, w, c, bits], kind=kind, seed=seed, args=args,
@@ -114,31 +134,52 @@ def run_case(name, shape, kind, seed, args, tmp, keep_files):
                dec_sha256=synth.image_sha256(dec),
                dec_vs_src_maxabs=int(np.abs(diff).max()) if diff.size else 0,
                dec_vs_src_mse=mse)
-    if keep_files:
-        open(os.path.join(GOLD, f"{name}.j2k"), "wb").write(jb)
-        np.save(os.path.join(GOLD, f"{name}.dec.npy"), dec)
+    if keep_dir:
+        with open(os.path.join(keep_dir, f"{name}.j2k"), "wb") as f:
+            f.write(jb)
+        np.save(os.path.join(keep_dir, f"{name}.dec.npy"), dec)
     return rec
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
+    build_ref()
+    cases = LARGE if a.large else CASES
+    if a.only:
+        cases = [cs for cs in cases if cs[0] in a.only]
+    mname = "manifest_large.json" if a.large else "manifest.json"
+    committed = {}
+    if os.path.exists(os.path.join(GOLD, mname)):
+        with open(os.path.join(GOLD, mname)) as f:
+            committed = json.load(f)
+    bad = 0
+    man = dict(committed)
     with tempfile.TemporaryDirectory() as tmp:
-        if a.large:
-            man = {}
-            for case in LARGE:
-                print("large", case[0], flush=True)
-                man[case[0]] = run_case(*case, tmp, keep_files=False)
-                for f in os.listdir(tmp):
-                    os.unlink(os.path.join(tmp, f))
-            json.dump(man, open(os.path.join(GOLD, "manifest_large.json"), "w"), indent=1)
-        else:
-            man = {}
-            for case in CASES:
-                man[case[0]] = run_case(*case, tmp, keep_files=True)
-            json.dump(man, open(os.path.join(GOLD, "manifest.json"), "w"), indent=1)
-    print("ok", len(man))
+        keep = None if (a.large or a.check) else GOLD
+        for case in cases:
+            rec = run_case(*case, tmp, keep_dir=keep)
+            if a.check:
+                ref = committed.get(case[0])
+                same = ref is not None and all(ref[k] == rec[k] for k in ("j2k_sha256", "dec_sha256", "image_sha256"))
+                if not a.large and same:
+                    with open(os.path.join(GOLD, f"{case[0]}.j2k"), "rb") as f:
+                        same = sha(f.read()) == rec["j2k_sha256"]
+                    same = same and synth.image_sha256(np.load(os.path.join(GOLD, f"{case[0]}.dec.npy"))) == rec["dec_sha256"]
+                print(case[0], "ok" if same else "MISMATCH", flush=True)
+                bad += not same
+            else:
+                man[case[0]] = rec
+                print(case[0], rec["j2k_len"], flush=True)
+    if a.check:
+        print("mismatches", bad)
+        sys.exit(1 if bad else 0)
+    with open(os.path.join(GOLD, mname), "w") as f:
+        json.dump(man, f, indent=1)
+    print("ok", len(cases))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,303 @@
+// oracle/ref_driver.cpp -- fixture / baseline driver over the REFERENCE grk_*
+// C API (oracle/_ref/libgrok.so, built from /root/reference by oracle/ref.mk).
+//
+// Test infrastructure only: it regenerates tests/golden/ (oracle/make_golden.py)
+// and times the reference CPU path for bench.py's cpu_baseline leg.  The
+// product never runs it.
+//
+// It does what grk_compress / grk_decompress do for the options the fixtures
+// use, minus the image-file layer: the image arrives as raw int32 planes.
+//   encode: grk_set_default_encoder_parameters, then the CLI mapping of
+//           src/bin/jp2/grk_compress.cpp (-I :1107, -n :999, -b :1027-1042,
+//           -d :1069, -t :994, -T :1480, -Y :1383, -r :812-846, -q :848-880,
+//           -p :1050, -c :1003-1023, -M :1132, -S/-E :1101-1105, -u :1516,
+//           -P :1077-1098, -cinema2K/4K :537-561 + :1146-1163), the
+//           post-parse defaults (:1579-1583 lossless layer, :1997-1998 MCT,
+//           :2015 rate-control algorithm), image geometry as PNMFormat sets it
+//           (PNMFormat.cpp:399-417), then grk_create_compress ->
+//           grk_setup_encoder -> grk_start_compress -> grk_encode ->
+//           grk_end_compress into a memory stream (grk_compress.cpp:2090-2130).
+//   decode: grk_create_decompress -> grk_setup_decoder (cp_reduce / cp_layer)
+//           -> grk_read_header -> grk_set_decode_area -> grk_decode ->
+//           grk_end_decompress (grk_decompress.cpp:1427-1530).
+//
+// usage:
+//   ref_driver enc IN.i32 OUT.j2k W H C BITS SGND [options]
+//   ref_driver dec IN.j2k OUT.i32 [-r reduce] [-l layers] [-d x0,y0,x1,y1]
+//   ref_driver bench IN.i32 W H C BITS SGND THREADS REPS [options]   (enc+dec timing)
+// IN.i32 / OUT.i32: planar int32 little-endian (c, h, w).  dec prints
+// "x0 y0 x1 y1 numcomps prec sgnd" of the decoded image on stdout.
+#include <grok.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+static void err_cb(const char *msg, void *) { fprintf(stderr, "[grk error] %s", msg); }
+
+static std::vector<uint8_t> read_file(const char *p) {
+    std::vector<uint8_t> v;
+    FILE *f = fopen(p, "rb");
+    if (!f) { perror(p); exit(2); }
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    v.resize((size_t)n);
+    if (n && fread(v.data(), 1, (size_t)n, f) != (size_t)n) { perror(p); exit(2); }
+    fclose(f);
+    return v;
+}
+
+static void write_file(const char *p, const void *d, size_t n) {
+    FILE *f = fopen(p, "wb");
+    if (!f || fwrite(d, 1, n, f) != n) { perror(p); exit(2); }
+    fclose(f);
+}
+
+static GRK_PROG_ORDER prog(const char *s) {
+    if (!strncmp(s, "LRCP", 4)) return GRK_LRCP;
+    if (!strncmp(s, "RLCP", 4)) return GRK_RLCP;
+    if (!strncmp(s, "RPCL", 4)) return GRK_RPCL;
+    if (!strncmp(s, "PCRL", 4)) return GRK_PCRL;
+    if (!strncmp(s, "CPRL", 4)) return GRK_CPRL;
+    return GRK_PROG_UNKNOWN;
+}
+
+// grk_compress option subset -> parameters (citations in the header)
+static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
+    grk_set_default_encoder_parameters(p);
+    p->tcp_mct = 255;
+    p->rateControlAlgorithm = 255;
+    uint32_t cinema = 0, fps = 0;
+    for (int i = 0; i < argc; ++i) {
+        std::string a = argv[i];
+        const char *v = i + 1 < argc ? argv[i + 1] : "";
+        if (a == "-I") { p->irreversible = true; continue; }
+        if (a == "-S") { p->csty |= 0x02; continue; }
+        if (a == "-E") { p->csty |= 0x04; continue; }
+        ++i;
+        if (a == "-n") p->numresolution = (uint32_t)atoi(v);
+        else if (a == "-b") { if (sscanf(v, "%u,%u", &p->cblockw_init, &p->cblockh_init) != 2) return false; }
+        else if (a == "-d") { if (sscanf(v, "%u,%u", &p->image_offset_x0, &p->image_offset_y0) != 2) return false; }
+        else if (a == "-t") { if (sscanf(v, "%u,%u", &p->cp_tdx, &p->cp_tdy) != 2) return false; p->tile_size_on = true; }
+        else if (a == "-T") { if (sscanf(v, "%u,%u", &p->cp_tx0, &p->cp_ty0) != 2) return false; }
+        else if (a == "-Y") p->tcp_mct = (uint8_t)atoi(v);
+        else if (a == "-p") p->prog_order = prog(v);
+        else if (a == "-M") p->cblk_sty = (uint8_t)(atoi(v) & 0x7f);
+        else if (a == "-u") { p->tp_flag = (uint8_t)v[0]; p->tp_on = 1; }
+        else if (a == "-A") p->rateControlAlgorithm = (uint32_t)atoi(v);
+        else if (a == "-r" || a == "-q") {
+            double *dst = a == "-r" ? p->tcp_rates : p->tcp_distoratio;
+            p->tcp_numlayers = 0;
+            const char *s = v;
+            while (sscanf(s, "%lf", &dst[p->tcp_numlayers]) == 1) {
+                p->tcp_numlayers++;
+                while (*s && *s != ',') s++;
+                if (!*s) break;
+                s++;
+            }
+            if (a == "-r") {
+                p->cp_disto_alloc = 1;
+                for (uint32_t k = 0; k < p->tcp_numlayers; ++k)
+                    if (p->tcp_rates[k] == 1) p->tcp_rates[k] = 0;
+            } else {
+                p->cp_fixed_quality = 1;
+            }
+        } else if (a == "-c") {
+            const char *s = v;
+            uint32_t rs = 0;
+            char sep;
+            int ret;
+            do {
+                sep = 0;
+                ret = sscanf(s, "[%u,%u]%c", &p->prcw_init[rs], &p->prch_init[rs], &sep);
+                if (!(ret == 2 && sep == 0) && !(ret == 3 && sep == ',')) return false;
+                p->csty |= 0x01;
+                rs++;
+                s = strpbrk(s, "]") + 2;
+            } while (sep == ',');
+            p->res_spec = rs;
+        } else if (a == "-P") {
+            const char *s = v;
+            uint32_t n = 0;
+            grk_poc *P = p->POC;
+            while (sscanf(s, "T%u=%u,%u,%u,%u,%u,%4s", &P[n].tile, &P[n].resno0, &P[n].compno0, &P[n].layno1,
+                          &P[n].resno1, &P[n].compno1, P[n].progorder) == 7) {
+                P[n].prg1 = prog(P[n].progorder);
+                n++;
+                while (*s && *s != '/') s++;
+                if (!*s) break;
+                s++;
+            }
+            p->numpocs = n;
+        } else if (a == "-cinema2K" || a == "-cinema4K") {
+            cinema = a == "-cinema2K" ? GRK_PROFILE_CINEMA_2K : GRK_PROFILE_CINEMA_4K;
+            fps = (uint32_t)atoi(v);
+        } else {
+            fprintf(stderr, "unknown option %s\n", a.c_str());
+            return false;
+        }
+    }
+    if (cinema) {  // checkCinema (grk_compress.cpp:537-561)
+        p->rsiz = (uint16_t)cinema;
+        p->framerate = (int)fps;
+        p->max_comp_size = fps == 48 ? GRK_CINEMA_48_COMP : GRK_CINEMA_24_COMP;
+        p->max_cs_size = fps == 48 ? GRK_CINEMA_48_CS : GRK_CINEMA_24_CS;
+    }
+    if (p->tcp_numlayers == 0) {  // grk_compress.cpp:1579-1583
+        p->tcp_rates[0] = 0;
+        p->tcp_numlayers = 1;
+        p->cp_disto_alloc = 1;
+    }
+    return true;
+}
+
+static grk_image *make_image(const int32_t *planes, uint32_t w, uint32_t h, uint32_t c, uint32_t bits, uint32_t sgnd,
+                             const grk_cparameters *p) {
+    std::vector<grk_image_cmptparm> cm(c);
+    memset(cm.data(), 0, c * sizeof(grk_image_cmptparm));
+    for (uint32_t k = 0; k < c; ++k) {
+        cm[k].prec = bits;
+        cm[k].sgnd = sgnd;
+        cm[k].dx = 1;
+        cm[k].dy = 1;
+        cm[k].w = w;
+        cm[k].h = h;
+    }
+    grk_image *img = grk_image_create(c, cm.data(), c >= 3 ? GRK_CLRSPC_SRGB : GRK_CLRSPC_GRAY);
+    if (!img) return nullptr;
+    img->x0 = p->image_offset_x0;
+    img->y0 = p->image_offset_y0;
+    img->x1 = p->image_offset_x0 + w;
+    img->y1 = p->image_offset_y0 + h;
+    for (uint32_t k = 0; k < c; ++k) memcpy(img->comps[k].data, planes + (size_t)k * w * h, (size_t)w * h * 4);
+    return img;
+}
+
+// returns the codestream length, 0 on failure
+static size_t encode(grk_cparameters *p, const int32_t *planes, uint32_t w, uint32_t h, uint32_t c, uint32_t bits,
+                     uint32_t sgnd, std::vector<uint8_t> &out) {
+    grk_image *img = make_image(planes, w, h, c, bits, sgnd, p);
+    if (!img) return 0;
+    if (p->tcp_mct == 255) p->tcp_mct = c >= 3 ? 1 : 0;       // grk_compress.cpp:1997-1998
+    if (p->rateControlAlgorithm == 255) p->rateControlAlgorithm = 0;  // :2015
+    const size_t cap = (size_t)w * h * c * ((bits + 7) / 8) * 3 / 2 + (1 << 20);
+    uint8_t *buf = new uint8_t[cap];
+    grk_stream *st = grk_stream_create_mem_stream(buf, cap, false, false);
+    grk_codec *codec = grk_create_compress(GRK_CODEC_J2K, st);
+    grk_set_error_handler(err_cb, nullptr);
+    bool ok = codec && grk_setup_encoder(codec, p, img) && grk_start_compress(codec, img) && grk_encode(codec) &&
+              grk_end_compress(codec);
+    size_t n = ok ? grk_stream_get_write_mem_stream_length(st) : 0;
+    if (ok) out.assign(buf, buf + n);
+    if (codec) grk_destroy_codec(codec);
+    grk_stream_destroy(st);
+    grk_image_destroy(img);
+    delete[] buf;
+    return n;
+}
+
+static grk_image *decode(const uint8_t *cs, size_t len, uint32_t reduce, uint32_t layers, const uint32_t *area,
+                         grk_codec **codec_out, grk_stream **st_out) {
+    grk_stream *st = grk_stream_create_mem_stream((uint8_t *)cs, len, false, true);
+    grk_codec *codec = grk_create_decompress(GRK_CODEC_J2K, st);
+    grk_set_error_handler(err_cb, nullptr);
+    grk_dparameters dp;
+    grk_set_default_decoder_parameters(&dp);
+    dp.cp_reduce = reduce;
+    dp.cp_layer = layers;
+    grk_header_info hi;
+    memset(&hi, 0, sizeof(hi));
+    grk_image *img = nullptr;
+    bool ok = codec && grk_setup_decoder(codec, &dp) && grk_read_header(codec, &hi, &img);
+    if (ok) ok = grk_set_decode_area(codec, img, area[0], area[1], area[2], area[3]);
+    if (ok) ok = grk_decode(codec, nullptr, img) && grk_end_decompress(codec);
+    *codec_out = codec;
+    *st_out = st;
+    return ok ? img : nullptr;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
+        return 2;
+    }
+    const std::string mode = argv[1];
+    if (mode == "enc" || mode == "bench") {
+        const bool bench = mode == "bench";
+        const int need = bench ? 11 : 9;
+        if (argc < need) return 2;
+        int ai = bench ? 3 : 4;
+        const uint32_t w = (uint32_t)atoi(argv[ai]), h = (uint32_t)atoi(argv[ai + 1]), c = (uint32_t)atoi(argv[ai + 2]);
+        const uint32_t bits = (uint32_t)atoi(argv[ai + 3]), sgnd = (uint32_t)atoi(argv[ai + 4]);
+        uint32_t threads = 0, reps = 1;
+        ai += 5;
+        if (bench) { threads = (uint32_t)atoi(argv[ai]); reps = (uint32_t)atoi(argv[ai + 1]); ai += 2; }
+        std::vector<uint8_t> in = read_file(argv[2]);
+        if (in.size() != (size_t)w * h * c * 4) { fprintf(stderr, "input size mismatch\n"); return 2; }
+        grk_initialize(nullptr, threads);  // returns "plugin loaded": none is, CPU path
+        std::vector<uint8_t> cs;
+        double t_enc = 0, t_dec = 0;
+        for (uint32_t r = 0; r < reps; ++r) {
+            grk_cparameters p;
+            if (!parse_enc_opts(&p, argc - ai, argv + ai)) return 2;
+            auto t0 = std::chrono::steady_clock::now();
+            if (!encode(&p, (const int32_t *)in.data(), w, h, c, bits, sgnd, cs)) { fprintf(stderr, "encode failed\n"); return 1; }
+            auto t1 = std::chrono::steady_clock::now();
+            t_enc += std::chrono::duration<double, std::milli>(t1 - t0).count();
+            if (bench) {
+                grk_codec *codec;
+                grk_stream *st;
+                const uint32_t area[4] = {0, 0, 0, 0};
+                auto t2 = std::chrono::steady_clock::now();
+                grk_image *img = decode(cs.data(), cs.size(), 0, 0, area, &codec, &st);
+                auto t3 = std::chrono::steady_clock::now();
+                if (!img) { fprintf(stderr, "decode failed\n"); return 1; }
+                t_dec += std::chrono::duration<double, std::milli>(t3 - t2).count();
+                grk_destroy_codec(codec);
+                grk_stream_destroy(st);
+            }
+        }
+        if (bench) {
+            printf("{\"enc_ms\": %.3f, \"dec_ms\": %.3f, \"reps\": %u, \"threads\": %u, \"bytes\": %zu}\n", t_enc / reps,
+                   t_dec / reps, reps, threads, cs.size());
+        } else {
+            write_file(argv[3], cs.data(), cs.size());
+        }
+        grk_deinitialize();
+        return 0;
+    }
+    if (mode == "dec") {
+        uint32_t reduce = 0, layers = 0, area[4] = {0, 0, 0, 0};
+        for (int i = 4; i + 1 < argc; i += 2) {
+            std::string a = argv[i];
+            if (a == "-r") reduce = (uint32_t)atoi(argv[i + 1]);
+            else if (a == "-l") layers = (uint32_t)atoi(argv[i + 1]);
+            else if (a == "-d") {
+                if (sscanf(argv[i + 1], "%u,%u,%u,%u", &area[0], &area[1], &area[2], &area[3]) != 4) return 2;
+            } else return 2;
+        }
+        std::vector<uint8_t> cs = read_file(argv[2]);
+        grk_initialize(nullptr, 0);
+        grk_codec *codec;
+        grk_stream *st;
+        grk_image *img = decode(cs.data(), cs.size(), reduce, layers, area, &codec, &st);
+        if (!img) { fprintf(stderr, "decode failed\n"); return 1; }
+        std::vector<int32_t> out;
+        for (uint32_t k = 0; k < img->numcomps; ++k) {
+            const grk_image_comp &cm = img->comps[k];
+            out.insert(out.end(), cm.data, cm.data + (size_t)cm.w * cm.h);
+        }
+        write_file(argv[3], out.data(), out.size() * 4);
+        printf("%u %u %u %u %u %u %u %u %u\n", img->x0, img->y0, img->x1, img->y1, img->numcomps, img->comps[0].prec,
+               img->comps[0].sgnd, img->comps[0].w, img->comps[0].h);
+        grk_destroy_codec(codec);
+        grk_stream_destroy(st);
+        grk_deinitialize();
+        return 0;
+    }
+    return 2;
+}

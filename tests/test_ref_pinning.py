@@ -1,0 +1,49 @@
+"""Pin the golden fixtures to the reference itself (CPU, build container only).
+
+oracle/ref.mk compiles Grok v5.1.0's libgrok straight from /root/reference
+(no CMake), oracle/ref_driver.cpp drives it through the grk_* C API, and
+oracle/make_golden.py --check regenerates every committed fixture with it and
+compares: codestream bytes, the reference decode, and the input image hash.
+Together with tests/test_oracle_golden.py (restated oracle == fixtures) and
+the -m gpu parity tests (HIP path == fixtures), this closes the chain
+reference == fixtures == oracle == GPU.
+
+Skipped where /root/reference does not exist (the GPU box).
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HAVE_REF = os.path.isdir("/root/reference/src/lib/jp2")
+
+pytestmark = pytest.mark.skipif(not HAVE_REF, reason="reference sources not present (GPU box)")
+
+
+def _check(*args):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "make_golden.py"), "--check", *args],
+                       cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_reference_builds_and_exports_grk_api():
+    subprocess.run(["make", "-s", "-f", "oracle/ref.mk", "-j8"], cwd=ROOT, check=True, timeout=900)
+    lib = os.path.join(ROOT, "oracle", "_ref", "libgrok.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    for s in ("grk_create_compress", "grk_setup_encoder", "grk_encode", "grk_decode", "grk_read_header",
+              "grk_plugin_load", "grk_plugin_encode", "grk_plugin_decode"):
+        assert s in syms
+
+
+def test_small_fixtures_regenerate_bit_exact():
+    out = _check()
+    assert "mismatches 0" in out
+
+
+def test_c1_config_hash_regenerates():
+    out = _check("--large", "--only", "C1_512_gray8")
+    assert "C1_512_gray8 ok" in out
