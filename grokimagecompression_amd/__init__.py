@@ -200,6 +200,25 @@ def _torch():
     return torch
 
 
+def _check_out(out, shape, device):
+    """Validate a caller-supplied output (shape, int32, contiguous, device)
+    before raw pointers to it cross the C ABI."""
+    if isinstance(out, np.ndarray):
+        if out.shape != tuple(shape) or out.dtype != np.int32 or not out.flags.c_contiguous:
+            raise GrkGpuError("out must be a C-contiguous int32 array of shape %s (got %s %s)"
+                              % (tuple(shape), out.shape, out.dtype))
+        return False
+    torch = _torch()
+    if not isinstance(out, torch.Tensor):
+        raise GrkGpuError("out must be a numpy array or a torch tensor")
+    if tuple(out.shape) != tuple(shape) or out.dtype != torch.int32 or not out.is_contiguous():
+        raise GrkGpuError("out must be a contiguous int32 tensor of shape %s (got %s %s)"
+                          % (tuple(shape), tuple(out.shape), out.dtype))
+    if not out.is_cuda or out.device.index != device:
+        raise GrkGpuError("out must live on cuda:%d (got %s)" % (device, out.device))
+    return True
+
+
 def _stream_handle(device):
     torch = _torch()
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
@@ -284,13 +303,13 @@ class Codec:
     def decompress_tiles(self, buf, tile_begin, tile_end, out):
         """Decode tiles [tile_begin, tile_end) of a codestream into `out`
         ((c,h,w) int32 numpy array or cuda tensor); other tiles untouched."""
-        c = out.shape[0]
-        on_dev = not isinstance(out, np.ndarray)
+        d = read_header(buf)
+        c = d.numcomps
+        on_dev = _check_out(out, (c, d.y1 - d.y0, d.x1 - d.x0), self.device)
         if on_dev:
             lib().grkgpu_set_stream(self._ctx, _stream_handle(out.device))
             ptrs = (ctypes.c_void_p * c)(*[out[k].data_ptr() for k in range(c)])
         else:
-            assert out.dtype == np.int32 and out.flags.c_contiguous
             ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
         bp, bn, keep = _buf_ptr(buf)
         _check(lib().grkgpu_decompress_tiles(self._ctx, bp, bn, tile_begin, tile_end, ptrs, 1 if on_dev else 0))
@@ -302,6 +321,11 @@ class Codec:
         resolution numres-1-reduce (grk_decompress -r), ceil(x / 2^reduce)
         in every coordinate.  window = (x0, y0, x1, y1) in image coordinates:
         only that region (grk_set_decode_area), clipped to the image."""
+        if reduce and window is not None:
+            # the window ABI has no reduce parameter (grkgpu_decompress_window
+            # decodes at full resolution); refuse rather than mix coordinate
+            # systems (codec.cpp decompress_impl rejects the same combination)
+            raise GrkGpuError("window decode at a reduced resolution is not supported")
         d = read_header(buf)
         if reduce:
             cd = lambda v: -(-v >> reduce)  # noqa: E731
@@ -312,7 +336,10 @@ class Codec:
             if d.x1 <= d.x0 or d.y1 <= d.y0:
                 raise GrkGpuError("decode window outside the image")
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
-        on_dev = device_out or (out is not None and not isinstance(out, np.ndarray))
+        if out is not None:
+            on_dev = _check_out(out, (c, h, w), self.device)
+        else:
+            on_dev = bool(device_out)
         if on_dev:
             torch = _torch()
             if out is None:

@@ -17,6 +17,7 @@
 #include <array>
 #include <chrono>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -80,21 +81,32 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf, mqsort;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf;
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
 };
 
+// Device check, cached per device index (hipGetDeviceProperties is slow and
+// the stage entry points run it per call).  device < 0: the calling thread's
+// current HIP device (the stage entry points work on the caller's device).
 static int check_device(int device) {
+    static std::mutex mu;
+    static int ok[64] = {};  // 0 unknown, 1 gfx950, -1 unusable
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return set_err(GRKGPU_ENODEV, "no HIP device available (MI355X / gfx950 required; no CPU fallback)");
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return set_err(GRKGPU_ENODEV, "hipGetDevice failed");
     if (device < 0 || device >= n) return set_err(GRKGPU_ENODEV, "device index out of range");
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 64 && ok[device] == 1) return GRKGPU_OK;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return set_err(GRKGPU_ENODEV, "hipGetDeviceProperties failed");
-    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+        if (device < 64) ok[device] = -1;
         return set_err(GRKGPU_ENODEV, std::string("unsupported device arch ") + prop.gcnArchName + " (gfx950 required)");
+    }
+    if (device < 64) ok[device] = 1;
     return GRKGPU_OK;
 }
 
@@ -158,7 +170,13 @@ int grkgpu_get_stats(grkgpu_ctx *c, grkgpu_stats *out) {
 
 void grkgpu_free(void *p) { free(p); }
 
-size_t grkgpu_t1_scratch_bytes(void) { return sizeof(T1Scratch) + 32 * (size_t)sym_slot_bytes(64, 64); }
+// Per-block scratch of the T1 stage entry points: the block state, then either
+// 32 symbol-stream slots (encode) or the unstuffed-stream region of a segment
+// of up to GRKGPU_T1_MAX_SEG bytes (decode).
+static uint32_t t1_stage_dec_words() { return t1_unstuff_region_words(GRKGPU_T1_MAX_SEG); }
+size_t grkgpu_t1_scratch_bytes(void) {
+    return sizeof(T1Scratch) + std::max<size_t>(32 * (size_t)sym_slot_bytes(64, 64), (size_t)t1_stage_dec_words() * 4);
+}
 
 }  // extern "C"
 
@@ -489,7 +507,6 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     HIPCHK(c->results.ensure((size_t)nblk * sizeof(EncResult) + 256));
-    HIPCHK(c->mqsort.ensure(t1_mq_sort_words(nblk) * 4 + 256));
     HIPCHK(c->h_results.ensure((size_t)nblk * sizeof(EncResult) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     symoff.push_back(sym_total);
@@ -568,7 +585,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
-                            c->results.as<EncResult>(), s, c->mqsort.as<uint32_t>()));
+                            c->results.as<EncResult>(), s));
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(hipMemcpyAsync(c->h_results.p, c->results.p, (size_t)nblk * sizeof(EncResult), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -890,36 +907,20 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
-    // GRKGPU_T1_SORT=1: deal the blocks to decoder lanes longest segment
-    // first (counting sort on len / 32), so the 64 blocks of a wavefront end
-    // together.  Block order is free (every DecBlock carries its destination).
-    // Off by default: no gain measured with 12 frames in flight (2390-2450
-    // Mpix/s either way over 6-step runs) and 2 % slower for a lone frame.
-    if (getenv("GRKGPU_T1_SORT") && atoi(getenv("GRKGPU_T1_SORT")) != 0) {
-        constexpr uint32_t NB = 4096;
-        std::vector<uint32_t> cnt(NB + 1, 0);
-        auto key = [](const DecBlock &d) { return NB - 1 - std::min<uint32_t>(d.len >> 5, NB - 1); };
-        for (auto &d : db) cnt[key(d) + 1]++;
-        for (uint32_t b = 0; b < NB; ++b) cnt[b + 1] += cnt[b];
-        std::vector<DecBlock> sorted(db.size());
-        for (auto &d : db) sorted[cnt[key(d)]++] = d;
-        db.swap(sorted);
-    }
     double t_t2 = now_ms();
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
-    // v4 decoder: per-block unstuffed-stream regions (16-byte units in pad)
-    const bool flat = t1_dec_flat_enabled();
+    // per-block unstuffed-stream regions (16-byte units in pad)
     uint64_t uwords = 0;
     for (auto &d : db) {
         d.pad = (uint32_t)(uwords / 4);
-        if (flat) uwords += t1_unstuff_region_words(d.len);
+        uwords += t1_unstuff_region_words(d.len);
     }
     if (uwords / 4 > 0xffffffffull) return set_err(GRKGPU_EUNSUPPORTED, "codestream too large for one call");
-    if (flat) HIPCHK(c->ubuf.ensure(uwords * 4 + 256));
+    HIPCHK(c->ubuf.ensure(uwords * 4 + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     memcpy(c->h_blocks.p, db.data(), (size_t)nblk * sizeof(DecBlock));
@@ -946,7 +947,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (win && arena) HIPCHK(hipMemsetAsync(c->coef.p, 0, arena * 4, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
-                            c->coef.as<int32_t>(), s, flat ? c->ubuf.as<uint32_t>() : nullptr));
+                            c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(), 0));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
     HIPCHK(hipEventRecord(c->ev[3], s));
@@ -1037,7 +1038,7 @@ extern "C" int grkgpu_dcshift_mct_fwd(int32_t *const *planes, uint32_t numcomps,
                                       uint32_t stride, const int32_t *shift, int32_t mct, int32_t irreversible,
                                       void *stream) {
     if (!planes || !shift || numcomps < 1 || numcomps > 16) return set_err(GRKGPU_EINVAL, "bad arguments");
-    int rc = check_device(0);
+    int rc = check_device(-1);
     if (rc) return rc;
     PlanePtrs p{};
     ShiftArr sh{};
@@ -1051,7 +1052,7 @@ extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps,
                                       int32_t irreversible, void *stream) {
     if (!planes || !prec || !sgnd || numcomps < 1 || numcomps > 16 || stride < w)
         return set_err(GRKGPU_EINVAL, "bad arguments (stride must be >= w)");
-    int rc = check_device(0);
+    int rc = check_device(-1);
     if (rc) return rc;
     PlanePtrs p{};
     ShiftArr sh{}, mn{}, mx{};
@@ -1090,7 +1091,7 @@ static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, 
                       uint32_t numres, int32_t irrev, void *stream, bool inverse) {
     if (!buf || !scratch || x1 <= x0 || y1 <= y0 || numres < 1 || numres > 33)
         return set_err(GRKGPU_EINVAL, "bad arguments");
-    int rc = check_device(0);
+    int rc = check_device(-1);
     if (rc) return rc;
     TileComp tc;
     dwt_stage_geom(x0, y0, x1, y1, numres, irrev, inverse, tc);
@@ -1138,7 +1139,7 @@ static_assert(sizeof(grkgpu_dec_block) == sizeof(DecBlock), "DecBlock ABI");
 extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
                                        void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream) {
     if (!blocks || !coef || !scratch || !out || !results) return set_err(GRKGPU_EINVAL, "null argument");
-    int rc = check_device(0);
+    int rc = check_device(-1);
     if (rc) return rc;
     // scratch layout: nblocks T1Scratch records, then 32 fixed symbol slots per block
     uint8_t *sym = (uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch);
@@ -1150,9 +1151,12 @@ extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t 
 extern "C" int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t nblocks, const uint8_t *data,
                                        void *scratch, int32_t *dst, void *stream) {
     if (!blocks || !data || !scratch || !dst) return set_err(GRKGPU_EINVAL, "null argument");
-    int rc = check_device(0);
+    int rc = check_device(-1);
     if (rc) return rc;
-    HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (T1Scratch *)scratch, dst,
-                            (hipStream_t)stream));
+    // scratch layout: nblocks T1Scratch records, then one fixed-size
+    // unstuffed-stream region per block
+    uint32_t *ubuf = (uint32_t *)((uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch));
+    HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (T1Scratch *)scratch, dst, (hipStream_t)stream,
+                            ubuf, t1_stage_dec_words()));
     return GRKGPU_OK;
 }

@@ -34,7 +34,7 @@ struct DecBlock {
     uint32_t len, numpasses, numbps, w, h, orient, dstride;
     int32_t irrev;
     float step;
-    uint32_t pad;       // v4 decoder: unstuffed-stream region offset / 16 bytes
+    uint32_t pad;       // unstuffed-stream region offset / 16 bytes (launch_t1_decode)
 };
 
 struct GatherItem { uint64_t src, dst; uint32_t len, pad; };  // pad: 0 = header blob, 1 = MQ slab
@@ -80,14 +80,12 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t *sortbuf = nullptr);
-// words of launch_t1_encode's sortbuf for n blocks (MQ lane order)
-inline size_t t1_mq_sort_words(uint32_t n) { return 1024 + 2 * (size_t)n; }
-// ubuf (optional): unstuffed-stream arena for the v4 decoder, block i's region
-// at blocks[i].pad * 16 bytes (t1_unstuff_region_words); null selects v3.
+                            hipStream_t s);
+// ubuf: unstuffed-stream arena; block i's region at ubuf + i * fixed_words
+// words, or (fixed_words == 0) at blocks[i].pad * 16 bytes
+// (t1_unstuff_region_words words each).
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
-                            int32_t *tiles, hipStream_t s, uint32_t *ubuf = nullptr);
-bool t1_dec_flat_enabled();
+                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words);
 // 32-bit words of a block's unstuffed-stream region (header + words + carries)
 inline uint32_t t1_unstuff_region_words(uint32_t len) { return 4 + unstuff_word_cap(len) + unstuff_carry_cap(len); }
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,

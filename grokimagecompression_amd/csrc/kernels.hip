@@ -202,46 +202,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
                    S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4);
 }
 
-// MQ lane order.  A wavefront of the MQ kernel codes 64 blocks, one per lane,
-// and lasts as long as its longest block, so the blocks are dealt to lanes
-// longest first (symbol count from the modelling pass): a bucketed counting
-// sort in three small kernels -- keys + histogram, exclusive scan, scatter.
-constexpr uint32_t MQ_BUCKETS = 1024;
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
-
-__global__ __launch_bounds__(256) void k_mq_keys(const T1Scratch *__restrict__ scr, const EncResult *__restrict__ res,
-                                                 uint32_t n, uint32_t *__restrict__ key, uint32_t *__restrict__ hist) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t nb = min(res[i].numbps, 32u);
-    const uint32_t *c = scr[i].cnt;
-    uint32_t tot = 0;
-    for (uint32_t p = 0; p < nb; ++p) tot += c[p * 4] + c[p * 4 + 1] + c[p * 4 + 2];
-    const uint32_t b = MQ_BUCKETS - 1 - min(tot >> 6, MQ_BUCKETS - 1);  // longest first
-    key[i] = b;
-    atomicAdd(&hist[b], 1u);
-}
-
-__global__ __launch_bounds__(MQ_BUCKETS) void k_mq_scan(uint32_t *__restrict__ hist) {
-    __shared__ uint32_t s[MQ_BUCKETS];
-    const uint32_t t = threadIdx.x, own = hist[t];
-    s[t] = own;
-    __syncthreads();
-    for (uint32_t off = 1; off < MQ_BUCKETS; off <<= 1) {
-        const uint32_t v = t >= off ? s[t - off] : 0u;
-        __syncthreads();
-        s[t] += v;
-        __syncthreads();
-    }
-    hist[t] = s[t] - own;  // exclusive prefix = first slot of bucket t
-}
-
-__global__ __launch_bounds__(256) void k_mq_scatter(const uint32_t *__restrict__ key, uint32_t *__restrict__ slot,
-                                                    uint32_t n, uint32_t *__restrict__ perm) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    perm[atomicAdd(&slot[key[i]], 1u)] = i;
-}
 
 // MQ coding, one lane per block (lane j codes block perm[j], or j).
 template <int LANES, int MINW = 1>
@@ -273,79 +234,23 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     r.len = len;
 }
 
-template <int LANES>
-__global__ __launch_bounds__(LANES) void k_t1_encode_lane(const EncBlock *__restrict__ blocks, uint32_t n,
-                                                          T1Scratch *__restrict__ scr, uint8_t *__restrict__ out,
-                                                          EncResult *__restrict__ res) {
-    __shared__ uint8_t s_zc[2048];
-    __shared__ uint8_t s_sc[256];
-    __shared__ uint32_t s_mq[48];
-    __shared__ uint32_t s_cx[LANES * 21];
-    t1_tables_init<LANES>(s_zc, s_sc, s_mq);
-    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
-    if (i >= n) return;
-    const EncBlock b = blocks[i];
-    EncResult &r = res[i];
-    const T1Tables T{s_zc, s_sc, s_mq};
-    uint32_t len;
-    uint32_t np = t1_encode_lane(b.w, b.h, r.numbps, scr[i].pa, scr[i].st, T, b.orient, s_cx + threadIdx.x * 21,
-                                 (uint32_t *)(out + b.out_off), r.rate, &len);
-    r.numpasses = np;
-    r.len = len;
+// T1 decoder (t1_flat.h t1_decode_v5).  Pass 1, lane per block: remove the MQ
+// byte stuffing into a plain bit stream + carry events (region of block i at
+// ubuf + i * fixed_words words, or at blocks[i].pad * 16 bytes when
+// fixed_words == 0: header {nwords, ncarry}, words, carries).  Pass 2, lane
+// per block: the pass / stripe / column walk over the unstuffed stream.
+__device__ __forceinline__ size_t ub_region(const DecBlock &b, uint32_t i, uint32_t fixed_words) {
+    return fixed_words ? (size_t)i * fixed_words : (size_t)b.pad * 4;
 }
 
-template <int LANES>
-__global__ __launch_bounds__(LANES) void k_t1_decode_lane(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                          const uint8_t *__restrict__ data,
-                                                          T1Scratch *__restrict__ scr) {
-    __shared__ uint8_t s_zc[2048];
-    __shared__ uint8_t s_sc[256];
-    __shared__ uint32_t s_mq[48];
-    __shared__ uint32_t s_cx[LANES * 21];
-    t1_tables_init<LANES>(s_zc, s_sc, s_mq);
-    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
-    if (i >= n) return;
-    const DecBlock b = blocks[i];
-    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
-    const T1Tables T{s_zc, s_sc, s_mq};
-    T1Scratch &S = scr[i];
-    t1_decode_lane(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, b.orient, S.st, T,
-                   s_cx + threadIdx.x * 21, S.pa, S.pb);
-}
-
-template <int LANES, int MINW = 1>
-__global__ __launch_bounds__(LANES, MINW) void k_t1_decode_v3(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                        const uint8_t *__restrict__ data,
-                                                        T1Scratch *__restrict__ scr) {
-    __shared__ uint8_t s_zc[2048];
-    __shared__ uint8_t s_sc[256];
-    __shared__ uint32_t s_mq[48];
-    __shared__ uint32_t s_cx[LANES * 21];
-    for (uint32_t k = threadIdx.x; k < 2048; k += LANES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
-    for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
-    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
-    __syncthreads();
-    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
-    if (i >= n) return;
-    const DecBlock b = blocks[i];
-    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
-    const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
-    T1Scratch &S = scr[i];
-    t1_decode_v3(data + b.data_off, b.len, b.numpasses, b.numbps, b.w, b.h, S.st, T, s_cx + threadIdx.x * 21, S.pa,
-                 S.pb);
-}
-
-// Decoder v4 (t1_flat.h).  Pass 1, lane per block: remove the MQ byte
-// stuffing into a plain bit stream + carry events (region at blocks[i].pad *
-// 16 bytes: header {nwords, ncarry}, words, carries).  Pass 2, lane per block:
-// one MQ decision per loop iteration.
 __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                   const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf) {
+                                                   const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf,
+                                                   uint32_t fixed_words) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
     const DecBlock b = blocks[i];
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
-    uint32_t *region = ubuf + (size_t)b.pad * 4;
+    uint32_t *region = ubuf + ub_region(b, i, fixed_words);
     uint32_t *words = region + 4, *carries = words + unstuff_word_cap(b.len);
     const uintptr_t pa = (uintptr_t)(data + b.data_off);
     const uint4 *src = (const uint4 *)(pa & ~(uintptr_t)15);
@@ -375,9 +280,9 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     region[1] = nc;
 }
 
-template <int LANES, bool FLAT, int MINW = 1>
-__global__ __launch_bounds__(LANES, MINW) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                        const uint32_t *__restrict__ ubuf,
+template <int LANES>
+__global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                        const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
                                                         T1Scratch *__restrict__ scr) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
@@ -393,13 +298,9 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_decode_ub(const DecBlock *__
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
     T1Scratch &S = scr[i];
-    const uint32_t *region = ubuf + (size_t)b.pad * 4;
-    if (FLAT)
-        t1_decode_flat(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h,
-                       S.st, T, s_cx + threadIdx.x * 21, S.pa, S.pb);
-    else
-        t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h,
-                     S.st, T, s_cx + threadIdx.x * 21, S.pa, S.pb);
+    const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
+    t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, S.st, T,
+                 s_cx + threadIdx.x * 21, S.pa, S.pb);
 }
 
 // One workgroup per block, lane = column: values from the bit-plane rows
@@ -486,184 +387,35 @@ hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32
     return hipGetLastError();
 }
 
-// Decoder selection (GRKGPU_T1_DEC): v5 (default) = v3's pass / stripe /
-// column walk over the unstuffed bit stream (k_t1_unstuff + branch-free MQ
-// renormalisation); v3 = byte-level MQ input; v4 = flat (one decision per
-// loop step; correct but measured 2.2x slower than v3 on the 8K frame);
-// v2 = first lane decoder.  v4 / v5 need the unstuff pass.
-static int t1_dec_mode() {
-    static const int m = [] {
-        const char *e = getenv("GRKGPU_T1_DEC");
-        if (e && !strcmp(e, "v4")) return 4;
-        if (e && !strcmp(e, "v3")) return 3;
-        if (e && !strcmp(e, "v2")) return 2;
-        return 5;
-    }();
-    return m;
-}
-bool t1_dec_flat_enabled() { return t1_dec_mode() >= 4; }
-
-static int t1_mq_lanes() {
-    static int lanes = [] {
-        const char *e = getenv("GRKGPU_MQ_LANES");
-        int v = e ? atoi(e) : 64;  // 64 blocks per wavefront: see t1_dec_lanes
-        return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 64;
-    }();
-    return lanes;
-}
-
-static int t1_lanes() {
-    static int lanes = [] {
-        const char *e = getenv("GRKGPU_T1_LANES");
-        int v = e ? atoi(e) : 16;
-        return (v == 4 || v == 8 || v == 16 || v == 32) ? v : 16;
-    }();
-    return lanes;
-}
-
-template <int L>
-static void launch_enc_lane(const EncBlock *blocks, uint32_t n, T1Scratch *scr, uint8_t *out, EncResult *res,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_t1_encode_lane<L>, dim3((n + L - 1) / L), dim3(L), 0, s, blocks, n, scr, out, res);
-}
-
-static int t1_minw() {
-    static int v = [] {
-        const char *e = getenv("GRKGPU_T1_MINW");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
-template <int L>
-static void launch_dec_lane(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scr, hipStream_t s) {
-    const bool v2 = t1_dec_mode() == 2;
-    const dim3 g((n + L - 1) / L);
-    if (v2) { hipLaunchKernelGGL(k_t1_decode_lane<L>, g, dim3(L), 0, s, blocks, n, data, scr); return; }
-    switch (t1_minw()) {
-        case 2: hipLaunchKernelGGL((k_t1_decode_v3<L, 2>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        case 3: hipLaunchKernelGGL((k_t1_decode_v3<L, 3>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        case 4: hipLaunchKernelGGL((k_t1_decode_v3<L, 4>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        case 5: hipLaunchKernelGGL((k_t1_decode_v3<L, 5>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        case 6: hipLaunchKernelGGL((k_t1_decode_v3<L, 6>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        case 8: hipLaunchKernelGGL((k_t1_decode_v3<L, 8>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-        default: hipLaunchKernelGGL((k_t1_decode_v3<L, 1>), g, dim3(L), 0, s, blocks, n, data, scr); break;
-    }
-}
-
-static int mq_minw() {
-    static int v = [] {
-        const char *e = getenv("GRKGPU_MQ_MINW");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
-template <int L>
-static void launch_mq(const EncBlock *blocks, uint32_t n, const T1Scratch *scr, const uint8_t *sym,
-                      const uint64_t *sym_off, uint8_t *out, EncResult *res, const uint32_t *perm, hipStream_t s) {
-    const dim3 g((n + L - 1) / L);
-    switch (mq_minw()) {
-        case 2: hipLaunchKernelGGL((k_t1_mq<L, 2>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
-        case 4: hipLaunchKernelGGL((k_t1_mq<L, 4>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
-        case 6: hipLaunchKernelGGL((k_t1_mq<L, 6>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
-        case 8: hipLaunchKernelGGL((k_t1_mq<L, 8>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
-        default: hipLaunchKernelGGL((k_t1_mq<L, 1>), g, dim3(L), 0, s, blocks, n, scr, sym, sym_off, out, res, perm); break;
-    }
-}
+// MQ encoder: 64 blocks (lanes) per wavefront.  The coder is a serial chain
+// per block, so throughput = resident blocks / block time: 64 lanes per
+// wavefront keep 4x more blocks resident per wave slot than 16.
+constexpr int MQ_LANES = 64;
+// T1 decoder: 64 blocks (lanes) per wavefront, same reasoning (8K frame batch,
+// 12 frames in flight: 2.0-2.2 vs 1.25 Gpix/s with 16; a lone frame decodes
+// ~10% faster with 16).
+constexpr int DEC_LANES = 64;
 
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t *sortbuf) {
+                            hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
-    static const bool lane = getenv("GRKGPU_T1_ENC") && !strcmp(getenv("GRKGPU_T1_ENC"), "lane");
-    if (lane) {
-        switch (t1_lanes()) {
-            case 8: launch_enc_lane<8>(blocks, n, scratch, out, res, s); break;
-            case 32: launch_enc_lane<32>(blocks, n, scratch, out, res, s); break;
-            case 64: launch_enc_lane<64>(blocks, n, scratch, out, res, s); break;
-            default: launch_enc_lane<16>(blocks, n, scratch, out, res, s); break;
-        }
-        return hipGetLastError();
-    }
     if (maxdepth > 32) maxdepth = 32;
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res);
-    // sortbuf (MQ_BUCKETS + 2n words): histogram / bucket slots, keys, permutation
-    const uint32_t *perm = nullptr;
-    // GRKGPU_MQ_SORT=1 (off by default: no measured gain, see codec.cpp T1_SORT)
-    const bool sort = getenv("GRKGPU_MQ_SORT") && atoi(getenv("GRKGPU_MQ_SORT")) != 0;  // read per call (tests)
-    if (sortbuf && sort) {
-        uint32_t *hist = sortbuf, *key = sortbuf + MQ_BUCKETS, *pm = key + n;
-        hipError_t e = hipMemsetAsync(hist, 0, MQ_BUCKETS * 4, s);
-        if (e != hipSuccess) return e;
-        const dim3 g((n + 255) / 256);
-        hipLaunchKernelGGL(k_mq_keys, g, dim3(256), 0, s, scratch, res, n, key, hist);
-        hipLaunchKernelGGL(k_mq_scan, dim3(1), dim3(MQ_BUCKETS), 0, s, hist);
-        hipLaunchKernelGGL(k_mq_scatter, g, dim3(256), 0, s, key, hist, n, pm);
-        perm = pm;
-    }
-    switch (t1_mq_lanes()) {
-        case 4: launch_mq<4>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
-        case 8: launch_mq<8>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
-        case 16: launch_mq<16>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
-        case 64: launch_mq<64>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
-        default: launch_mq<32>(blocks, n, scratch, sym, sym_off, out, res, perm, s); break;
-    }
+    hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s, blocks, n,
+                       scratch, sym, sym_off, out, res, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 
-
-
-// Lanes (= code-blocks) per wavefront of the v4/v5 decoder.  The decoder is
-// latency-bound per block, so throughput = resident blocks / block time:
-// 64 lanes per wavefront keep 4x more blocks resident per wave slot than 16
-// (8K frame batch, 12 frames in flight: 2.0-2.2 vs 1.25 Gpix/s); a lone
-// frame decodes ~10% faster with 16 (GRKGPU_T1_DEC_LANES=16).
-static int t1_dec_lanes() {
-    static int lanes = [] {
-        const char *e = getenv("GRKGPU_T1_DEC_LANES");
-        int v = e ? atoi(e) : 64;
-        return (v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
-    }();
-    return lanes;
-}
-
-template <int L>
-static void launch_dec_flat(const DecBlock *blocks, uint32_t n, const uint32_t *ubuf, T1Scratch *scr, hipStream_t s) {
-    const dim3 g((n + L - 1) / L);
-    if (t1_dec_mode() == 4) {
-        hipLaunchKernelGGL((k_t1_decode_ub<L, true>), g, dim3(L), 0, s, blocks, n, ubuf, scr);
-        return;
-    }
-    switch (t1_minw()) {
-        case 4: hipLaunchKernelGGL((k_t1_decode_ub<L, false, 4>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
-        case 5: hipLaunchKernelGGL((k_t1_decode_ub<L, false, 5>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
-        default: hipLaunchKernelGGL((k_t1_decode_ub<L, false>), g, dim3(L), 0, s, blocks, n, ubuf, scr); break;
-    }
-}
-
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
-                            int32_t *tiles, hipStream_t s, uint32_t *ubuf) {
+                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words) {
     if (!n) return hipSuccess;
-    if (ubuf && t1_dec_flat_enabled()) {
-        hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf);
-        switch (t1_dec_lanes()) {
-            case 8: launch_dec_flat<8>(blocks, n, ubuf, scratch, s); break;
-            case 32: launch_dec_flat<32>(blocks, n, ubuf, scratch, s); break;
-            case 64: launch_dec_flat<64>(blocks, n, ubuf, scratch, s); break;
-            default: launch_dec_flat<16>(blocks, n, ubuf, scratch, s); break;
-        }
-    } else {
-        switch (t1_lanes()) {
-            case 4: launch_dec_lane<4>(blocks, n, data, scratch, s); break;
-            case 8: launch_dec_lane<8>(blocks, n, data, scratch, s); break;
-            case 32: launch_dec_lane<32>(blocks, n, data, scratch, s); break;
-            default: launch_dec_lane<16>(blocks, n, data, scratch, s); break;
-        }
-    }
+    hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words);
+    hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0, s,
+                       blocks, n, (const uint32_t *)ubuf, fixed_words, scratch);
     hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
     return hipGetLastError();
 }

@@ -194,7 +194,10 @@ typedef struct {
     uint32_t pad;
 } grkgpu_dec_block;
 
-/* scratch: >= nblocks * grkgpu_t1_scratch_bytes() device bytes */
+/* scratch: >= nblocks * grkgpu_t1_scratch_bytes() device bytes.  Decode:
+ * every segment at most GRKGPU_T1_MAX_SEG bytes (w*h*4 + 64 for a 64x64
+ * block, the encoder's slab bound). */
+#define GRKGPU_T1_MAX_SEG (64 * 64 * 4 + 64)
 size_t grkgpu_t1_scratch_bytes(void);
 int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
                             void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream);

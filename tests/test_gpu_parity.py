@@ -60,22 +60,6 @@ def test_encode_fused_mct_dwt(codec, monkeypatch, name):
     assert codec.compress(img, bits, p, offset=off) == open(f"{GOLD}/{name}.j2k", "rb").read()
 
 
-@pytest.mark.parametrize("name", ["rgb12_I", "rgb8_128x96", "g8_tiles64", "g16_uniform_64", "g8_b32_I"])
-def test_sorted_lane_order(codec, monkeypatch, name):
-    """Opt-in longest-first lane order of the MQ encoder (GRKGPU_MQ_SORT) and
-    the decoder (GRKGPU_T1_SORT): same bytes / samples as the reference."""
-    import grokimagecompression_amd as grk
-    monkeypatch.setenv("GRKGPU_MQ_SORT", "1")
-    monkeypatch.setenv("GRKGPU_T1_SORT", "1")
-    m = MAN[name]
-    img, bits = _img(m)
-    p, off = grk.CParams.from_cli(m["args"])
-    gold = open(f"{GOLD}/{name}.j2k", "rb").read()
-    assert codec.compress(img, bits, p, offset=off) == gold
-    d = codec.decompress(gold)
-    assert np.array_equal(d, np.load(f"{GOLD}/{name}.dec.npy"))
-
-
 def test_device_resident_roundtrip(codec):
     import torch
     import grokimagecompression_amd as grk
