@@ -34,12 +34,31 @@ class ImageDesc(ctypes.Structure):
                 ("numcomps", ctypes.c_uint32), ("prec", ctypes.c_uint32 * MAXC), ("sgnd", ctypes.c_int32 * MAXC)]
 
 
+class Poc(ctypes.Structure):
+    """grk_poc (grok.h:393-410): grk_compress -P T<tile>=r0,c0,l1,r1,c1,PROG."""
+    _fields_ = [("tile", ctypes.c_uint32), ("resno0", ctypes.c_uint32), ("compno0", ctypes.c_uint32),
+                ("layno1", ctypes.c_uint32), ("resno1", ctypes.c_uint32), ("compno1", ctypes.c_uint32),
+                ("prog", ctypes.c_int32)]
+
+
+PROGS = {"LRCP": 0, "RLCP": 1, "RPCL": 2, "PCRL": 3, "CPRL": 4}
+CSTY_PRT, CSTY_SOP, CSTY_EPH = 1, 2, 4
+PROFILE_CINEMA_2K, PROFILE_CINEMA_4K = 3, 4
+
+
 class CParams(ctypes.Structure):
-    """grk_cparameters subset (grok.h:447-570)."""
+    """grk_cparameters subset (grok.h:447-570), mirrored by include/grk_mi355x.h."""
     _fields_ = [("numresolution", ctypes.c_uint32), ("cblockw_init", ctypes.c_uint32),
                 ("cblockh_init", ctypes.c_uint32), ("irreversible", ctypes.c_int32), ("tcp_mct", ctypes.c_int32),
                 ("tile_size_on", ctypes.c_int32), ("cp_tdx", ctypes.c_uint32), ("cp_tdy", ctypes.c_uint32),
-                ("cp_tx0", ctypes.c_uint32), ("cp_ty0", ctypes.c_uint32)]
+                ("cp_tx0", ctypes.c_uint32), ("cp_ty0", ctypes.c_uint32),
+                ("tcp_numlayers", ctypes.c_uint32), ("tcp_rates", ctypes.c_double * 100),
+                ("tcp_distoratio", ctypes.c_double * 100), ("cp_disto_alloc", ctypes.c_int32),
+                ("cp_fixed_quality", ctypes.c_int32), ("rate_control_algorithm", ctypes.c_int32),
+                ("csty", ctypes.c_uint32), ("res_spec", ctypes.c_uint32), ("prcw_init", ctypes.c_uint32 * 33),
+                ("prch_init", ctypes.c_uint32 * 33), ("prog_order", ctypes.c_int32), ("numpocs", ctypes.c_uint32),
+                ("POC", Poc * 32), ("tp_on", ctypes.c_int32), ("tp_flag", ctypes.c_int32), ("rsiz", ctypes.c_uint32),
+                ("framerate", ctypes.c_uint32), ("max_cs_size", ctypes.c_uint64), ("max_comp_size", ctypes.c_uint64)]
 
     @classmethod
     def make(cls, numresolution=6, cblk=(64, 64), irreversible=False, mct=-1, tiles=None, tile_offset=(0, 0)):
@@ -52,41 +71,92 @@ class CParams(ctypes.Structure):
         if tiles:
             p.tile_size_on = 1
             p.cp_tdx, p.cp_tdy = tiles
-            p.cp_tx0, p.cp_ty0 = tile_offset
+        p.cp_tx0, p.cp_ty0 = tile_offset
         return p
 
     @classmethod
     def from_cli(cls, args):
-        """Map grk_compress command-line options (-I -n -b -t -T -Y) to params;
-        returns (params, image_offset)."""
-        kw, off, i = {}, (0, 0), 0
+        """Map grk_compress command-line options to params (the option
+        handling of grk_compress.cpp:564-1620); returns (params, image_offset)."""
+        p = cls.make()
+        off, i = (0, 0), 0
+        cinema = 0
         while i < len(args):
             a = args[i]
+            v = args[i + 1] if i + 1 < len(args) else ""
             if a == "-I":
-                kw["irreversible"] = True
-            elif a == "-n":
-                kw["numresolution"] = int(args[i + 1]); i += 1
-            elif a == "-b":
-                kw["cblk"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
-            elif a == "-t":
-                kw["tiles"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
-            elif a == "-T":
-                kw["tile_offset"] = tuple(int(v) for v in args[i + 1].split(",")); i += 1
-            elif a == "-Y":
-                kw["mct"] = int(args[i + 1]); i += 1
-            elif a == "-d":
-                off = tuple(int(v) for v in args[i + 1].split(",")); i += 1
+                p.irreversible = 1
+            elif a in ("-S", "-SOP"):
+                p.csty |= CSTY_SOP
+            elif a in ("-E", "-EPH"):
+                p.csty |= CSTY_EPH
             else:
-                raise ValueError("unsupported grk_compress option %s" % a)
+                i += 1
+                if a == "-n":
+                    p.numresolution = int(v)
+                elif a == "-b":
+                    p.cblockw_init, p.cblockh_init = (int(x) for x in v.split(","))
+                elif a == "-t":
+                    p.tile_size_on = 1
+                    p.cp_tdx, p.cp_tdy = (int(x) for x in v.split(","))
+                elif a == "-T":
+                    p.cp_tx0, p.cp_ty0 = (int(x) for x in v.split(","))
+                elif a == "-Y":
+                    p.tcp_mct = int(v)
+                elif a == "-d":
+                    off = tuple(int(x) for x in v.split(","))
+                elif a == "-p":
+                    p.prog_order = PROGS[v[:4]]
+                elif a == "-A":
+                    p.rate_control_algorithm = int(v)
+                elif a == "-u":
+                    p.tp_on = 1
+                    p.tp_flag = ord(v[0])
+                elif a in ("-r", "-q"):
+                    vals = [float(x) for x in v.split(",")]
+                    p.tcp_numlayers = len(vals)
+                    for k, x in enumerate(vals):
+                        if a == "-r":
+                            p.tcp_rates[k] = 0.0 if x == 1 else x
+                        else:
+                            p.tcp_distoratio[k] = x
+                    if a == "-r":
+                        p.cp_disto_alloc = 1
+                    else:
+                        p.cp_fixed_quality = 1
+                elif a == "-c":
+                    sizes = [tuple(int(y) for y in t.strip("[]").split(",")) for t in v.replace("],[", "];[").split(";")]
+                    p.csty |= CSTY_PRT
+                    p.res_spec = len(sizes)
+                    for k, (w, h) in enumerate(sizes):
+                        p.prcw_init[k], p.prch_init[k] = w, h
+                elif a == "-P":
+                    n = 0
+                    for ent in v.split("/"):
+                        t, rest = ent[1:].split("=")
+                        r0, c0, l1, r1, c1, pr = rest.split(",")
+                        p.POC[n] = Poc(int(t), int(r0), int(c0), int(l1), int(r1), int(c1), PROGS[pr[:4]])
+                        n += 1
+                    p.numpocs = n
+                elif a in ("-cinema2K", "-cinema4K", "-w", "-x"):
+                    cinema = PROFILE_CINEMA_2K if a in ("-cinema2K", "-w") else PROFILE_CINEMA_4K
+                    p.framerate = int(v)
+                else:
+                    raise ValueError("unsupported grk_compress option %s" % a)
             i += 1
-        return cls.make(**kw), off
+        if cinema:  # checkCinema (grk_compress.cpp:537-561)
+            p.rsiz = cinema
+            p.max_comp_size = 520833 if p.framerate == 48 else 1041666
+            p.max_cs_size = 651041 if p.framerate == 48 else 1302083
+        return p, off
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("h2d_ms", ctypes.c_float), ("dcshift_mct_ms", ctypes.c_float), ("dwt_ms", ctypes.c_float),
                 ("t1_ms", ctypes.c_float), ("gather_ms", ctypes.c_float), ("d2h_ms", ctypes.c_float),
                 ("host_t2_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("num_cblks", ctypes.c_uint64),
-                ("cs_bytes", ctypes.c_uint64)]
+                ("cs_bytes", ctypes.c_uint64), ("mq_symbols", ctypes.c_uint64), ("rate_ms", ctypes.c_float),
+                ("pad", ctypes.c_float)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -145,7 +215,7 @@ def lib():
         L.grkgpu_dwt_scratch_bytes.restype = ctypes.c_size_t
         L.grkgpu_dwt_scratch_bytes.argtypes = [U32, U32, U32, U32, U32]
         L.grkgpu_t1_scratch_bytes.restype = ctypes.c_size_t
-        L.grkgpu_t1_encode_blocks.argtypes = [VP, U32, VP, VP, VP, VP, VP]
+        L.grkgpu_t1_encode_blocks.argtypes = [VP, U32, VP, VP, VP, VP, ctypes.c_int, VP]
         L.grkgpu_t1_decode_blocks.argtypes = [VP, U32, VP, VP, VP, VP]
         _lib = L
     return _lib

@@ -10,8 +10,10 @@
 //   host header + Tier-2 parse -> H2D codestream -> ONE T1 decode launch ->
 //   per tile/component inverse DWT levels -> inverse MCT + DC shift.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <array>
@@ -24,6 +26,7 @@
 #include "../../include/grk_mi355x.h"
 #include "codestream.h"
 #include "grk_device.h"
+#include "t2.h"
 
 using namespace grkgpu;
 
@@ -121,6 +124,7 @@ int grkgpu_device_count(void) {
     return n;
 }
 
+// grk_set_default_encoder_parameters (grok.cpp) + grk_compress's defaults
 void grkgpu_default_cparams(grkgpu_cparams *p) {
     memset(p, 0, sizeof(*p));
     p->numresolution = 6;
@@ -128,6 +132,8 @@ void grkgpu_default_cparams(grkgpu_cparams *p) {
     p->cblockh_init = 64;
     p->irreversible = 0;
     p->tcp_mct = -1;
+    p->prog_order = GRKGPU_LRCP;
+    p->tcp_numlayers = 0;  // -> one lossless layer (disto_alloc set then, grk_compress.cpp:1579-1583)
 }
 
 int grkgpu_create(int device, grkgpu_ctx **out) {
@@ -183,10 +189,91 @@ size_t grkgpu_t1_scratch_bytes(void) {
 // ---------------------------------------------------------------------------
 // shared helpers
 // ---------------------------------------------------------------------------
-static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *p, CodingParams &cp) {
-    if (!img || !p) return set_err(GRKGPU_EINVAL, "null image/params");
+static bool cinema_compliant(const grkgpu_image_desc *img, uint32_t rsiz) {
+    // J2KProfile::is_cinema_compliant (j2kprofile.cpp:1083-1135)
+    if (img->numcomps != 3) return false;
+    for (uint32_t k = 0; k < 3; ++k)
+        if (img->prec[k] != 12 || img->sgnd[k]) return false;
+    const uint32_t w = img->x1 - img->x0, h = img->y1 - img->y0;
+    if (rsiz == GRKGPU_PROFILE_CINEMA_2K) return w <= 2048 && h <= 1080;
+    return w <= 4096 && h <= 2160;
+}
+
+// J2KProfile::set_cinema_parameters (j2kprofile.cpp:941-1081)
+static void set_cinema_parameters(grkgpu_cparams *p, const grkgpu_image_desc *img) {
+    p->tile_size_on = 0;
+    p->cp_tdx = p->cp_tdy = 1;
+    p->tp_flag = 'C';
+    p->tp_on = 1;
+    p->cp_tx0 = p->cp_ty0 = 0;
+    p->cblockw_init = p->cblockh_init = 32;
+    p->irreversible = 1;
+    if (p->tcp_numlayers > 1) {
+        p->tcp_rates[0] = p->tcp_rates[p->tcp_numlayers - 1];
+        p->tcp_numlayers = 1;
+    }
+    if (p->rsiz == GRKGPU_PROFILE_CINEMA_2K) {
+        if (p->numresolution > 6) p->numresolution = 6;
+    } else {
+        if (p->numresolution < 2) p->numresolution = 1;
+        else if (p->numresolution > 7) p->numresolution = 7;
+    }
+    p->csty |= GRKGPU_CSTY_PRT;
+    p->res_spec = p->numresolution - 1;
+    for (uint32_t i = 0; i < p->res_spec; i++) p->prcw_init[i] = p->prch_init[i] = 256;
+    p->prog_order = GRKGPU_CPRL;
+    if (p->rsiz == GRKGPU_PROFILE_CINEMA_4K) {  // initialise_4K_poc (j2kprofile.cpp:922-939)
+        const uint32_t nr = p->numresolution;
+        p->POC[0] = {1, 0, 0, 1, nr - 1, 3, GRKGPU_CPRL};
+        p->POC[1] = {1, nr - 1, 0, 1, nr, 3, GRKGPU_CPRL};
+        p->numpocs = 2;
+    } else {
+        p->numpocs = 0;
+    }
+    p->cp_disto_alloc = 1;
+    const uint64_t kCs = 1302083u, kComp = 1041666u;  // GRK_CINEMA_24_CS / _COMP (grok.h:316-318)
+    if (p->max_cs_size == 0 || p->max_cs_size > kCs) p->max_cs_size = kCs;
+    if (p->max_comp_size == 0 || p->max_comp_size > kComp) p->max_comp_size = kComp;
+    const double w = img->x1 - img->x0, h = img->y1 - img->y0;
+    p->tcp_rates[0] = ((double)img->numcomps * w * h * img->prec[0]) / ((double)p->max_cs_size * 8 * 1 * 1);
+}
+
+// j2k_setup_encoder (j2k.cpp:1609-2050) with the grk_compress post-parse
+// defaults (grk_compress.cpp:1579-1583 one lossless layer, :1997-1998 MCT)
+// and the cinema profiles, for the options grkgpu_cparams carries.  Layer
+// rates stay compression ratios here; update_rates converts them to bytes.
+static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin, CodingParams &cp) {
+    if (!img || !pin) return set_err(GRKGPU_EINVAL, "null image/params");
+    grkgpu_cparams P = *pin;  // the profiles rewrite the parameters, as the reference does
+    grkgpu_cparams *p = &P;
     if (img->numcomps < 1 || img->numcomps > 16) return set_err(GRKGPU_EINVAL, "numcomps must be 1..16");
     if (img->x1 <= img->x0 || img->y1 <= img->y0) return set_err(GRKGPU_EINVAL, "empty image");
+    for (uint32_t k = 0; k < img->numcomps; ++k)
+        if (img->prec[k] < 1 || img->prec[k] > 16) return set_err(GRKGPU_EUNSUPPORTED, "precision must be 1..16");
+    if (p->tcp_numlayers > 100) return set_err(GRKGPU_EINVAL, "at most 100 quality layers");
+    if (p->tcp_numlayers == 0) {
+        p->tcp_rates[0] = 0;
+        p->tcp_numlayers = 1;
+        p->cp_disto_alloc = 1;
+    }
+    if (p->cp_disto_alloc && p->cp_fixed_quality) return set_err(GRKGPU_EINVAL, "-r and -q cannot be used together");
+    {  // max codestream size vs layer rates (j2k.cpp:1663-1689)
+        const double image_bytes = ((double)img->numcomps * (img->x1 - img->x0) * (img->y1 - img->y0) * img->prec[0]) / 8;
+        const uint32_t L = p->tcp_numlayers;
+        if (p->max_cs_size == 0) {
+            if (p->tcp_rates[L - 1] > 0) p->max_cs_size = (uint64_t)floor(image_bytes / p->tcp_rates[L - 1]);
+        } else {
+            const double min_rate = image_bytes / (double)p->max_cs_size;
+            for (uint32_t i = 0; i < L; i++)
+                if (p->tcp_rates[i] < min_rate) p->tcp_rates[i] = min_rate;
+        }
+    }
+    if (p->rsiz == GRKGPU_PROFILE_CINEMA_2K || p->rsiz == GRKGPU_PROFILE_CINEMA_4K) {
+        if (cinema_compliant(img, p->rsiz)) set_cinema_parameters(p, img);
+        else p->rsiz = 0;  // "Non-profile-3/4 codestream will be generated"
+    } else if (p->rsiz != 0) {
+        return set_err(GRKGPU_EUNSUPPORTED, "only the 2K / 4K digital cinema profiles are supported");
+    }
     if (p->numresolution < 1 || p->numresolution > 33) return set_err(GRKGPU_EINVAL, "numresolution must be 1..33");
     auto pow2 = [](uint32_t v) { return v >= 4 && v <= 64 && (v & (v - 1)) == 0; };
     if (!pow2(p->cblockw_init) || !pow2(p->cblockh_init))
@@ -194,7 +281,6 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *p, C
     cp.numcomps = img->numcomps;
     cp.image = {img->x0, img->y0, img->x1, img->y1};
     for (uint32_t k = 0; k < img->numcomps; ++k) {
-        if (img->prec[k] < 1 || img->prec[k] > 16) return set_err(GRKGPU_EUNSUPPORTED, "precision must be 1..16");
         cp.prec[k] = img->prec[k];
         cp.sgnd[k] = img->sgnd[k] ? 1 : 0;
         cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
@@ -214,11 +300,67 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *p, C
         cp.tw = ceildiv(img->x1 - cp.tx0, cp.tdx);
         cp.th = ceildiv(img->y1 - cp.ty0, cp.tdy);
     } else {
-        cp.tx0 = cp.ty0 = 0;
-        cp.tdx = img->x1; cp.tdy = img->y1;
+        cp.tx0 = p->cp_tx0; cp.ty0 = p->cp_ty0;
+        if (cp.tx0 > img->x0 || cp.ty0 > img->y0) return set_err(GRKGPU_EINVAL, "tile origin after the image origin");
+        cp.tdx = img->x1 - cp.tx0; cp.tdy = img->y1 - cp.ty0;
         cp.tw = cp.th = 1;
     }
     if ((uint64_t)cp.tw * cp.th > 65535) return set_err(GRKGPU_EINVAL, "too many tiles");
+    // layers and rate control (j2k.cpp:1841-1857)
+    cp.numlayers = p->tcp_numlayers;
+    cp.disto_alloc = p->cp_disto_alloc ? 1 : 0;
+    cp.fixed_quality = p->cp_fixed_quality ? 1 : 0;
+    cp.rate_algo = p->rate_control_algorithm == 1 ? 1 : 0;
+    for (uint32_t j = 0; j < cp.numlayers; ++j) {
+        const bool prof = p->rsiz != 0;
+        if (cp.fixed_quality) cp.distoratio[j] = p->tcp_distoratio[j];
+        if (prof || !cp.fixed_quality) cp.rates[j] = p->tcp_rates[j];
+    }
+    cp.rsiz = (uint16_t)p->rsiz;
+    cp.max_cs_size = p->max_cs_size;
+    cp.max_comp_size = p->max_comp_size;
+    // coding style, precincts (j2k.cpp:1989-2041), progression, tile-parts
+    if (p->csty & ~7u) return set_err(GRKGPU_EINVAL, "unknown csty bits");
+    cp.csty = p->csty;
+    if (p->prog_order < 0 || p->prog_order > 4) return set_err(GRKGPU_EINVAL, "unknown progression order");
+    cp.prog = (uint32_t)p->prog_order;
+    if ((cp.csty & CSTY_PRT) && p->res_spec) {
+        uint32_t q = 0;
+        for (int32_t r = (int32_t)cp.numres - 1; r >= 0; --r, ++q) {
+            uint32_t w, h;
+            if (q < p->res_spec) {
+                w = p->prcw_init[q];
+                h = p->prch_init[q];
+            } else {
+                const uint32_t rs = p->res_spec;
+                w = p->prcw_init[rs - 1] >> (q - (rs - 1));
+                h = p->prch_init[rs - 1] >> (q - (rs - 1));
+            }
+            cp.prcw[r] = (uint8_t)(w < 1 ? 1 : floorlog2((int32_t)w));
+            cp.prch[r] = (uint8_t)(h < 1 ? 1 : floorlog2((int32_t)h));
+        }
+    } else {
+        cp.csty &= ~CSTY_PRT;
+        for (uint32_t r = 0; r < cp.numres; ++r) cp.prcw[r] = cp.prch[r] = 15;
+    }
+    if (p->numpocs) {
+        // POC entries of tile 1 (the reference copies tile-matching entries,
+        // j2k.cpp:1866-1890); more than one tile with POCs is not supported
+        if (p->numpocs > 32) return set_err(GRKGPU_EINVAL, "at most 32 progression order changes");
+        if (cp.tw * cp.th != 1) return set_err(GRKGPU_EUNSUPPORTED, "progression order changes need a single tile");
+        uint32_t n = 0;
+        for (uint32_t i = 0; i < p->numpocs; ++i) {
+            if (p->POC[i].tile != 1) continue;
+            const grkgpu_poc &src = p->POC[n];  // sic: indexed by the entry count (j2k.cpp:1872-1878)
+            if (src.prog < 0 || src.prog > 4) return set_err(GRKGPU_EINVAL, "unknown POC progression");
+            cp.pocs[n] = {src.resno0, src.compno0, src.layno1, src.resno1, src.compno1, (uint32_t)src.prog};
+            ++n;
+        }
+        if (!n) return set_err(GRKGPU_EINVAL, "Problem with specified progression order changes");
+        cp.numpocs = n;
+    }
+    cp.tp_on = p->tp_on != 0;
+    cp.tp_flag = (char)p->tp_flag;
     generate_qcd(cp);
     return GRKGPU_OK;
 }
@@ -458,6 +600,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     uint64_t arena = 0, llarena = 0;
     std::vector<uint64_t> lloff(ntiles * nc);
     std::vector<EncBlock> eb;
+    struct BlkInfo { uint32_t compno, level, orient; float stepsize; };  // distortion weights (t1_getwmsedec)
+    std::vector<BlkInfo> binfo;
     std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
     uint64_t sym_total = 0;
     uint32_t maxdepth = 1;
@@ -486,6 +630,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 b.qmfbid = cp.irrev ? 0 : 1;
                 b.inv_step = (int32_t)band.inv_step;
                 eb.push_back(b);
+                uint32_t resno = 0;
+                while (&tc.res[resno].bands[0] > &band || &tc.res[resno].bands[2] < &band) ++resno;
+                binfo.push_back({k, tc.numres - 1 - resno, band.bandno, band.stepsize});
                 const uint32_t bound = std::min<uint32_t>(band.numbps, 32);
                 symoff.push_back(sym_total);
                 sym_total += (uint64_t)bound * sym_slot_bytes(b.w, b.h);
@@ -586,52 +733,207 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
                             c->results.as<EncResult>(), s));
+    // per-pass distortion only when some layer is rate-controlled
+    // (TileProcessor::needs_rate_control, TileProcessor.cpp:260-266)
+    bool need_rc = false;
+    for (uint32_t l = 0; l < cp.numlayers; ++l)
+        need_rc = need_rc || (cp.disto_alloc && cp.rates[l] > 0.0) || (cp.fixed_quality && cp.distoratio[l] > 0.0f);
+    if (need_rc)
+        HIPCHK(launch_t1_dist(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
+                              c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), c->results.as<EncResult>(), s));
     HIPCHK(hipEventRecord(c->ev[4], s));
-    HIPCHK(hipMemcpyAsync(c->h_results.p, c->results.p, (size_t)nblk * sizeof(EncResult), hipMemcpyDeviceToHost, s));
+    if (nblk)
+        HIPCHK(hipMemcpy2DAsync(c->h_results.p, sizeof(EncResult), c->results.p, sizeof(EncResult),
+                                need_rc ? sizeof(EncResult) : ENC_RESULT_RATE_BYTES, nblk, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const EncResult *res = c->h_results.as<EncResult>();
 
-    // Tier-2 + headers on the host (j2k_encode :2059, j2k_write_sot :5065,
-    // T2::encode_packets): only header BITS are produced here; the code-block
-    // bytes never visit the host -- a gather kernel assembles the codestream
-    // in HBM and one D2H copies it into the pinned output buffer.
+    // Tier-2 + headers on the host (j2k_encode :2059, j2k_post_write_tile
+    // :2196, T2::encode_packets): only header BITS are produced here; the
+    // code-block bytes never visit the host -- a gather kernel assembles the
+    // codestream in HBM and one D2H copies it into the pinned output buffer.
     double t_t2 = now_ms();
-    std::vector<BlockT2> bt(nblk);
+    const uint32_t L = cp.numlayers;
+    std::vector<EncCblkState> cst(nblk);
+    std::vector<EncPass> passes;
+    std::vector<EncLayer> layers((size_t)nblk * L, EncLayer{0, 0, 0, 0.0});
+    std::vector<double> blk_disto(nblk, 0.0);
+    const double *mct_norms = nullptr;
+    uint32_t mct_numcomps = 0;
+    if (cp.mct == 1) {  // TileProcessor::t1_encode (TileProcessor.cpp:1535-1551), mct.cpp:65-79
+        static const double kRev[3] = {1.732, .8292, .8292}, kIrrev[3] = {1.732, 1.805, 1.573};
+        mct_norms = cp.irrev ? kIrrev : kRev;
+        mct_numcomps = 3;
+    } else {
+        mct_numcomps = nc;
+    }
+    uint64_t nsym = 0;
     for (uint32_t i = 0; i < nblk; ++i) {
         const EncResult &r = res[i];
         if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
         if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
-        bt[i].numbps = r.numbps;
-        bt[i].numpasses = r.numpasses;
-        bt[i].rate = r.rate;
-        bt[i].datalen = r.numpasses ? r.rate[r.numpasses - 1] : 0;
-        bt[i].dev_off = eb[i].out_off;
-        if (bt[i].datalen > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+        const uint32_t np = r.numpasses;
+        if (np && r.rate[np - 1] > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+        nsym += r.nsym;
+        EncCblkState &st = cst[i];
+        st.numbps = r.numbps;
+        st.numpasses = np;
+        st.pass0 = (uint32_t)passes.size();
+        st.dev_off = eb[i].out_off;
+        double cum = 0.0;
+        for (uint32_t k = 0; k < np; ++k) {
+            EncPass ps;
+            ps.rate = r.rate[k];
+            ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
+            ps.term = k == np - 1;  // cblksty 0: only the last pass is terminated (t1_enc_is_term_pass)
+            ps.slope = 0;
+            if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
+                const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                const BlkInfo &bi = binfo[i];
+                cum += t1_wmsedec(r.nmsedec[k], bi.compno, bi.level, bi.orient, bpno, cp.irrev ? 0 : 1,
+                                  (double)bi.stepsize, mct_norms, mct_numcomps);
+            }
+            ps.dd = cum;
+            passes.push_back(ps);
+        }
+        blk_disto[i] = cum;
+    }
+    // tile-parts of every tile (j2k_calculate_tp, j2k.cpp:2990-3048): needed
+    // for the TLM marker and the rate bookkeeping even outside the shard
+    const uint32_t ntot = cp.tw * cp.th;
+    std::vector<std::vector<uint32_t>> tp_counts(ntot);  // [tile][poc entry]
+    uint32_t total_tile_parts = 0;
+    for (uint32_t t = 0; t < ntot; ++t) {
+        Tile tmp;
+        const Tile *tp = nullptr;
+        if (t >= tb && t < te) tp = &tiles[t - tb];
+        else if (cp.tp_on) {
+            tmp.index = t;
+            tmp.r = tile_rect(cp, t);
+            tmp.comps.resize(nc);
+            for (uint32_t k = 0; k < nc; ++k) build_tilecomp(tmp.comps[k], tmp.r, cp, k, true);
+            tp = &tmp;
+        }
+        if (tp) tp_counts[t] = tile_part_counts(cp, *tp);
+        else tp_counts[t].assign(num_poc_entries(cp), 1);
+        uint32_t n = 0;
+        for (uint32_t v : tp_counts[t]) n += v;
+        if (n > 255) return set_err(GRKGPU_EUNSUPPORTED, "more than 255 tile-parts in a tile");
+        total_tile_parts += n;
     }
     ByteBuf hdr;
     hdr.v.reserve(1 << 20);
     std::vector<PlanItem> plan;
     plan.reserve(nblk + 64);
+    size_t tlm_at = 0;
+    ByteBuf mainhdr;
+    write_main_header(mainhdr, cp, &tlm_at, total_tile_parts);
     if (parts & GRKGPU_PART_HEADER) {
-        write_main_header(hdr, cp);
+        hdr.putn(mainhdr.v.data(), mainhdr.size());
         plan.push_back({0, (uint32_t)hdr.size(), 0});
     }
-    for (auto &tile : tiles) {
-        size_t sot = hdr.size();
-        hdr.put16(0xFF90); hdr.put16(10); hdr.put16(tile.index); hdr.put32(0); hdr.put8(0); hdr.put8(1);
-        hdr.put16(0xFF93);
-        plan.push_back({sot, 14, 0});
-        size_t first = plan.size() - 1;
-        for (uint32_t resno = 0; resno < cp.numres; ++resno)  // LRCP, one layer
-            for (uint32_t k = 0; k < nc; ++k) {
-                TileComp &tc = tile.comps[k];
-                Resolution &r = tc.res[resno];
-                for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) encode_packet(tc, resno, precno, bt, hdr, plan);
+    // j2k_update_rates (j2k.cpp:2806-2926): layer ratios -> byte budgets per tile
+    const double header_size = (double)mainhdr.size();
+    const double bits_empty = 8.0, size_pixel = (double)nc * cp.prec[0];
+    const uint32_t width = iw, height = ih;
+    auto tile_rates = [&](const Rect &tr, uint32_t ntp, double *rates) {
+        const double offset = (double)(cp.tp_on ? (float)((ntp - 1) * 14) : 0.0f) / L;
+        const uint64_t npix = (uint64_t)tr.w() * tr.h();
+        for (uint32_t k = 0; k < L; ++k) {
+            rates[k] = cp.rates[k];
+            if (rates[k] > 0.0f) rates[k] = (size_pixel * (double)npix) / (rates[k] * bits_empty) - offset;
+        }
+        rates[L] = 0;
+        const double sot_adjust = ((double)npix * header_size) / ((double)width * height);
+        double *r = rates;
+        if (*r > 0.0) {
+            *r -= sot_adjust;
+            if (*r < 30.0f) *r = 30.0f;
+        }
+        ++r;
+        const uint32_t last_res = L - 1;
+        for (uint32_t k = 1; k < last_res; ++k) {
+            if (*r > 0.0) {
+                *r -= sot_adjust;
+                if (*r < *(r - 1) + 10.0) *r = (*(r - 1)) + 20.0;
             }
-        uint64_t psot = 0;
-        for (size_t i = first; i < plan.size(); ++i) psot += plan[i].len;
-        hdr.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
+            ++r;
+        }
+        if (*r > 0.0) {
+            *r -= (sot_adjust + 2.0);
+            if (*r < *(r - 1) + 10.0) *r = (*(r - 1)) + 20.0;
+        }
+    };
+    // tile buffer bound for the rate allocator (j2k_post_write_tile :2196-2222,
+    // j2k_get_specific_header_sizes :4346-4366, then SOT / POC / SOD / EOC room)
+    const bool cinema = cp.rsiz == RSIZ_CINEMA_2K || cp.rsiz == RSIZ_CINEMA_4K;
+    uint64_t tile_bound;
+    {
+        uint64_t ts = 0;
+        for (uint32_t k = 0; k < nc; ++k) ts += (uint64_t)cp.tdx * cp.tdy * cp.prec[k];
+        ts = (uint64_t)((double)ts * 0.1625);
+        uint32_t max_tp = 0;
+        for (auto &v : tp_counts) {
+            uint32_t n = 0;
+            for (uint32_t x : v) n += x;
+            max_tp = std::max(max_tp, n);
+        }
+        uint64_t spec = 12ull * max_tp;
+        if (!cinema) {
+            const uint64_t coc = 6 + ((cp.csty & CSTY_PRT) ? 5 + cp.numres : 5);
+            spec += (uint64_t)(nc - 1) * coc * 2;
+        }
+        spec += 4 + 9ull * num_poc_entries(cp);
+        ts += spec;
+        if (ts < 256ull * nc) ts = 256ull * nc;
+        const uint64_t pocsz = (!cinema && cp.numpocs) ? 4 + (5 + 2 * (nc <= 256 ? 1 : 2)) * cp.numpocs : 0;
+        tile_bound = ts - 12 - pocsz - 4;
     }
+    std::vector<uint8_t> tlm;  // TLM records (j2k_update_tlm, j2k.cpp:6649-6660)
+    double t_rate = 0;
+    std::vector<PacketId> order;
+    for (auto &tile : tiles) {
+        TileEnc tenc;
+        tenc.tile = &tile;
+        tenc.cblk = &cst;
+        tenc.passes = &passes;
+        tenc.layers = &layers;
+        init_enc_pocs(cp, tenc);
+        CodingParams cpt = cp;
+        uint32_t ntp = 0;
+        for (uint32_t v : tp_counts[tile.index]) ntp += v;
+        tile_rates(tile.r, ntp, cpt.rates);
+        tenc.distotile = 0;
+        for (auto &tc : tile.comps) for_each_cblk(tc, [&](Band &, Cblk &cb) { tenc.distotile += blk_disto[cb.gidx]; });
+        const double tr0 = now_ms();
+        if (!rate_allocate(cpt, tenc, tile_bound)) return set_err(GRKGPU_EINVAL, "rate allocation failed");
+        t_rate += now_ms() - tr0;
+        tenc.packno = 0;
+        uint32_t tpno = 0;
+        for (uint32_t pino = 0; pino < tenc.pocs.size(); ++pino) {
+            for (uint32_t tpn = 0; tpn < tp_counts[tile.index][pino]; ++tpn) {
+                const size_t sot = hdr.size();
+                hdr.put16(0xFF90); hdr.put16(10); hdr.put16(tile.index); hdr.put32(0); hdr.put8(tpno); hdr.put8(ntp);
+                if (tpno == 0 && !cinema && cp.numpocs) write_poc(hdr, cpt);
+                hdr.put16(0xFF93);
+                plan.push_back({sot, (uint32_t)(hdr.size() - sot), 0});
+                const size_t first = plan.size() - 1;
+                encode_packet_order(cpt, tenc, pino, tpn, order);
+                for (auto &pk : order)
+                    if (pk.layno < L) write_packet(cpt, tenc, pk, hdr, plan);
+                uint64_t psot = 0;
+                for (size_t i = first; i < plan.size(); ++i) psot += plan[i].len;
+                hdr.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
+                if (cinema) {
+                    tlm.push_back((uint8_t)tile.index);
+                    for (int b = 3; b >= 0; --b) tlm.push_back((uint8_t)(psot >> (8 * b)));
+                }
+                ++tpno;
+            }
+        }
+    }
+    if ((parts & GRKGPU_PART_HEADER) && tlm_at && tlm.size() == 5ull * total_tile_parts)
+        memcpy(hdr.v.data() + tlm_at, tlm.data(), tlm.size());  // j2k_write_updated_tlm (:2555-2577)
     if (parts & GRKGPU_PART_EOC) {
         size_t eoc = hdr.size();
         hdr.put16(0xFFD9);
@@ -678,6 +980,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     st.total_ms = (float)(t_end - t_start);
     st.num_cblks = nblk;
     st.cs_bytes = total;
+    st.mq_symbols = nsym;
+    st.rate_ms = (float)t_rate;
     return GRKGPU_OK;
 }
 
@@ -802,6 +1106,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
     std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
+    std::vector<std::vector<std::pair<size_t, uint32_t>>> tpocs(ntiles);  // tile-part header POC segments
     while (pos + 2 <= len) {
         uint32_t m = rd16(csb + pos);
         if (m == 0xFFD9) break;
@@ -814,9 +1119,12 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         pos += 12;
         while (pos + 4 <= end && rd16(csb + pos) != 0xFF93) {
             uint32_t mm = rd16(csb + pos);
-            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5F)
-                return set_err(GRKGPU_EUNSUPPORTED, "tile-part header coding markers not supported");
-            pos += 2 + rd16(csb + pos + 2);
+            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5E || mm == 0xFF61)
+                return set_err(GRKGPU_EUNSUPPORTED, "tile-part header COD/QCD/COC/QCC/RGN/PPT markers not supported");
+            const uint32_t ml = rd16(csb + pos + 2);
+            if (ml < 2 || pos + 2 + ml > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part header marker");
+            if (mm == 0xFF5F) tpocs[isot].push_back({pos + 4, ml - 2});  // j2k_read_poc on the tile's tcp
+            pos += 2 + ml;
         }
         pos += 2;
         if (pos > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part");
@@ -863,19 +1171,22 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             tlen = tilebuf.size();
             base = 0;
         }
+        // packets in the tile's progression (T2::decode_packets, T2.cpp:194-258),
+        // POC entries of the main header followed by the tile's own
+        CodingParams tcp = cp;
+        for (auto &pc : tpocs[t])
+            if (!parse_poc(csb + pc.first, pc.second, tcp)) return set_err(GRKGPU_ECORRUPT, "Error reading POC marker");
+        std::vector<PacketId> order;
+        decode_packet_order(tcp, tile, order);
         size_t off = 0;
-        bool stop = false;
-        for (uint32_t layno = 0; layno < cp.numlayers && !stop; ++layno)
-            for (uint32_t resno = 0; resno < cp.numres && !stop; ++resno)
-                for (uint32_t k = 0; k < nc && !stop; ++k) {
-                    Resolution &r = tile.comps[k].res[resno];
-                    for (uint32_t precno = 0; precno < r.pw * r.ph; ++precno) {
-                        if (off >= tlen) { stop = true; break; }
-                        int64_t used = decode_packet(tile.comps[k], resno, precno, layno, td + off, tlen - off, base + off);
-                        if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
-                        off += (size_t)used;
-                    }
-                }
+        uint32_t packno = 0;
+        for (const auto &pk : order) {
+            if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
+            int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
+                                         base + off, tcp.csty, &packno);
+            if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
+            off += (size_t)used;
+        }
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
             const BandNeed need = win ? window_need(tc, wr) : BandNeed();
@@ -888,7 +1199,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 d.orient = band.bandno;
                 d.irrev = cp.irrev;
                 d.step = band.stepsize;
-                d.numpasses = cb.numpasses;
+                // passes beyond the last bit-plane are not decoded (t1_decode_cblk
+                // stops at bpno < 0, t1.cpp:1086-1090)
+                d.numpasses = std::min<uint32_t>(cb.numpasses, cb.numbps ? 3 * cb.numbps - 2 : 0);
                 d.numbps = cb.numbps;
                 d.len = cb.seglen;
                 if (cb.chunks.size() == 1 && contiguous) {
@@ -1137,7 +1450,8 @@ static_assert(sizeof(grkgpu_enc_result) == sizeof(EncResult), "EncResult ABI");
 static_assert(sizeof(grkgpu_dec_block) == sizeof(DecBlock), "DecBlock ABI");
 
 extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
-                                       void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream) {
+                                       void *scratch, uint8_t *out, grkgpu_enc_result *results, int with_distortion,
+                                       void *stream) {
     if (!blocks || !coef || !scratch || !out || !results) return set_err(GRKGPU_EINVAL, "null argument");
     int rc = check_device(-1);
     if (rc) return rc;
@@ -1145,6 +1459,9 @@ extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t 
     uint8_t *sym = (uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch);
     HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, (T1Scratch *)scratch, sym, nullptr, 32, out,
                             (EncResult *)results, (hipStream_t)stream));
+    if (with_distortion)
+        HIPCHK(launch_t1_dist((const EncBlock *)blocks, nblocks, coef, (const T1Scratch *)scratch, sym, nullptr,
+                              (EncResult *)results, (hipStream_t)stream));
     return GRKGPU_OK;
 }
 

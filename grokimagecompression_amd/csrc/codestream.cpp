@@ -130,7 +130,7 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
         Resolution &res = tc.res[resno];
         const uint32_t lev = cp.numres - 1 - resno;
         res.r = {ceildivpow2(tr.x0, lev), ceildivpow2(tr.y0, lev), ceildivpow2(tr.x1, lev), ceildivpow2(tr.y1, lev)};
-        const uint32_t pdx = 15, pdy = 15;  // default precinct 2^15
+        const uint32_t pdx = cp.prcw[resno], pdy = cp.prch[resno];  // log2 precinct size (COD SPcod I_i)
         uint32_t tpx0 = (res.r.x0 >> pdx) << pdx, tpy0 = (res.r.y0 >> pdy) << pdy;
         uint32_t bpx1 = ceildivpow2(res.r.x1, pdx) << pdx, bpy1 = ceildivpow2(res.r.y1, pdy) << pdy;
         res.pw = (res.r.x0 == res.r.x1) ? 0 : ((bpx1 - tpx0) >> pdx);
@@ -195,22 +195,50 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
 // ---------------------------------------------------------------------------
 // headers (codestream/j2k.cpp marker writers :3117-5540)
 // ---------------------------------------------------------------------------
-void write_main_header(ByteBuf &cs, const CodingParams &cp) {
+void write_poc(ByteBuf &cs, const CodingParams &cp) {
+    const uint32_t n = cp.numpocs, room = cp.numcomps <= 256 ? 1 : 2;
+    cs.put16(0xFF5F); cs.put16(2 + (5 + 2 * room) * n);  // Lpoc = getPocSize - 2 (j2k.cpp:4208-4216)
+    for (uint32_t i = 0; i < n; ++i) {
+        const PocSpec &q = cp.pocs[i];
+        cs.put8(q.resno0);
+        if (room == 2) cs.put16(q.compno0); else cs.put8(q.compno0);
+        cs.put16(q.layno1);
+        cs.put8(q.resno1);
+        if (room == 2) cs.put16(q.compno1); else cs.put8(q.compno1);
+        cs.put8(q.prg);
+    }
+}
+
+void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at, uint32_t total_tile_parts) {
     const uint32_t nc = cp.numcomps, nd = cp.numres - 1, nb = 3 * nd + 1;
+    const bool prt = (cp.csty & CSTY_PRT) != 0;
     cs.put16(0xFF4F);  // SOC
-    cs.put16(0xFF51); cs.put16(38 + 3 * nc); cs.put16(0);  // SIZ, Rsiz = 0
+    cs.put16(0xFF51); cs.put16(38 + 3 * nc); cs.put16(cp.rsiz);  // SIZ
     cs.put32(cp.image.x1); cs.put32(cp.image.y1); cs.put32(cp.image.x0); cs.put32(cp.image.y0);
     cs.put32(cp.tdx); cs.put32(cp.tdy); cs.put32(cp.tx0); cs.put32(cp.ty0);
     cs.put16(nc);
     for (uint32_t k = 0; k < nc; ++k) { cs.put8((cp.prec[k] - 1) + ((uint32_t)cp.sgnd[k] << 7)); cs.put8(1); cs.put8(1); }
-    cs.put16(0xFF52); cs.put16(12);  // COD
-    cs.put8(0); cs.put8(cp.prog); cs.put16(cp.numlayers); cs.put8((uint32_t)cp.mct);
+    // COD (j2k_write_cod + j2k_write_SPCod_SPCoc, j2k.cpp:3723-3770, 6905-6950)
+    cs.put16(0xFF52); cs.put16(12 + (prt ? cp.numres : 0));
+    cs.put8(cp.csty); cs.put8(cp.prog); cs.put16(cp.numlayers); cs.put8((uint32_t)cp.mct);
     cs.put8(nd); cs.put8(cp.cblkw - 2); cs.put8(cp.cblkh - 2); cs.put8(cp.cblksty); cs.put8(cp.irrev ? 0 : 1);
+    if (prt)
+        for (uint32_t r = 0; r < cp.numres; ++r) cs.put8(cp.prcw[r] + (cp.prch[r] << 4));
     cs.put16(0xFF5C); cs.put16(3 + nb * (cp.irrev ? 2 : 1));  // QCD
     cs.put8((2u << 5) | (cp.irrev ? 2u : 0u));
     for (uint32_t i = 0; i < nb; ++i) {
         if (cp.irrev) cs.put16((cp.ss[i].expn << 11) | cp.ss[i].mant);
         else cs.put8(cp.ss[i].expn << 3);
+    }
+    if (tlm_at) *tlm_at = 0;
+    if (cp.rsiz == RSIZ_CINEMA_2K || cp.rsiz == RSIZ_CINEMA_4K) {
+        // TLM (j2k_write_tlm, j2k.cpp:5027-5063): Ztlm 0, Stlm 0x50 (8-bit
+        // tile index, 32-bit lengths); records patched once every tile-part is
+        // written (j2k_write_updated_tlm, :2555-2577)
+        cs.put16(0xFF55); cs.put16(4 + 5 * total_tile_parts); cs.put8(0); cs.put8(0x50);
+        if (tlm_at) *tlm_at = cs.size();
+        for (uint32_t i = 0; i < 5 * total_tile_parts; ++i) cs.put8(0);
+        if (cp.rsiz == RSIZ_CINEMA_4K) write_poc(cs, cp);  // main-header POC (j2k.cpp:2353-2356)
     }
     static const char kCom[] = "Created by Grok     version 5.1.0";  // j2k.cpp:1798
     cs.put16(0xFF64); cs.put16(4 + (uint32_t)strlen(kCom)); cs.put16(1);
@@ -221,45 +249,6 @@ void write_main_header(ByteBuf &cs, const CodingParams &cp) {
 // packet header bit writer (codestream/BitIO.cpp)
 // ---------------------------------------------------------------------------
 namespace {
-struct BitWriter {
-    ByteBuf &out;
-    uint32_t buf = 0, ct = 8;
-    explicit BitWriter(ByteBuf &o) : out(o) {}
-    void byteout() { out.put8(buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
-    void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
-    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
-    void flush() { byteout(); if (ct == 7) byteout(); }
-    void numpasses(uint32_t n) {
-        if (n == 1) write(0, 1);
-        else if (n == 2) write(2, 2);
-        else if (n <= 5) write(0xc | (n - 3), 4);
-        else if (n <= 36) write(0x1e0 | (n - 6), 9);
-        else write(0xff80 | (n - 37), 16);
-    }
-    void comma(int32_t n) { while (--n >= 0) write(1, 1); write(0, 1); }
-    // TagTree::encode (TagTree.cpp:251-287)
-    void tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
-        int32_t stk[64], sp = 0, node = (int32_t)leaf;
-        while (t.nodes[node].parent >= 0) { stk[sp++] = node; node = t.nodes[node].parent; }
-        int64_t low = 0;
-        for (;;) {
-            TagTree::Node &n = t.nodes[node];
-            if (low > n.low) n.low = low; else low = n.low;
-            while (low < threshold) {
-                if (low >= n.value) {
-                    if (!n.known) { write(1, 1); n.known = 1; }
-                    break;
-                }
-                write(0, 1);
-                ++low;
-            }
-            n.low = low;
-            if (sp == 0) break;
-            node = stk[--sp];
-        }
-    }
-};
-
 struct BitReader {
     const uint8_t *p;
     size_t n, off = 0;
@@ -305,83 +294,41 @@ struct BitReader {
 };
 }  // namespace
 
-void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk, ByteBuf &out,
-                   std::vector<PlanItem> &plan) {
-    const size_t hstart = out.size();
-    Resolution &res = tc.res[resno];
-    const uint32_t layno = 0;
-    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
-        Band &b = res.bands[bandno];
-        Precinct &pr = b.precs[precno];
-        if (b.empty() || pr.cblks.empty()) continue;
-        pr.incl.reset(); pr.imsb.reset();
-        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
-            pr.cblks[cb].included = false;
-            pr.imsb.setvalue(cb, (int64_t)b.numbps - (int64_t)blk[pr.cblks[cb].gidx].numbps);
-        }
-    }
-    BitWriter w(out);
-    w.write(1, 1);  // Grok always signals a non-empty packet (T2.cpp:924-927)
-    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
-        Band &b = res.bands[bandno];
-        Precinct &pr = b.precs[precno];
-        if (b.empty() || pr.cblks.empty()) continue;
-        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb)
-            if (!pr.cblks[cb].included && blk[pr.cblks[cb].gidx].numpasses) pr.incl.setvalue(cb, layno);
-        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
-            Cblk &c = pr.cblks[cb];
-            const BlockT2 &bt = blk[c.gidx];
-            const uint32_t np = bt.numpasses;
-            if (!c.included) w.tagtree(pr.incl, cb, layno + 1);
-            else w.write(np != 0, 1);
-            if (!np) continue;
-            if (!c.included) { c.numlenbits = 3; w.tagtree(pr.imsb, cb, INT64_MAX); }
-            w.numpasses(np);
-            // cblksty 0: only the last pass is terminated -> one segment
-            const uint32_t len = bt.rate[np - 1];
-            int32_t inc = floorlog2((int32_t)len) + 1 - ((int32_t)c.numlenbits + floorlog2((int32_t)np));
-            if (inc < 0) inc = 0;
-            w.comma(inc);
-            c.numlenbits += (uint32_t)inc;
-            w.write(len, c.numlenbits + (uint32_t)floorlog2((int32_t)np));
-        }
-    }
-    w.flush();
-    plan.push_back({hstart, (uint32_t)(out.size() - hstart), 0});
-    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
-        Band &b = res.bands[bandno];
-        Precinct &pr = b.precs[precno];
-        if (b.empty() || pr.cblks.empty()) continue;
-        for (auto &c : pr.cblks) {
-            const BlockT2 &bt = blk[c.gidx];
-            if (!bt.numpasses) continue;
-            uint32_t L = bt.rate[bt.numpasses - 1];
-            if (L) plan.push_back({bt.dev_off, L, 1});
-            c.included = true;
-        }
-    }
-}
-
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off) {
+                      uint64_t base_off, uint32_t csty, uint32_t *packno) {
     Resolution &res = tc.res[resno];
     if (layno == 0) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
             Band &b = res.bands[bandno];
+            if (b.empty() || precno >= b.precs.size()) continue;
             Precinct &pr = b.precs[precno];
-            if (b.empty() || pr.cblks.empty()) continue;
+            if (pr.cblks.empty()) continue;
             pr.incl.reset(); pr.imsb.reset();
             for (auto &c : pr.cblks) { c.included = false; c.numpasses = 0; c.chunks.clear(); c.seglen = 0; }
         }
     }
-    BitReader r(p, n);
+    size_t hstart = 0;
+    // SOP (T2::read_packet_header, T2.cpp:346-365): a missing marker is only a
+    // warning there; a packet counter that does not match is an error
+    if (csty & CSTY_SOP) {
+        if (n >= 6 && p[0] == 0xFF && p[1] == 0x91) {
+            const uint32_t cnt = ((uint32_t)p[4] << 8) | p[5];
+            if (packno) {
+                if (cnt != (*packno & 0xFFFF)) return -1;
+                ++*packno;
+            }
+            hstart = 6;
+        }
+    }
+    BitReader r(p + hstart, n - hstart);
     struct Seg { Cblk *c; uint32_t len; };
     std::vector<Seg> segs;
-    if (r.read(1)) {
+    if (n > hstart && r.read(1)) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
             Band &b = res.bands[bandno];
+            if (b.empty() || precno >= b.precs.size()) continue;
             Precinct &pr = b.precs[precno];
-            if (b.empty() || pr.cblks.empty()) continue;
+            if (pr.cblks.empty()) continue;
             for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
                 Cblk &c = pr.cblks[cb];
                 uint32_t inc = c.included ? r.read(1) : (r.tagtree(pr.incl, cb, layno + 1) <= (int64_t)layno);
@@ -389,20 +336,23 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                 if (!inc) continue;
                 if (!c.included) {
                     int64_t k = r.tagtree(pr.imsb, cb, INT64_MAX);
-                    // corrupt streams: a missing-MSB count above the band's
-                    // bit-planes has no code-block to decode (T2.cpp:1188-1200)
-                    if (r.err || k < 0 || k > (int64_t)b.numbps) return -1;
-                    c.numbps = (uint32_t)((int64_t)b.numbps - k);
+                    if (r.err || k < 0) return -1;
+                    // more missing bit-planes than the band has: the reference
+                    // warns and takes the band's count (T2.cpp:516-521)
+                    c.numbps = k > (int64_t)b.numbps ? b.numbps : (uint32_t)((int64_t)b.numbps - k);
+                    if (c.numbps > 16 + 33 * 5) return -1;  // T2.cpp:523-529
                     c.numlenbits = 3;
                     c.included = true;
                 }
                 uint32_t np = r.numpasses();
                 c.numlenbits += r.comma();
-                uint32_t L = r.read(c.numlenbits + (uint32_t)floorlog2((int32_t)np));
+                // one segment per block (cblksty 0): at most 109 passes per
+                // segment, larger counts are truncated (T2.cpp:566-577)
+                if (np > 109) np = 109;
+                const uint32_t bits = c.numlenbits + (uint32_t)floorlog2((int32_t)np);
+                if (bits > 32) return -1;  // "too many bits in segment length", T2.cpp:590-593
+                uint32_t L = r.read(bits);
                 c.numpasses += np;
-                // cblksty 0: at most 3 * numbps - 2 passes; more can only come
-                // from a corrupt header and would overrun the decoder's pass tables
-                if (c.numpasses > (c.numbps ? 3 * c.numbps - 2 : 0) || c.numpasses > 3u * 31 - 2) return -1;
                 segs.push_back({&c, L});
                 if (r.err) return -1;
             }
@@ -410,15 +360,17 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
     }
     r.align();
     if (r.err) return -1;
-    size_t off = r.off;
-    for (auto &s : segs) {
+    size_t off = hstart + r.off;
+    // EPH (T2.cpp:405-418 / 640-652): skipped when present
+    if ((csty & CSTY_EPH) && off + 2 <= n && p[off] == 0xFF && p[off + 1] == 0x92) off += 2;
+    for (auto &sg : segs) {
         // T2::read_packet_data (T2.cpp:686-698): a segment running past the
         // tile data is truncated to what is there (the decoder reads the
         // missing tail as the 0xFF fill), not an error
-        if (off + s.len > n) s.len = (uint32_t)(n - off);
-        if (s.len) s.c->chunks.push_back({base_off + off, s.len});
-        s.c->seglen += s.len;
-        off += s.len;
+        if (off + sg.len > n) sg.len = (uint32_t)(n - off);
+        if (sg.len) sg.c->chunks.push_back({base_off + off, sg.len});
+        sg.c->seglen += sg.len;
+        off += sg.len;
     }
     return (int64_t)off;
 }
@@ -428,6 +380,31 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
 // ---------------------------------------------------------------------------
 static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
 static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
+
+// POC marker body (j2k_read_poc, j2k.cpp:4367-4440): entries are appended;
+// layno1 / compno1 are clamped to the layer / component counts.
+bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp) {
+    const uint32_t room = cp.numcomps <= 256 ? 1 : 2, chunk = 5 + 2 * room;
+    if (!size || size % chunk) return false;
+    const uint32_t n = cp.numpocs + size / chunk;
+    if (n >= 32) return false;
+    for (uint32_t i = cp.numpocs; i < n; ++i) {
+        PocSpec &q = cp.pocs[i];
+        q.resno0 = p[0];
+        q.compno0 = room == 2 ? rd16(p + 1) : p[1];
+        p += 1 + room;
+        q.layno1 = std::min<uint32_t>(rd16(p), cp.numlayers);
+        q.resno1 = p[2];
+        q.compno1 = room == 2 ? rd16(p + 3) : p[3];
+        p += 3 + room;
+        q.prg = p[0];
+        p += 1;
+        q.compno1 = std::min<uint32_t>(q.compno1, cp.numcomps);
+        if (q.prg > 4) return false;
+    }
+    cp.numpocs = n;
+    return true;
+}
 
 bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err) {
     if (len < 4 || rd16(cs) != 0xFF4F) { err = "missing SOC"; return false; }
@@ -464,7 +441,8 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             have_siz = true;
         } else if (m == 0xFF52) {
             if (L < 12) { err = "Error reading COD marker"; return false; }
-            if (p[0] != 0) { err = "precincts/SOP/EPH (Scod != 0) not supported"; return false; }
+            if (p[0] & ~7u) { err = "unknown Scod bits"; return false; }
+            cp.csty = p[0];
             cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
             cp.numres = p[5] + 1u; cp.cblkw = p[6] + 2u; cp.cblkh = p[7] + 2u; cp.cblksty = p[8];
             cp.irrev = p[9] == 0;
@@ -473,6 +451,18 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             if (cp.numres > 33) { err = "Number of resolutions is greater than GRK_J2K_MAXRLVLS"; return false; }
             if (p[6] > 8 || p[7] > 8 || p[6] + p[7] > 8) { err = "Error reading SPCod SPCoc element, invalid code-block size"; return false; }
             if (p[9] > 1) { err = "Invalid qmfbid"; return false; }
+            if (cp.prog > 4) { err = "Unknown progression order in COD marker"; return false; }
+            // precinct partition (SPcod I_i, one byte per resolution; j2k.cpp read_SPCod_SPCoc)
+            if (cp.csty & CSTY_PRT) {
+                if (L != 12 + cp.numres) { err = "Error reading SPCod SPCoc element"; return false; }
+                for (uint32_t r = 0; r < cp.numres; ++r) {
+                    cp.prcw[r] = p[10 + r] & 0xf;
+                    cp.prch[r] = p[10 + r] >> 4;
+                    if ((r && (!cp.prcw[r] || !cp.prch[r]))) { err = "invalid precinct size"; return false; }
+                }
+            } else {
+                for (uint32_t r = 0; r < cp.numres; ++r) cp.prcw[r] = cp.prch[r] = 15;
+            }
             have_cod = true;
         } else if (m == 0xFF5C) {
             if (L < 4) { err = "Error reading QCD marker"; return false; }  // j2k.cpp:4075
@@ -484,8 +474,10 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
                 else { uint32_t v = rd16(p + 1 + 2 * i); cp.ss[i] = {v >> 11, v & 0x7ff}; }
             }
             have_qcd = true;
-        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF5F || m == 0xFF5E || m == 0xFF60) {
-            err = "COC/QCC/POC/RGN/PPM markers not supported";
+        } else if (m == 0xFF5F) {
+            if (!parse_poc(p, L - 2, cp)) { err = "Error reading POC marker"; return false; }
+        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF5E || m == 0xFF60) {
+            err = "COC/QCC/RGN/PPM markers not supported";
             return false;
         }
         pos += 2 + L;
@@ -493,7 +485,6 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
     if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
     // j2k_read_header stops at the first SOT; a stream that ends before it is truncated
     if (first_sot == 0) { err = "truncated main header (no SOT)"; return false; }
-    if (cp.prog != 0) { err = "only LRCP progression supported"; return false; }
     if (cp.cblksty != 0) { err = "code-block mode switches not supported"; return false; }
     if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
     for (uint32_t k = 0; k < cp.numcomps; ++k) cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));

@@ -25,6 +25,16 @@ inline int32_t floorlog2(int32_t a) { int32_t l = 0; while (a > 1) { a >>= 1; l+
 
 struct StepSize { uint32_t expn = 0, mant = 0; };
 
+// One progression-order change (grk_poc, grok.h:393-410; POC marker
+// j2k.cpp:4227-4306): resolutions [resno0, resno1), components [compno0,
+// compno1), layers [0, layno1), progression prg.
+struct PocSpec {
+    uint32_t resno0 = 0, compno0 = 0, layno1 = 0, resno1 = 0, compno1 = 0, prg = 0;
+};
+
+constexpr uint32_t CSTY_PRT = 1, CSTY_SOP = 2, CSTY_EPH = 4;  // Scod bits (j2k.h J2K_CP_CSTY_*)
+constexpr uint16_t RSIZ_CINEMA_2K = 3, RSIZ_CINEMA_4K = 4;     // grok.h:160-161
+
 // Coding parameters as j2k_setup_encoder derives them (codestream/j2k.cpp:1609-2050)
 struct CodingParams {
     uint32_t numcomps = 0;
@@ -37,6 +47,27 @@ struct CodingParams {
     uint32_t numlayers = 1, prog = 0, cblksty = 0;
     StepSize ss[3 * 33 + 1];
     int32_t shift[16] = {};
+    // coding style (Scod): precinct partition, SOP, EPH; log2 precinct size per resolution
+    uint32_t csty = 0;
+    uint8_t prcw[33], prch[33];
+    // progression-order changes (0 = none)
+    uint32_t numpocs = 0;
+    PocSpec pocs[32];
+    uint16_t rsiz = 0;
+    // tile-parts (grk_cparameters tp_on / tp_flag; tp_pos derived, j2k.cpp:2955-2958)
+    bool tp_on = false;
+    char tp_flag = 0;
+    uint32_t tp_pos = 0;
+    // rate control (grk_cparameters cp_disto_alloc / cp_fixed_quality /
+    // rateControlAlgorithm; tcp->rates in bytes after j2k_update_rates)
+    uint32_t disto_alloc = 1, fixed_quality = 0, rate_algo = 0;
+    double rates[100] = {};
+    double distoratio[100] = {};
+    uint64_t max_cs_size = 0, max_comp_size = 0;
+    uint32_t nb_tile_parts = 1;  // per tile (tcp->m_nb_tile_parts)
+    CodingParams() {
+        for (int i = 0; i < 33; ++i) prcw[i] = prch[i] = 15;
+    }
 };
 
 // TagTree (codestream/TagTree.cpp)
@@ -115,13 +146,6 @@ struct ByteBuf {
     size_t size() const { return v.size(); }
 };
 
-// Encoder-side per-block results needed by T2.
-struct BlockT2 {
-    uint32_t numbps, numpasses, datalen;
-    const uint32_t *rate;     // cumulative rates (numpasses)
-    uint64_t dev_off;         // offset of the block's MQ bytes in the device slab
-};
-
 // The codestream is assembled on the device: the host writes headers into a
 // small blob and a plan of (source, length) runs; a gather kernel copies the
 // runs (header bytes or code-block bytes) into their final positions.
@@ -131,16 +155,60 @@ struct PlanItem {
     uint32_t kind;
 };
 
-void write_main_header(ByteBuf &cs, const CodingParams &cp);
-// one packet (T2.cpp:859-1110), layer 0 containing all passes: header bits go
-// to `hdr`, the packet's runs are appended to `plan`
-void encode_packet(TileComp &tc, uint32_t resno, uint32_t precno, const std::vector<BlockT2> &blk, ByteBuf &hdr,
-                   std::vector<PlanItem> &plan);
+// main header up to (not including) the first SOT: SOC SIZ COD QCD [TLM] [POC] COM
+// (j2k_setup_header_writing, j2k.cpp:2330-2374).  tlm_at receives the offset
+// of the TLM marker's tile-part records (0 without TLM).
+// packet-header bit writer / reader (codestream/BitIO.cpp): after an 0xFF
+// byte only 7 bits are used (bit stuffing)
+struct BitWriter {
+    ByteBuf &out;
+    uint32_t buf = 0, ct = 8;
+    explicit BitWriter(ByteBuf &o) : out(o) {}
+    void byteout() { out.put8(buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
+    void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
+    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    void flush() { byteout(); if (ct == 7) byteout(); }
+    void numpasses(uint32_t n) {
+        if (n == 1) write(0, 1);
+        else if (n == 2) write(2, 2);
+        else if (n <= 5) write(0xc | (n - 3), 4);
+        else if (n <= 36) write(0x1e0 | (n - 6), 9);
+        else write(0xff80 | (n - 37), 16);
+    }
+    void comma(int32_t n) { while (--n >= 0) write(1, 1); write(0, 1); }
+    // TagTree::encode (TagTree.cpp:251-287)
+    void tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
+        int32_t stk[64], sp = 0, node = (int32_t)leaf;
+        while (t.nodes[node].parent >= 0) { stk[sp++] = node; node = t.nodes[node].parent; }
+        int64_t low = 0;
+        for (;;) {
+            TagTree::Node &n = t.nodes[node];
+            if (low > n.low) n.low = low; else low = n.low;
+            while (low < threshold) {
+                if (low >= n.value) {
+                    if (!n.known) { write(1, 1); n.known = 1; }
+                    break;
+                }
+                write(0, 1);
+                ++low;
+            }
+            n.low = low;
+            if (sp == 0) break;
+            node = stk[--sp];
+        }
+    }
+};
 
+void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at = nullptr, uint32_t total_tile_parts = 0);
+// POC marker (j2k_write_poc_in_memory, j2k.cpp:4227-4306)
+void write_poc(ByteBuf &cs, const CodingParams &cp);
 // decoder
 bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err);
-// returns bytes consumed or -1
+// POC marker segment body of `size` bytes (main or tile-part header)
+bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp);
+// returns bytes consumed or -1 (T2::read_packet_header / read_packet_data,
+// T2.cpp:314-725); csty: SOP / EPH markers; packno: SOP packet counter
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off);
+                      uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr);
 
 }  // namespace grkgpu

@@ -23,9 +23,19 @@ struct EncBlock {
 };
 
 struct EncResult {
-    uint32_t numbps, numpasses, len, pad;
-    uint32_t rate[GRK_MAX_PASSES];  // cumulative, after Grok's fix-ups
+    uint32_t numbps, numpasses, len, pad;  // pad != 0: numbps above the band's bound
+    uint32_t nsym, pad1, pad2, pad3;       // nsym: MQ symbols coded
+    uint32_t rate[GRK_MAX_PASSES];         // cumulative, after Grok's fix-ups
+    int32_t nmsedec[GRK_MAX_PASSES];       // per-pass distortion sums (launch_t1_dist only)
 };
+// bytes of an EncResult without the distortion sums (what a D2H needs when
+// no rate control runs)
+constexpr size_t ENC_RESULT_RATE_BYTES = 32 + 4 * GRK_MAX_PASSES;
+
+// Normalised-MSE decrease tables (t1_generate_luts.cpp:290-318, restated):
+// index = the 7 magnitude bits from the coded bit-plane down.
+struct NmseLut { int16_t sig[128], sig0[128], ref[128], ref0[128]; };
+const NmseLut &nmse_lut();
 
 // One code-block to decode (t1/Tier1.cpp:98-175 decodeBlockInfo).
 struct DecBlock {
@@ -81,6 +91,11 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
                             hipStream_t s);
+// Per-pass distortion sums of the blocks k_t1_model coded (same sym /
+// sym_off layout): nmsedec[pass] of every block, in the pass order of
+// t1_encode_cblk (t1.cpp:1222-1260).
+hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coef, const T1Scratch *scratch,
+                          const uint8_t *sym, const uint64_t *sym_off, EncResult *res, hipStream_t s);
 // ubuf: unstuffed-stream arena; block i's region at ubuf + i * fixed_words
 // words, or (fixed_words == 0) at blocks[i].pad * 16 bytes
 // (t1_unstuff_region_words words each).

@@ -10,8 +10,11 @@
 
 #include "grk_device.h"
 #include "t1_flat.h"
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 namespace grkgpu {
 
@@ -232,6 +235,78 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
                               s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len);
     r.numpasses = np;
     r.len = len;
+    uint32_t nsym = 0;
+    const uint32_t *c = scr[i].cnt;
+    for (uint32_t q = 0; q < r.numbps && q < 32; ++q) nsym += c[q * 4] + c[q * 4 + 1] + c[q * 4 + 2];
+    r.nsym = nsym;
+}
+
+// Per-pass distortion sums (the nmsedec of t1_enc_sigpass / refpass /
+// clnpass, t1.cpp:197-338, 443-555, 639-782 with t1_getnmsedec_sig/_ref
+// :155-166): one wavefront per block, lane = column.  A sample contributes
+// to the plane of its most significant bit (significance: to the SPP when
+// the modelling kernel found it significant during that plane's SPP, else
+// to the cleanup pass) and to every lower plane's refinement pass.  The
+// SPP membership comes from the post-SPP significance rows k_t1_model left
+// behind each plane's symbol stream.
+__global__ __launch_bounds__(64) void k_t1_dist(const EncBlock *__restrict__ blocks, const int32_t *__restrict__ coef,
+                                                const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
+                                                const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res,
+                                                NmseLut lutv) {
+    __shared__ NmseLut lut;
+    {
+        const int16_t *src = &lutv.sig[0];
+        int16_t *dst = &lut.sig[0];
+        for (uint32_t k = threadIdx.x; k < 512; k += 64) dst[k] = src[k];
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x, x = threadIdx.x;
+    const EncBlock b = blocks[i];
+    EncResult &r = res[i];
+    const uint32_t numbps = r.numbps;
+    if (numbps == 0 || r.pad) return;
+    const int32_t *src = coef + b.coef_off;
+    uint32_t m[64];
+#pragma unroll
+    for (int y = 0; y < 64; ++y) {
+        uint32_t ng;
+        m[y] = ((uint32_t)y < b.h && x < b.w) ? quant_mag(src[(size_t)y * b.stride + x], b.qmfbid, b.inv_step, &ng) : 0;
+    }
+    uint32_t cap;
+    const uint64_t off = sym_block_off(sym_off, i, &cap);
+    const uint32_t slot = sym_slot_bytes(b.w, b.h);
+    for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
+        const uint64_t *post = (const uint64_t *)(sym + off + (uint64_t)p * slot + sym_stream_bytes(b.w, b.h));
+        int32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+        for (int y = 0; y < 64; ++y) {
+            if ((uint32_t)y >= b.h) break;
+            const uint32_t mag = m[y];
+            const uint32_t win = p > 0 ? (mag >> p) & 127u : mag & 127u;
+            if ((mag >> (p + 6)) == 1u) {
+                const int32_t v = p > 0 ? lut.sig[win] : lut.sig0[win];
+                if ((post[y] >> x) & 1u) a0 += v; else a2 += v;
+            } else if (mag >> (p + 7)) {
+                a1 += p > 0 ? lut.ref[win] : lut.ref0[win];
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            a0 += __shfl_xor(a0, o);
+            a1 += __shfl_xor(a1, o);
+            a2 += __shfl_xor(a2, o);
+        }
+        if (x == 0) {
+            if (p == (int32_t)numbps - 1) {
+                r.nmsedec[0] = a2;
+            } else {
+                const uint32_t base = 1 + 3 * (numbps - 2 - (uint32_t)p);
+                r.nmsedec[base] = a0;
+                r.nmsedec[base + 1] = a1;
+                r.nmsedec[base + 2] = a2;
+            }
+        }
+    }
 }
 
 // T1 decoder (t1_flat.h t1_decode_v5).  Pass 1, lane per block: remove the MQ
@@ -407,6 +482,34 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
                        scratch, sym, sym_off, res);
     hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s, blocks, n,
                        scratch, sym, sym_off, out, res, (const uint32_t *)nullptr);
+    return hipGetLastError();
+}
+
+// t1_generate_luts.cpp:290-318: floor((u^2 - v^2) * 2^6 + 0.5) / 2^6 * 8192
+// with t = i / 2^6, clamped at 0 (host double arithmetic, as generated)
+static NmseLut make_nmse_lut() {
+    NmseLut L;
+    for (int i = 0; i < 128; ++i) {
+        const double t = i / 64.0;
+        double u = t, v = t - 1.5;
+        L.sig[i] = (int16_t)std::max(0, (int)(floor((u * u - v * v) * 64.0 + 0.5) / 64.0 * 8192.0));
+        L.sig0[i] = (int16_t)std::max(0, (int)(floor((u * u) * 64.0 + 0.5) / 64.0 * 8192.0));
+        u = t - 1.0;
+        v = (i & 64) ? t - 1.5 : t - 0.5;
+        L.ref[i] = (int16_t)std::max(0, (int)(floor((u * u - v * v) * 64.0 + 0.5) / 64.0 * 8192.0));
+        L.ref0[i] = (int16_t)std::max(0, (int)(floor((u * u) * 64.0 + 0.5) / 64.0 * 8192.0));
+    }
+    return L;
+}
+const NmseLut &nmse_lut() {
+    static const NmseLut L = make_nmse_lut();
+    return L;
+}
+
+hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coef, const T1Scratch *scratch,
+                          const uint8_t *sym, const uint64_t *sym_off, EncResult *res, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_t1_dist, dim3(n), dim3(64), 0, s, blocks, coef, scratch, sym, sym_off, res, nmse_lut());
     return hipGetLastError();
 }
 

@@ -1,0 +1,1072 @@
+// t2.cpp -- host Tier-2: packet iteration (progressions, POC, tile-parts),
+// packet headers, quality layers and PCRD rate control.  See t2.h.
+//
+// Everything here decides codestream BYTES, so it restates the reference's
+// behaviour exactly, quirks included (each function cites what it follows).
+// The iteration is written as plain nested loops that emit the whole packet
+// order at once instead of the reference's resumable pi_next() generators; the
+// order, the skip conditions and the duplicate suppression ("include" array)
+// are the same.
+#include "t2.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace grkgpu {
+
+namespace {
+
+const char *prog_string(uint32_t prg) {
+    static const char *s[5] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
+    return prg < 5 ? s[prg] : "";
+}
+
+uint32_t ceildiv64(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+uint32_t floordivpow2(uint32_t a, uint32_t b) { return a >> b; }
+
+// ---------------------------------------------------------------------------
+// packet iterator state (PacketIter / grk_pi_comp / grk_pi_resolution)
+// ---------------------------------------------------------------------------
+struct PiRes { uint32_t pdx = 0, pdy = 0, pw = 0, ph = 0; };
+struct PiComp {
+    uint32_t dx = 1, dy = 1, numres = 0;
+    PiRes res[33];
+};
+struct Range {  // grk_poc fields a PacketIter walks
+    uint32_t resno0 = 0, resno1 = 0, compno0 = 0, compno1 = 0, layno0 = 0, layno1 = 0, precno0 = 0, precno1 = 0;
+    uint32_t tx0 = 0, ty0 = 0, tx1 = 0, ty1 = 0, prg = 0;
+};
+struct Pi {
+    Range poc;
+    std::vector<PiComp> comps;
+    uint32_t tx0 = 0, ty0 = 0, tx1 = 0, ty1 = 0, dx = 0, dy = 0;
+    bool tp_on = false;
+    uint32_t step_p = 0, step_c = 0, step_r = 0, step_l = 0;
+    std::vector<uint8_t> *include = nullptr;
+};
+
+// grk_get_all_encoding_parameters (PacketIter.cpp:762-870): tile extent,
+// per (component, resolution) precinct exponents and counts, the smallest
+// precinct step on the reference grid, the largest precinct count / resolution
+// count.
+struct TileGeom {
+    uint32_t tx0, tx1, ty0, ty1, dx_min, dy_min, max_prec, max_res;
+    std::vector<PiComp> comps;
+};
+
+TileGeom tile_geom(const CodingParams &cp, const Tile &tile) {
+    TileGeom g;
+    g.tx0 = tile.r.x0; g.tx1 = tile.r.x1; g.ty0 = tile.r.y0; g.ty1 = tile.r.y1;
+    g.max_prec = 0; g.max_res = 0;
+    g.dx_min = g.dy_min = 0x7fffffff;
+    g.comps.resize(cp.numcomps);
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        PiComp &c = g.comps[k];
+        c.numres = cp.numres;
+        g.max_res = std::max(g.max_res, cp.numres);
+        for (uint32_t r = 0; r < cp.numres; ++r) {
+            const uint32_t level = cp.numres - 1 - r;
+            c.res[r].pdx = cp.prcw[r];
+            c.res[r].pdy = cp.prch[r];
+            const uint64_t dx = (uint64_t)1 << (cp.prcw[r] + level), dy = (uint64_t)1 << (cp.prch[r] + level);
+            if (dx < UINT_MAX) g.dx_min = std::min<uint32_t>(g.dx_min, (uint32_t)dx);
+            if (dy < UINT_MAX) g.dy_min = std::min<uint32_t>(g.dy_min, (uint32_t)dy);
+            if (tile.comps.empty()) continue;
+            const Resolution &res = tile.comps[k].res[r];
+            c.res[r].pw = res.pw;
+            c.res[r].ph = res.ph;
+            g.max_prec = std::max(g.max_prec, res.pw * res.ph);
+        }
+    }
+    return g;
+}
+
+void setup_pi(Pi &pi, const TileGeom &g, const CodingParams &cp, std::vector<uint8_t> *include) {
+    pi.comps = g.comps;
+    pi.tx0 = g.tx0; pi.tx1 = g.tx1; pi.ty0 = g.ty0; pi.ty1 = g.ty1;
+    pi.dx = g.dx_min; pi.dy = g.dy_min;
+    pi.step_p = 1;
+    pi.step_c = g.max_prec;
+    pi.step_r = cp.numcomps * pi.step_c;
+    pi.step_l = g.max_res * pi.step_r;
+    pi.include = include;
+}
+
+// update_pi_dxy_for_comp / update_pi_dxy (PacketIter.cpp:220-250)
+void dxy_for_comp(Pi &pi, const PiComp &c) {
+    for (uint32_t r = 0; r < c.numres; ++r) {
+        const uint64_t dx = (uint64_t)c.dx << (c.res[r].pdx + c.numres - 1 - r);
+        const uint64_t dy = (uint64_t)c.dy << (c.res[r].pdy + c.numres - 1 - r);
+        if (dx < UINT_MAX) pi.dx = !pi.dx ? (uint32_t)dx : std::min<uint32_t>(pi.dx, (uint32_t)dx);
+        if (dy < UINT_MAX) pi.dy = !pi.dy ? (uint32_t)dy : std::min<uint32_t>(pi.dy, (uint32_t)dy);
+    }
+}
+void dxy_all(Pi &pi) {
+    pi.dx = pi.dy = 0;
+    for (auto &c : pi.comps) dxy_for_comp(pi, c);
+}
+
+bool take(Pi &pi, uint32_t l, uint32_t r, uint32_t c, uint32_t p, std::vector<PacketId> &out) {
+    const size_t idx = (size_t)l * pi.step_l + (size_t)r * pi.step_r + (size_t)c * pi.step_c + (size_t)p * pi.step_p;
+    if (idx >= pi.include->size()) pi.include->resize(idx + 1, 0);
+    if ((*pi.include)[idx]) return false;
+    (*pi.include)[idx] = 1;
+    out.push_back({l, r, c, p});
+    return true;
+}
+
+// pi_next_lrcp / pi_next_rlcp (PacketIter.cpp:252-348)
+void walk_lrcp(Pi &pi, bool rl, std::vector<PacketId> &out) {
+    Range &q = pi.poc;
+    auto body = [&](uint32_t l, uint32_t r) {
+        for (uint32_t c = q.compno0; c < q.compno1; ++c) {
+            const PiComp &comp = pi.comps[c];
+            if (r >= comp.numres) continue;
+            const PiRes &res = comp.res[r];
+            if (!pi.tp_on) q.precno1 = res.pw * res.ph;
+            for (uint32_t p = q.precno0; p < q.precno1; ++p) {
+                if (p >= res.pw * res.ph) continue;
+                take(pi, l, r, c, p, out);
+            }
+        }
+    };
+    if (!rl) {
+        for (uint32_t l = q.layno0; l < q.layno1; ++l)
+            for (uint32_t r = q.resno0; r < q.resno1; ++r) body(l, r);
+    } else {
+        for (uint32_t r = q.resno0; r < q.resno1; ++r)
+            for (uint32_t l = q.layno0; l < q.layno1; ++l) body(l, r);
+    }
+}
+
+// The position-driven progressions (RPCL / PCRL / CPRL, PacketIter.cpp:350-657):
+// precinct index of (x, y) in resolution r of component c, or -1 when (x, y)
+// is not a precinct origin there.  Returns -2 for the reference's "Precinct
+// index invalid" abort (CPRL only).
+int64_t prec_at(const Pi &pi, const PiComp &comp, uint32_t r, uint32_t x, uint32_t y, bool check) {
+    const PiRes &res = comp.res[r];
+    const uint32_t levelno = comp.numres - 1 - r;
+    if (levelno >= 33) return -1;
+    const uint32_t trx0 = ceildiv64(pi.tx0, (uint64_t)comp.dx << levelno);
+    const uint32_t try0 = ceildiv64(pi.ty0, (uint64_t)comp.dy << levelno);
+    const uint32_t trx1 = ceildiv64(pi.tx1, (uint64_t)comp.dx << levelno);
+    const uint32_t try1 = ceildiv64(pi.ty1, (uint64_t)comp.dy << levelno);
+    const uint32_t rpx = res.pdx + levelno, rpy = res.pdy + levelno;
+    if (!(((uint64_t)y % ((uint64_t)comp.dy << rpy) == 0) ||
+          ((y == pi.ty0) && (((uint64_t)try0 << levelno) % ((uint64_t)1 << rpy)))))
+        return -1;
+    if (!(((uint64_t)x % ((uint64_t)comp.dx << rpx) == 0) ||
+          ((x == pi.tx0) && (((uint64_t)trx0 << levelno) % ((uint64_t)1 << rpx)))))
+        return -1;
+    if (res.pw == 0 || res.ph == 0) return -1;
+    if (trx0 == trx1 || try0 == try1) return -1;
+    const uint32_t ax = floordivpow2(ceildiv64(x, (uint64_t)comp.dx << levelno), res.pdx), bx = floordivpow2(trx0, res.pdx);
+    const uint32_t ay = floordivpow2(ceildiv64(y, (uint64_t)comp.dy << levelno), res.pdy), by = floordivpow2(try0, res.pdy);
+    if (check && (bx > ax || by > ay)) return -2;
+    const uint32_t precno = (ax - bx) + (ay - by) * res.pw;
+    if (precno >= res.pw * res.ph) return -1;
+    return precno;
+}
+
+void walk_positional(Pi &pi, std::vector<PacketId> &out) {
+    Range &q = pi.poc;
+    auto set_extent = [&]() {
+        if (!pi.tp_on) { q.ty0 = pi.ty0; q.tx0 = pi.tx0; q.ty1 = pi.ty1; q.tx1 = pi.tx1; }
+    };
+    auto layers = [&](uint32_t r, uint32_t c, uint32_t p) {
+        for (uint32_t l = q.layno0; l < q.layno1; ++l) take(pi, l, r, c, p, out);
+    };
+    if (q.prg == PROG_RPCL) {
+        dxy_all(pi);
+        set_extent();
+        for (uint32_t r = q.resno0; r < q.resno1; ++r)
+            for (uint32_t y = q.ty0; y < q.ty1; y += pi.dy - (y % pi.dy))
+                for (uint32_t x = q.tx0; x < q.tx1; x += pi.dx - (x % pi.dx))
+                    for (uint32_t c = q.compno0; c < q.compno1; ++c) {
+                        const PiComp &comp = pi.comps[c];
+                        if (r >= comp.numres) continue;
+                        const int64_t p = prec_at(pi, comp, r, x, y, false);
+                        if (p >= 0) layers(r, c, (uint32_t)p);
+                    }
+    } else if (q.prg == PROG_PCRL) {
+        dxy_all(pi);
+        set_extent();
+        for (uint32_t y = q.ty0; y < q.ty1; y += pi.dy - (y % pi.dy))
+            for (uint32_t x = q.tx0; x < q.tx1; x += pi.dx - (x % pi.dx))
+                for (uint32_t c = q.compno0; c < q.compno1; ++c) {
+                    const PiComp &comp = pi.comps[c];
+                    for (uint32_t r = q.resno0; r < std::min(q.resno1, comp.numres); ++r) {
+                        const int64_t p = prec_at(pi, comp, r, x, y, false);
+                        if (p >= 0) layers(r, c, (uint32_t)p);
+                    }
+                }
+    } else {  // CPRL
+        for (uint32_t c = q.compno0; c < q.compno1; ++c) {
+            const PiComp &comp = pi.comps[c];
+            pi.dx = pi.dy = 0;
+            dxy_for_comp(pi, comp);
+            set_extent();
+            for (uint32_t y = q.ty0; y < q.ty1; y += pi.dy - (y % pi.dy))
+                for (uint32_t x = q.tx0; x < q.tx1; x += pi.dx - (x % pi.dx))
+                    for (uint32_t r = q.resno0; r < std::min(q.resno1, comp.numres); ++r) {
+                        const int64_t p = prec_at(pi, comp, r, x, y, true);
+                        if (p == -2) return;  // "Precinct index invalid": pi_next returns false
+                        if (p >= 0) layers(r, c, (uint32_t)p);
+                    }
+        }
+    }
+}
+
+void walk(Pi &pi, std::vector<PacketId> &out) {
+    switch (pi.poc.prg) {
+        case PROG_LRCP: walk_lrcp(pi, false, out); break;
+        case PROG_RLCP: walk_lrcp(pi, true, out); break;
+        case PROG_RPCL: case PROG_PCRL: case PROG_CPRL: walk_positional(pi, out); break;
+        default: break;
+    }
+}
+
+// pi_update_encode_poc_and_final / pi_update_encode_not_poc (PacketIter.cpp:925-1033)
+void update_encode_pocs(const CodingParams &cp, std::vector<EncPoc> &pocs, const TileGeom &g, bool poc) {
+    if (poc) {
+        for (size_t i = 0; i < pocs.size(); ++i) {
+            EncPoc &p = pocs[i];
+            p.compS = p.compno0; p.compE = p.compno1;
+            p.resS = p.resno0; p.resE = p.resno1;
+            p.layE = p.layno1;
+            p.prg = p.prg1;
+            p.prcS = 0;
+            // the reference's quirk: later entries start at layE when their
+            // layer end grows, else at 0 (PacketIter.cpp:978-980)
+            p.layS = i == 0 ? 0 : (p.layE > pocs[i - 1].layE ? p.layE : 0);
+            p.prcE = g.max_prec;
+            p.txS = g.tx0; p.txE = g.tx1; p.tyS = g.ty0; p.tyE = g.ty1;
+            p.dx = g.dx_min; p.dy = g.dy_min;
+        }
+    } else {
+        for (auto &p : pocs) {
+            p.compS = 0; p.compE = cp.numcomps;
+            p.resS = 0; p.resE = g.max_res;
+            p.layS = 0; p.layE = cp.numlayers;
+            p.prg = cp.prog;
+            p.prcS = 0; p.prcE = g.max_prec;
+            p.txS = g.tx0; p.txE = g.tx1; p.tyS = g.ty0; p.tyE = g.ty1;
+            p.dx = g.dx_min; p.dy = g.dy_min;
+        }
+    }
+}
+
+// The tile-part position T2 works with is TileProcessor::tp_pos, copied from
+// the coding parameters when the tile processor is created
+// (TileProcessor.cpp:1627-1638, j2k_setup_header_writing j2k.cpp:2328-2333)
+// -- BEFORE j2k_calculate_tp sets m_tp_pos (j2k_init_info, the first header
+// procedure).  So packets are divided among tile-parts by the FIRST
+// progression letter only, whatever -u names; e.g. "-u R" with LRCP writes
+// the whole tile into each of its numres tile-parts.  The tile-part COUNT does
+// use the real position (j2k_get_num_tp).  Restated as is.
+constexpr uint32_t kStaleTpPos = 0;
+
+bool is_cinema(const CodingParams &cp) { return cp.rsiz == RSIZ_CINEMA_2K || cp.rsiz == RSIZ_CINEMA_4K; }
+
+// pi_check_next_level (PacketIter.cpp:1101-1180)
+bool check_next_level(int32_t pos, const EncPoc &t, const char *prog) {
+    if (pos < 0) return false;
+    switch (prog[pos]) {
+        case 'R': return t.res_t == t.resE ? check_next_level(pos - 1, t, prog) : true;
+        case 'C': return t.comp_t == t.compE ? check_next_level(pos - 1, t, prog) : true;
+        case 'L': return t.lay_t == t.layE ? check_next_level(pos - 1, t, prog) : true;
+        case 'P':
+            if (t.prg == PROG_LRCP || t.prg == PROG_RLCP)
+                return t.prc_t == t.prcE ? check_next_level(pos - 1, t, prog) : true;
+            if (t.tx0_t == t.txE) return t.ty0_t == t.tyE ? check_next_level(pos - 1, t, prog) : true;
+            return true;
+    }
+    return false;
+}
+
+// pi_init_encode (PacketIter.cpp:1532-1799): the range of pi for tile-part
+// tpnum of POC pino; the tile-part odometer state lives in `t`.
+void init_encode(Pi &pi, const CodingParams &cp, EncPoc &t, uint32_t tpnum, uint32_t tppos, bool final_pass) {
+    const char *prog = prog_string(t.prg);
+    Range &q = pi.poc;
+    q.prg = t.prg;
+    const bool split = cp.tp_on && ((!is_cinema(cp) && final_pass) || is_cinema(cp));
+    if (!split) {
+        q.resno0 = t.resS; q.resno1 = t.resE;
+        q.compno0 = t.compS; q.compno1 = t.compE;
+        q.layno0 = t.layS; q.layno1 = t.layE;
+        q.precno0 = t.prcS; q.precno1 = t.prcE;
+        q.tx0 = t.txS; q.ty0 = t.tyS; q.tx1 = t.txE; q.ty1 = t.tyE;
+        return;
+    }
+    const bool lr = t.prg == PROG_LRCP || t.prg == PROG_RLCP;
+    for (uint32_t i = tppos + 1; i < 4; i++) {
+        switch (prog[i]) {
+            case 'R': q.resno0 = t.resS; q.resno1 = t.resE; break;
+            case 'C': q.compno0 = t.compS; q.compno1 = t.compE; break;
+            case 'L': q.layno0 = t.layS; q.layno1 = t.layE; break;
+            case 'P':
+                if (lr) { q.precno0 = t.prcS; q.precno1 = t.prcE; }
+                else { q.tx0 = t.txS; q.ty0 = t.tyS; q.tx1 = t.txE; q.ty1 = t.tyE; }
+                break;
+        }
+    }
+    if (tpnum == 0) {
+        for (int32_t i = (int32_t)tppos; i >= 0; i--) {
+            switch (prog[i]) {
+                case 'C': t.comp_t = t.compS; q.compno0 = t.comp_t; q.compno1 = t.comp_t + 1; t.comp_t += 1; break;
+                case 'R': t.res_t = t.resS; q.resno0 = t.res_t; q.resno1 = t.res_t + 1; t.res_t += 1; break;
+                case 'L': t.lay_t = t.layS; q.layno0 = t.lay_t; q.layno1 = t.lay_t + 1; t.lay_t += 1; break;
+                case 'P':
+                    if (lr) {
+                        t.prc_t = t.prcS; q.precno0 = t.prc_t; q.precno1 = t.prc_t + 1; t.prc_t += 1;
+                    } else {
+                        t.tx0_t = t.txS; t.ty0_t = t.tyS;
+                        q.tx0 = t.tx0_t; q.tx1 = t.tx0_t + t.dx - (t.tx0_t % t.dx);
+                        q.ty0 = t.ty0_t; q.ty1 = t.ty0_t + t.dy - (t.ty0_t % t.dy);
+                        t.tx0_t = q.tx1; t.ty0_t = q.ty1;
+                    }
+                    break;
+            }
+        }
+        return;
+    }
+    uint32_t incr_top = 1, resetX = 0;
+    for (int32_t i = (int32_t)tppos; i >= 0; i--) {
+        switch (prog[i]) {
+            case 'C': q.compno0 = t.comp_t - 1; q.compno1 = t.comp_t; break;
+            case 'R': q.resno0 = t.res_t - 1; q.resno1 = t.res_t; break;
+            case 'L': q.layno0 = t.lay_t - 1; q.layno1 = t.lay_t; break;
+            case 'P':
+                if (lr) { q.precno0 = t.prc_t - 1; q.precno1 = t.prc_t; }
+                else {
+                    q.tx0 = t.tx0_t - t.dx - (t.tx0_t % t.dx); q.tx1 = t.tx0_t;
+                    q.ty0 = t.ty0_t - t.dy - (t.ty0_t % t.dy); q.ty1 = t.ty0_t;
+                }
+                break;
+        }
+        if (incr_top != 1) continue;
+        switch (prog[i]) {
+            case 'R':
+                if (t.res_t == t.resE) {
+                    if (check_next_level(i - 1, t, prog)) {
+                        t.res_t = t.resS; q.resno0 = t.res_t; q.resno1 = t.res_t + 1; t.res_t += 1; incr_top = 1;
+                    } else incr_top = 0;
+                } else {
+                    q.resno0 = t.res_t; q.resno1 = t.res_t + 1; t.res_t += 1; incr_top = 0;
+                }
+                break;
+            case 'C':
+                if (t.comp_t == t.compE) {
+                    if (check_next_level(i - 1, t, prog)) {
+                        t.comp_t = t.compS; q.compno0 = t.comp_t; q.compno1 = t.comp_t + 1; t.comp_t += 1; incr_top = 1;
+                    } else incr_top = 0;
+                } else {
+                    q.compno0 = t.comp_t; q.compno1 = t.comp_t + 1; t.comp_t += 1; incr_top = 0;
+                }
+                break;
+            case 'L':
+                if (t.lay_t == t.layE) {
+                    if (check_next_level(i - 1, t, prog)) {
+                        t.lay_t = t.layS; q.layno0 = t.lay_t; q.layno1 = t.lay_t + 1; t.lay_t += 1; incr_top = 1;
+                    } else incr_top = 0;
+                } else {
+                    q.layno0 = t.lay_t; q.layno1 = t.lay_t + 1; t.lay_t += 1; incr_top = 0;
+                }
+                break;
+            case 'P':
+                if (lr) {
+                    if (t.prc_t == t.prcE) {
+                        if (check_next_level(i - 1, t, prog)) {
+                            t.prc_t = t.prcS; q.precno0 = t.prc_t; q.precno1 = t.prc_t + 1; t.prc_t += 1; incr_top = 1;
+                        } else incr_top = 0;
+                    } else {
+                        q.precno0 = t.prc_t; q.precno1 = t.prc_t + 1; t.prc_t += 1; incr_top = 0;
+                    }
+                } else {
+                    if (t.tx0_t >= t.txE) {
+                        if (t.ty0_t >= t.tyE) {
+                            if (check_next_level(i - 1, t, prog)) {
+                                t.ty0_t = t.tyS; q.ty0 = t.ty0_t; q.ty1 = t.ty0_t + t.dy - (t.ty0_t % t.dy);
+                                t.ty0_t = q.ty1; incr_top = 1; resetX = 1;
+                            } else {
+                                incr_top = 0; resetX = 0;
+                            }
+                        } else {
+                            q.ty0 = t.ty0_t; q.ty1 = t.ty0_t + t.dy - (t.ty0_t % t.dy);
+                            t.ty0_t = q.ty1; incr_top = 0; resetX = 1;
+                        }
+                        if (resetX == 1) {
+                            t.tx0_t = t.txS; q.tx0 = t.tx0_t; q.tx1 = t.tx0_t + t.dx - (t.tx0_t % t.dx);
+                            t.tx0_t = q.tx1;
+                        }
+                    } else {
+                        q.tx0 = t.tx0_t; q.tx1 = t.tx0_t + t.dx - (t.tx0_t % t.dx);
+                        t.tx0_t = q.tx1; incr_top = 0;
+                    }
+                }
+                break;
+        }
+    }
+}
+
+// pi_initialise_encode (PacketIter.cpp:1357-1530): fresh iterators (one per
+// POC entry, sharing one include array), ranges from the POC entries when
+// the tile has them and (cinema or final pass), else the whole tile.  Only
+// the first iterator carries tp_on (the others are calloc'ed zero there).
+void initialise_encode(const CodingParams &cp, TileEnc &te, bool final_pass, std::vector<Pi> &pis,
+                       std::vector<uint8_t> &include, TileGeom &g) {
+    g = tile_geom(cp, *te.tile);
+    pis.assign(te.pocs.size(), Pi());
+    include.assign((size_t)cp.numlayers * g.max_res * cp.numcomps * std::max<uint32_t>(g.max_prec, 1), 0);
+    for (auto &pi : pis) setup_pi(pi, g, cp, &include);
+    pis[0].tp_on = cp.tp_on;
+    update_encode_pocs(cp, te.pocs, g, cp.numpocs && (is_cinema(cp) || final_pass));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// decoder packet order: T2::decode_packets over pi_create_decode
+// (PacketIter.cpp:1187-1355, pi_update_decode_poc / _not_poc :1035-1099)
+// ---------------------------------------------------------------------------
+void decode_packet_order(const CodingParams &cp, const Tile &tile, std::vector<PacketId> &out) {
+    const TileGeom g = tile_geom(cp, tile);
+    std::vector<uint8_t> include((size_t)(cp.numlayers + 1) * g.max_res * cp.numcomps * std::max<uint32_t>(g.max_prec, 1), 0);
+    const uint32_t n = num_poc_entries(cp);
+    out.clear();
+    for (uint32_t pino = 0; pino < n; ++pino) {
+        Pi pi;
+        setup_pi(pi, g, cp, &include);
+        Range &q = pi.poc;
+        if (cp.numpocs) {
+            const PocSpec &p = cp.pocs[pino];
+            q.prg = p.prg;
+            q.resno0 = p.resno0; q.compno0 = p.compno0; q.layno0 = 0; q.precno0 = 0;
+            q.resno1 = p.resno1; q.compno1 = p.compno1;
+            q.layno1 = std::min(p.layno1, cp.numlayers);
+            q.precno1 = g.max_prec;
+        } else {
+            q.prg = cp.prog;
+            q.resno0 = 0; q.compno0 = 0; q.layno0 = 0; q.precno0 = 0;
+            q.resno1 = g.max_res; q.compno1 = cp.numcomps; q.layno1 = cp.numlayers; q.precno1 = g.max_prec;
+        }
+        // a POC range past the components the tile has: no packets there
+        q.compno1 = std::min(q.compno1, cp.numcomps);
+        walk(pi, out);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// encoder: tile-part plan
+// ---------------------------------------------------------------------------
+void init_enc_pocs(const CodingParams &cp, TileEnc &te) {
+    te.pocs.assign(num_poc_entries(cp), EncPoc());
+    for (uint32_t i = 0; i < cp.numpocs; ++i) {
+        EncPoc &p = te.pocs[i];
+        const PocSpec &s = cp.pocs[i];
+        p.resno0 = s.resno0; p.compno0 = s.compno0; p.layno1 = s.layno1;
+        p.resno1 = s.resno1; p.compno1 = s.compno1; p.prg1 = s.prg;
+    }
+}
+
+std::vector<uint32_t> tile_part_counts(CodingParams &cp, const Tile &tile) {
+    // pi_update_encoding_parameters then j2k_get_num_tp per POC entry
+    TileEnc te;
+    init_enc_pocs(cp, te);
+    const TileGeom g = tile_geom(cp, tile);
+    update_encode_pocs(cp, te.pocs, g, cp.numpocs != 0);
+    std::vector<uint32_t> counts;
+    const char *prog = prog_string(cp.prog);
+    for (auto &p : te.pocs) {
+        uint32_t tpnum = 1;
+        if (cp.tp_on) {
+            for (uint32_t i = 0; i < 4; ++i) {
+                switch (prog[i]) {
+                    case 'C': tpnum *= p.compE; break;
+                    case 'R': tpnum *= p.resE; break;
+                    case 'P': tpnum *= p.prcE; break;
+                    case 'L': tpnum *= p.layE; break;
+                }
+                if (cp.tp_flag == prog[i]) {
+                    cp.tp_pos = i;
+                    break;
+                }
+            }
+        }
+        counts.push_back(tpnum);
+    }
+    return counts;
+}
+
+void encode_packet_order(const CodingParams &cp, TileEnc &te, uint32_t pino, uint32_t tp_num,
+                         std::vector<PacketId> &out) {
+    std::vector<Pi> pis;
+    std::vector<uint8_t> include;
+    TileGeom g;
+    initialise_encode(cp, te, true, pis, include, g);
+    init_encode(pis[pino], cp, te.pocs[pino], tp_num, kStaleTpPos, true);
+    out.clear();
+    walk(pis[pino], out);
+}
+
+// ---------------------------------------------------------------------------
+// packet writer / simulator (T2::encode_packet T2.cpp:859-1060,
+// T2::encode_packet_simulate :1300-1506)
+// ---------------------------------------------------------------------------
+namespace {
+
+// Bit counter with the simulator's buffer bound: BitIO(0, length) fails once
+// a byte would land past `length` (BitIO.cpp:71-85); every such failure makes
+// the packet "not fit", so counting the header bytes and comparing at the end
+// is equivalent.
+struct BitCount {
+    uint64_t bytes = 0;
+    uint32_t buf = 0, ct = 8;
+    void byteout() { ++bytes; ct = (buf == 0xff) ? 7 : 8; buf = 0; }
+    void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
+    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    void flush() { byteout(); if (ct == 7) byteout(); }
+    void numpasses(uint32_t n) {
+        if (n == 1) write(0, 1);
+        else if (n == 2) write(2, 2);
+        else if (n <= 5) write(0xc | (n - 3), 4);
+        else if (n <= 36) write(0x1e0 | (n - 6), 9);
+        else write(0xff80 | (n - 37), 16);
+    }
+    void comma(int32_t n) { while (--n >= 0) write(1, 1); write(0, 1); }
+    void tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
+        int32_t stk[64], sp = 0, node = (int32_t)leaf;
+        while (t.nodes[node].parent >= 0) { stk[sp++] = node; node = t.nodes[node].parent; }
+        int64_t low = 0;
+        for (;;) {
+            TagTree::Node &n = t.nodes[node];
+            if (low > n.low) n.low = low; else low = n.low;
+            while (low < threshold) {
+                if (low >= n.value) {
+                    if (!n.known) { write(1, 1); n.known = 1; }
+                    break;
+                }
+                write(0, 1);
+                ++low;
+            }
+            n.low = low;
+            if (sp == 0) break;
+            node = stk[--sp];
+        }
+    }
+};
+
+// Packet header body shared by the writer and the simulator: inclusion,
+// missing MSBs, pass counts, length indicators.
+template <class W>
+void packet_header(const CodingParams &cp, TileEnc &te, Resolution &res, uint32_t precno, uint32_t layno, W &w) {
+    std::vector<EncCblkState> &cs = *te.cblk;
+    std::vector<EncLayer> &lay = *te.layers;
+    const std::vector<EncPass> &passes = *te.passes;
+    const uint32_t L = cp.numlayers;
+    if (layno == 0) {
+        for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+            Band &b = res.bands[bandno];
+            if (b.empty() || precno >= b.precs.size()) continue;
+            Precinct &pr = b.precs[precno];
+            if (pr.cblks.empty()) continue;
+            pr.incl.reset();
+            pr.imsb.reset();
+            for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+                EncCblkState &s = cs[pr.cblks[cb].gidx];
+                s.incl_cur = 0;
+                if (b.numbps >= s.numbps) pr.imsb.setvalue(cb, (int64_t)b.numbps - (int64_t)s.numbps);
+            }
+        }
+    }
+    w.write(1, 1);  // Grok always signals a non-empty packet (T2.cpp:924-927)
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        if (b.empty() || precno >= b.precs.size()) continue;
+        Precinct &pr = b.precs[precno];
+        if (pr.cblks.empty()) continue;
+        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+            const EncCblkState &s = cs[pr.cblks[cb].gidx];
+            if (!s.incl_cur && lay[(size_t)pr.cblks[cb].gidx * L + layno].numpasses) pr.incl.setvalue(cb, layno);
+        }
+        for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
+            EncCblkState &s = cs[pr.cblks[cb].gidx];
+            const EncLayer &ly = lay[(size_t)pr.cblks[cb].gidx * L + layno];
+            if (!s.incl_cur) w.tagtree(pr.incl, cb, layno + 1);
+            else w.write(ly.numpasses != 0, 1);
+            if (!ly.numpasses) continue;
+            if (!s.incl_cur) {
+                s.numlenbits = 3;
+                w.tagtree(pr.imsb, cb, INT64_MAX);
+            }
+            w.numpasses(ly.numpasses);
+            const uint32_t nb = s.incl_cur + ly.numpasses;
+            int32_t increment = 0;
+            uint32_t nump = 0, len = 0;
+            for (uint32_t pn = s.incl_cur; pn < nb; ++pn) {
+                const EncPass &ps = passes[s.pass0 + pn];
+                ++nump;
+                len += ps.len;
+                if (ps.term || pn == nb - 1) {
+                    increment = std::max<int32_t>(increment, floorlog2((int32_t)len) + 1 -
+                                                                 ((int32_t)s.numlenbits + floorlog2((int32_t)nump)));
+                    len = 0;
+                    nump = 0;
+                }
+            }
+            w.comma(increment);
+            s.numlenbits += (uint32_t)increment;
+            for (uint32_t pn = s.incl_cur; pn < nb; ++pn) {
+                const EncPass &ps = passes[s.pass0 + pn];
+                ++nump;
+                len += ps.len;
+                if (ps.term || pn == nb - 1) {
+                    w.write(len, s.numlenbits + (uint32_t)floorlog2((int32_t)nump));
+                    len = 0;
+                    nump = 0;
+                }
+            }
+        }
+    }
+    w.flush();
+}
+
+}  // namespace
+
+bool write_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ByteBuf &hdr, std::vector<PlanItem> &plan) {
+    Resolution &res = te.tile->comps[pk.compno].res[pk.resno];
+    const size_t hstart = hdr.size();
+    if (cp.csty & CSTY_SOP) {
+        const uint32_t n = te.packno % 0x10000;
+        hdr.put8(0xFF); hdr.put8(0x91); hdr.put8(0); hdr.put8(4); hdr.put8(n >> 8); hdr.put8(n & 0xff);
+    }
+    {
+        BitWriter w(hdr);
+        packet_header(cp, te, res, pk.precno, pk.layno, w);
+    }
+    if (cp.csty & CSTY_EPH) { hdr.put8(0xFF); hdr.put8(0x92); }
+    plan.push_back({hstart, (uint32_t)(hdr.size() - hstart), 0});
+    const uint32_t L = cp.numlayers;
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        if (b.empty() || pk.precno >= b.precs.size()) continue;
+        Precinct &pr = b.precs[pk.precno];
+        for (auto &c : pr.cblks) {
+            EncCblkState &s = (*te.cblk)[c.gidx];
+            const EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + pk.layno];
+            if (!ly.numpasses) continue;
+            if (ly.len) plan.push_back({s.dev_off + ly.data_off, ly.len, 1});
+            s.incl_cur += ly.numpasses;
+        }
+    }
+    ++te.packno;
+    return true;
+}
+
+namespace {
+
+// T2::encode_packet_simulate (T2.cpp:1300-1506): bytes of one packet, or
+// false when it does not fit in `length`.  Unsigned wrap-around of `length`
+// (SOP / EPH subtractions) is the reference's.
+bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, uint64_t length, uint64_t *bytes) {
+    Resolution &res = te.tile->comps[pk.compno].res[pk.resno];
+    uint64_t written = 0;
+    if (cp.csty & CSTY_SOP) { length -= 6; written += 6; }
+    BitCount w;
+    packet_header(cp, te, res, pk.precno, pk.layno, w);
+    if (w.bytes > length) return false;
+    written += w.bytes;
+    length -= w.bytes;
+    if (cp.csty & CSTY_EPH) { length -= 2; written += 2; }
+    const uint32_t L = cp.numlayers;
+    for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+        Band &b = res.bands[bandno];
+        if (b.empty() || pk.precno >= b.precs.size()) continue;
+        Precinct &pr = b.precs[pk.precno];
+        for (auto &c : pr.cblks) {
+            EncCblkState &s = (*te.cblk)[c.gidx];
+            const EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + pk.layno];
+            if (!ly.numpasses) continue;
+            if (ly.len > length) return false;
+            s.incl_cur += ly.numpasses;
+            written += ly.len;
+            length -= ly.len;
+        }
+    }
+    *bytes = written;
+    return true;
+}
+
+// T2::encode_packets_simulate (T2.cpp:126-192): the tile's packets of layers
+// [0, max_layers) in THRESH_CALC order -- per component tile-part for the 4K
+// cinema profile with a per-component size cap -- against max_len bytes.
+bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len) {
+    const uint32_t pocno = cp.rsiz == RSIZ_CINEMA_4K ? 2 : 1;
+    const uint32_t max_comp = cp.max_comp_size > 0 ? cp.numcomps : 1;
+    std::vector<Pi> pis;
+    std::vector<uint8_t> include;
+    TileGeom g;
+    initialise_encode(cp, te, false, pis, include, g);
+    std::vector<PacketId> order;
+    for (uint32_t compno = 0; compno < max_comp; ++compno) {
+        uint64_t comp_len = 0;
+        for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc) {
+            init_encode(pis[poc], cp, te.pocs[poc], compno, kStaleTpPos, false);
+            order.clear();
+            walk(pis[poc], order);
+            for (const auto &pk : order) {
+                if (pk.layno >= max_layers) continue;
+                uint64_t b = 0;
+                if (!simulate_packet(cp, te, pk, max_len, &b)) return false;
+                comp_len += b;
+                max_len -= b;
+            }
+            if (cp.max_comp_size && comp_len > cp.max_comp_size) return false;
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// layer formation (TileProcessor.cpp:281-852)
+// ---------------------------------------------------------------------------
+template <class F>
+void for_each_block(TileEnc &te, F f) {
+    for (auto &tc : te.tile->comps)
+        for (auto &res : tc.res)
+            for (uint32_t b = 0; b < res.numbands; ++b)
+                for (auto &pr : res.bands[b].precs)
+                    for (auto &c : pr.cblks) f(c);
+}
+
+void set_layer(TileEnc &te, uint32_t gidx, uint32_t layno, uint32_t L, uint32_t cumul) {
+    EncCblkState &s = (*te.cblk)[gidx];
+    EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
+    const std::vector<EncPass> &P = *te.passes;
+    ly.numpasses = cumul - s.incl_prev;
+    if (!ly.numpasses) {
+        ly.disto = 0;
+        return;
+    }
+    if (s.incl_prev == 0) {
+        ly.len = P[s.pass0 + cumul - 1].rate;
+        ly.data_off = 0;
+        ly.disto = P[s.pass0 + cumul - 1].dd;
+    } else {
+        ly.len = P[s.pass0 + cumul - 1].rate - P[s.pass0 + s.incl_prev - 1].rate;
+        ly.data_off = P[s.pass0 + s.incl_prev - 1].rate;
+        ly.disto = P[s.pass0 + cumul - 1].dd - P[s.pass0 + s.incl_prev - 1].dd;
+    }
+    te.distolayer[layno] += ly.disto;
+}
+
+// makelayer_final (TileProcessor.cpp:783-852)
+void makelayer_final(CodingParams &cp, TileEnc &te, uint32_t layno) {
+    const uint32_t L = cp.numlayers;
+    te.distolayer[layno] = 0;
+    for_each_block(te, [&](Cblk &c) {
+        EncCblkState &s = (*te.cblk)[c.gidx];
+        if (layno == 0) { s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0; }
+        uint32_t cumul = s.incl_prev;
+        if (s.numpasses > s.incl_prev) cumul = s.numpasses;
+        set_layer(te, c.gidx, layno, L, cumul);
+        if ((*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
+    });
+}
+
+// make_layer_simple (TileProcessor.cpp:675-780)
+void make_layer_simple(CodingParams &cp, TileEnc &te, uint32_t layno, double thresh, bool final) {
+    const uint32_t L = cp.numlayers;
+    const std::vector<EncPass> &P = *te.passes;
+    te.distolayer[layno] = 0;
+    for_each_block(te, [&](Cblk &c) {
+        EncCblkState &s = (*te.cblk)[c.gidx];
+        if (layno == 0) { s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0; }
+        uint32_t cumul;
+        if (thresh == 0) {
+            cumul = s.numpasses;
+        } else {
+            cumul = s.incl_prev;
+            for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
+                const EncPass &ps = P[s.pass0 + pn];
+                uint32_t dr;
+                double dd;
+                if (cumul == 0) { dr = ps.rate; dd = ps.dd; }
+                else {
+                    dr = ps.rate - P[s.pass0 + cumul - 1].rate;
+                    dd = ps.dd - P[s.pass0 + cumul - 1].dd;
+                }
+                if (!dr) {
+                    if (dd != 0) cumul = pn + 1;
+                    continue;
+                }
+                const double slope = dd / dr;
+                if (thresh - slope < DBL_EPSILON) cumul = pn + 1;
+            }
+        }
+        set_layer(te, c.gidx, layno, L, cumul);
+        if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
+    });
+}
+
+// makelayer_feasible (TileProcessor.cpp:281-364)
+void makelayer_feasible(CodingParams &cp, TileEnc &te, uint32_t layno, uint16_t thresh, bool final) {
+    const uint32_t L = cp.numlayers;
+    const std::vector<EncPass> &P = *te.passes;
+    te.distolayer[layno] = 0;
+    for_each_block(te, [&](Cblk &c) {
+        EncCblkState &s = (*te.cblk)[c.gidx];
+        if (layno == 0) s.incl_prev = 0;
+        uint32_t cumul = s.incl_prev;
+        for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
+            const EncPass &ps = P[s.pass0 + pn];
+            if (ps.slope) {
+                if (ps.slope <= thresh) break;
+                cumul = pn + 1;
+            }
+        }
+        set_layer(te, c.gidx, layno, L, cumul);
+        if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
+    });
+}
+
+bool layer_needs_rate_control(const CodingParams &cp, uint32_t layno) {
+    return (cp.disto_alloc == 1 && cp.rates[layno] > 0.0) || (cp.fixed_quality == 1 && cp.distoratio[layno] > 0.0f);
+}
+
+// make_single_lossless_layer (TileProcessor.cpp:272-279)
+bool single_lossless(CodingParams &cp, TileEnc &te) {
+    if (cp.numlayers == 1 && !layer_needs_rate_control(cp, 0)) {
+        makelayer_final(cp, te, 0);
+        return true;
+    }
+    return false;
+}
+
+// max squared error of the tile (maxSE, used only for fixed-quality layers)
+double tile_max_se(const CodingParams &cp, TileEnc &te) {
+    double maxSE = 0;
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        uint64_t numpix = 0;
+        TileComp &tc = te.tile->comps[k];
+        for (auto &res : tc.res)
+            for (uint32_t b = 0; b < res.numbands; ++b)
+                for (auto &pr : res.bands[b].precs)
+                    for (auto &c : pr.cblks) numpix += (uint64_t)c.r.w() * c.r.h();
+        const double m = (double)(((uint64_t)1 << cp.prec[k]) - 1);
+        maxSE += m * m * (double)numpix;
+    }
+    return maxSE;
+}
+
+// pcrd_bisect_simple (TileProcessor.cpp:508-667)
+bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
+    double cumdisto[100];
+    const double K = 1;
+    double min_slope = DBL_MAX, max_slope = -1;
+    if (single_lossless(cp, te)) return true;
+    const std::vector<EncPass> &P = *te.passes;
+    for_each_block(te, [&](Cblk &c) {
+        const EncCblkState &s = (*te.cblk)[c.gidx];
+        for (uint32_t pn = 0; pn < s.numpasses; ++pn) {
+            const EncPass &ps = P[s.pass0 + pn];
+            int32_t dr;
+            double dd;
+            if (pn == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
+            else { dr = (int32_t)(ps.rate - P[s.pass0 + pn - 1].rate); dd = ps.dd - P[s.pass0 + pn - 1].dd; }
+            if (dr == 0) continue;
+            const double r = dd / dr;
+            if (r < min_slope) min_slope = r;
+            if (r > max_slope) max_slope = r;
+        }
+    });
+    const double maxSE = tile_max_se(cp, te);
+    double upper = max_slope;
+    for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
+        if (layer_needs_rate_control(cp, layno)) {
+            double lower = min_slope;
+            const uint64_t maxlen = cp.rates[layno] > 0.0f ? std::min<uint64_t>((uint64_t)ceil(cp.rates[layno]), len) : len;
+            double prevthresh = -1;
+            const double distotarget = te.distotile - ((K * maxSE) / pow(10.0, cp.distoratio[layno] / 10.0));
+            double thresh = 0;
+            for (uint32_t i = 0; i < 128; ++i) {
+                thresh = (upper == -1) ? lower : (lower + upper) / 2;
+                make_layer_simple(cp, te, layno, thresh, false);
+                if (prevthresh != -1 && (fabs(prevthresh - thresh)) < 0.001) break;
+                prevthresh = thresh;
+                if (cp.fixed_quality) {
+                    const double achieved = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
+                    if (achieved < distotarget) { upper = thresh; continue; }
+                    lower = thresh;
+                } else {
+                    if (!simulate_tile(cp, te, layno + 1, maxlen)) { lower = thresh; continue; }
+                    upper = thresh;
+                }
+            }
+            const double good = (upper == -1) ? thresh : upper;
+            make_layer_simple(cp, te, layno, good, true);
+            cumdisto[layno] = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
+            upper = lower - 1;
+        } else {
+            makelayer_final(cp, te, layno);
+            return true;
+        }
+    }
+    return true;
+}
+
+// RateControl::convexHull + slopeToLog (RateControl.cpp:31-175)
+uint16_t slope_to_log(double slope) {
+    static const double cutoff = pow(2, 64), scale = 256 / log(2), shift = 1 << 16;
+    if (slope > cutoff) slope = cutoff;
+    double ls = log(slope) * scale - log(cutoff) * scale + shift;
+    if (ls < 1) ls = 1;
+    if (ls > 0xFFFF) ls = 0xFFFF;
+    return (uint16_t)ls;
+}
+
+void convex_hull(EncPass *pass, uint32_t n) {
+    std::vector<double> cache(n);
+    for (uint32_t p = 0; p < n; p++) {
+        EncPass *cur = pass + p;
+        double dd = 0, dr = 0;
+        int pi = (int)p;
+        EncPass *ip = pass + pi;
+        while (1) {
+            dr += ip->len;
+            dd += pi == 0 ? ip->dd : ip->dd - (ip - 1)->dd;
+            if (dd <= 0) { cur->slope = 0; break; }
+            pi--;
+            ip--;
+            if (pi == -1) {
+                cache[p] = dd / dr;
+                cur->slope = slope_to_log(cache[p]);
+                break;
+            }
+            if (ip->slope == 0) continue;
+            if (dr == 0) ip->slope = 0;
+            else if ((cache[pi] * dr) <= dd) ip->slope = 0;
+            else {
+                cache[p] = dd / dr;
+                cur->slope = slope_to_log(cache[p]);
+                if (cur->slope >= ip->slope) ip->slope = 0;
+                break;
+            }
+        }
+    }
+}
+
+// pcrd_bisect_feasible (TileProcessor.cpp:371-506)
+bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
+    double cumdisto[100];
+    const double K = 1;
+    const bool sl = single_lossless(cp, te);
+    uint32_t min_slope = USHRT_MAX;
+    if (!sl) {
+        for_each_block(te, [&](Cblk &c) {
+            EncCblkState &s = (*te.cblk)[c.gidx];
+            EncPass *P = te.passes->data() + s.pass0;
+            convex_hull(P, s.numpasses);
+            for (uint32_t pn = 0; pn < s.numpasses; ++pn)
+                if (P[pn].slope && P[pn].slope < min_slope) min_slope = P[pn].slope;
+        });
+    }
+    if (sl) {
+        makelayer_final(cp, te, 0);
+        return true;
+    }
+    const double maxSE = tile_max_se(cp, te);
+    uint32_t upper = USHRT_MAX;
+    for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
+        uint32_t lower = min_slope;
+        const uint64_t maxlen = cp.rates[layno] > 0.0f ? std::min<uint64_t>((uint64_t)ceil(cp.rates[layno]), len) : len;
+        uint32_t prevthresh = 0;
+        if (layer_needs_rate_control(cp, layno)) {
+            const double distotarget = te.distotile - ((K * maxSE) / pow(10.0, cp.distoratio[layno] / 10.0));
+            for (uint32_t i = 0; i < 128; ++i) {
+                const uint32_t thresh = (lower + upper) >> 1;
+                if (prevthresh != 0 && prevthresh == thresh) break;
+                makelayer_feasible(cp, te, layno, (uint16_t)thresh, false);
+                prevthresh = thresh;
+                if (cp.fixed_quality) {
+                    const double achieved = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
+                    if (achieved < distotarget) { upper = thresh; continue; }
+                    lower = thresh;
+                } else {
+                    if (!simulate_tile(cp, te, layno + 1, maxlen)) { lower = thresh; continue; }
+                    upper = thresh;
+                }
+            }
+            makelayer_feasible(cp, te, layno, (uint16_t)upper, true);
+            cumdisto[layno] = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
+            upper = lower - 1;
+        } else {
+            makelayer_final(cp, te, layno);
+        }
+    }
+    return true;
+}
+
+}  // namespace
+
+bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
+    te.distolayer.assign(cp.numlayers + 1, 0.0);
+    if (!(cp.disto_alloc || cp.fixed_quality)) return true;
+    if (cp.rate_algo == 0) return pcrd_simple(cp, te, len);
+    return pcrd_feasible(cp, te, len);
+}
+
+// ---------------------------------------------------------------------------
+// distortion (t1.cpp:912-930, dwt_utils.cpp:132-166, mct.cpp:65-79)
+// ---------------------------------------------------------------------------
+namespace {
+// sqrt energy gains (HTParams.cpp:54-96), float as in the reference
+const float kG97L[34] = {1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f, 8.2388e+00f,
+    1.1652e+01f, 1.6479e+01f, 2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f, 1.3183e+02f,
+    1.8643e+02f, 2.6366e+02f, 3.7287e+02f, 5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f, 2.1093e+03f,
+    2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f, 1.1932e+04f, 1.6874e+04f, 2.3864e+04f, 3.3748e+04f,
+    4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
+const float kG97H[34] = {1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f, 1.1809e+01f,
+    1.6701e+01f, 2.3620e+01f, 3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f, 1.8896e+02f,
+    2.6723e+02f, 3.7792e+02f, 5.3446e+02f, 7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f, 3.0233e+03f,
+    4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f, 1.7103e+04f, 2.4187e+04f, 3.4205e+04f, 4.8373e+04f,
+    6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
+const float kG53L[34] = {1.0000e+00f, 1.2247e+00f, 1.3229e+00f, 1.5411e+00f, 1.7139e+00f, 1.9605e+00f, 2.2044e+00f,
+    2.5047e+00f, 2.8277e+00f, 3.2049e+00f, 3.6238e+00f, 4.1033e+00f, 4.6423e+00f, 5.2548e+00f, 5.9462e+00f,
+    6.7299e+00f, 7.6159e+00f, 8.6193e+00f, 9.7544e+00f, 1.1039e+01f, 1.2493e+01f, 1.4139e+01f, 1.6001e+01f,
+    1.8108e+01f, 2.0493e+01f, 2.3192e+01f, 2.6246e+01f, 2.9702e+01f, 3.3614e+01f, 3.8041e+01f, 4.3051e+01f,
+    4.8721e+01f, 5.5138e+01f, 6.2399e+01f};
+const float kG53H[34] = {1.0458e+00f, 1.3975e+00f, 1.4389e+00f, 1.7287e+00f, 1.8880e+00f, 2.1841e+00f, 2.4392e+00f,
+    2.7830e+00f, 3.1341e+00f, 3.5576e+00f, 4.0188e+00f, 4.5532e+00f, 5.1494e+00f, 5.8301e+00f, 6.5963e+00f,
+    7.4663e+00f, 8.4489e+00f, 9.5623e+00f, 1.0821e+01f, 1.2247e+01f, 1.3860e+01f, 1.5685e+01f, 1.7751e+01f,
+    2.0089e+01f, 2.2735e+01f, 2.5729e+01f, 2.9117e+01f, 3.2952e+01f, 3.7292e+01f, 4.2203e+01f, 4.7761e+01f,
+    5.4051e+01f, 6.1170e+01f, 6.9226e+01f};
+
+double getnorm(uint32_t level, uint32_t orient, bool rev) {
+    const float *Lg = rev ? kG53L : kG97L, *Hg = rev ? kG53H : kG97H;
+    // float products, widened on return (dwt_utils.cpp:143-166)
+    switch (orient) {
+        case 0: return (double)(float)(Lg[level] * Lg[level]);
+        case 1: case 2: return (double)(float)(Lg[level + 1] * Hg[level]);
+        case 3: return (double)(float)(Hg[level] * Hg[level]);
+    }
+    return 0;
+}
+}  // namespace
+
+double t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno, uint32_t qmfbid,
+                  double stepsize, const double *mct_norms, uint32_t mct_numcomps) {
+    double w1 = 1, w2, wmsedec;
+    if (mct_norms && compno < mct_numcomps) w1 = mct_norms[compno];
+    w2 = getnorm(level, orient, qmfbid == 1);
+    wmsedec = w1 * w2 * stepsize * (1 << bpno);
+    wmsedec *= wmsedec * nmsedec / 8192.0;
+    return wmsedec;
+}
+
+}  // namespace grkgpu

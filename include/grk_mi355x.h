@@ -70,7 +70,22 @@ typedef struct {
     int32_t sgnd[GRKGPU_MAX_COMPS];
 } grkgpu_image_desc;
 
-/* grk_cparameters subset (grok.h:447-570) */
+/* One progression-order change (grk_poc, grok.h:393-410; grk_compress -P
+ * "T<tile>=resno0,compno0,layno1,resno1,compno1,PROG"). */
+typedef struct {
+    uint32_t tile;                       /* 1-based tile index the entry applies to */
+    uint32_t resno0, compno0, layno1, resno1, compno1;
+    int32_t prog;                        /* GRKGPU_LRCP .. GRKGPU_CPRL */
+} grkgpu_poc;
+
+enum { GRKGPU_LRCP = 0, GRKGPU_RLCP = 1, GRKGPU_RPCL = 2, GRKGPU_PCRL = 3, GRKGPU_CPRL = 4 };
+#define GRKGPU_CSTY_PRT 0x01 /* user precinct sizes (grk_compress -c) */
+#define GRKGPU_CSTY_SOP 0x02 /* SOP marker before each packet (-SOP) */
+#define GRKGPU_CSTY_EPH 0x04 /* EPH marker after each packet header (-EPH) */
+#define GRKGPU_PROFILE_CINEMA_2K 0x0003 /* grok.h:160 */
+#define GRKGPU_PROFILE_CINEMA_4K 0x0004 /* grok.h:161 */
+
+/* grk_cparameters subset (grok.h:447-570); field meaning as there */
 typedef struct {
     uint32_t numresolution;                /* default 6 */
     uint32_t cblockw_init, cblockh_init;   /* default 64, 64 (powers of 2, <= 64) */
@@ -78,6 +93,25 @@ typedef struct {
     int32_t tcp_mct;                       /* -1: auto (RGB->YCC iff >= 3 comps), 0, 1 */
     int32_t tile_size_on;
     uint32_t cp_tdx, cp_tdy, cp_tx0, cp_ty0;
+    /* quality layers and rate control (grk_compress -r / -q / -A) */
+    uint32_t tcp_numlayers;                /* 0: one lossless layer */
+    double tcp_rates[100];                 /* per layer compression ratio, decreasing; 0 = lossless */
+    double tcp_distoratio[100];            /* per layer PSNR (fixed quality) */
+    int32_t cp_disto_alloc, cp_fixed_quality;
+    int32_t rate_control_algorithm;        /* 0: bisect all passes, 1: feasible truncation points */
+    /* coding style, precincts, progression (-c, -SOP, -EPH, -p, -P, -u) */
+    uint32_t csty;                         /* GRKGPU_CSTY_* */
+    uint32_t res_spec;                     /* precinct sizes given, highest resolution first */
+    uint32_t prcw_init[33], prch_init[33];
+    int32_t prog_order;                    /* GRKGPU_LRCP .. */
+    uint32_t numpocs;
+    grkgpu_poc POC[32];
+    int32_t tp_on;                         /* tile-parts: one per change of tp_flag's dimension */
+    int32_t tp_flag;                       /* 'R', 'L', 'C' */
+    /* profiles (-cinema2K / -cinema4K fps): rsiz + the size caps */
+    uint32_t rsiz;
+    uint32_t framerate;
+    uint64_t max_cs_size, max_comp_size;
 } grkgpu_cparams;
 
 typedef struct grkgpu_ctx grkgpu_ctx;
@@ -86,6 +120,9 @@ typedef struct grkgpu_ctx grkgpu_ctx;
 typedef struct {
     float h2d_ms, dcshift_mct_ms, dwt_ms, t1_ms, gather_ms, d2h_ms, host_t2_ms, total_ms;
     uint64_t num_cblks, cs_bytes;
+    uint64_t mq_symbols;  /* MQ symbols coded (encode) */
+    float rate_ms;        /* host rate allocation (PCRD) time */
+    float pad;
 } grkgpu_stats;
 
 const char *grkgpu_version(void);
@@ -181,8 +218,12 @@ typedef struct {
 } grkgpu_enc_block;
 
 typedef struct {
-    uint32_t numbps, numpasses, len, pad;
+    uint32_t numbps, numpasses, len, pad;  /* pad != 0: numbps above the band's bound */
+    uint32_t nsym, pad1, pad2, pad3;       /* nsym: MQ symbols coded */
     uint32_t rate[96];    /* cumulative pass rates after Grok's fix-ups */
+    int32_t nmsedec[96];  /* per-pass normalised distortion decrease (t1.cpp
+                             nmsedec; distortiondec = t1_getwmsedec of it,
+                             t1.cpp:912-930); filled when with_distortion */
 } grkgpu_enc_result;
 
 typedef struct {
@@ -200,7 +241,8 @@ typedef struct {
 #define GRKGPU_T1_MAX_SEG (64 * 64 * 4 + 64)
 size_t grkgpu_t1_scratch_bytes(void);
 int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
-                            void *scratch, uint8_t *out, grkgpu_enc_result *results, void *stream);
+                            void *scratch, uint8_t *out, grkgpu_enc_result *results, int with_distortion,
+                            void *stream);
 int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t nblocks, const uint8_t *data,
                             void *scratch, int32_t *dst, void *stream);
 

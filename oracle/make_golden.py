@@ -78,6 +78,27 @@ CASES = [
     ("rgb12_tiles_I", (150, 200, 3, 12), "smooth", 48, ["-I", "-t", "64,64"]),
     ("g8_b32_I", (130, 100, 1, 8), "smooth", 49, ["-I", "-b", "32,32"]),
     ("g8_1x37_I", (37, 1, 1, 8), "smooth", 50, ["-I"]),
+    # round 2: quality layers + rate control (PCRD), precincts, progressions,
+    # POC, SOP / EPH, tile-parts, cinema profiles
+    ("g8_r40_20_10", (96, 128, 1, 8), "smooth", 60, ["-r", "40,20,10"]),
+    ("g8_r5", (100, 77, 1, 8), "uniform", 61, ["-r", "5"]),
+    ("rgb8_r20_I", (96, 128, 3, 8), "smooth", 62, ["-I", "-r", "20"]),
+    ("rgb12_r30_10_1_I", (80, 96, 3, 12), "smooth", 63, ["-I", "-r", "30,10,1"]),
+    ("g12_r8_A1", (70, 90, 1, 12), "smooth", 64, ["-r", "16,8", "-A", "1"]),
+    ("rgb8_r10_tiles", (150, 200, 3, 8), "smooth", 65, ["-r", "10", "-t", "64,64"]),
+    ("g8_prec", (130, 100, 1, 8), "smooth", 66, ["-c", "[32,32],[16,16]"]),
+    ("rgb8_prec_rpcl", (96, 128, 3, 8), "smooth", 67, ["-c", "[64,64],[32,32]", "-p", "RPCL"]),
+    ("rgb8_prec_pcrl", (96, 128, 3, 8), "smooth", 68, ["-c", "[64,64],[32,32]", "-p", "PCRL"]),
+    ("rgb8_prec_cprl", (96, 128, 3, 8), "smooth", 69, ["-c", "[64,64],[32,32]", "-p", "CPRL"]),
+    ("rgb8_rlcp_layers", (96, 128, 3, 8), "smooth", 70, ["-p", "RLCP", "-r", "30,10"]),
+    ("g8_sop_eph", (96, 128, 1, 8), "smooth", 71, ["-S", "-E", "-r", "20,5"]),
+    ("rgb8_tp_R", (96, 128, 3, 8), "smooth", 72, ["-u", "R", "-r", "8"]),
+    ("rgb8_tp_C_cprl", (96, 128, 3, 8), "smooth", 73, ["-u", "C", "-p", "CPRL", "-c", "[32,32]"]),
+    ("rgb8_tp_L", (96, 128, 3, 8), "smooth", 74, ["-u", "L", "-r", "30,10,3"]),
+    ("rgb8_poc", (96, 128, 3, 8), "smooth", 75, ["-P", "T1=0,0,1,3,3,LRCP/T1=3,0,1,6,3,RPCL"]),
+    ("rgb12_cinema4k", (216, 384, 3, 12), "smooth", 76, ["-cinema4K", "24"]),
+    ("rgb12_cinema2k", (108, 192, 3, 12), "smooth", 77, ["-cinema2K", "24"]),
+    ("rgb12_cinema4k_48", (120, 256, 3, 12), "uniform", 78, ["-cinema4K", "48"]),
 ]
 
 # BASELINE.json configs (hash-only)
@@ -87,6 +108,10 @@ LARGE = [
     ("C3_8k_rgb12_I", (4320, 7680, 3, 12), "smooth", 3, ["-I"]),
     ("C3_8k_rgb12", (4320, 7680, 3, 12), "smooth", 3, []),
     ("C4_16k_gray16_tiled", (16384, 16384, 1, 16), "smooth", 4, ["-t", "1024,1024", "-n", "7"]),
+    # round 2: the secondary C3 run (rate-controlled) and C5, the DCI 4K cinema frame
+    ("C3_8k_rgb12_I_r20", (4320, 7680, 3, 12), "smooth", 3, ["-I", "-r", "20"]),
+    ("C5_dci4k_rgb12_cinema", (2160, 4096, 3, 12), "smooth", 5, ["-cinema4K", "24"]),
+    ("C5b_dci2k_rgb12_cinema", (1080, 2048, 3, 12), "smooth", 6, ["-cinema2K", "24"]),
 ]
 
 

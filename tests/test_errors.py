@@ -86,13 +86,14 @@ def test_cod_qcd_field_checks():
     cs = _cs("g8_256")
     cod = _marker(cs, 0xFF52)
     p = cod + 4
-    _rejects(_patch(cs, p + 1, ">B", 1))              # RLCP progression
+    _rejects(_patch(cs, p + 1, ">B", 5))              # unknown progression order
     _rejects(_patch(cs, p + 2, ">H", 0))              # zero layers
     _rejects(_patch(cs, p + 5, ">B", 33))             # 34 resolutions
     _rejects(_patch(cs, p + 6, ">B", 9))              # 2^11-wide code-blocks
     _rejects(_patch(cs, p + 8, ">B", 1))              # BYPASS mode switch
     _rejects(_patch(cs, p + 9, ">B", 2))              # qmfbid 2
-    _rejects(_patch(cs, p, ">B", 1))                  # Scod: user precincts
+    _rejects(_patch(cs, p, ">B", 1))                  # Scod: user precincts, but no precinct sizes
+    _rejects(_patch(cs, p, ">B", 8))                  # unknown Scod bit
     _rejects(_patch(cs, cod + 2, ">H", 4))            # COD too short
     qcd = _marker(cs, 0xFF5C)
     _rejects(_patch(cs, qcd + 4, ">B", 1))            # scalar-derived quantisation

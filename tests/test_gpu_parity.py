@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import synth
-from conftest import GOLD, load_manifest
+from conftest import GOLD, load_manifest, oracle_supported
 
 pytestmark = pytest.mark.gpu
 MAN = load_manifest()
@@ -155,7 +155,8 @@ def test_mct_stage_vs_oracle(oracle, irrev):
     assert np.array_equal(t.cpu().numpy(), np.stack(ref))
 
 
-@pytest.mark.parametrize("name", ["C1_512_gray8", "C2_4k_rgb8", "C3_8k_rgb12_I", "C3_8k_rgb12"])
+@pytest.mark.parametrize("name", ["C1_512_gray8", "C2_4k_rgb8", "C3_8k_rgb12_I", "C3_8k_rgb12", "C3_8k_rgb12_I_r20",
+                                  "C5_dci4k_rgb12_cinema", "C5b_dci2k_rgb12_cinema"])
 def test_large_config_hashes(codec, name):
     """BASELINE.json configs at full size: codestream sha256 == reference's,
     decoded-image sha256 == reference decoder's."""
@@ -187,7 +188,7 @@ def test_large_tiled_16k(codec):
     assert torch.equal(d, t)
 
 
-@pytest.mark.parametrize("name", sorted(MAN))
+@pytest.mark.parametrize("name", sorted(n for n in MAN if oracle_supported(MAN[n]["args"])))
 def test_reduced_decode_matches_oracle(codec, oracle, name):
     """grk_decompress -r: every reduce level of every golden codestream, GPU
     vs the oracle's reduced decode (bit-exact, 9/7 included).  The oracle's

@@ -10,9 +10,9 @@ import numpy as np
 import pytest
 
 import synth
-from conftest import GOLD, load_manifest
+from conftest import GOLD, load_manifest, oracle_supported
 
-MAN = load_manifest()
+MAN = {k: v for k, v in load_manifest().items() if oracle_supported(v["args"])}
 
 
 @pytest.mark.parametrize("name", sorted(MAN))
