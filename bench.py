@@ -1,52 +1,80 @@
 """bench.py -- Mpixels/s encode+decode of 8K RGB frames, 5/3 lossless & 9/7 lossy.
 
-Workload (BASELINE.json configs[2], the metric's 8K RGB case): one synthetic
-7680x4320 12-bit RGB frame per GPU (tests/golden/synth.py "smooth", seed 3 on
-rank 0 -- the same image whose reference codestream hashes are pinned in
-tests/golden/manifest_large.json).  One step = encode + decode of the frame
-with the 9/7 irreversible path (grk_compress -I) + encode + decode with the
-5/3 lossless path (default options), i.e. 2 frames' worth of pixels through
-both directions.  The frame is HBM-resident when timing starts; decoded planes
-are written back to HBM.  The codestream crosses PCIe once each way because
-Tier-2 / headers run on the host.
+Workload (BASELINE.json configs[2], the metric's 8K RGB case): synthetic
+7680x4320 12-bit RGB frames (tests/golden/synth.py "smooth", seed 3 + rank --
+the image whose reference codestream hashes are pinned in
+tests/golden/manifest_large.json).  One step = per pair of codec contexts,
+encode + decode of the frame with the 9/7 irreversible path (grk_compress -I)
+and encode + decode with the 5/3 lossless path; 6 such pairs (12 frames) are in
+flight per GPU, each on its own codec context, HIP stream and host thread.
 
-Multi-GPU: one process per GPU (torch.distributed.run), each encodes/decodes
-its own frame -- a frame batch, no data-path collective;
-"scaling": "weak".  value = frames*pixels of all ranks / max-over-ranks time.
+  value            frames already resident in HBM when the timed region
+                   starts (the task's contract); the codestream crosses PCIe
+                   once each way per frame inside the region because Tier-2 /
+                   headers run on the host.
+  pcie_inclusive   the same steps with each frame's input starting in pinned
+                   host memory and copied H2D inside the timed region (SURVEY
+                   8(d)'s "includes H2D of the input" reading).
+  t1               MQ symbols/s and code-blocks/s (batch and lone frame).
+  e2e_frac         value / (8e12 / B_e2e), B_e2e = C (ceil(prec/8) + 4 * 4/3 + 4).
+  roofline         the forward 9/7 DWT (dominant HBM kernel), HIP events.
+  cpu_baseline     the REFERENCE (Grok 5.1.0 libgrok compiled from source,
+                   oracle/_ref) on the host cores, one frame pair.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each codes its own
+frames -- a frame batch, no data-path collective; "scaling":
+"weak".  value = frames*pixels of all ranks / max-over-ranks time.
+`python bench.py --gpus N` run directly (no WORLD_SIZE) launches the N ranks
+itself before anything touches a GPU.
+
+--workload c5: DCI 4K 12-bit cinema frames (-cinema4K 24, BASELINE configs[4]),
+encode + decode, frame batch.  --workload c4: the 16K 16-bit tiled image
+(configs[3]) with its 256 tiles sharded over the ranks.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden"), os.path.join(ROOT, "oracle")]
 
+
+def _arg(name, default):
+    for i, a in enumerate(sys.argv):
+        if a.startswith(name):
+            return a.split("=", 1)[1] if "=" in a else (sys.argv[i + 1] if i + 1 < len(sys.argv) else default)
+    return default
+
+
+# --gpus N without a torch.distributed launcher: start the N ranks now, as
+# child processes, before anything touches a GPU, and exit with their status.
+if int(_arg("--gpus", "1")) > 1 and "WORLD_SIZE" not in os.environ:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    n = _arg("--gpus", "1")
+    sys.exit(subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", n,
+                              "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+                             + sys.argv[1:]))
+
 # Frames in flight run on their own HIP streams; HIP maps streams onto at most
 # GPU_MAX_HW_QUEUES hardware queues per process (4 by default on the box),
 # which would serialise the 12 streams' kernels in groups of 3.  The runtime
-# reads the value when the process starts, so with fewer than 16 the bench
-# reruns itself as a child process with 16 (nothing has touched the GPU yet)
-# and exits with the child's status.
-def _concurrency_arg():
-    for i, a in enumerate(sys.argv):
-        if a.startswith("--concurrency"):
-            v = a.split("=", 1)[1] if "=" in a else (sys.argv[i + 1] if i + 1 < len(sys.argv) else "12")
-            return int(v)
-    return 12
-
-
-# one hardware queue per codec stream plus torch's own (gpurun caps the knob at 32)
-HW_QUEUES = min(32, max(16, _concurrency_arg() + 4))
+# reads the value when the process starts, so with fewer than needed the bench
+# reruns itself as a child process (nothing has touched the GPU yet) and exits
+# with the child's status.
+HW_QUEUES = min(32, max(16, int(_arg("--concurrency", "12")) + 4))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < HW_QUEUES:
-    import subprocess
     sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, GPU_MAX_HW_QUEUES=str(HW_QUEUES))))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-H, W, C, BITS = 4320, 7680, 3, 12
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -60,18 +88,50 @@ def dwt_bytes(h, w, c, numres=6):
     return tot * c
 
 
+def b_e2e(c, prec):
+    """HBM bytes read per pixel end to end."""
+    return c * (-(-prec // 8) + 4.0 * 4.0 / 3.0 + 4.0)
+
+
+def cpu_reference(img, bits, args_list, threads, label):
+    """Time the reference (oracle/_ref/ref_driver over Grok's libgrok) on the
+    host: encode + decode of img for each argument list; returns seconds."""
+    drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    if not os.path.exists(drv):
+        return None
+    c, h, w = img.shape
+    path = "/tmp/grk_bench_%d.i32" % os.getpid()
+    np.ascontiguousarray(img, dtype="<i4").tofile(path)
+    tot = 0.0
+    try:
+        for a in args_list:
+            r = subprocess.run([drv, "bench", path, str(w), str(h), str(c), str(bits), "0", str(threads), "1"] + a,
+                               capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                return None
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            tot += (d["enc_ms"] + d["dec_ms"]) / 1e3
+    finally:
+        os.unlink(path)
+    return tot
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive leg")
     ap.add_argument("--concurrency", type=int, default=12, help="frames in flight per GPU: 1, or an even number (half 9/7, half 5/3)")
+    ap.add_argument("--workload", default="8k", choices=["8k", "c5", "c4"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -82,101 +142,116 @@ def main():
     import grokimagecompression_amd as grk
     import synth
 
-    img = synth.synth_image(H, W, C, BITS, 3 + rank)
+    if args.workload == "c4":
+        return bench_c4(args, grk, synth, dist, world, rank, local)
+
+    if args.workload == "c5":
+        H, W, C, BITS = 2160, 4096, 3, 12
+        img = synth.synth_image(H, W, C, BITS, 5 + rank)
+        pa, _ = grk.CParams.from_cli(["-cinema4K", "24"])
+        pb = pa
+        tags = ("cin", "cin")
+        wl = ("DCI 4K 4096x2160 12-bit RGB frame batch, -cinema4K 24 (9/7, CPRL, 256^2 precincts, 2 POCs, "
+              "tile-part per component, PCRD to 1,302,083 B), enc+dec")
+    else:
+        H, W, C, BITS = 4320, 7680, 3, 12
+        img = synth.synth_image(H, W, C, BITS, 3 + rank)
+        pa = grk.CParams.make(irreversible=True)
+        pb = grk.CParams.make(irreversible=False)
+        tags = ("97", "53")
+        wl = "8K 7680x4320 12-bit RGB frame per GPU; 9/7 (-I) + 5/3 lossless, enc+dec; 6 resolutions, 64x64 code-blocks, 1 layer LRCP"
     frame = torch.from_numpy(img).to("cuda:%d" % local)
-    # two codec contexts (each with its own HIP stream and host thread): the
-    # 9/7 and the 5/3 frame of a step are coded concurrently, so the T1
-    # kernels of one overlap the other's (T1 is latency-bound and leaves most
-    # SIMD issue slots free) and host Tier-2 overlaps device work.
+    host_frame = torch.from_numpy(img).pin_memory()
     ncodec = max(1, args.concurrency)
     assert ncodec == 1 or ncodec % 2 == 0, "--concurrency must be 1 or even"
     codecs = [grk.Codec(local) for _ in range(ncodec)]
-    p97 = grk.CParams.make(irreversible=True)
-    p53 = grk.CParams.make(irreversible=False)
-    npairs = max(1, ncodec // 2)              # (9/7 frame, 5/3 frame) pairs per step
+    npairs = max(1, ncodec // 2)
     outs = [(torch.empty_like(frame), torch.empty_like(frame)) for _ in range(npairs)]
-    out97, out53 = outs[0]
     st = {}
-
-    # one torch stream per codec (the codec runs on the caller's current
-    # stream, which torch keeps per host thread)
     streams = [torch.cuda.Stream(device=local) for _ in range(ncodec)]
     torch.cuda.synchronize()
 
-    def pipe(codec, p, out, tag):
+    def pipe(codec, p, out, tag, src):
         with torch.cuda.stream(streams[codecs.index(codec)]):
-            b = codec.compress(frame, BITS, p, view=True)
+            b = codec.compress(src, BITS, p, view=True)
             st["enc" + tag] = codec.stats()
             n = len(b)
             codec.decompress(b, out=out)
             st["dec" + tag] = codec.stats()
             st["bytes" + tag] = n
 
-    pool = None
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=ncodec) if ncodec > 1 else None
+    jobs = [(codecs[0], pa, outs[0][0], tags[0]), (codecs[0], pb, outs[0][1], tags[1])] if pool is None else \
+        [j for i in range(npairs) for j in ((codecs[2 * i], pa, outs[i][0], tags[0]),
+                                            (codecs[2 * i + 1], pb, outs[i][1], tags[1]))]
 
-    if ncodec > 1:
-        from concurrent.futures import ThreadPoolExecutor
-        pool = ThreadPoolExecutor(max_workers=ncodec)
-
-    jobs = [(codecs[0], p97, out97, "97"), (codecs[0], p53, out53, "53")] if pool is None else \
-        [j for i in range(npairs) for j in ((codecs[2 * i], p97, outs[i][0], "97"),
-                                            (codecs[2 * i + 1], p53, outs[i][1], "53"))]
-
-    def run_steps(n):
+    def run_steps(n, src):
         """n steps; each frame's pipeline runs its n iterations back to back on
-        its own thread/stream (no barrier between steps, so no pipeline waits
-        for the slowest one before starting its next frame)."""
+        its own thread/stream (no barrier between steps)."""
         if pool is None:
             for _ in range(n):
                 for j in jobs:
-                    pipe(*j)
+                    pipe(*j, src)
         else:
             def loop(j):
                 for _ in range(n):
-                    pipe(*j)
+                    pipe(*j, src)
             for x in [pool.submit(loop, j) for j in jobs]:
                 x.result()
-        st["bytes"] = (st["bytes97"], st["bytes53"])
-
-    run_steps(args.warmup)
-    assert torch.equal(out53, frame), "5/3 round trip is not lossless"
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    run_steps(args.steps)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(n, src):
+        barrier()
+        t0 = time.perf_counter()
+        run_steps(n, src)
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64, device="cuda:%d" % local)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
-    pix_per_step = 2 * npairs * H * W  # npairs x (one frame through 9/7 + one through 5/3)
+    run_steps(args.warmup, frame)
+    if args.workload == "8k":
+        assert torch.equal(outs[0][1], frame), "5/3 round trip is not lossless"
+    elapsed = timed(args.steps, frame)
+    pix_per_step = 2 * npairs * H * W
     value = world * pix_per_step * args.steps / elapsed / 1e6
     ms_per_step = 1e3 * elapsed / args.steps
+    nsym_step = npairs * (st["enc" + tags[0]]["mq_symbols"] + st["enc" + tags[1]]["mq_symbols"])
+    ncb_step = npairs * (st["enc" + tags[0]]["num_cblks"] + st["enc" + tags[1]]["num_cblks"])
 
-    # roofline: the forward 9/7 DWT of the frame = 5 level launches (one per
-    # decomposition level, all 3 components in each), B_DWT / the HIP-event
-    # time around those launches on the codec's stream (= per-launch bytes /
-    # mean launch duration).  traffic: HBM bytes per launch from the committed
-    # rocprofv3 PMC summary (scripts/pmc_bench.sh), when present.
-    # measured in isolation after the timed region (the timed region overlaps
-    # frames, so kernel durations there include contention): 3 x 9/7 encodes
-    # on one context, nothing else in flight, min of the HIP-event DWT times.
+    # PCIe-inclusive leg: inputs start in pinned host memory
+    pcie = None
+    if not args.no_pcie:
+        psteps = max(2, args.steps // 2)
+        run_steps(1, host_frame)
+        el = timed(psteps, host_frame)
+        pcie = {"value": round(world * pix_per_step * psteps / el / 1e6, 2), "unit": "Mpixels/s",
+                "ms_per_step": round(1e3 * el / psteps, 3), "steps": psteps,
+                "h2d_bytes_per_frame": int(img.nbytes),
+                "note": "same steps, each frame's int32 planes copied H2D from pinned host memory inside the timed region"}
+
+    # roofline: forward 9/7 DWT of the frame, measured alone after the timed
+    # region on one context (HIP events on the codec stream around the level
+    # launches): per-launch algorithmic bytes / mean launch duration.
     bdwt = dwt_bytes(H, W, C)
     nlaunch = 5
     torch.cuda.synchronize()
     iso = []
+    p97 = grk.CParams.make(irreversible=True)
     with torch.cuda.stream(streams[0]):
         for _ in range(3):
             codecs[0].compress(frame, BITS, p97, view=True)
-            iso.append(codecs[0].stats()["dwt_ms"])
-    dwt_ms = min(iso)
+            iso.append(codecs[0].stats())
+    best = min(iso, key=lambda s: s["dwt_ms"])
+    dwt_ms = best["dwt_ms"]
     achieved = bdwt / (dwt_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
@@ -191,43 +266,133 @@ def main():
                 "kernel_ms_per_launch": round(dwt_ms / nlaunch, 4),
                 "measured": "HIP events on the codec stream, 9/7 encode run alone after the timed region"}
 
+    # T1 figures: batch throughput + a lone frame's encode / decode T1 kernels
+    with torch.cuda.stream(streams[0]):
+        b = codecs[0].compress(frame, BITS, pa, view=True)
+        se = codecs[0].stats()
+        codecs[0].decompress(b, out=outs[0][0])
+        sd = codecs[0].stats()
+    t1 = {"mq_symbols_per_step": int(nsym_step), "cblks_per_step": int(ncb_step),
+          "batch_enc_dec_msym_per_s": round(2 * nsym_step * args.steps * world / elapsed / 1e6, 1),
+          "batch_cblks_per_s": round(2 * ncb_step * args.steps * world / elapsed, 1),
+          "lone_frame": {"mq_symbols": int(se["mq_symbols"]), "cblks": int(se["num_cblks"]),
+                         "enc_t1_ms": round(se["t1_ms"], 3), "dec_t1_ms": round(sd["t1_ms"], 3),
+                         "enc_msym_per_s": round(se["mq_symbols"] / (se["t1_ms"] * 1e-3) / 1e6, 1),
+                         "dec_msym_per_s": round(se["mq_symbols"] / (sd["t1_ms"] * 1e-3) / 1e6, 1)},
+          "note": "symbols = MQ decisions of the encoder (the decoder decodes the same ones)"}
+    roof_mpix = HBM_PEAK_GBS * 1e9 / b_e2e(C, BITS) / 1e6
+    e2e = {"B_e2e_bytes_per_px": round(b_e2e(C, BITS), 3), "roofline_mpix_per_s": round(roof_mpix, 1),
+           "frac": round(value / world / roof_mpix, 5)}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        import pyoracle
-        pyoracle.build()
         ncpu = min(16, os.cpu_count() or 1)
-        t0 = time.perf_counter()
-        b = pyoracle.encode(img, BITS, pyoracle.params(irreversible=True, nthreads=ncpu))
-        pyoracle.decode(b, nthreads=ncpu)
-        b = pyoracle.encode(img, BITS, pyoracle.params(irreversible=False, nthreads=ncpu))
-        pyoracle.decode(b, nthreads=ncpu)
-        ct = time.perf_counter() - t0
-        cpu = {"value": round(2 * H * W / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "port",
-               "sample": "1 step (8K 12-bit RGB frame: 9/7 enc+dec + 5/3 enc+dec) through the C oracle "
-                         "(oracle/grk_oracle.c, byte-identical to Grok 5.1.0), %d threads" % ncpu,
-               "seconds": round(ct, 2)}
+        if args.workload == "c5":
+            refargs = [["-cinema4K", "24"]]
+            npx = H * W
+        else:
+            refargs = [["-I"], []]
+            npx = 2 * H * W
+        ct = cpu_reference(img, BITS, refargs, ncpu, args.workload)
+        if ct is not None:
+            cpu = {"value": round(npx / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "reference",
+                   "sample": "%s through Grok 5.1.0's own libgrok (compiled from /root/reference by "
+                             "oracle/ref.mk), %d threads, encode+decode in memory" %
+                             ("1 DCI 4K cinema frame" if args.workload == "c5" else
+                              "1 step (8K 12-bit RGB frame: 9/7 enc+dec + 5/3 enc+dec)", ncpu),
+                   "seconds": round(ct, 2)}
+        else:
+            import pyoracle
+            pyoracle.build()
+            t0 = time.perf_counter()
+            for irr in (True, False):
+                bb = pyoracle.encode(img, BITS, pyoracle.params(irreversible=irr, nthreads=ncpu))
+                pyoracle.decode(bb, nthreads=ncpu)
+            ct = time.perf_counter() - t0
+            cpu = {"value": round(2 * H * W / ct / 1e6, 3), "unit": "Mpixels/s", "cores": ncpu, "kind": "port",
+                   "sample": "1 step through the C oracle (oracle/grk_oracle.c), %d threads" % ncpu,
+                   "seconds": round(ct, 2)}
 
     if rank == 0:
         def r(d):
             return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
+        metric = "Mpixels/sec encode+decode, 8K RGB 5/3 lossless & 9/7 lossy" if args.workload == "8k" else \
+            "Mpixels/sec encode+decode, DCI 4K cinema frames"
         line = {
-            "metric": "Mpixels/sec encode+decode, 8K RGB 5/3 lossless & 9/7 lossy",
+            "metric": metric,
             "value": round(value, 2), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32/f32 (integer encode, f32 9/7 decode)",
-            "data": "synthetic (tests/golden/synth.py smooth+2% noise, seed 3+rank)",
-            "config": {"workload": "8K 7680x4320 12-bit RGB frame per GPU; 9/7 (-I) + 5/3 lossless, enc+dec; "
-                                   "6 resolutions, 64x64 code-blocks, 1 layer LRCP",
-                       "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
+            "data": "synthetic (tests/golden/synth.py smooth+2% noise, seed %d+rank)" % (5 if args.workload == "c5" else 3),
+            "config": {"workload": wl, "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
                        "parallelism": "frame-batch x%d (no collectives)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "codestream_bytes": {"9/7": st["bytes"][0], "5/3": st["bytes"][1]},
-            "stage_ms": {k: r(st[k]) for k in ("enc97", "dec97", "enc53", "dec53")},
+            "pcie_inclusive": pcie,
+            "t1": t1,
+            "e2e_frac": e2e,
+            "codestream_bytes": {tags[0]: st["bytes" + tags[0]], tags[1]: st["bytes" + tags[1]]},
+            "stage_ms": {k: r(st[k]) for k in ("enc" + tags[0], "dec" + tags[0], "enc" + tags[1], "dec" + tags[1])},
         }
         print(json.dumps(line), flush=True)
     for c in codecs:
         c.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_c4(args, grk, synth, dist, world, rank, local):
+    """C4: 16384^2 16-bit gray, 1024^2 tiles, 7 resolutions; the 256 tiles are
+    split into contiguous ranges over the ranks (grokimagecompression_amd.shard),
+    each rank encodes and decodes its range; the compressed bytes stay on their
+    rank (host concatenation is shard.assemble, outside the timed region)."""
+    from grokimagecompression_amd import shard
+    H = W = 16384
+    BITS = 16
+    p, _ = grk.CParams.from_cli(["-t", "1024,1024", "-n", "7"])
+    ntiles = 256
+    b, e = shard.tile_range(ntiles, rank, world)
+    rows = (b // 16 * 1024, min(H, ((e + 15) // 16) * 1024)) if e > b else (0, 0)
+    # every rank holds the whole image's rows it needs only (its tile rows)
+    img = np.zeros((1, H, W), dtype=np.int32)
+    if e > b:
+        img[0, rows[0]:rows[1]] = synth.synth_plane(H, W, BITS, 4, 0, "smooth", rows=rows)
+    frame = torch.from_numpy(img).to("cuda:%d" % local)
+    del img
+    out = torch.empty_like(frame)
+    codec = grk.Codec(local)
+
+    def step():
+        cs = codec.compress_tiles(frame, BITS, p, b, e, parts=grk.PART_ALL if world == 1 else grk.PART_TILES)
+        full = cs if world == 1 else None
+        return cs, full
+
+    cs, full = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cs, _ = step()
+        if world == 1:
+            codec.decompress_tiles(cs, b, e, out)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "Mpixels/sec encode(+decode at N=1), 16K tiled, tile shards",
+                          "value": round(H * W * args.steps / el / 1e6, 2), "unit": "Mpixels/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+                          "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                          "dtype": "int32", "data": "synthetic (synth.py smooth, seed 4)",
+                          "config": {"workload": "16384^2 16-bit gray, 1024^2 tiles, 7 resolutions, tiles sharded "
+                                                 "over ranks", "parallelism": "tile-shard x%d" % world}}), flush=True)
+    codec.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -330,8 +330,17 @@ class Codec:
         on_dev = not isinstance(img, np.ndarray)
         if on_dev:
             torch = _torch()
-            assert img.dtype == torch.int32 and img.is_cuda and img.is_contiguous()
-            lib().grkgpu_set_stream(self._ctx, _stream_handle(img.device))
+            if img.dtype != torch.int32 or not img.is_contiguous():
+                raise GrkGpuError("image tensor must be contiguous int32")
+            if img.is_cuda:
+                if img.device.index != self.device:
+                    raise GrkGpuError("image tensor on %s, codec on cuda:%d" % (img.device, self.device))
+                lib().grkgpu_set_stream(self._ctx, _stream_handle(img.device))
+            else:
+                # host tensor (pinned or not): the library copies it H2D on the
+                # caller's current stream
+                on_dev = False
+                lib().grkgpu_set_stream(self._ctx, _stream_handle(torch.device("cuda", self.device)))
             ptrs = (ctypes.c_void_p * c)(*[img[k].data_ptr() for k in range(c)])
         else:
             img = np.ascontiguousarray(img, dtype=np.int32)
