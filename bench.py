@@ -323,7 +323,7 @@ def main():
             "value": round(value, 2), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32/f32 (integer encode, f32 9/7 decode)",
-            "data": "synthetic (tests/golden/synth.py smooth+2% noise, seed %d+rank)" % (5 if args.workload == "c5" else 3),
+            "data": "synthetic (tests/golden/synth.py smooth+2%% noise, seed %d+rank)" % (5 if args.workload == "c5" else 3),
             "config": {"workload": wl, "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
                        "parallelism": "frame-batch x%d (no collectives)" % world},
             "roofline": roofline,

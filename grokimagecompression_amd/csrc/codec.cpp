@@ -88,6 +88,11 @@ struct grkgpu_ctx {
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
+    // grkgpu_encode_blocks output (valid until the next call on the context)
+    HostBuf h_slab;
+    std::vector<grkgpu_block_info> bexp;
+    std::vector<uint32_t> bexp_rate;
+    std::vector<double> bexp_dist;
 };
 
 // Device check, cached per device index (hipGetDeviceProperties is slow and
@@ -576,9 +581,12 @@ static BandNeed window_need(const TileComp &tc, const Rect &win) {
 // ---------------------------------------------------------------------------
 // Encode tiles [tb, te) (a tile shard: j2k_encode's per-tile loop,
 // j2k.cpp:2088-2111) and emit [main header][their tile-parts][EOC] per `parts`.
+// export_blocks: stop after Tier-1 and hand the per-code-block results to the
+// caller instead of writing a codestream (grkgpu_encode_blocks).
 static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                          const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen,
-                         uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL) {
+                         uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL,
+                         bool export_blocks = false, int force_dist = 0) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
@@ -600,7 +608,12 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     uint64_t arena = 0, llarena = 0;
     std::vector<uint64_t> lloff(ntiles * nc);
     std::vector<EncBlock> eb;
-    struct BlkInfo { uint32_t compno, level, orient; float stepsize; };  // distortion weights (t1_getwmsedec)
+    struct BlkInfo {  // position + distortion weights (t1_getwmsedec)
+        uint32_t compno, level, orient;
+        float stepsize;
+        uint32_t tileno, resno, precno, cblkno;
+        Rect r;
+    };
     std::vector<BlkInfo> binfo;
     std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
     uint64_t sym_total = 0;
@@ -632,7 +645,17 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 eb.push_back(b);
                 uint32_t resno = 0;
                 while (&tc.res[resno].bands[0] > &band || &tc.res[resno].bands[2] < &band) ++resno;
-                binfo.push_back({k, tc.numres - 1 - resno, band.bandno, band.stepsize});
+                uint32_t precno = 0, cblkno = 0;
+                for (size_t q = 0; q < band.precs.size(); ++q) {
+                    const auto &cv = band.precs[q].cblks;
+                    if (!cv.empty() && &cb >= &cv.front() && &cb <= &cv.back()) {
+                        precno = (uint32_t)q;
+                        cblkno = (uint32_t)(&cb - &cv.front());
+                        break;
+                    }
+                }
+                binfo.push_back({k, tc.numres - 1 - resno, band.bandno, band.stepsize, tile.index, resno, precno,
+                                 cblkno, cb.r});
                 const uint32_t bound = std::min<uint32_t>(band.numbps, 32);
                 symoff.push_back(sym_total);
                 sym_total += (uint64_t)bound * sym_slot_bytes(b.w, b.h);
@@ -735,7 +758,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                             c->results.as<EncResult>(), s));
     // per-pass distortion only when some layer is rate-controlled
     // (TileProcessor::needs_rate_control, TileProcessor.cpp:260-266)
-    bool need_rc = false;
+    bool need_rc = force_dist != 0;
     for (uint32_t l = 0; l < cp.numlayers; ++l)
         need_rc = need_rc || (cp.disto_alloc && cp.rates[l] > 0.0) || (cp.fixed_quality && cp.distoratio[l] > 0.0f);
     if (need_rc)
@@ -797,6 +820,42 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             passes.push_back(ps);
         }
         blk_disto[i] = cum;
+    }
+    if (export_blocks) {
+        // the MQ slab to pinned host memory, then one record per block
+        HIPCHK(c->h_slab.ensure(out_total + 256));
+        if (out_total) HIPCHK(hipMemcpyAsync(c->h_slab.p, c->mqout.p, out_total, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        c->bexp.assign(nblk, grkgpu_block_info{});
+        c->bexp_rate.resize(passes.size() + 1);
+        c->bexp_dist.resize(passes.size() + 1);
+        for (size_t k = 0; k < passes.size(); ++k) {
+            c->bexp_rate[k] = passes[k].rate;
+            c->bexp_dist[k] = passes[k].dd;
+        }
+        for (uint32_t i = 0; i < nblk; ++i) {
+            grkgpu_block_info &o = c->bexp[i];
+            const BlkInfo &bi = binfo[i];
+            o.tileno = bi.tileno; o.compno = bi.compno; o.resno = bi.resno; o.bandno = bi.orient;
+            o.precno = bi.precno; o.cblkno = bi.cblkno;
+            o.x0 = bi.r.x0; o.y0 = bi.r.y0; o.x1 = bi.r.x1; o.y1 = bi.r.y1;
+            o.numbps = cst[i].numbps;
+            o.numpasses = cst[i].numpasses;
+            o.len = res[i].len;
+            o.data = c->h_slab.as<uint8_t>() + eb[i].out_off;
+            o.rate = c->bexp_rate.data() + cst[i].pass0;
+            o.distortion = c->bexp_dist.data() + cst[i].pass0;
+        }
+        grkgpu_stats &st0 = c->stats;
+        memset(&st0, 0, sizeof(st0));
+        hipEventElapsedTime(&st0.h2d_ms, c->ev[0], c->ev[1]);
+        hipEventElapsedTime(&st0.dcshift_mct_ms, c->ev[1], c->ev[2]);
+        hipEventElapsedTime(&st0.dwt_ms, c->ev[2], c->ev[3]);
+        hipEventElapsedTime(&st0.t1_ms, c->ev[3], c->ev[4]);
+        st0.num_cblks = nblk;
+        st0.mq_symbols = nsym;
+        st0.total_ms = (float)(now_ms() - t_start);
+        return GRKGPU_OK;
     }
     // tile-parts of every tile (j2k_calculate_tp, j2k.cpp:2990-3048): needed
     // for the TLM marker and the rate bookkeeping even outside the shard
@@ -1004,6 +1063,18 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     memcpy(o, v, n);
     *out = o;
     *outlen = n;
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_encode_blocks(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                                    const int32_t *const *planes, int planes_on_device, int with_distortion,
+                                    const grkgpu_block_info **blocks, uint32_t *nblocks) {
+    if (!blocks || !nblocks) return set_err(GRKGPU_EINVAL, "null argument");
+    int rc = compress_impl(c, img, p, planes, planes_on_device, nullptr, nullptr, 0, 0xffffffffu, GRKGPU_PART_ALL,
+                           true, with_distortion);
+    if (rc) return rc;
+    *blocks = c->bexp.data();
+    *nblocks = (uint32_t)c->bexp.size();
     return GRKGPU_OK;
 }
 

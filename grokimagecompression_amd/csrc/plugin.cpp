@@ -1,15 +1,36 @@
 // libgrok_plugin.so: Grok's minpf plugin ABI on top of libgrk_mi355x.so
-// (include/grk_plugin_abi.h).  Host side: grok.cpp:810-861.
+// (include/grk_plugin_abi.h).  Host side: grok.cpp:810-955,
+// TileProcessor.cpp:994-1012, plugin_bridge.cpp:24-258.
+//
+// Encode: the host (grk_compress, or any grk_* user) calls
+// grk_plugin_encode(params, cb) -> plugin_encode(params, internal_cb).  The
+// plugin reads the input image, codes every tile-component up to and
+// including Tier-1 on the GPU (grkgpu_encode_blocks), describes the result as
+// a grk_plugin_tile and calls back; the host's grk_encode_with_plugin then
+// skips DC shift / MCT / DWT / T1 and runs rate control + Tier-2 on the
+// plugin's code-blocks.  Pass rates follow the bridge's convention: the host
+// takes rate + 1, clamps it to the block length and steps back over a
+// trailing 0xFF (plugin_bridge.cpp:236-255), so a pass whose final rate is R
+// is handed over as R - 1.
 #include "../../include/grk_plugin_abi.h"
 #include "../../include/grk_mi355x.h"
 
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <memory>
 #include <mutex>
+#include <string>
+#include <vector>
 
 #define PLUGIN_API __attribute__((visibility("default")))
 
 namespace {
 std::mutex g_mu;
 grkgpu_ctx *g_ctx = nullptr;  // one GPU context per loaded plugin (grok's plugin manager is a global too)
+bool g_verbose = false;
 
 int32_t exit_plugin(void) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -20,6 +41,224 @@ int32_t exit_plugin(void) {
 // minpf object factory: Grok never calls these for the T1 plugin (Plugin.cpp:24-31)
 void *create_object(minpf_object_params *) { return nullptr; }
 int32_t destroy_object(void *) { return 0; }
+
+void log(const char *msg) {
+    if (g_verbose) fprintf(stderr, "[grok mi355x plugin] %s\n", msg);
+}
+
+// ---- input image: binary PGM / PPM, as grk_compress's PNMFormat reads it
+// (PNMFormat.cpp:343-460: precision = bits of maxval, at least 8; 1 byte per
+// sample up to 8 bits, else 2 big-endian bytes) ----
+struct Pnm {
+    uint32_t w = 0, h = 0, c = 0, prec = 0;
+    std::vector<int32_t> planes;  // (c, h, w)
+};
+
+bool pnm_token(FILE *f, uint32_t *v) {
+    int ch;
+    do {
+        ch = fgetc(f);
+        if (ch == '#')
+            while (ch != '\n' && ch != EOF) ch = fgetc(f);
+    } while (ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r');
+    if (ch < '0' || ch > '9') return false;
+    uint64_t x = 0;
+    while (ch >= '0' && ch <= '9') {
+        x = x * 10 + (uint32_t)(ch - '0');
+        if (x > 0xffffffffu) return false;
+        ch = fgetc(f);
+    }
+    *v = (uint32_t)x;
+    return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r';
+}
+
+bool read_pnm(const char *path, Pnm &img) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    std::unique_ptr<FILE, int (*)(FILE *)> guard(f, fclose);
+    char magic[2];
+    if (fread(magic, 1, 2, f) != 2 || magic[0] != 'P' || (magic[1] != '5' && magic[1] != '6')) return false;
+    uint32_t maxval;
+    if (!pnm_token(f, &img.w) || !pnm_token(f, &img.h) || !pnm_token(f, &maxval)) return false;
+    if (!img.w || !img.h || !maxval || maxval > 65535) return false;
+    img.c = magic[1] == '6' ? 3 : 1;
+    uint32_t prec = 1;
+    while (prec < 16 && (maxval >> prec)) ++prec;
+    img.prec = prec < 8 ? 8 : prec;
+    const bool one = img.prec < 9;
+    const uint64_t area = (uint64_t)img.w * img.h;
+    img.planes.resize(area * img.c);
+    std::vector<uint8_t> row((size_t)img.w * img.c * (one ? 1 : 2));
+    for (uint32_t y = 0; y < img.h; ++y) {
+        if (fread(row.data(), 1, row.size(), f) != row.size()) return false;
+        for (uint32_t x = 0; x < img.w; ++x)
+            for (uint32_t k = 0; k < img.c; ++k) {
+                const size_t i = (size_t)x * img.c + k;
+                const int32_t v = one ? row[i] : (int32_t)((row[2 * i] << 8) | row[2 * i + 1]);
+                img.planes[(size_t)k * area + (size_t)y * img.w + x] = v;
+            }
+    }
+    return true;
+}
+
+// grk_cparameters -> grkgpu_cparams (the subset that shapes the partition
+// and the Tier-1 output; rate control and Tier-2 stay with the host)
+bool map_params(const grkp_cparameters *g, uint32_t numcomps, grkgpu_cparams *p) {
+    grkgpu_default_cparams(p);
+    p->numresolution = g->numresolution;
+    p->cblockw_init = g->cblockw_init;
+    p->cblockh_init = g->cblockh_init;
+    p->irreversible = g->irreversible ? 1 : 0;
+    // tcp_mct 255 = "decide from the image" (grk_compress.cpp:1997-1998)
+    p->tcp_mct = g->tcp_mct == 255 ? -1 : g->tcp_mct;
+    if (g->tcp_mct == 2 || g->mct_data) return false;  // custom MCT
+    if (g->cblk_sty || g->isHT || g->roi_compno >= 0) return false;
+    if (g->subsampling_dx != 1 || g->subsampling_dy != 1) return false;
+    if (g->tile_size_on) return false;  // the host hands ONE plugin tile to every tile (j2k.cpp:2059-2069)
+    p->cp_tx0 = g->cp_tx0;
+    p->cp_ty0 = g->cp_ty0;
+    p->tcp_numlayers = g->tcp_numlayers;
+    for (int i = 0; i < 100; ++i) {
+        p->tcp_rates[i] = g->tcp_rates[i];
+        p->tcp_distoratio[i] = g->tcp_distoratio[i];
+    }
+    p->cp_disto_alloc = (int32_t)g->cp_disto_alloc;
+    p->cp_fixed_quality = (int32_t)g->cp_fixed_quality;
+    p->rate_control_algorithm = g->rateControlAlgorithm == 255 ? 0 : (int32_t)g->rateControlAlgorithm;
+    p->csty = g->csty;
+    p->res_spec = g->res_spec;
+    for (int i = 0; i < 33; ++i) {
+        p->prcw_init[i] = g->prcw_init[i];
+        p->prch_init[i] = g->prch_init[i];
+    }
+    p->prog_order = g->prog_order;
+    p->numpocs = g->numpocs > 32 ? 32 : g->numpocs;
+    for (uint32_t i = 0; i < p->numpocs; ++i)
+        p->POC[i] = {g->POC[i].tile, g->POC[i].resno0, g->POC[i].compno0, g->POC[i].layno1, g->POC[i].resno1,
+                     g->POC[i].compno1, g->POC[i].prg1};
+    p->tp_on = g->tp_on;
+    p->tp_flag = g->tp_flag;
+    p->rsiz = g->rsiz;
+    p->framerate = (uint32_t)g->framerate;
+    p->max_cs_size = g->max_cs_size;
+    p->max_comp_size = g->max_comp_size;
+    (void)numcomps;
+    return true;
+}
+
+// Does layer l need rate control (TileProcessor::layer_needs_rate_control,
+// TileProcessor.cpp:254-260)?  The cinema profiles always do: their layer
+// rate comes from the profile's size caps (j2k set_cinema_parameters).
+bool layer_rc(const grkp_cparameters *g, uint32_t l) {
+    if (g->rsiz == GRKGPU_PROFILE_CINEMA_2K || g->rsiz == GRKGPU_PROFILE_CINEMA_4K) return true;
+    return (g->cp_disto_alloc && g->tcp_rates[l] > 0) || (g->cp_fixed_quality && g->tcp_distoratio[l] > 0);
+}
+bool needs_distortion(const grkp_cparameters *g) {
+    for (uint32_t l = 0; l < g->tcp_numlayers && l < 100; ++l)
+        if (layer_rc(g, l)) return true;
+    return false;
+}
+
+// The grk_plugin_tile tree over the exported code-blocks: the host walks it
+// by (component, resolution, band, precinct, code-block) index
+// (plugin_bridge.cpp:150-156), so every level is an index-addressed array.
+struct TileTree {
+    grk_plugin_tile tile{};
+    std::vector<grk_plugin_tile_component> comps;
+    std::vector<grk_plugin_tile_component *> comp_ptrs;
+    std::vector<std::vector<grk_plugin_resolution>> res;
+    std::vector<std::vector<grk_plugin_resolution *>> res_ptrs;
+    std::vector<std::unique_ptr<grk_plugin_band>> bands;
+    std::vector<std::vector<grk_plugin_band *>> band_ptrs;
+    std::vector<std::unique_ptr<grk_plugin_precinct>> precs;
+    std::vector<std::vector<grk_plugin_precinct *>> prec_ptrs;
+    std::vector<grk_plugin_code_block> blocks;
+    std::vector<std::vector<grk_plugin_code_block *>> block_ptrs;
+};
+
+bool build_tree(const grkgpu_block_info *b, uint32_t n, uint32_t numcomps, uint32_t numres, TileTree &T) {
+    // sizes per level from the block list (canonical order)
+    std::vector<std::vector<std::vector<uint32_t>>> nprec(numcomps, std::vector<std::vector<uint32_t>>(numres, {0, 0, 0}));
+    std::vector<std::vector<std::vector<std::vector<uint32_t>>>> nblk(
+        numcomps, std::vector<std::vector<std::vector<uint32_t>>>(numres, std::vector<std::vector<uint32_t>>(3)));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (b[i].tileno != 0 || b[i].compno >= numcomps || b[i].resno >= numres) return false;
+        const uint32_t bi = b[i].resno == 0 ? 0 : b[i].bandno - 1;
+        if (bi > 2) return false;
+        auto &np = nprec[b[i].compno][b[i].resno][bi];
+        np = std::max(np, b[i].precno + 1);
+        auto &nb = nblk[b[i].compno][b[i].resno][bi];
+        if (nb.size() < np) nb.resize(np, 0);
+        nb[b[i].precno] = std::max(nb[b[i].precno], b[i].cblkno + 1);
+    }
+    T.blocks.assign(n, grk_plugin_code_block{});
+    T.comps.assign(numcomps, grk_plugin_tile_component{});
+    T.comp_ptrs.resize(numcomps);
+    T.res.assign(numcomps, std::vector<grk_plugin_resolution>(numres));
+    T.res_ptrs.assign(numcomps, std::vector<grk_plugin_resolution *>(numres));
+    std::vector<std::vector<std::vector<grk_plugin_band *>>> bandp(numcomps, std::vector<std::vector<grk_plugin_band *>>(numres));
+    std::vector<std::vector<std::vector<std::vector<grk_plugin_precinct *>>>> precp(
+        numcomps, std::vector<std::vector<std::vector<grk_plugin_precinct *>>>(numres, std::vector<std::vector<grk_plugin_precinct *>>(3)));
+    for (uint32_t k = 0; k < numcomps; ++k) {
+        T.comp_ptrs[k] = &T.comps[k];
+        T.comps[k].numResolutions = numres;
+        for (uint32_t r = 0; r < numres; ++r) {
+            T.res_ptrs[k][r] = &T.res[k][r];
+            grk_plugin_resolution &R = T.res[k][r];
+            R.level = numres - 1 - r;
+            R.numBands = r == 0 ? 1 : 3;
+            T.band_ptrs.emplace_back(R.numBands);
+            for (uint32_t bi = 0; bi < R.numBands; ++bi) {
+                T.bands.emplace_back(new grk_plugin_band());
+                grk_plugin_band *B = T.bands.back().get();
+                B->orient = r == 0 ? 0 : bi + 1;
+                B->numPrecincts = nprec[k][r][bi];
+                T.band_ptrs.back()[bi] = B;
+                T.prec_ptrs.emplace_back(B->numPrecincts);
+                for (uint32_t q = 0; q < B->numPrecincts; ++q) {
+                    T.precs.emplace_back(new grk_plugin_precinct());
+                    grk_plugin_precinct *P = T.precs.back().get();
+                    P->numBlocks = q < nblk[k][r][bi].size() ? nblk[k][r][bi][q] : 0;
+                    T.block_ptrs.emplace_back(P->numBlocks, nullptr);
+                    P->blocks = T.block_ptrs.back().data();
+                    T.prec_ptrs.back()[q] = P;
+                }
+                B->precincts = T.prec_ptrs.back().data();
+                precp[k][r][bi] = T.prec_ptrs.back();
+            }
+            R.bands = T.band_ptrs.back().data();
+        }
+        T.comps[k].resolutions = T.res_ptrs[k].data();
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const grkgpu_block_info &s = b[i];
+        grk_plugin_code_block &o = T.blocks[i];
+        o.x0 = s.x0; o.y0 = s.y0; o.x1 = s.x1; o.y1 = s.y1;
+        o.numPix = (size_t)(s.x1 - s.x0) * (s.y1 - s.y0);
+        o.compressedData = (uint8_t *)s.data;
+        o.compressedDataLength = s.len;
+        o.numBitPlanes = s.numbps;
+        if (s.numpasses > 67) return false;
+        o.numPasses = s.numpasses;
+        size_t prev = 0;
+        for (uint32_t k = 0; k < s.numpasses; ++k) {
+            o.passes[k].distortionDecrease = s.distortion[k];
+            o.passes[k].rate = s.rate[k] ? s.rate[k] - 1 : 0;  // the host adds one back
+            o.passes[k].length = s.rate[k] - prev;
+            prev = s.rate[k];
+        }
+        const uint32_t bi = s.resno == 0 ? 0 : s.bandno - 1;
+        precp[s.compno][s.resno][bi][s.precno]->blocks[s.cblkno] = &o;
+    }
+    T.tile.decode_flags = 0;
+    T.tile.numComponents = numcomps;
+    T.tile.tileComponents = T.comp_ptrs.data();
+    return true;
+}
+
+using ImageCreate = grkp_image *(*)(uint32_t, grkp_image_cmptparm *, int32_t);
+using ImageDestroy = void (*)(grkp_image *);
+
 }  // namespace
 
 extern "C" {
@@ -38,15 +277,97 @@ PLUGIN_API minpf_exit_func minpf_post_load_plugin(const char *, const minpf_plat
 // grk_plugin_init (grok.cpp:877-890): false keeps the host on its CPU path.
 PLUGIN_API bool plugin_init(grk_plugin_init_info info) {
     std::lock_guard<std::mutex> lk(g_mu);
+    g_verbose = info.verbose;
     if (g_ctx) return true;
     return grkgpu_create(info.deviceId < 0 ? 0 : info.deviceId, &g_ctx) == GRKGPU_OK;
 }
 
 PLUGIN_API uint32_t plugin_get_debug_state(void) { return GRK_PLUGIN_STATE_NO_DEBUG; }
 
-// -1 = not handled: the host codes the tile on its own path (plugin_interface.h)
-PLUGIN_API int32_t plugin_encode(void *, void *) { return -1; }
-PLUGIN_API int32_t plugin_batch_encode(const char *, const char *, void *, void *) { return -1; }
+// grk_plugin_encode (grok.cpp:917-935).  -1 = not handled (the host then runs
+// its CPU path, grk_compress.cpp:2206-2222).
+PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CALLBACK cb) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx || !params || !cb) return -1;
+    auto create = (ImageCreate)dlsym(RTLD_DEFAULT, "grk_image_create");
+    auto destroy = (ImageDestroy)dlsym(RTLD_DEFAULT, "grk_image_destroy");
+    if (!create || !destroy) {
+        log("host grk_image_create not found");
+        return -1;
+    }
+    // A single layer without rate control is formed by the host's
+    // make_single_lossless_layer BEFORE the loop that copies the plugin's
+    // passes in (TileProcessor.cpp:521 vs :537, :374 vs :404), so the host
+    // would write an empty layer: decline, the host encodes on its CPU path.
+    if (params->tcp_numlayers <= 1 && !layer_rc(params, 0)) {
+        log("single lossless layer: the host forms it before taking the plugin's passes; declined");
+        return -1;
+    }
+    // Fixed quality (-q) targets tile->distotile, which only the host's own
+    // T1 accumulates (T1Encoder.cpp:51); with a plugin tile it stays 0 and
+    // the PSNR search degenerates (TileProcessor.cpp:611-635): decline.
+    if (params->cp_fixed_quality) {
+        log("fixed-quality layers need the host's own T1 distortion total; declined");
+        return -1;
+    }
+    Pnm pnm;
+    if (!read_pnm(params->infile, pnm)) {
+        log("input is not a binary PGM / PPM");
+        return -1;
+    }
+    grkgpu_image_desc d{};
+    d.x0 = params->image_offset_x0;
+    d.y0 = params->image_offset_y0;
+    d.x1 = d.x0 + pnm.w;
+    d.y1 = d.y0 + pnm.h;
+    d.numcomps = pnm.c;
+    for (uint32_t k = 0; k < pnm.c; ++k) d.prec[k] = pnm.prec;
+    grkgpu_cparams p;
+    if (!map_params(params, pnm.c, &p)) {
+        log("coding options outside the plugin's path");
+        return -1;
+    }
+    std::vector<const int32_t *> planes(pnm.c);
+    const size_t area = (size_t)pnm.w * pnm.h;
+    for (uint32_t k = 0; k < pnm.c; ++k) planes[k] = pnm.planes.data() + k * area;
+    const grkgpu_block_info *blocks = nullptr;
+    uint32_t nblocks = 0;
+    if (grkgpu_encode_blocks(g_ctx, &d, &p, planes.data(), 0, needs_distortion(params) ? 1 : 0, &blocks, &nblocks)) {
+        log(grkgpu_last_error());
+        return -1;
+    }
+    // resolutions after the profile rules (cinema may clamp them)
+    uint32_t numres = params->numresolution;
+    for (uint32_t i = 0; i < nblocks; ++i) numres = std::max(numres, blocks[i].resno + 1);
+    TileTree T;
+    if (!build_tree(blocks, nblocks, pnm.c, numres, T)) {
+        log("block layout not representable as a plugin tile");
+        return -1;
+    }
+    // the host's image (its allocator owns the component buffers, which
+    // grk_start_compress moves into the codec, j2k.cpp:2141-2151)
+    std::vector<grkp_image_cmptparm> cm(pnm.c);
+    for (uint32_t k = 0; k < pnm.c; ++k) cm[k] = {1, 1, pnm.w, pnm.h, 0, 0, pnm.prec, 0};
+    grkp_image *img = create(pnm.c, cm.data(), pnm.c >= 3 ? 2 /* sRGB */ : 3 /* gray */);
+    if (!img) return -1;
+    img->x0 = d.x0; img->y0 = d.y0; img->x1 = d.x1; img->y1 = d.y1;
+    for (uint32_t k = 0; k < pnm.c; ++k)
+        if (img->comps[k].data) memcpy(img->comps[k].data, planes[k], area * 4);
+    plugin_encode_user_callback_info info{};
+    info.input_file_name = params->infile;
+    info.outputFileNameIsRelative = false;
+    info.output_file_name = params->outfile;
+    info.encoder_parameters = params;
+    info.image = img;
+    info.tile = &T.tile;
+    cb(&info);
+    destroy(img);
+    return info.error_code ? -1 : 0;
+}
+
+PLUGIN_API int32_t plugin_batch_encode(const char *, const char *, grkp_cparameters *, PLUGIN_ENCODE_USER_CALLBACK) {
+    return -1;
+}
 PLUGIN_API bool plugin_is_batch_complete(void) { return true; }
 PLUGIN_API void plugin_stop_batch_encode(void) {}
 PLUGIN_API int32_t plugin_decode(void *, void *) { return -1; }

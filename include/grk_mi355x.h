@@ -162,6 +162,28 @@ int grkgpu_compress_tiles(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const g
                           const int32_t *const *planes, int planes_on_device, uint32_t tile_begin,
                           uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
 
+/* Tier-1 only (the tile hot path of TileProcessor::encode_tile up to and
+ * including t1_encode, TileProcessor.cpp:994-1012; SURVEY 8(b)
+ * "grkgpu_encode_tile"): DC shift + MCT + DWT + T1 of every tile on the GPU,
+ * results handed back per code-block in the reference's order (tile,
+ * component, resolution, band, precinct, code-block) so a host Tier-2 -- the
+ * reference's own, through its plugin interface -- can finish the
+ * codestream.  Rates are the cumulative pass rates after the reference's
+ * fix-ups (t1.cpp:1299-1325); distortion the cumulative distortion decrease
+ * (t1.cpp:1249-1254), computed when with_distortion != 0.  Pointers stay
+ * valid until the next call on ctx. */
+typedef struct {
+    uint32_t tileno, compno, resno, bandno, precno, cblkno;
+    uint32_t x0, y0, x1, y1;             /* code-block rectangle, band coordinates */
+    uint32_t numbps, numpasses, len, pad;
+    const uint8_t *data;                 /* len MQ bytes */
+    const uint32_t *rate;                /* numpasses cumulative rates */
+    const double *distortion;            /* numpasses cumulative distortion decrease */
+} grkgpu_block_info;
+int grkgpu_encode_blocks(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                         const int32_t *const *planes, int planes_on_device, int with_distortion,
+                         const grkgpu_block_info **blocks, uint32_t *nblocks);
+
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
 

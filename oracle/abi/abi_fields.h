@@ -1,0 +1,52 @@
+// oracle/abi/abi_fields.h -- the plugin-boundary fields whose layout
+// include/grk_plugin_abi.h must share with the reference's grok.h /
+// plugin_interface.h.  Each TU (abi_ref.cpp over the reference headers,
+// abi_ours.cpp over ours) defines the T_* type names and expands this list
+// into an offset table; abi_check compares the two.  Test infrastructure.
+#define ABI_FIELDS(F, S)                                                                              \
+    S(CPARAMS) F(CPARAMS, tile_size_on) F(CPARAMS, cp_tx0) F(CPARAMS, cp_tdx) F(CPARAMS, cp_disto_alloc) \
+    F(CPARAMS, cp_fixed_quality) F(CPARAMS, cp_comment) F(CPARAMS, cp_comment_len)                    \
+    F(CPARAMS, cp_is_binary_comment) F(CPARAMS, cp_num_comments) F(CPARAMS, csty) F(CPARAMS, prog_order) \
+    F(CPARAMS, POC) F(CPARAMS, numpocs) F(CPARAMS, tcp_numlayers) F(CPARAMS, tcp_rates)                 \
+    F(CPARAMS, tcp_distoratio) F(CPARAMS, numresolution) F(CPARAMS, cblockw_init) F(CPARAMS, cblockh_init) \
+    F(CPARAMS, cblk_sty) F(CPARAMS, isHT) F(CPARAMS, irreversible) F(CPARAMS, roi_compno)              \
+    F(CPARAMS, roi_shift) F(CPARAMS, res_spec) F(CPARAMS, prcw_init) F(CPARAMS, prch_init)             \
+    F(CPARAMS, infile) F(CPARAMS, outfile) F(CPARAMS, image_offset_x0) F(CPARAMS, image_offset_y0)     \
+    F(CPARAMS, subsampling_dx) F(CPARAMS, subsampling_dy) F(CPARAMS, decod_format) F(CPARAMS, cod_format) \
+    F(CPARAMS, raw_cp) F(CPARAMS, max_comp_size) F(CPARAMS, tp_on) F(CPARAMS, tp_flag) F(CPARAMS, tcp_mct) \
+    F(CPARAMS, mct_data) F(CPARAMS, max_cs_size) F(CPARAMS, rsiz) F(CPARAMS, framerate)                \
+    F(CPARAMS, write_capture_resolution_from_file) F(CPARAMS, capture_resolution_from_file)           \
+    F(CPARAMS, write_capture_resolution) F(CPARAMS, capture_resolution) F(CPARAMS, write_display_resolution) \
+    F(CPARAMS, display_resolution) F(CPARAMS, rateControlAlgorithm) F(CPARAMS, numThreads)            \
+    F(CPARAMS, deviceId) F(CPARAMS, duration) F(CPARAMS, kernelBuildOptions) F(CPARAMS, repeats)       \
+    F(CPARAMS, verbose)                                                                               \
+    S(POC) F(POC, resno0) F(POC, compno0) F(POC, layno1) F(POC, resno1) F(POC, compno1) F(POC, layno0) \
+    F(POC, precno0) F(POC, precno1) F(POC, prg1) F(POC, prg) F(POC, progorder) F(POC, tile) F(POC, tx0) \
+    F(POC, layS) F(POC, layE) F(POC, txS) F(POC, dx) F(POC, lay_t) F(POC, ty0_t)                      \
+    S(IMAGE) F(IMAGE, x0) F(IMAGE, y1) F(IMAGE, numcomps) F(IMAGE, color_space) F(IMAGE, comps)         \
+    F(IMAGE, icc_profile_buf) F(IMAGE, icc_profile_len) F(IMAGE, capture_resolution)                  \
+    F(IMAGE, display_resolution) F(IMAGE, iptc_buf) F(IMAGE, iptc_len) F(IMAGE, xmp_buf) F(IMAGE, xmp_len) \
+    S(COMP) F(COMP, dx) F(COMP, w) F(COMP, h) F(COMP, x0) F(COMP, prec) F(COMP, sgnd) F(COMP, resno_decoded) \
+    F(COMP, data) F(COMP, owns_data) F(COMP, alpha)                                                   \
+    S(CMPTPARM) F(CMPTPARM, dx) F(CMPTPARM, w) F(CMPTPARM, x0) F(CMPTPARM, prec) F(CMPTPARM, sgnd)     \
+    S(PASS) F(PASS, distortionDecrease) F(PASS, rate) F(PASS, length)                                 \
+    S(CBLK) F(CBLK, x0) F(CBLK, y1) F(CBLK, contextStream) F(CBLK, numPix) F(CBLK, compressedData)     \
+    F(CBLK, compressedDataLength) F(CBLK, numBitPlanes) F(CBLK, numPasses) F(CBLK, passes) F(CBLK, sortedIndex) \
+    S(PREC) F(PREC, numBlocks) F(PREC, blocks)                                                        \
+    S(BAND) F(BAND, orient) F(BAND, numPrecincts) F(BAND, precincts) F(BAND, stepsize)                \
+    S(RES) F(RES, level) F(RES, numBands) F(RES, bands)                                               \
+    S(TCOMP) F(TCOMP, numResolutions) F(TCOMP, resolutions)                                           \
+    S(TILE) F(TILE, decode_flags) F(TILE, numComponents) F(TILE, tileComponents)                      \
+    S(INIT) F(INIT, deviceId) F(INIT, verbose)                                                        \
+    S(CBINFO) F(CBINFO, input_file_name) F(CBINFO, outputFileNameIsRelative) F(CBINFO, output_file_name) \
+    F(CBINFO, encoder_parameters) F(CBINFO, image) F(CBINFO, tile) F(CBINFO, error_code)              \
+    S(MINPF_REG) F(MINPF_REG, version) F(MINPF_REG, createFunc) F(MINPF_REG, destroyFunc)            \
+    S(MINPF_SVC) F(MINPF_SVC, version) F(MINPF_SVC, registerObject) F(MINPF_SVC, invokeService)
+
+#define ABI_EMIT_S(tag) {#tag, "sizeof", sizeof(T_##tag)},
+#define ABI_EMIT_F(tag, field) {#tag, #field, offsetof(T_##tag, field)},
+
+struct AbiEntry {
+    const char *type, *field;
+    size_t value;
+};

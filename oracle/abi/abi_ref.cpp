@@ -1,0 +1,22 @@
+// Layout table of the reference's plugin-boundary types (grok.h,
+// plugin/plugin_interface.h, plugin/minpf_plugin.h).  Test infrastructure.
+#include <stddef.h>
+#include "plugin/plugin_interface.h"
+#include "abi_fields.h"
+using T_CPARAMS = grk_cparameters;
+using T_POC = grk_poc;
+using T_IMAGE = grk_image;
+using T_COMP = grk_image_comp;
+using T_CMPTPARM = grk_image_cmptparm;
+using T_PASS = grk_plugin_pass;
+using T_CBLK = grk_plugin_code_block;
+using T_PREC = grk_plugin_precinct;
+using T_BAND = grk_plugin_band;
+using T_RES = grk_plugin_resolution;
+using T_TCOMP = grk_plugin_tile_component;
+using T_TILE = grk_plugin_tile;
+using T_INIT = grk_plugin_init_info;
+using T_CBINFO = grk::plugin_encode_user_callback_info;
+using T_MINPF_REG = grk::minpf_register_params;
+using T_MINPF_SVC = grk::minpf_platform_services;
+extern const AbiEntry abi_ref[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

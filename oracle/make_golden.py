@@ -99,6 +99,12 @@ CASES = [
     ("rgb12_cinema4k", (216, 384, 3, 12), "smooth", 76, ["-cinema4K", "24"]),
     ("rgb12_cinema2k", (108, 192, 3, 12), "smooth", 77, ["-cinema2K", "24"]),
     ("rgb12_cinema4k_48", (120, 256, 3, 12), "uniform", 78, ["-cinema4K", "48"]),
+    # rate control over precinct partitions / POC (plugin-tree coverage)
+    ("rgb8_prec_r20_rpcl", (150, 200, 3, 8), "smooth", 79, ["-c", "[32,32],[16,16]", "-p", "RPCL", "-r", "20,5"]),
+    ("g12_prec_r12_A1", (130, 170, 1, 12), "smooth", 80, ["-c", "[64,64],[32,32],[16,16]", "-r", "12", "-A", "1",
+                                                          "-b", "32,32"]),
+    ("rgb8_poc_r15_I", (96, 128, 3, 8), "smooth", 81, ["-I", "-r", "15,4",
+                                                       "-P", "T1=0,0,2,3,3,CPRL/T1=3,0,2,6,3,LRCP"]),
 ]
 
 # BASELINE.json configs (hash-only)

@@ -45,7 +45,7 @@ LIBSRCS := util/BufferedStream.cpp util/logger.cpp util/mem_stream.cpp util/grok
   t1/t1_part1/t1.cpp t1/t1_part1/mqc_enc.cpp t1/t1_part1/mqc_dec.cpp t1/t1_part1/T1Part1.cpp
 OBJS := $(LIBSRCS:%.cpp=$(OUT)/obj/%.o)
 
-all: $(OUT)/libgrok.so $(OUT)/ref_driver
+all: $(OUT)/libgrok.so $(OUT)/ref_driver $(OUT)/abi_check
 
 $(GEN)/grk_config.h: $(SRC)/grk_config.h.cmake.in
 	@mkdir -p $(GEN)
@@ -84,3 +84,7 @@ clean:
 	rm -rf $(OUT)
 
 .PHONY: all clean
+
+# layout check of include/grk_plugin_abi.h against the reference headers
+$(OUT)/abi_check: oracle/abi/abi_check.cpp oracle/abi/abi_ref.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_fields.h include/grk_plugin_abi.h $(GEN)/grk_config.h
+	$(CXX) -std=c++17 -O0 -w $(INC) -o $@ oracle/abi/abi_check.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_ref.cpp

@@ -25,6 +25,15 @@
 //   ref_driver enc IN.i32 OUT.j2k W H C BITS SGND [options]
 //   ref_driver dec IN.j2k OUT.i32 [-r reduce] [-l layers] [-d x0,y0,x1,y1]
 //   ref_driver bench IN.i32 W H C BITS SGND THREADS REPS [options]   (enc+dec timing)
+//   ref_driver plugin PLUGIN_DIR IN.i32 OUT.j2k W H C BITS [options]
+//       the reference host driving OUR accelerator plugin (libgrok_plugin.so in
+//       PLUGIN_DIR) exactly as grk_compress's plugin_main does
+//       (grk_compress.cpp:2163-2305 + plugin_compress_callback :1770-2161):
+//       grk_initialize(plugin_dir) -> grk_plugin_init -> grk_plugin_encode(
+//       params, cb); cb runs grk_setup_encoder -> grk_start_compress ->
+//       grk_encode_with_plugin(tile) -> grk_end_compress.  The input goes
+//       through a PGM / PPM file, the format the plugin reads.  Exit 0 iff
+//       the plugin handled the image; 3 if it declined (host CPU fallback).
 // IN.i32 / OUT.i32: planar int32 little-endian (c, h, w).  dec prints
 // "x0 y0 x1 y1 numcomps prec sgnd" of the decoded image on stdout.
 #include <grok.h>
@@ -220,15 +229,91 @@ static grk_image *decode(const uint8_t *cs, size_t len, uint32_t reduce, uint32_
     return ok ? img : nullptr;
 }
 
+// ---- plugin mode ----
+static bool g_cb_ok = false;
+static std::vector<uint8_t> g_cb_out;
+
+static bool plugin_cb(grk_plugin_encode_user_callback_info *info) {
+    grk_cparameters *p = info->encoder_parameters;
+    grk_image *img = info->image;
+    g_cb_ok = false;
+    if (!img) return false;
+    if (p->tcp_mct == 255) p->tcp_mct = img->numcomps >= 3 ? 1 : 0;        // grk_compress.cpp:1997-1998
+    if (p->rateControlAlgorithm == 255) p->rateControlAlgorithm = 0;        // :2015-2017
+    const size_t cap = (size_t)(img->x1 - img->x0) * (img->y1 - img->y0) * img->numcomps * 3 + (1 << 20);
+    uint8_t *buf = new uint8_t[cap];
+    grk_stream *st = grk_stream_create_mem_stream(buf, cap, false, false);
+    grk_codec *codec = grk_create_compress(GRK_CODEC_J2K, st);
+    grk_set_error_handler(err_cb, nullptr);
+    bool ok = codec && grk_setup_encoder(codec, p, img) && grk_start_compress(codec, img) &&
+              grk_encode_with_plugin(codec, info->tile) && grk_end_compress(codec);
+    if (ok) g_cb_out.assign(buf, buf + grk_stream_get_write_mem_stream_length(st));
+    if (codec) grk_destroy_codec(codec);
+    grk_stream_destroy(st);
+    delete[] buf;
+    g_cb_ok = ok;
+    return ok;
+}
+
+static bool write_pnm(const char *path, const int32_t *planes, uint32_t w, uint32_t h, uint32_t c, uint32_t bits) {
+    if ((c != 1 && c != 3) || bits < 8 || bits > 16) return false;
+    FILE *f = fopen(path, "wb");
+    if (!f) return false;
+    fprintf(f, "P%c\n%u %u\n%u\n", c == 1 ? '5' : '6', w, h, (1u << bits) - 1);
+    const bool one = bits <= 8;
+    std::vector<uint8_t> row((size_t)w * c * (one ? 1 : 2));
+    for (uint32_t y = 0; y < h; ++y) {
+        for (uint32_t x = 0; x < w; ++x)
+            for (uint32_t k = 0; k < c; ++k) {
+                const uint32_t v = (uint32_t)planes[(size_t)k * w * h + (size_t)y * w + x];
+                const size_t i = (size_t)x * c + k;
+                if (one) row[i] = (uint8_t)v;
+                else { row[2 * i] = (uint8_t)(v >> 8); row[2 * i + 1] = (uint8_t)v; }
+            }
+        fwrite(row.data(), 1, row.size(), f);
+    }
+    return fclose(f) == 0;
+}
+
+static int plugin_mode(int argc, char **argv) {
+    if (argc < 9) return 2;
+    const char *dir = argv[2];
+    const uint32_t w = (uint32_t)atoi(argv[5]), h = (uint32_t)atoi(argv[6]), c = (uint32_t)atoi(argv[7]);
+    const uint32_t bits = (uint32_t)atoi(argv[8]);
+    std::vector<uint8_t> in = read_file(argv[3]);
+    if (in.size() != (size_t)w * h * c * 4) { fprintf(stderr, "input size mismatch\n"); return 2; }
+    const std::string pnm = std::string(argv[4]) + (c == 1 ? ".pgm" : ".ppm");
+    if (!write_pnm(pnm.c_str(), (const int32_t *)in.data(), w, h, c, bits)) { fprintf(stderr, "pnm\n"); return 2; }
+    if (!grk_initialize(dir, 0)) { fprintf(stderr, "plugin not loaded from %s\n", dir); return 4; }
+    grk_plugin_init_info ii;
+    ii.deviceId = 0;
+    ii.verbose = getenv("GRKGPU_PLUGIN_VERBOSE") != nullptr;
+    if (!grk_plugin_init(ii)) { fprintf(stderr, "grk_plugin_init failed\n"); return 4; }
+    grk_cparameters p;
+    if (!parse_enc_opts(&p, argc - 9, argv + 9)) return 2;
+    snprintf(p.infile, sizeof(p.infile), "%s", pnm.c_str());
+    snprintf(p.outfile, sizeof(p.outfile), "%s", argv[4]);
+    p.decod_format = GRK_PXM_FMT;
+    p.cod_format = GRK_J2K_FMT;
+    const int32_t rc = grk_plugin_encode(&p, plugin_cb);
+    remove(pnm.c_str());
+    if (rc != 0) { fprintf(stderr, "plugin declined (rc %d)\n", rc); grk_deinitialize(); return 3; }
+    if (!g_cb_ok) { fprintf(stderr, "host encode with plugin tile failed\n"); grk_deinitialize(); return 1; }
+    write_file(argv[4], g_cb_out.data(), g_cb_out.size());
+    grk_deinitialize();
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
         return 2;
     }
     const std::string mode = argv[1];
+    if (mode == "plugin") return plugin_mode(argc, argv);
     if (mode == "enc" || mode == "bench") {
         const bool bench = mode == "bench";
-        const int need = bench ? 11 : 9;
+        const int need = bench ? 10 : 9;
         if (argc < need) return 2;
         int ai = bench ? 3 : 4;
         const uint32_t w = (uint32_t)atoi(argv[ai]), h = (uint32_t)atoi(argv[ai + 1]), c = (uint32_t)atoi(argv[ai + 2]);

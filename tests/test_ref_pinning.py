@@ -47,3 +47,14 @@ def test_small_fixtures_regenerate_bit_exact():
 def test_c1_config_hash_regenerates():
     out = _check("--large", "--only", "C1_512_gray8")
     assert "C1_512_gray8 ok" in out
+
+
+def test_plugin_abi_layout_matches_reference_headers():
+    """include/grk_plugin_abi.h re-declares grok.h's plugin-boundary structs;
+    oracle/abi/ compiles one offset/size table over the reference's headers
+    and one over ours and compares them field by field."""
+    subprocess.run(["make", "-s", "-f", "oracle/ref.mk", "-j8", "oracle/_ref/abi_check"], cwd=ROOT, check=True,
+                   timeout=900)
+    r = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "abi_check")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert " 0 mismatches" in r.stdout
