@@ -34,6 +34,12 @@ class ImageDesc(ctypes.Structure):
                 ("numcomps", ctypes.c_uint32), ("prec", ctypes.c_uint32 * MAXC), ("sgnd", ctypes.c_int32 * MAXC)]
 
 
+class DParams(ctypes.Structure):
+    """grkgpu_dparams (grk_dparameters subset, grok.h:694-735)."""
+    _fields_ = [("cp_reduce", ctypes.c_uint32), ("cp_layer", ctypes.c_uint32), ("DA_x0", ctypes.c_uint32),
+                ("DA_y0", ctypes.c_uint32), ("DA_x1", ctypes.c_uint32), ("DA_y1", ctypes.c_uint32)]
+
+
 class Poc(ctypes.Structure):
     """grk_poc (grok.h:393-410): grk_compress -P T<tile>=r0,c0,l1,r1,c1,PROG."""
     _fields_ = [("tile", ctypes.c_uint32), ("resno0", ctypes.c_uint32), ("compno0", ctypes.c_uint32),
@@ -208,6 +214,7 @@ def lib():
         L.grkgpu_decompress_reduced.argtypes = [VP, VP, ctypes.c_size_t, U32, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_decompress_window.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, U32, U32, P(ImageDesc), P(VP),
                                                ctypes.c_int]
+        L.grkgpu_decompress_ex.argtypes = [VP, VP, ctypes.c_size_t, P(DParams), P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_dcshift_mct_fwd.argtypes = [P(VP), U32, U32, U32, U32, P(I32), I32, I32, VP]
         L.grkgpu_mct_inv_dcshift.argtypes = [P(VP), U32, U32, U32, U32, P(U32), P(I32), I32, I32, VP]
         L.grkgpu_dwt_fwd.argtypes = [VP, VP, U32, U32, U32, U32, U32, I32, VP]
@@ -394,12 +401,13 @@ class Codec:
         _check(lib().grkgpu_decompress_tiles(self._ctx, bp, bn, tile_begin, tile_end, ptrs, 1 if on_dev else 0))
         return out
 
-    def decompress(self, buf, device_out=False, out=None, reduce=0, window=None):
+    def decompress(self, buf, device_out=False, out=None, reduce=0, window=None, layers=0):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
         device_out / out is a cuda tensor).  reduce > 0: the image at
         resolution numres-1-reduce (grk_decompress -r), ceil(x / 2^reduce)
         in every coordinate.  window = (x0, y0, x1, y1) in image coordinates:
-        only that region (grk_set_decode_area), clipped to the image."""
+        only that region (grk_set_decode_area), clipped to the image.
+        layers > 0: only the first `layers` quality layers (grk_decompress -l)."""
         if reduce and window is not None:
             # the window ABI has no reduce parameter (grkgpu_decompress_window
             # decodes at full resolution); refuse rather than mix coordinate
@@ -430,11 +438,13 @@ class Codec:
                 out = np.empty((c, h, w), dtype=np.int32)
             ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
         bp, bn, keep = _buf_ptr(buf)
-        if window is not None:
-            _check(lib().grkgpu_decompress_window(self._ctx, bp, bn, *[int(v) for v in window], None, ptrs,
-                                                  1 if on_dev else 0))
-        elif reduce:
-            _check(lib().grkgpu_decompress_reduced(self._ctx, bp, bn, reduce, None, ptrs, 1 if on_dev else 0))
+        if layers < 0:
+            raise GrkGpuError("layers must be >= 0")
+        if window is not None or reduce or layers:
+            dp = DParams(cp_reduce=reduce, cp_layer=layers)
+            if window is not None:
+                dp.DA_x0, dp.DA_y0, dp.DA_x1, dp.DA_y1 = [int(v) for v in window]
+            _check(lib().grkgpu_decompress_ex(self._ctx, bp, bn, ctypes.byref(dp), None, ptrs, 1 if on_dev else 0))
         else:
             _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
         return out

@@ -1136,9 +1136,16 @@ static uint32_t ceil_pow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t
 // meeting the window are parsed, only code-blocks whose coefficients reach it
 // are decoded (window_need), the inverse DWT runs on those tiles and MCT +
 // DC shift on the window; the output planes are the window.
+//
+// max_layers > 0: only the first max_layers quality layers are decoded
+// (grk_decompress -l, cp_layer, grok.h:703-709; tcp->num_layers_to_decode,
+// j2k.cpp:3861-3865): the packets of later layers are parsed and stepped over
+// and their passes still count toward the block's pass total
+// (T2::skip_packet_data, T2.cpp:758-819), so T1 runs those passes over the
+// 0xFF fill past the decoded bytes, exactly as the reference does.
 static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
                            int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te,
-                           uint32_t reduce = 0, const Rect *win = nullptr) {
+                           uint32_t reduce = 0, const Rect *win = nullptr, uint32_t max_layers = 0) {
     if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     double t_start = now_ms();
     CodingParams cp;
@@ -1253,8 +1260,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         uint32_t packno = 0;
         for (const auto &pk : order) {
             if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
+            const bool skip = max_layers && pk.layno >= max_layers;
             int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
-                                         base + off, tcp.csty, &packno);
+                                         base + off, tcp.csty, &packno, skip);
             if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
             off += (size_t)used;
         }
@@ -1286,6 +1294,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 } else {
                     d.len = 0;
                 }
+                // no bytes: the block stays zero (T1Part1::decode returns before
+                // t1_decode_cblk when the block has no data, T1Part1.cpp:139-140)
+                if (!d.len) d.numpasses = 0;
                 db.push_back(d);
             }, numres_dec, win ? &need : nullptr);
         }
@@ -1408,6 +1419,16 @@ extern "C" int grkgpu_decompress_window(grkgpu_ctx *c, const uint8_t *csb, size_
                                         int planes_on_device) {
     const Rect w{x0, y0, x1, y1};
     return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, 0, &w);
+}
+
+extern "C" int grkgpu_decompress_ex(grkgpu_ctx *c, const uint8_t *csb, size_t len, const grkgpu_dparams *dp,
+                                    grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device) {
+    if (!dp) return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu);
+    const bool win = dp->DA_x0 || dp->DA_y0 || dp->DA_x1 || dp->DA_y1;
+    const Rect w{dp->DA_x0, dp->DA_y0, dp->DA_x1, dp->DA_y1};
+    if (win && (dp->DA_x1 <= dp->DA_x0 || dp->DA_y1 <= dp->DA_y0)) return set_err(GRKGPU_EINVAL, "empty decode area");
+    return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, dp->cp_reduce,
+                           win ? &w : nullptr, dp->cp_layer);
 }
 
 extern "C" int grkgpu_decompress_tiles(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t tile_begin,

@@ -295,7 +295,7 @@ struct BitReader {
 }  // namespace
 
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off, uint32_t csty, uint32_t *packno) {
+                      uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data) {
     Resolution &res = tc.res[resno];
     if (layno == 0) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
@@ -368,8 +368,12 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
         // tile data is truncated to what is there (the decoder reads the
         // missing tail as the 0xFF fill), not an error
         if (off + sg.len > n) sg.len = (uint32_t)(n - off);
-        if (sg.len) sg.c->chunks.push_back({base_off + off, sg.len});
-        sg.c->seglen += sg.len;
+        // a layer beyond the decoded ones (T2::skip_packet_data, T2.cpp:
+        // 758-819): its passes still count, its bytes are stepped over
+        if (!skip_data) {
+            if (sg.len) sg.c->chunks.push_back({base_off + off, sg.len});
+            sg.c->seglen += sg.len;
+        }
         off += sg.len;
     }
     return (int64_t)off;

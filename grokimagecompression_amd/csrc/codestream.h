@@ -207,8 +207,9 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
 // POC marker segment body of `size` bytes (main or tile-part header)
 bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp);
 // returns bytes consumed or -1 (T2::read_packet_header / read_packet_data,
-// T2.cpp:314-725); csty: SOP / EPH markers; packno: SOP packet counter
+// T2.cpp:314-725); csty: SOP / EPH markers; packno: SOP packet counter;
+// skip_data: a layer beyond the decoded ones (T2::skip_packet)
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr);
+                      uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr, bool skip_data = false);
 
 }  // namespace grkgpu

@@ -258,6 +258,18 @@ bool build_tree(const grkgpu_block_info *b, uint32_t n, uint32_t numcomps, uint3
 
 using ImageCreate = grkp_image *(*)(uint32_t, grkp_image_cmptparm *, int32_t);
 using ImageDestroy = void (*)(grkp_image *);
+using CompAlloc = bool (*)(grkp_image_comp *);
+
+bool read_file(const char *path, std::vector<uint8_t> &out) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    std::unique_ptr<FILE, int (*)(FILE *)> guard(f, fclose);
+    if (fseek(f, 0, SEEK_END)) return false;
+    const long n = ftell(f);
+    if (n < 0 || fseek(f, 0, SEEK_SET)) return false;
+    out.resize((size_t)n);
+    return fread(out.data(), 1, out.size(), f) == out.size();
+}
 
 }  // namespace
 
@@ -370,8 +382,89 @@ PLUGIN_API int32_t plugin_batch_encode(const char *, const char *, grkp_cparamet
 }
 PLUGIN_API bool plugin_is_batch_complete(void) { return true; }
 PLUGIN_API void plugin_stop_batch_encode(void) {}
-PLUGIN_API int32_t plugin_decode(void *, void *) { return -1; }
-PLUGIN_API int32_t plugin_init_batch_decode(const char *, const char *, void *, void *) { return -1; }
+// grk_plugin_decode (grok.cpp:1031-1051), driven by grk_decompress's
+// plugin_main (grk_decompress.cpp:1186-1319) with its decode_callback
+// (:1336-1367).  The decode runs first, on the GPU, so that anything the
+// plugin cannot take (JP2 boxes, a single-tile request, a window at a reduced
+// resolution, a corrupt or unsupported stream) is declined with -1 before the
+// host has been called: the host then decodes on its CPU path.  Then:
+//   HEADER     the host reads the main header into its own grk_image;
+//   (plugin)   component geometry of the decoded region + the samples, in
+//              buffers of the host's allocator
+//              (grk_image_single_component_data_alloc);
+//   POST_T1    the host writes the output file (post_decode);
+//   CLEAN      the host releases stream, codec and image.
+PLUGIN_API int32_t plugin_decode(grkp_decompress_parameters *params, PLUGIN_DECODE_USER_CALLBACK cb) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx || !params || !cb) return -1;
+    auto comp_alloc = (CompAlloc)dlsym(RTLD_DEFAULT, "grk_image_single_component_data_alloc");
+    if (!comp_alloc) {
+        log("host grk_image_single_component_data_alloc not found");
+        return -1;
+    }
+    const char *infile = params->infile[0] ? params->infile : params->core.infile;
+    const char *outfile = params->outfile[0] ? params->outfile : params->core.outfile;
+    if (params->nb_tile_to_decode) {
+        log("single-tile decode (grk_get_decoded_tile) not taken; declined");
+        return -1;
+    }
+    std::vector<uint8_t> cs;
+    if (!read_file(infile, cs) || cs.size() < 4 || cs[0] != 0xFF || cs[1] != 0x4F || cs[2] != 0xFF || cs[3] != 0x51) {
+        log("input is not a raw J2K codestream; declined");
+        return -1;
+    }
+    grkgpu_image_desc d{};
+    if (grkgpu_read_header(cs.data(), cs.size(), &d)) {
+        log(grkgpu_last_error());
+        return -1;
+    }
+    const uint32_t r = params->core.cp_reduce;
+    grkgpu_dparams dp{r, params->core.cp_layer, params->DA_x0, params->DA_y0, params->DA_x1, params->DA_y1};
+    const bool win = dp.DA_x0 || dp.DA_y0 || dp.DA_x1 || dp.DA_y1;
+    // decoded region: reduced coordinates ceil(x / 2^r), or the window clipped to the image
+    auto cdiv = [r](uint32_t v) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); };
+    uint32_t x0 = cdiv(d.x0), y0 = cdiv(d.y0), x1 = cdiv(d.x1), y1 = cdiv(d.y1);
+    if (win) {
+        x0 = std::max(d.x0, dp.DA_x0); y0 = std::max(d.y0, dp.DA_y0);
+        x1 = std::min(d.x1, dp.DA_x1); y1 = std::min(d.y1, dp.DA_y1);
+        if (x1 <= x0 || y1 <= y0) return -1;
+    }
+    const uint32_t w = x1 - x0, h = y1 - y0, nc = d.numcomps;
+    std::vector<int32_t> samples((size_t)w * h * nc);
+    std::vector<int32_t *> planes(nc);
+    for (uint32_t k = 0; k < nc; ++k) planes[k] = samples.data() + (size_t)k * w * h;
+    if (grkgpu_decompress_ex(g_ctx, cs.data(), cs.size(), &dp, nullptr, planes.data(), 0)) {
+        log(grkgpu_last_error());
+        return -1;
+    }
+    PluginDecodeCallbackInfo info(infile, outfile ? outfile : "", params, GRKP_J2K_FMT, GRK_DECODE_HEADER);
+    info.deviceId = params->deviceId < 0 ? 0 : (size_t)params->deviceId;
+    int32_t rc = cb(&info);
+    if (rc == 0 && info.image && info.image->numcomps == nc) {
+        grkp_image *img = info.image;
+        if (win) {  // grk_set_decode_area's image bounds (j2k.cpp j2k_set_decode_area)
+            img->x0 = x0; img->y0 = y0; img->x1 = x1; img->y1 = y1;
+        }
+        for (uint32_t k = 0; k < nc && rc == 0; ++k) {
+            grkp_image_comp &cm = img->comps[k];
+            cm.x0 = x0; cm.y0 = y0; cm.w = w; cm.h = h;
+            if (!comp_alloc(&cm)) rc = -1;
+            else memcpy(cm.data, planes[k], (size_t)w * h * 4);
+        }
+        if (rc == 0) {
+            info.decode_flags = GRK_DECODE_POST_T1;
+            rc = cb(&info);
+        }
+    } else if (rc == 0) {
+        rc = -1;
+    }
+    info.decode_flags = GRK_PLUGIN_DECODE_CLEAN;
+    cb(&info);
+    return rc;
+}
+PLUGIN_API int32_t plugin_init_batch_decode(const char *, const char *, grkp_decompress_parameters *, void *) {
+    return -1;
+}
 PLUGIN_API int32_t plugin_batch_decode(void) { return -1; }
 PLUGIN_API void plugin_stop_batch_decode(void) {}
 PLUGIN_API void plugin_debug_mqc_next_cxd(void *, uint32_t) {}

@@ -204,6 +204,16 @@ int grkgpu_decompress_reduced(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, ui
  * meeting the window and the code-blocks reaching it are decoded. */
 int grkgpu_decompress_window(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t x0, uint32_t y0, uint32_t x1,
                              uint32_t y1, grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
+/* Decode with grk_decompress's options (grk_dparameters, grok.h:694-735):
+ * cp_reduce (-r), cp_layer (-l, 0 = all layers) and the decode area (-d,
+ * grk_set_decode_area; all four 0 = the whole image).  A window at a reduced
+ * resolution is GRKGPU_EINVAL.  img (if given) receives the decoded geometry. */
+typedef struct {
+    uint32_t cp_reduce, cp_layer;
+    uint32_t DA_x0, DA_y0, DA_x1, DA_y1;
+} grkgpu_dparams;
+int grkgpu_decompress_ex(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, const grkgpu_dparams *p,
+                         grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
 /* Decode only tiles [tile_begin, tile_end) (a tile shard; the reference's
  * tile-by-tile decode, grk_decode_tile_data / j2k.cpp decode_tiles); the
  * other tiles' samples in planes are left untouched.  Host planes are written

@@ -16,10 +16,15 @@
  *                     whose grk_encode_with_plugin skips those stages and runs
  *                     rate control + Tier-2 on the plugin's code-blocks
  *                     (TileProcessor.cpp:994-1012, plugin_bridge.cpp:144-258).
- *   plugin_decode  -> host header + Tier-2 into the plugin's code-block
- *                     buffers (plugin_bridge.cpp:24-87), then T1 + inverse DWT +
- *                     inverse MCT on the GPU into the host's image, then the
- *                     host's post-decode (grk_decompress.cpp:1336-1367).
+ *   plugin_decode  -> the whole decode (host Tier-2 of this library + T1 +
+ *                     inverse DWT + inverse MCT / DC shift on the GPU), with
+ *                     grk_decompress's -r / -l / -d; the host reads the header
+ *                     into its own image (callback, GRK_DECODE_HEADER), the
+ *                     plugin fills the samples, the host writes the output
+ *                     (GRK_DECODE_POST_T1) and releases (GRK_PLUGIN_DECODE_CLEAN)
+ *                     -- grk_decompress.cpp:1336-1367.  The host's own T2 hand-
+ *                     off (plugin_bridge.cpp:24-87) takes single-segment blocks
+ *                     only, so the plugin keeps Tier-2.
  *   batch / debug  -> "not handled" (-1 / no-ops), as the reference's stub.
  *
  * The structures that cross this boundary are re-declared here with the
@@ -31,6 +36,9 @@
 #include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
+#ifdef __cplusplus
+#include <string>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -240,6 +248,112 @@ typedef struct plugin_encode_user_callback_info {
 } plugin_encode_user_callback_info;
 typedef void (*PLUGIN_ENCODE_USER_CALLBACK)(plugin_encode_user_callback_info *info);
 
+/* ---- decode side ---- */
+enum { GRKP_UNK_FMT = 0, GRKP_J2K_FMT = 1, GRKP_JP2_FMT = 2 }; /* GRK_SUPPORTED_FILE_FMT, grok.h:98-111 */
+
+typedef struct grkp_jp2_color {     /* grk_jp2_color, grok.h:612-618 */
+    uint8_t *icc_profile_buf;
+    uint32_t icc_profile_len;
+    void *jp2_cdef;
+    void *jp2_pclr;
+    uint8_t jp2_has_colour_specification_box;
+} grkp_jp2_color;
+
+typedef struct grkp_header_info {   /* grk_header_info, grok.h:620-689 */
+    uint32_t cblockw_init, cblockh_init;
+    bool irreversible;
+    uint32_t mct;
+    uint16_t rsiz;
+    uint32_t numresolutions;
+    uint8_t csty, cblk_sty;
+    uint32_t prcw_init[GRKP_MAXRLVLS];
+    uint32_t prch_init[GRKP_MAXRLVLS];
+    uint32_t cp_tx0, cp_ty0, cp_tdx, cp_tdy, cp_tw, cp_th;
+    uint32_t tcp_numlayers;
+    uint32_t enumcs;
+    grkp_jp2_color color;
+    uint8_t *xml_data;
+    size_t xml_data_len;
+    size_t num_comments;
+    char *comment[GRKP_NUM_COMMENTS];
+    uint16_t comment_len[GRKP_NUM_COMMENTS];
+    bool isBinaryComment[GRKP_NUM_COMMENTS];
+    bool has_capture_resolution;
+    double capture_resolution[2];
+    bool has_display_resolution;
+    double display_resolution[2];
+} grkp_header_info;
+
+typedef struct grkp_dparameters {   /* grk_dparameters, grok.h:694-735 */
+    uint32_t cp_reduce;             /* grk_decompress -r */
+    uint32_t cp_layer;              /* grk_decompress -l (0 = all) */
+    char infile[GRKP_PATH_LEN];
+    char outfile[GRKP_PATH_LEN];
+    int32_t decod_format, cod_format;
+    uint32_t DA_x0, DA_x1, DA_y0, DA_y1;
+    bool m_verbose;
+    uint16_t tile_index;
+    uint32_t nb_tile_to_decode;
+    uint32_t flags;
+} grkp_dparameters;
+
+typedef struct grkp_precision {     /* grk_precision, grok.h:741-744 */
+    uint32_t prec;
+    int32_t mode;
+} grkp_precision;
+
+typedef struct grkp_decompress_parameters { /* grk_decompress_parameters, grok.h:748-795 */
+    grkp_dparameters core;
+    char infile[GRKP_PATH_LEN];
+    char outfile[GRKP_PATH_LEN];
+    int32_t decod_format;
+    uint32_t cod_format;
+    char indexfilename[GRKP_PATH_LEN];
+    uint32_t DA_x0, DA_x1, DA_y0, DA_y1; /* grk_decompress -d x0,y0,x1,y1 */
+    bool m_verbose;
+    uint16_t tile_index;
+    uint32_t nb_tile_to_decode;
+    grkp_precision *precision;
+    uint32_t nb_precision;
+    bool force_rgb, upsample, split_pnm, serialize_xml;
+    uint32_t compression;
+    int32_t compressionLevel;
+    int32_t deviceId;
+    uint32_t duration, kernelBuildOptions, repeats;
+    bool verbose;
+    uint32_t numThreads;
+} grkp_decompress_parameters;
+
+typedef int (*GRKP_INIT_DECODERS)(grkp_header_info *header_info, grkp_image *image); /* GROK_INIT_DECODERS, grok.h:1854 */
+
+#ifdef __cplusplus
+/* plugin_interface.h:86-118: what the plugin hands the host's internal decode
+ * callback (a C++ object: std::string members, built by the plugin). */
+struct PluginDecodeCallbackInfo {
+    PluginDecodeCallbackInfo(std::string input, std::string output, grkp_decompress_parameters *params,
+                             int32_t format, uint32_t flags)
+        : deviceId(0), init_decoders_func(nullptr), inputFile(input), outputFile(output), decod_format(format),
+          cod_format(GRKP_UNK_FMT), l_stream(nullptr), l_codec(nullptr), decoder_parameters(params), header_info(),
+          image(nullptr), plugin_owns_image(false), tile(nullptr), error_code(0), decode_flags(flags) {}
+    size_t deviceId;
+    GRKP_INIT_DECODERS init_decoders_func;
+    std::string inputFile;
+    std::string outputFile;
+    int32_t decod_format;
+    int32_t cod_format;
+    void *l_stream;
+    void *l_codec;
+    grkp_decompress_parameters *decoder_parameters;
+    grkp_header_info header_info;
+    grkp_image *image;
+    bool plugin_owns_image;
+    grk_plugin_tile *tile;
+    int32_t error_code;
+    uint32_t decode_flags;
+};
+typedef int32_t (*PLUGIN_DECODE_USER_CALLBACK)(PluginDecodeCallbackInfo *info);
+#endif
+
 /* Object id registered with the host (the reference stub uses "SamplePlugin",
  * Plugin.cpp:17). */
 #define GRKGPU_PLUGIN_ID "GrokMI355X"
@@ -252,9 +366,13 @@ int32_t plugin_batch_encode(const char *input_dir, const char *output_dir, grkp_
                             PLUGIN_ENCODE_USER_CALLBACK user_callback);
 bool plugin_is_batch_complete(void);
 void plugin_stop_batch_encode(void);
-int32_t plugin_decode(void *decode_parameters, void *user_callback);
-int32_t plugin_init_batch_decode(const char *input_dir, const char *output_dir, void *decode_parameters,
-                                 void *user_callback);
+#ifdef __cplusplus
+int32_t plugin_decode(grkp_decompress_parameters *decode_parameters, PLUGIN_DECODE_USER_CALLBACK user_callback);
+#else
+int32_t plugin_decode(grkp_decompress_parameters *decode_parameters, void *user_callback);
+#endif
+int32_t plugin_init_batch_decode(const char *input_dir, const char *output_dir,
+                                 grkp_decompress_parameters *decode_parameters, void *user_callback);
 int32_t plugin_batch_decode(void);
 void plugin_stop_batch_decode(void);
 /* debug hooks (plugin_interface.h:44-45; the stub's name for the first is

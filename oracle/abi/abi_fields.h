@@ -41,7 +41,25 @@
     S(CBINFO) F(CBINFO, input_file_name) F(CBINFO, outputFileNameIsRelative) F(CBINFO, output_file_name) \
     F(CBINFO, encoder_parameters) F(CBINFO, image) F(CBINFO, tile) F(CBINFO, error_code)              \
     S(MINPF_REG) F(MINPF_REG, version) F(MINPF_REG, createFunc) F(MINPF_REG, destroyFunc)            \
-    S(MINPF_SVC) F(MINPF_SVC, version) F(MINPF_SVC, registerObject) F(MINPF_SVC, invokeService)
+    S(MINPF_SVC) F(MINPF_SVC, version) F(MINPF_SVC, registerObject) F(MINPF_SVC, invokeService)            \
+    S(HINFO) F(HINFO, cblockw_init) F(HINFO, irreversible) F(HINFO, mct) F(HINFO, rsiz) F(HINFO, numresolutions) \
+    F(HINFO, csty) F(HINFO, cblk_sty) F(HINFO, prcw_init) F(HINFO, prch_init) F(HINFO, cp_tx0) F(HINFO, cp_th)   \
+    F(HINFO, tcp_numlayers) F(HINFO, enumcs) F(HINFO, color) F(HINFO, xml_data) F(HINFO, xml_data_len)        \
+    F(HINFO, num_comments) F(HINFO, comment) F(HINFO, comment_len) F(HINFO, isBinaryComment)                  \
+    F(HINFO, has_capture_resolution) F(HINFO, capture_resolution) F(HINFO, has_display_resolution)            \
+    F(HINFO, display_resolution)                                                                              \
+    S(DPARAMS) F(DPARAMS, cp_reduce) F(DPARAMS, cp_layer) F(DPARAMS, infile) F(DPARAMS, outfile)              \
+    F(DPARAMS, decod_format) F(DPARAMS, cod_format) F(DPARAMS, DA_x0) F(DPARAMS, DA_y1) F(DPARAMS, m_verbose) \
+    F(DPARAMS, tile_index) F(DPARAMS, nb_tile_to_decode) F(DPARAMS, flags)                                    \
+    S(DECOMP) F(DECOMP, core) F(DECOMP, infile) F(DECOMP, outfile) F(DECOMP, decod_format) F(DECOMP, cod_format) \
+    F(DECOMP, indexfilename) F(DECOMP, DA_x0) F(DECOMP, DA_x1) F(DECOMP, DA_y0) F(DECOMP, DA_y1)              \
+    F(DECOMP, m_verbose) F(DECOMP, tile_index) F(DECOMP, nb_tile_to_decode) F(DECOMP, precision)              \
+    F(DECOMP, nb_precision) F(DECOMP, force_rgb) F(DECOMP, serialize_xml) F(DECOMP, compression)              \
+    F(DECOMP, compressionLevel) F(DECOMP, deviceId) F(DECOMP, repeats) F(DECOMP, verbose) F(DECOMP, numThreads) \
+    S(DCBINFO) F(DCBINFO, deviceId) F(DCBINFO, init_decoders_func) F(DCBINFO, inputFile) F(DCBINFO, outputFile) \
+    F(DCBINFO, decod_format) F(DCBINFO, cod_format) F(DCBINFO, l_stream) F(DCBINFO, l_codec)                  \
+    F(DCBINFO, decoder_parameters) F(DCBINFO, header_info) F(DCBINFO, image) F(DCBINFO, plugin_owns_image)    \
+    F(DCBINFO, tile) F(DCBINFO, error_code) F(DCBINFO, decode_flags)
 
 #define ABI_EMIT_S(tag) {#tag, "sizeof", sizeof(T_##tag)},
 #define ABI_EMIT_F(tag, field) {#tag, #field, offsetof(T_##tag, field)},

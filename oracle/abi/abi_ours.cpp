@@ -18,4 +18,8 @@ using T_INIT = grk_plugin_init_info;
 using T_CBINFO = plugin_encode_user_callback_info;
 using T_MINPF_REG = minpf_register_params;
 using T_MINPF_SVC = minpf_platform_services;
+using T_HINFO = grkp_header_info;
+using T_DPARAMS = grkp_dparameters;
+using T_DECOMP = grkp_decompress_parameters;
+using T_DCBINFO = PluginDecodeCallbackInfo;
 extern const AbiEntry abi_ours[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

@@ -19,4 +19,8 @@ using T_INIT = grk_plugin_init_info;
 using T_CBINFO = grk::plugin_encode_user_callback_info;
 using T_MINPF_REG = grk::minpf_register_params;
 using T_MINPF_SVC = grk::minpf_platform_services;
+using T_HINFO = grk_header_info;
+using T_DPARAMS = grk_dparameters;
+using T_DECOMP = grk_decompress_parameters;
+using T_DCBINFO = grk::PluginDecodeCallbackInfo;
 extern const AbiEntry abi_ref[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

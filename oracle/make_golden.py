@@ -107,6 +107,35 @@ CASES = [
                                                        "-P", "T1=0,0,2,3,3,CPRL/T1=3,0,2,6,3,LRCP"]),
 ]
 
+# Reference decodes with grk_decompress options (-l layers, -r reduce), per
+# case: stored as <case>.<tag>.dec.npy, tag = the options without dashes
+# ("l1", "r1l2"), with the decoded header in the manifest under "variants".
+# Not g8_off35 -r 1: at an odd image offset the reference sizes the reduced
+# component as ceil(w / 2^r) instead of ceil(x1 / 2^r) - ceil(x0 / 2^r)
+# (27 x 31 for a 26 x 30 image) and returns uninitialised samples in the
+# extra row / column -- its output differs from run to run.
+DEC_VARIANTS = {
+    "g8_r40_20_10": [["-l", "1"], ["-l", "2"], ["-r", "1", "-l", "2"]],
+    "rgb12_r30_10_1_I": [["-l", "1"], ["-l", "2"], ["-r", "2"]],
+    "rgb8_rlcp_layers": [["-l", "1"]],
+    "rgb8_tp_L": [["-l", "2"]],
+    "g8_sop_eph": [["-l", "1"]],
+    "rgb8_poc_r15_I": [["-l", "1"]],
+    "rgb8_prec_r20_rpcl": [["-l", "1"], ["-r", "1"]],
+    "g12_prec_r12_A1": [["-r", "2"]],
+    "rgb8_128x96": [["-r", "1"]],
+    "rgb12_I": [["-r", "2"]],
+    "g8_off_tiles": [["-r", "2"]],
+    "rgb12_cinema4k": [["-r", "1"]],
+    "rgb8_prec_cprl": [["-r", "1"]],
+    "g16_I": [["-r", "3"]],
+}
+
+
+def variant_tag(args):
+    return "".join(a.lstrip("-") for a in args)
+
+
 # BASELINE.json configs (hash-only)
 LARGE = [
     ("C1_512_gray8", (512, 512, 1, 8), "smooth", 1, []),
@@ -169,6 +198,15 @@ def run_case(name, shape, kind, seed, args, tmp, keep_dir=None):
         with open(os.path.join(keep_dir, f"{name}.j2k"), "wb") as f:
             f.write(jb)
         np.save(os.path.join(keep_dir, f"{name}.dec.npy"), dec)
+    variants = {}
+    for vargs in DEC_VARIANTS.get(name, []):
+        vdec, hdr = ref_decode(jb, tmp, vargs)
+        tag = variant_tag(vargs)
+        variants[tag] = dict(args=vargs, dec_sha256=synth.image_sha256(vdec), header=list(hdr))
+        if keep_dir:
+            np.save(os.path.join(keep_dir, f"{name}.{tag}.dec.npy"), vdec)
+    if variants:
+        rec["variants"] = variants
     return rec
 
 
@@ -195,11 +233,15 @@ def main():
             rec = run_case(*case, tmp, keep_dir=keep)
             if a.check:
                 ref = committed.get(case[0])
-                same = ref is not None and all(ref[k] == rec[k] for k in ("j2k_sha256", "dec_sha256", "image_sha256"))
+                same = ref is not None and all(ref.get(k) == rec.get(k)
+                                               for k in ("j2k_sha256", "dec_sha256", "image_sha256", "variants"))
                 if not a.large and same:
                     with open(os.path.join(GOLD, f"{case[0]}.j2k"), "rb") as f:
                         same = sha(f.read()) == rec["j2k_sha256"]
                     same = same and synth.image_sha256(np.load(os.path.join(GOLD, f"{case[0]}.dec.npy"))) == rec["dec_sha256"]
+                    for tag, v in rec.get("variants", {}).items():
+                        vd = np.load(os.path.join(GOLD, f"{case[0]}.{tag}.dec.npy"))
+                        same = same and synth.image_sha256(vd) == v["dec_sha256"]
                 print(case[0], "ok" if same else "MISMATCH", flush=True)
                 bad += not same
             else:

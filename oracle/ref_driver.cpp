@@ -34,6 +34,11 @@
 //       grk_encode_with_plugin(tile) -> grk_end_compress.  The input goes
 //       through a PGM / PPM file, the format the plugin reads.  Exit 0 iff
 //       the plugin handled the image; 3 if it declined (host CPU fallback).
+//   ref_driver plugin-dec PLUGIN_DIR IN.j2k OUT.i32 [-r reduce] [-l layers] [-d x0,y0,x1,y1]
+//       grk_decompress's plugin_main (grk_decompress.cpp:1186-1319):
+//       grk_plugin_decode(params, decode_callback) with decode_callback /
+//       pre_decode / post_decode restated (:1336-1557) -- post_decode writes
+//       the planes as dec does.  Exit 0 iff the plugin decoded; 3 if declined.
 // IN.i32 / OUT.i32: planar int32 little-endian (c, h, w).  dec prints
 // "x0 y0 x1 y1 numcomps prec sgnd" of the decoded image on stdout.
 #include <grok.h>
@@ -304,6 +309,107 @@ static int plugin_mode(int argc, char **argv) {
     return 0;
 }
 
+// ---- plugin decode mode: grk_decompress's decode_callback (grk_decompress.cpp:1336-1557) ----
+static std::string g_dec_out;
+
+static int dec_pre(grk_plugin_decode_callback_info *info) {
+    grk_decompress_parameters *p = info->decoder_parameters;
+    const char *infile = info->input_file_name ? info->input_file_name : p->infile;
+    int failed = 0;
+    if (!info->l_stream) info->l_stream = grk_stream_create_mapped_file_read_stream(infile);
+    if (!info->l_stream) return 1;
+    if (!info->l_codec) {
+        info->l_codec = grk_create_decompress(GRK_CODEC_J2K, info->l_stream);
+        grk_set_error_handler(err_cb, nullptr);
+        if (!grk_setup_decoder(info->l_codec, &p->core)) failed = 1;
+    }
+    if (!failed && (info->decode_flags & GRK_DECODE_HEADER)) {
+        if (!grk_read_header(info->l_codec, &info->header_info, &info->image)) failed = 1;
+        else if (info->init_decoders_func) return info->init_decoders_func(&info->header_info, info->image);
+    }
+    if (!failed && info->decode_flags != GRK_DECODE_HEADER) {
+        if (info->tile) info->tile->decode_flags = info->decode_flags;
+        if (!grk_set_decode_area(info->l_codec, info->image, p->DA_x0, p->DA_y0, p->DA_x1, p->DA_y1) ||
+            !grk_decode(info->l_codec, info->tile, info->image) || !grk_end_decompress(info->l_codec))
+            failed = 1;
+    }
+    grk_stream_destroy(info->l_stream);
+    info->l_stream = nullptr;
+    grk_destroy_codec(info->l_codec);
+    info->l_codec = nullptr;
+    if (failed && info->image) {
+        grk_image_destroy(info->image);
+        info->image = nullptr;
+    }
+    return failed;
+}
+
+static int dec_post(grk_plugin_decode_callback_info *info) {
+    grk_image *img = info->image;
+    if (!img) return 1;
+    std::vector<int32_t> out;
+    for (uint32_t k = 0; k < img->numcomps; ++k) {
+        const grk_image_comp &cm = img->comps[k];
+        if (!cm.data) return 1;
+        out.insert(out.end(), cm.data, cm.data + (size_t)cm.w * cm.h);
+    }
+    write_file(g_dec_out.c_str(), out.data(), out.size() * 4);
+    printf("%u %u %u %u %u %u %u %u %u\n", img->x0, img->y0, img->x1, img->y1, img->numcomps, img->comps[0].prec,
+           img->comps[0].sgnd, img->comps[0].w, img->comps[0].h);
+    return 0;
+}
+
+static int32_t dec_callback(grk_plugin_decode_callback_info *info) {
+    int rc = -1;
+    if (info->decode_flags & GRK_DECODE_T1) info->init_decoders_func = nullptr;
+    if (info->decode_flags & GRK_PLUGIN_DECODE_CLEAN) {
+        if (info->l_stream) grk_stream_destroy(info->l_stream);
+        info->l_stream = nullptr;
+        if (info->l_codec) grk_destroy_codec(info->l_codec);
+        info->l_codec = nullptr;
+        if (info->image && !info->plugin_owns_image) {
+            grk_image_destroy(info->image);
+            info->image = nullptr;
+        }
+        rc = 0;
+    }
+    if (info->decode_flags & (GRK_DECODE_HEADER | GRK_DECODE_T1 | GRK_DECODE_T2)) {
+        rc = dec_pre(info);
+        if (rc) return rc;
+    }
+    if (info->decode_flags & GRK_DECODE_POST_T1) rc = dec_post(info);
+    return rc;
+}
+
+static int plugin_dec_mode(int argc, char **argv) {
+    if (argc < 5) return 2;
+    grk_decompress_parameters p;
+    memset(&p, 0, sizeof(p));
+    grk_set_default_decoder_parameters(&p.core);
+    for (int i = 5; i + 1 < argc; i += 2) {
+        std::string a = argv[i];
+        if (a == "-r") p.core.cp_reduce = (uint32_t)atoi(argv[i + 1]);
+        else if (a == "-l") p.core.cp_layer = (uint32_t)atoi(argv[i + 1]);
+        else if (a == "-d") {
+            if (sscanf(argv[i + 1], "%u,%u,%u,%u", &p.DA_x0, &p.DA_y0, &p.DA_x1, &p.DA_y1) != 4) return 2;
+        } else return 2;
+    }
+    snprintf(p.infile, sizeof(p.infile), "%s", argv[3]);
+    snprintf(p.outfile, sizeof(p.outfile), "%s", argv[4]);
+    p.decod_format = GRK_J2K_FMT;
+    p.cod_format = GRK_RAWL_FMT;
+    g_dec_out = argv[4];
+    if (!grk_initialize(argv[2], 0)) { fprintf(stderr, "plugin not loaded from %s\n", argv[2]); return 4; }
+    grk_plugin_init_info ii;
+    ii.deviceId = 0;
+    ii.verbose = getenv("GRKGPU_PLUGIN_VERBOSE") != nullptr;
+    if (!grk_plugin_init(ii)) { fprintf(stderr, "grk_plugin_init failed\n"); return 4; }
+    const int32_t rc = grk_plugin_decode(&p, dec_callback);
+    grk_deinitialize();
+    if (rc == -1) { fprintf(stderr, "plugin declined\n"); return 3; }
+    return rc ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
@@ -311,6 +417,7 @@ int main(int argc, char **argv) {
     }
     const std::string mode = argv[1];
     if (mode == "plugin") return plugin_mode(argc, argv);
+    if (mode == "plugin-dec") return plugin_dec_mode(argc, argv);
     if (mode == "enc" || mode == "bench") {
         const bool bench = mode == "bench";
         const int need = bench ? 10 : 9;

@@ -47,6 +47,26 @@ def test_decode_matches_reference(codec, name):
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
 
+VARIANTS = sorted((n, tag) for n in MAN for tag in MAN[n].get("variants", {}))
+
+
+@pytest.mark.parametrize("name,tag", VARIANTS)
+def test_decode_options_match_reference(codec, name, tag):
+    """grk_decompress -l (layers) / -r (reduce) against the reference's own
+    decode with those options (tests/golden/<case>.<tag>.dec.npy, written by
+    oracle/make_golden.py from oracle/_ref): bit-exact, 9/7 included.  -l
+    reproduces the reference's pass accounting (later layers' passes still
+    count, T2.cpp:758-819)."""
+    v = MAN[name]["variants"][tag]
+    a = v["args"]
+    reduce = int(a[a.index("-r") + 1]) if "-r" in a else 0
+    layers = int(a[a.index("-l") + 1]) if "-l" in a else 0
+    ref = np.load(f"{GOLD}/{name}.{tag}.dec.npy")
+    d = codec.decompress(open(f"{GOLD}/{name}.j2k", "rb").read(), reduce=reduce, layers=layers)
+    assert d.shape == ref.shape
+    assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
+
+
 @pytest.mark.parametrize("name", ["g8_off35", "rgb12_I", "rgb8_128x96", "rgb12_tiles_I", "g16_I", "rgb8_nomct",
                                   "g8_off_tiles"])
 def test_encode_fused_mct_dwt(codec, monkeypatch, name):

@@ -89,3 +89,67 @@ def test_plugin_encode_matches_reference(name, tmp_path):
 def test_plugin_declines(name, tmp_path):
     r, _ = _run(name, tmp_path)
     assert r.returncode == 3, r.stderr
+
+
+# ---- decode: grk_decompress's plugin_main / decode_callback over plugin_decode ----
+
+def _dec(name, tmp_path, extra=()):
+    out = tmp_path / "out.i32"
+    r = subprocess.run([DRIVER, "plugin-dec", PLUGIN_DIR, f"{GOLD}/{name}.j2k", str(out)] + list(extra),
+                       capture_output=True, text=True, timeout=120)
+    return r, out
+
+
+def _planes(r, out):
+    x0, y0, x1, y1, nc, prec, sgnd, w, h = map(int, r.stdout.split())
+    return np.fromfile(out, dtype="<i4").reshape(nc, h, w)
+
+
+DEC_CASES = ["g8_64", "g8_100x77", "g8_1x37", "g8_off35", "g8_off_tiles", "g16_128", "rgb8_128x96", "rgb8_nomct",
+             "rgb12_96x80", "g8_64_I", "rgb12_I", "rgb12_tiles_I", "g16_I", "g8_r40_20_10", "rgb12_r30_10_1_I",
+             "g12_r8_A1", "rgb8_prec_cprl", "rgb8_tp_C_cprl", "rgb8_poc", "g8_sop_eph", "rgb12_cinema4k",
+             "rgb8_poc_r15_I"]
+
+
+@pytest.mark.parametrize("name", DEC_CASES)
+def test_plugin_decode_matches_reference(name, tmp_path):
+    r, out = _dec(name, tmp_path)
+    assert r.returncode == 0, r.stderr
+    ref = np.load(f"{GOLD}/{name}.dec.npy")
+    d = _planes(r, out)
+    assert d.shape == ref.shape
+    assert np.array_equal(d, ref)
+
+
+@pytest.mark.parametrize("name,tag", sorted((n, t) for n in MAN for t in MAN[n].get("variants", {})))
+def test_plugin_decode_options_match_reference(name, tag, tmp_path):
+    """-r / -l through the host's decompress parameters (core.cp_reduce /
+    core.cp_layer) against the reference's own decode with those options."""
+    r, out = _dec(name, tmp_path, MAN[name]["variants"][tag]["args"])
+    assert r.returncode == 0, r.stderr
+    ref = np.load(f"{GOLD}/{name}.{tag}.dec.npy")
+    d = _planes(r, out)
+    assert d.shape == ref.shape
+    assert np.array_equal(d, ref)
+
+
+@pytest.mark.parametrize("name,win", [("rgb12_I", (10, 7, 60, 50)), ("g8_off_tiles", (20, 9, 170, 120)),
+                                      ("rgb8_prec_r20_rpcl", (0, 0, 33, 150))])
+def test_plugin_decode_window(name, win, tmp_path):
+    """-d x0,y0,x1,y1 (parameters DA_*, grk_set_decode_area): the window of
+    the reference's full decode."""
+    r, out = _dec(name, tmp_path, ["-d", ",".join(map(str, win))])
+    assert r.returncode == 0, r.stderr
+    m = MAN[name]
+    ox, oy = 0, 0
+    if "-d" in m["args"]:
+        ox, oy = map(int, m["args"][m["args"].index("-d") + 1].split(","))
+    ref = np.load(f"{GOLD}/{name}.dec.npy")
+    h, w = ref.shape[1:]
+    x0, y0, x1, y1 = max(win[0], ox), max(win[1], oy), min(win[2], ox + w), min(win[3], oy + h)
+    assert np.array_equal(_planes(r, out), ref[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox])
+
+
+def test_plugin_decode_declines_window_at_reduce(tmp_path):
+    r, _ = _dec("rgb12_I", tmp_path, ["-r", "1", "-d", "0,0,20,20"])
+    assert r.returncode == 3, r.stderr
