@@ -210,6 +210,8 @@ def lib():
         L.grkgpu_num_tiles.argtypes = [P(ImageDesc), P(CParams), P(U32)]
         L.grkgpu_compress_tiles.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32,
                                             P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
+        L.grkgpu_compress_tile_rows.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32, U32,
+                                                U32, P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
         L.grkgpu_decompress_tiles.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, P(VP), ctypes.c_int]
         L.grkgpu_decompress_reduced.argtypes = [VP, VP, ctypes.c_size_t, U32, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_decompress_window.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, U32, U32, P(ImageDesc), P(VP),
@@ -373,15 +375,28 @@ class Codec:
         lib().grkgpu_free(out)
         return b
 
-    def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False):
+    def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False,
+                       row0=None, height=None):
         """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
-        (plus the main header / EOC when `parts` asks for them) as bytes."""
-        d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
+        (plus the main header / EOC when `parts` asks for them) as bytes.
+        row0 / height: img holds only image rows [row0, row0 + img rows) of an
+        image `height` rows tall (a tile-row shard, grkgpu_compress_tile_rows)."""
+        if row0 is None:
+            d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
+            fn = lambda *a: lib().grkgpu_compress_tiles(*a)  # noqa: E731
+            extra = ()
+        else:
+            if height is None:
+                raise GrkGpuError("height (the full image height) is required with row0")
+            d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
+            d.y1 = offset[1] + height
+            fn = lambda *a: lib().grkgpu_compress_tile_rows(*a)  # noqa: E731
+            extra = (row0, img.shape[1])
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
-        _check(lib().grkgpu_compress_tiles(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs,
-                                           1 if on_dev else 0, tile_begin, tile_end, parts, ctypes.byref(out),
-                                           ctypes.byref(n)))
+        args = (self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0) + extra + \
+            (tile_begin, tile_end, parts, ctypes.byref(out), ctypes.byref(n))
+        _check(fn(*args))
         b = ctypes.string_at(out, n.value)
         lib().grkgpu_free(out)
         return b

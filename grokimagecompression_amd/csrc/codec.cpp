@@ -583,10 +583,13 @@ static BandNeed window_need(const TileComp &tc, const Rect &win) {
 // j2k.cpp:2088-2111) and emit [main header][their tile-parts][EOC] per `parts`.
 // export_blocks: stop after Tier-1 and hand the per-code-block results to the
 // caller instead of writing a codestream (grkgpu_encode_blocks).
+//
+// row0 / nrows: the planes hold only image rows [row0, row0 + nrows) (a tile-
+// row shard: a rank loads just the rows of its tiles); nrows = 0: all rows.
 static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                          const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen,
                          uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL,
-                         bool export_blocks = false, int force_dist = 0) {
+                         bool export_blocks = false, int force_dist = 0, uint32_t row0 = 0, uint32_t nrows = 0) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
@@ -600,7 +603,12 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     hipStream_t s = c->stream;
     double t_start = now_ms();
     const uint32_t nc = cp.numcomps, iw = cp.image.w(), ih = cp.image.h();
-    const uint64_t plane = (uint64_t)iw * ih;
+    if (nrows == 0) {
+        if (row0) return set_err(GRKGPU_EINVAL, "row0 without nrows");
+        nrows = ih;
+    }
+    if ((uint64_t)row0 + nrows > ih) return set_err(GRKGPU_EINVAL, "row range outside the image");
+    const uint64_t plane = (uint64_t)iw * nrows;  // samples per plane held by the caller
 
     // geometry for every tile of the shard, arena offsets, block table
     const uint32_t ntiles = te - tb;
@@ -622,6 +630,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         Tile &tile = tiles[t];
         tile.index = tb + t;
         tile.r = tile_rect(cp, tile.index);
+        if (tile.r.y0 - cp.image.y0 < row0 || tile.r.y1 - cp.image.y0 > row0 + nrows)
+            return set_err(GRKGPU_EINVAL, "a tile of the range lies outside the rows given");
         tile.comps.resize(nc);
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
@@ -721,7 +731,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, false);
             if (!fuse || dplan.levels.empty() || dplan.levels[0].size() == before) continue;
             DwtJob &j = dplan.levels[0].back();
-            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0);
             const bool mct3 = cp.mct && nc >= 3 && k < 3;
             for (uint32_t i = 0; i < 3; ++i) {
                 const uint32_t pk = mct3 ? i : k;
@@ -741,7 +751,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         if (fuse) break;
         PlanePtrs tsrc{}, tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
-            tsrc.p[k] = src.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0) * iw + (tile.r.x0 - cp.image.x0);
+            tsrc.p[k] = src.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0);
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
         HIPCHK(launch_dcshift_mct_fwd(tsrc, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
@@ -1094,6 +1104,25 @@ extern "C" int grkgpu_compress_tiles(grkgpu_ctx *c, const grkgpu_image_desc *img
     const uint8_t *v = nullptr;
     size_t n = 0;
     int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n, tile_begin, tile_end, parts);
+    if (rc) return rc;
+    uint8_t *o = (uint8_t *)malloc(n ? n : 1);
+    if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
+    memcpy(o, v, n);
+    *out = o;
+    *outlen = n;
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_compress_tile_rows(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                                         const int32_t *const *planes, int planes_on_device, uint32_t row0,
+                                         uint32_t nrows, uint32_t tile_begin, uint32_t tile_end, uint32_t parts,
+                                         uint8_t **out, size_t *outlen) {
+    if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    if (nrows == 0) return set_err(GRKGPU_EINVAL, "nrows must be > 0");
+    const uint8_t *v = nullptr;
+    size_t n = 0;
+    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n, tile_begin, tile_end, parts, false, 0, row0,
+                           nrows);
     if (rc) return rc;
     uint8_t *o = (uint8_t *)malloc(n ? n : 1);
     if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");

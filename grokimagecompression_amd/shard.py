@@ -3,16 +3,30 @@
 Tiles are independent through DC shift, MCT, DWT, T1 and T2, and a
 codestream is [main header][tile-parts in tile index order][EOC]
 (j2k.cpp:2088-2111, 2376-2435).  So with one process per GPU, rank r encodes
-a contiguous tile range and the tile-part bytes travel to rank 0, which
-concatenates them: no collective on the data path beyond that gather of
-compressed bytes (no RCCL reduction, no halo exchange).  Decode: every rank
-holds the codestream and decodes its own tile range.
+a contiguous tile range from just the image rows those tiles cover, and the
+tile-part bytes travel to rank 0, which concatenates them.  That gather of
+compressed bytes is the only exchange, and it runs on the HOST over a gloo
+group (data_group) even when the job's default group is NCCL (RCCL): no
+collective touches the GPU data path (north_star: "no RCCL collectives").
+Decode: every rank holds the codestream and decodes its own tile range.
 
 The encoder/decoder object only needs compress_tiles / decompress_tiles
-(grokimagecompression_amd.Codec); the group is any torch.distributed group
-(nccl on the GPU box, gloo in the CPU tests).
+(grokimagecompression_amd.Codec).
 """
 from . import PART_EOC, PART_HEADER, PART_TILES
+
+_DATA_GROUPS = {}
+
+
+def data_group(dist):
+    """The gloo group the compressed bytes travel over (created once per
+    process, collectively, on first use; the default group when that is
+    already gloo)."""
+    if dist.get_backend() == "gloo":
+        return None
+    if "gloo" not in _DATA_GROUPS:
+        _DATA_GROUPS["gloo"] = dist.new_group(backend="gloo")
+    return _DATA_GROUPS["gloo"]
 
 
 def tile_range(ntiles, rank, world):
@@ -23,33 +37,56 @@ def tile_range(ntiles, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
+def tile_rows(begin, end, image_h, tdy, ty0=0, y0=0, tw=1):
+    """Image rows [r0, r1) (relative to the image origin y0) covered by tiles
+    [begin, end) of a grid tw tiles wide with tile height tdy and origin ty0
+    (j2k tile geometry: tile row q spans [ty0 + q*tdy, ty0 + (q+1)*tdy) clipped
+    to the image)."""
+    if end <= begin:
+        return 0, 0
+    q0, q1 = begin // tw, (end - 1) // tw
+    r0 = max(y0, ty0 + q0 * tdy) - y0
+    r1 = min(y0 + image_h, ty0 + (q1 + 1) * tdy) - y0
+    return r0, r1
+
+
 def assemble(parts):
     """Concatenate per-rank payloads (rank 0 carries the main header, the last
     rank the EOC) in rank order = tile order."""
     return b"".join(parts)
 
 
-def compress_sharded(codec, img, prec, params, ntiles, dist=None, group=None, offset=(0, 0), sgnd=False):
+def compress_sharded(codec, img, prec, params, ntiles, dist=None, group=None, offset=(0, 0), sgnd=False,
+                     rows=None, height=None):
     """Encode this rank's tile range; returns the full codestream on rank 0
     (None elsewhere).  Without torch.distributed (dist=None) it is the
-    single-process path."""
-    world = dist.get_world_size(group) if dist is not None else 1
-    rank = dist.get_rank(group) if dist is not None else 0
+    single-process path.
+
+    img: the whole image, or (rows given) only this rank's rows: rows = (r0, r1)
+    of an image `height` rows tall, img holding rows [r0, r1)
+    (see tile_rows).  group: the group to gather over (default: data_group)."""
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
     b, e = tile_range(ntiles, rank, world)
     parts = PART_TILES | (PART_HEADER if rank == 0 else 0) | (PART_EOC if rank == world - 1 else 0)
-    mine = codec.compress_tiles(img, prec, params, b, e, parts, offset=offset, sgnd=sgnd)
+    if rows is None:
+        mine = codec.compress_tiles(img, prec, params, b, e, parts, offset=offset, sgnd=sgnd)
+    else:
+        mine = codec.compress_tiles(img, prec, params, b, e, parts, offset=offset, sgnd=sgnd, row0=rows[0],
+                                    height=height)
     if dist is None:
         return mine
+    g = group if group is not None else data_group(dist)
     gathered = [None] * world if rank == 0 else None
-    dist.gather_object(mine, gathered, dst=0, group=group)
+    dist.gather_object(mine, gathered, dst=0, group=g)
     return assemble(gathered) if rank == 0 else None
 
 
 def decompress_sharded(codec, buf, out, ntiles, dist=None, group=None):
     """Decode this rank's tile range of `buf` into `out` (other tiles are left
     untouched); returns the (begin, end) range decoded."""
-    world = dist.get_world_size(group) if dist is not None else 1
-    rank = dist.get_rank(group) if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
     b, e = tile_range(ntiles, rank, world)
     codec.decompress_tiles(buf, b, e, out)
     return b, e

@@ -162,6 +162,13 @@ int grkgpu_compress_tiles(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const g
                           const int32_t *const *planes, int planes_on_device, uint32_t tile_begin,
                           uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
 
+/* Same, with planes holding only image rows [row0, row0 + nrows) (relative to
+ * img->y0): a rank of a tile-row shard loads just the rows of its tiles.
+ * Every tile of [tile_begin, tile_end) must lie inside those rows. */
+int grkgpu_compress_tile_rows(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                              const int32_t *const *planes, int planes_on_device, uint32_t row0, uint32_t nrows,
+                              uint32_t tile_begin, uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
+
 /* Tier-1 only (the tile hot path of TileProcessor::encode_tile up to and
  * including t1_encode, TileProcessor.cpp:994-1012; SURVEY 8(b)
  * "grkgpu_encode_tile"): DC shift + MCT + DWT + T1 of every tile on the GPU,

@@ -4,8 +4,11 @@
   is byte-identical to the reference codestream; decompress_tiles over the
   shards reproduces the reference decoder's output (host and device planes);
 * two processes on cuda:0 (gloo for the gather of tile-part bytes): the full
-  C4 config (16384^2 16-bit, 1024^2 tiles) sharded across the ranks gives the
-  reference codestream hash, and each rank's tile-range decode is lossless.
+  C4 config (16384^2 16-bit, 1024^2 tiles) sharded across the ranks, each
+  rank generating and uploading ONLY the image rows of its tiles
+  (grkgpu_compress_tile_rows), gives the reference codestream hash, and each
+  rank's tile-range decode is lossless;
+* single process: row-slab encodes of every tiled golden equal the reference.
 """
 import hashlib
 import os
@@ -81,20 +84,20 @@ def _rank(rank, world, port, q):
     try:
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
         m = LARGE["C4_16k_gray16_tiled"]
-        img, bits = _img(m)
+        h_, w_, c_, bits = m["shape"]
         p, off = grk.CParams.from_cli(m["args"])
-        n = grk.num_tiles(img.shape, bits, p, off)
-        t = torch.from_numpy(img).cuda()
-        del img
+        n = grk.num_tiles((c_, h_, w_), bits, p, off)
+        b, e = shard.tile_range(n, rank, world)
+        r0, r1 = shard.tile_rows(b, e, h_, 1024, tw=16)
+        t = torch.from_numpy(synth.synth_plane(h_, w_, bits, m["seed"], 0, m["kind"], rows=(r0, r1))[None]).cuda()
         codec = grk.Codec(0)
-        cs = shard.compress_sharded(codec, t, bits, p, n, dist=dist, offset=off)
+        cs = shard.compress_sharded(codec, t, bits, p, n, dist=dist, offset=off, rows=(r0, r1), height=h_)
         h = hashlib.sha256(cs).hexdigest() if rank == 0 else None
         obj = [cs if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        out = torch.zeros_like(t)
-        b, e = shard.decompress_sharded(codec, obj[0], out, n, dist=dist)
-        r0, r1 = (b // 16) * 1024, ((e + 15) // 16) * 1024  # 1024^2 tiles, 16 per tile row
-        ok = bool(torch.equal(out[:, r0:r1], t[:, r0:r1])) and (e - b) % 16 == 0
+        out = torch.zeros((c_, h_, w_), dtype=torch.int32, device="cuda")
+        shard.decompress_sharded(codec, obj[0], out, n, dist=dist)
+        ok = bool(torch.equal(out[:, r0:r1], t)) and (e - b) % 16 == 0
         codec.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -119,3 +122,31 @@ def test_two_ranks_sharded_16k():
     assert all(v[2] is None for v in res.values()), res
     assert res[0][0] == LARGE["C4_16k_gray16_tiled"]["j2k_sha256"]
     assert res[0][1] and res[1][1]
+
+
+@pytest.mark.parametrize("name", TILED)
+def test_row_slab_shards_match_reference(codec, name):
+    """Each shard encoded from only the rows of its tiles
+    (grkgpu_compress_tile_rows) -- concatenated: the reference codestream."""
+    import grokimagecompression_amd as grk
+    m = MAN[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    ref = open(os.path.join(GOLD, name + ".j2k"), "rb").read()
+    n = grk.num_tiles(img.shape, bits, p, off)
+    tdx, tdy = p.cp_tdx, p.cp_tdy
+    tx0, ty0 = p.cp_tx0, p.cp_ty0
+    tw = -(-(off[0] + img.shape[2] - tx0) // tdx)
+    chunks = []
+    world = 3
+    for r in range(world):
+        b, e = shard.tile_range(n, r, world)
+        r0, r1 = shard.tile_rows(b, e, img.shape[1], tdy, ty0=ty0, y0=off[1], tw=tw)
+        parts = grk.PART_TILES | (grk.PART_HEADER if r == 0 else 0) | (grk.PART_EOC if r == world - 1 else 0)
+        chunks.append(codec.compress_tiles(np.ascontiguousarray(img[:, r0:r1]), bits, p, b, e, parts, offset=off,
+                                           row0=r0, height=img.shape[1]))
+    assert shard.assemble(chunks) == ref
+    # rows that miss a tile of the range are refused
+    with pytest.raises(grk.GrkGpuError):
+        codec.compress_tiles(np.ascontiguousarray(img[:, 1:3]), bits, p, 0, 1, grk.PART_ALL, offset=off, row0=1,
+                             height=img.shape[1])

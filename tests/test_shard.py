@@ -4,8 +4,12 @@
 * the codestream format the sharding relies on -- [main header][tile-parts in
   tile order][EOC] -- holds for the reference's own multi-tile golden
   codestreams (split at SOT/Psot, then reassembled);
+* tile_rows gives exactly the rows of a tile range (each rank loads only
+  those);
 * world_size-2 gloo run of compress_sharded / decompress_sharded with a
-  stand-in tile coder (the GPU coder is exercised by tests/test_gpu_shard.py).
+  stand-in tile coder (the GPU coder is exercised by tests/test_gpu_shard.py),
+  including a job whose default group reports NCCL: the tile-part bytes must
+  then travel over the separate gloo data group, never the default group.
 """
 import os
 import struct
@@ -59,23 +63,63 @@ def test_reference_codestream_is_header_tileparts_eoc(name):
         assert shard.assemble(chunks) == cs
 
 
+@pytest.mark.parametrize("h,tdy,ty0,y0,tw", [(150, 48, 1, 3, 4), (16384, 1024, 0, 0, 16), (100, 100, 0, 0, 1),
+                                              (77, 10, 5, 9, 3)])
+def test_tile_rows_cover_exactly(h, tdy, ty0, y0, tw):
+    th = -(-(y0 + h - ty0) // tdy)
+    ntiles = th * tw
+    for world in (1, 2, 3, 5):
+        for r in range(world):
+            b, e = shard.tile_range(ntiles, r, world)
+            r0, r1 = shard.tile_rows(b, e, h, tdy, ty0, y0, tw)
+            if b == e:
+                continue
+            want = set()
+            for t in range(b, e):
+                q = t // tw
+                lo, hi = max(y0, ty0 + q * tdy), min(y0 + h, ty0 + (q + 1) * tdy)
+                want.update(range(lo - y0, hi - y0))
+            assert (r0, r1) == (min(want), max(want) + 1)
+
+
 class FakeCoder:
     """Stand-in tile coder: tile t -> b'T<t>;', header b'H', EOC b'E'."""
 
     def __init__(self):
         self.decoded = []
 
-    def compress_tiles(self, img, prec, params, b, e, parts, offset=(0, 0), sgnd=False):
+    def compress_tiles(self, img, prec, params, b, e, parts, offset=(0, 0), sgnd=False, row0=None, height=None):
         return (b"H" if parts & 1 else b"") + b"".join(b"T%d;" % t for t in range(b, e)) + (b"E" if parts & 2 else b"")
 
     def decompress_tiles(self, buf, b, e, out):
         out.extend(range(b, e))
 
 
-def _worker(rank, world, port, ntiles, q):
+class NcclDefault:
+    """torch.distributed as a job whose default group is NCCL sees it: the
+    default group's backend reads "nccl" and a collective on the default
+    group fails; everything else is the real (gloo) module."""
+
+    def __init__(self, dist):
+        self._d = dist
+
+    def __getattr__(self, k):
+        return getattr(self._d, k)
+
+    def get_backend(self, group=None):
+        return "nccl" if group is None else self._d.get_backend(group)
+
+    def gather_object(self, obj, lst, dst=0, group=None):
+        assert group is not None, "compressed bytes gathered over the default (NCCL) group"
+        assert self._d.get_backend(group) == "gloo"
+        return self._d.gather_object(obj, lst, dst=dst, group=group)
+
+
+def _worker(rank, world, port, ntiles, q, nccl_default=False):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
-    cs = shard.compress_sharded(FakeCoder(), None, 8, None, ntiles, dist=dist)
+    d = NcclDefault(dist) if nccl_default else dist
+    cs = shard.compress_sharded(FakeCoder(), None, 8, None, ntiles, dist=d)
     dec = []
     shard.decompress_sharded(FakeCoder(), b"", dec, ntiles, dist=dist)
     q.put((rank, cs, dec))
@@ -83,12 +127,13 @@ def _worker(rank, world, port, ntiles, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("nccl_default", [False, True])
 @pytest.mark.parametrize("ntiles", [5, 256])
-def test_gloo_world2_sharded(ntiles):
+def test_gloo_world2_sharded(ntiles, nccl_default):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, ntiles, q)) for r in range(2)]
+    port = 29500 + (os.getpid() % 1000) + (7 if nccl_default else 0) + ntiles % 3
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ntiles, q, nccl_default)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (cs, dec)) for r, cs, dec in (q.get(timeout=120) for _ in procs))
