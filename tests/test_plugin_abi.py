@@ -84,7 +84,8 @@ def _register(L, rc=0):
 
 def test_exports_header_and_host_names():
     L = _load()
-    declared = set(re.findall(r"\b((?:plugin|minpf)_[a-z_]+)\s*\(", open(HDR).read()))
+    declared = set(re.findall(r"^[a-z_0-9 ]+\**\s*((?:plugin|minpf)_[a-z_]+)\s*\(", open(HDR).read(), re.M))
+    assert {"plugin_encode", "plugin_decode", "minpf_post_load_plugin"} <= declared
     for name in sorted(declared | set(HOST_NAMES)):
         assert hasattr(L, name), name
 
