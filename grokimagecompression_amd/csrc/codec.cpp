@@ -1148,6 +1148,31 @@ extern "C" int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_de
     return GRKGPU_OK;
 }
 
+extern "C" int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_header_info *hi) {
+    if (!cs || !hi) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    size_t sot = 0;
+    std::string err;
+    if (!parse_main_header(cs, len, cp, sot, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
+    memset(hi, 0, sizeof(*hi));
+    hi->cblockw_init = 1u << cp.cblkw;
+    hi->cblockh_init = 1u << cp.cblkh;
+    hi->irreversible = (uint32_t)cp.irrev;
+    hi->mct = (uint32_t)cp.mct;
+    hi->rsiz = cp.rsiz;
+    hi->numresolutions = cp.numres;
+    hi->csty = cp.csty;
+    hi->cblk_sty = cp.cblksty;
+    for (uint32_t r = 0; r < 33; ++r) {
+        hi->prcw_init[r] = 1u << cp.prcw[r];
+        hi->prch_init[r] = 1u << cp.prch[r];
+    }
+    hi->tx0 = cp.tx0; hi->ty0 = cp.ty0; hi->tdx = cp.tdx; hi->tdy = cp.tdy; hi->tw = cp.tw; hi->th = cp.th;
+    hi->numlayers = cp.numlayers;
+    hi->prog = cp.prog;
+    return GRKGPU_OK;
+}
+
 static uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
 static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
 

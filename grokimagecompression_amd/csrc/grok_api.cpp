@@ -1,0 +1,708 @@
+// libgrok.so: Grok's public grk_* C API (include/grk_api.h) over the MI355X
+// path (grk_mi355x.h).  A drop-in for the reference's libgrok under
+// grk_compress / grk_decompress; host code only.
+//
+// Reference behaviour followed (file:line of /root/reference/src/lib/jp2):
+//   grok.cpp:152-170 initialize, :342-347 / :518-544 default parameters,
+//   :381-466 decode calls, :470-592 compress calls, :620-800 streams and
+//   images; BufferedStream.cpp (mem / file streams); codestream/j2k.cpp
+//   j2k_read_header (image from SIZ), j2k_set_decode_area (window clip and
+//   image bounds), j2k_decode (cp_reduce / cp_layer).
+#include "../../include/grk_api.h"
+#include "../../include/grk_mi355x.h"
+
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#define GRK_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+// ---- messages ----
+struct Handler {
+    grk_msg_callback cb = nullptr;
+    void *user = nullptr;
+};
+Handler g_info, g_warn, g_err;
+
+void emit(const Handler &h, const char *fmt, ...) {
+    if (!h.cb) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf) - 1, fmt, ap);
+    va_end(ap);
+    strcat(buf, "\n");
+    h.cb(buf, h.user);
+}
+#define GRK_ERROR(...) emit(g_err, __VA_ARGS__)
+
+// ---- the GPU context: one per device, created on first use ----
+std::mutex g_mu;
+std::vector<grkgpu_ctx *> g_ctx;
+
+grkgpu_ctx *ctx_for(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (device < 0) device = 0;
+    if ((size_t)device >= g_ctx.size()) g_ctx.resize(device + 1, nullptr);
+    if (!g_ctx[device] && grkgpu_create(device, &g_ctx[device]) != GRKGPU_OK) {
+        GRK_ERROR("MI355X context on device %d: %s", device, grkgpu_last_error());
+        g_ctx[device] = nullptr;
+    }
+    return g_ctx[device];
+}
+
+// ---- streams (BufferedStream semantics for the calls the codec makes:
+// sequential read to the end, sequential write) ----
+struct MemBuf {
+    uint8_t *buf = nullptr;
+    size_t len = 0, off = 0, high = 0;
+    bool owns = false;
+    void *map = nullptr;  // mapped file (munmap on free)
+};
+
+size_t mem_read(void *dst, size_t n, void *u) {
+    MemBuf *m = (MemBuf *)u;
+    const size_t k = std::min(n, m->len - std::min(m->off, m->len));
+    if (!k) return (size_t)-1;  // end of stream (BufferedStream's convention)
+    memcpy(dst, m->buf + m->off, k);
+    m->off += k;
+    return k;
+}
+size_t mem_write(void *src, size_t n, void *u) {
+    MemBuf *m = (MemBuf *)u;
+    if (m->off + n > m->len) return (size_t)-1;
+    memcpy(m->buf + m->off, src, n);
+    m->off += n;
+    m->high = std::max(m->high, m->off);
+    return n;
+}
+bool mem_seek(uint64_t pos, void *u) {
+    MemBuf *m = (MemBuf *)u;
+    if (pos > m->len) return false;
+    m->off = (size_t)pos;
+    return true;
+}
+void mem_free(void *u) {
+    MemBuf *m = (MemBuf *)u;
+    if (m->map) munmap(m->map, m->len);
+    else if (m->owns) delete[] m->buf;
+    delete m;
+}
+size_t file_read(void *dst, size_t n, void *u) {
+    const size_t k = fread(dst, 1, n, (FILE *)u);
+    return k ? k : (size_t)-1;
+}
+size_t file_write(void *src, size_t n, void *u) { return fwrite(src, 1, n, (FILE *)u); }
+bool file_seek(uint64_t pos, void *u) { return fseeko((FILE *)u, (off_t)pos, SEEK_SET) == 0; }
+void file_free(void *u) { fclose((FILE *)u); }
+
+struct Stream {
+    bool input = true;
+    size_t buffer_size = 0;
+    grk_stream_read_fn read = nullptr;
+    grk_stream_zero_copy_read_fn zc_read = nullptr;
+    grk_stream_write_fn write = nullptr;
+    grk_stream_seek_fn seek = nullptr;
+    void *user = nullptr;
+    grk_stream_free_user_data_fn free_user = nullptr;
+    uint64_t user_len = 0;
+    MemBuf *mem = nullptr;  // set for memory / mapped streams
+
+    bool read_all(std::vector<uint8_t> &out) {
+        if (mem) {  // the whole buffer, no copy through callbacks
+            out.assign(mem->buf + std::min(mem->off, mem->len), mem->buf + mem->len);
+            mem->off = mem->len;
+            return true;
+        }
+        if (!read) return false;
+        out.clear();
+        std::vector<uint8_t> chunk(std::max<size_t>(buffer_size, 1 << 20));
+        for (;;) {
+            const size_t k = read(chunk.data(), chunk.size(), user);
+            if (k == (size_t)-1 || k == 0) break;
+            out.insert(out.end(), chunk.data(), chunk.data() + k);
+        }
+        return true;
+    }
+    bool write_all(const uint8_t *p, size_t n) {
+        if (!write) return false;
+        while (n) {
+            const size_t k = write((void *)p, n, user);
+            if (k == (size_t)-1 || k == 0) return false;
+            p += k;
+            n -= k;
+        }
+        return true;
+    }
+};
+
+// ---- codecs ----
+struct Codec {
+    bool decompressor = false;
+    Stream *stream = nullptr;
+    // compress
+    grk_cparameters cparams{};
+    grk_image *image = nullptr;
+    bool setup = false;
+    // decompress
+    grk_dparameters dparams{};
+    std::vector<uint8_t> cs;
+    bool have_header = false;
+    grkgpu_image_desc desc{};
+    grkgpu_header_info hinfo{};
+    bool window = false;
+    uint32_t win[4] = {0, 0, 0, 0};
+};
+
+uint32_t cdivpow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); }
+
+// grk_cparameters -> grkgpu_cparams (j2k_setup_encoder's reading of them,
+// codestream/j2k.cpp:1609-2050); false for options outside grk_mi355x.h
+bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p) {
+    grkgpu_default_cparams(p);
+    if (g->cblk_sty) { GRK_ERROR("code-block mode switches (cblk_sty %u) are not supported", g->cblk_sty); return false; }
+    if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
+    if (g->roi_compno >= 0) { GRK_ERROR("ROI is not supported"); return false; }
+    if (g->tcp_mct == 2 || g->mct_data) { GRK_ERROR("custom MCT is not supported"); return false; }
+    if (g->subsampling_dx != 1 || g->subsampling_dy != 1) { GRK_ERROR("subsampling is not supported"); return false; }
+    p->numresolution = g->numresolution;
+    p->cblockw_init = g->cblockw_init;
+    p->cblockh_init = g->cblockh_init;
+    p->irreversible = g->irreversible ? 1 : 0;
+    p->tcp_mct = g->tcp_mct == 255 ? -1 : (g->tcp_mct && numcomps >= 3 ? 1 : 0);
+    p->tile_size_on = g->tile_size_on ? 1 : 0;
+    p->cp_tdx = g->cp_tdx;
+    p->cp_tdy = g->cp_tdy;
+    p->cp_tx0 = g->cp_tx0;
+    p->cp_ty0 = g->cp_ty0;
+    p->tcp_numlayers = g->tcp_numlayers;
+    for (int i = 0; i < 100; ++i) {
+        p->tcp_rates[i] = g->tcp_rates[i];
+        p->tcp_distoratio[i] = g->tcp_distoratio[i];
+    }
+    p->cp_disto_alloc = (int32_t)g->cp_disto_alloc;
+    p->cp_fixed_quality = (int32_t)g->cp_fixed_quality;
+    // TileProcessor::rate_allocate_encode (TileProcessor.cpp:1661-1677): 0 bisect, anything else feasible
+    p->rate_control_algorithm = g->rateControlAlgorithm == 0 ? 0 : 1;
+    p->csty = g->csty;
+    p->res_spec = g->res_spec;
+    for (int i = 0; i < 33; ++i) {
+        p->prcw_init[i] = g->prcw_init[i];
+        p->prch_init[i] = g->prch_init[i];
+    }
+    p->prog_order = g->prog_order;
+    p->numpocs = g->numpocs > 32 ? 32 : g->numpocs;
+    for (uint32_t i = 0; i < p->numpocs; ++i)
+        p->POC[i] = {g->POC[i].tile, g->POC[i].resno0, g->POC[i].compno0, g->POC[i].layno1, g->POC[i].resno1,
+                     g->POC[i].compno1, g->POC[i].prg1};
+    p->tp_on = g->tp_on;
+    p->tp_flag = g->tp_flag;
+    p->rsiz = g->rsiz;
+    p->framerate = g->framerate > 0 ? (uint32_t)g->framerate : 0;
+    p->max_cs_size = g->max_cs_size;
+    p->max_comp_size = g->max_comp_size;
+    return true;
+}
+
+bool image_desc(const grk_image *img, grkgpu_image_desc *d) {
+    if (!img || !img->comps || img->numcomps == 0 || img->numcomps > GRKGPU_MAX_COMPS) {
+        GRK_ERROR("image: 1..%d components required", GRKGPU_MAX_COMPS);
+        return false;
+    }
+    memset(d, 0, sizeof(*d));
+    d->x0 = img->x0; d->y0 = img->y0; d->x1 = img->x1; d->y1 = img->y1;
+    d->numcomps = img->numcomps;
+    for (uint32_t k = 0; k < img->numcomps; ++k) {
+        const grk_image_comp &c = img->comps[k];
+        if (c.dx != 1 || c.dy != 1) { GRK_ERROR("component %u is subsampled: not supported", k); return false; }
+        if (c.w != img->x1 - img->x0 || c.h != img->y1 - img->y0) {
+            GRK_ERROR("component %u size differs from the image", k);
+            return false;
+        }
+        if (!c.data) { GRK_ERROR("component %u has no data", k); return false; }
+        d->prec[k] = c.prec;
+        d->sgnd[k] = (int32_t)c.sgnd;
+    }
+    return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// library
+// ---------------------------------------------------------------------------
+GRK_EXPORT const char *grk_version(void) { return "5.1.0"; }
+
+GRK_EXPORT bool grk_initialize(const char *, uint32_t) { return false; }  // "plugin loaded" (grok.cpp:152-160): none
+
+GRK_EXPORT void grk_deinitialize(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &c : g_ctx)
+        if (c) { grkgpu_destroy(c); c = nullptr; }
+}
+
+// ---------------------------------------------------------------------------
+// images (image.cpp grk_image_create / grok.cpp:760-797)
+// ---------------------------------------------------------------------------
+GRK_EXPORT void grk_image_single_component_data_free(grk_image_comp *comp) {
+    if (!comp || !comp->data || !comp->owns_data) return;
+    free(comp->data);
+    comp->data = nullptr;
+    comp->owns_data = false;
+}
+
+GRK_EXPORT bool grk_image_single_component_data_alloc(grk_image_comp *comp) {
+    if (!comp) return false;
+    const size_t n = (size_t)comp->w * comp->h * sizeof(int32_t);
+    void *p = nullptr;
+    if (posix_memalign(&p, 64, n ? n : 64)) return false;
+    grk_image_single_component_data_free(comp);
+    comp->data = (int32_t *)p;
+    comp->owns_data = true;
+    return true;
+}
+
+GRK_EXPORT void grk_image_all_components_data_free(grk_image *image) {
+    if (!image || !image->comps) return;
+    for (uint32_t k = 0; k < image->numcomps; ++k) grk_image_single_component_data_free(image->comps + k);
+}
+
+GRK_EXPORT grk_image *grk_image_create(uint32_t numcmpts, grk_image_cmptparm *cmptparms, GRK_COLOR_SPACE clrspc) {
+    if (!numcmpts || !cmptparms) return nullptr;
+    grk_image *img = (grk_image *)calloc(1, sizeof(grk_image));
+    if (!img) return nullptr;
+    img->color_space = clrspc;
+    img->numcomps = numcmpts;
+    img->comps = (grk_image_comp *)calloc(numcmpts, sizeof(grk_image_comp));
+    if (!img->comps) { free(img); return nullptr; }
+    for (uint32_t k = 0; k < numcmpts; ++k) {
+        grk_image_comp &c = img->comps[k];
+        const grk_image_cmptparm &p = cmptparms[k];
+        c.dx = p.dx; c.dy = p.dy; c.w = p.w; c.h = p.h; c.x0 = p.x0; c.y0 = p.y0;
+        c.prec = p.prec; c.sgnd = p.sgnd;
+        if (!grk_image_single_component_data_alloc(&c)) {
+            grk_image_all_components_data_free(img);
+            free(img->comps);
+            free(img);
+            return nullptr;
+        }
+        memset(c.data, 0, (size_t)c.w * c.h * 4);
+    }
+    return img;
+}
+
+GRK_EXPORT void grk_image_destroy(grk_image *image) {
+    if (!image) return;
+    grk_image_all_components_data_free(image);
+    free(image->comps);
+    free(image->icc_profile_buf);
+    free(image->iptc_buf);
+    free(image->xmp_buf);
+    free(image);
+}
+
+GRK_EXPORT uint8_t *grk_buffer_new(size_t len) { return new uint8_t[len]; }
+GRK_EXPORT void grk_buffer_delete(uint8_t *buffer) { delete[] buffer; }
+
+// ---------------------------------------------------------------------------
+// streams
+// ---------------------------------------------------------------------------
+GRK_EXPORT grk_stream *grk_stream_create(size_t buffer_size, bool is_input) {
+    Stream *s = new Stream();
+    s->input = is_input;
+    s->buffer_size = buffer_size;
+    return (grk_stream *)s;
+}
+
+GRK_EXPORT void grk_stream_destroy(grk_stream *stream) {
+    Stream *s = (Stream *)stream;
+    if (!s) return;
+    if (s->free_user && s->user) s->free_user(s->user);
+    delete s;
+}
+
+GRK_EXPORT void grk_stream_set_read_function(grk_stream *stream, grk_stream_read_fn fn) {
+    if (stream && ((Stream *)stream)->input) ((Stream *)stream)->read = fn;
+}
+GRK_EXPORT void grk_stream_set_zero_copy_read_function(grk_stream *stream, grk_stream_zero_copy_read_fn fn) {
+    if (stream && ((Stream *)stream)->input) ((Stream *)stream)->zc_read = fn;
+}
+GRK_EXPORT void grk_stream_set_write_function(grk_stream *stream, grk_stream_write_fn fn) {
+    if (stream && !((Stream *)stream)->input) ((Stream *)stream)->write = fn;
+}
+GRK_EXPORT void grk_stream_set_seek_function(grk_stream *stream, grk_stream_seek_fn fn) {
+    if (stream) ((Stream *)stream)->seek = fn;
+}
+GRK_EXPORT void grk_stream_set_user_data(grk_stream *stream, void *data, grk_stream_free_user_data_fn fn) {
+    if (!stream) return;
+    ((Stream *)stream)->user = data;
+    ((Stream *)stream)->free_user = fn;
+}
+GRK_EXPORT void grk_stream_set_user_data_length(grk_stream *stream, uint64_t len) {
+    if (stream) ((Stream *)stream)->user_len = len;
+}
+
+GRK_EXPORT grk_stream *grk_stream_create_mem_stream(uint8_t *buf, size_t len, bool owns, bool is_read) {
+    if (!buf || !len) return nullptr;
+    Stream *s = (Stream *)grk_stream_create(len, is_read);
+    MemBuf *m = new MemBuf();
+    m->buf = buf;
+    m->len = len;
+    m->owns = owns;
+    s->mem = m;
+    s->user = m;
+    s->free_user = mem_free;
+    s->user_len = len;
+    if (is_read) s->read = mem_read;
+    else s->write = mem_write;
+    s->seek = mem_seek;
+    return (grk_stream *)s;
+}
+
+GRK_EXPORT size_t grk_stream_get_write_mem_stream_length(grk_stream *stream) {
+    Stream *s = (Stream *)stream;
+    return s && s->mem && !s->input ? s->mem->high : 0;
+}
+
+GRK_EXPORT grk_stream *grk_stream_create_file_stream(const char *fname, size_t buffer_size, bool is_read) {
+    if (!fname) return nullptr;
+    FILE *f = fopen(fname, is_read ? "rb" : "wb");
+    if (!f) return nullptr;
+    Stream *s = (Stream *)grk_stream_create(buffer_size, is_read);
+    s->user = f;
+    s->free_user = file_free;
+    if (is_read) {
+        s->read = file_read;
+        struct stat st;
+        if (fstat(fileno(f), &st) == 0) s->user_len = (uint64_t)st.st_size;
+    } else {
+        s->write = file_write;
+    }
+    s->seek = file_seek;
+    return (grk_stream *)s;
+}
+
+GRK_EXPORT grk_stream *grk_stream_create_mapped_file_read_stream(const char *fname) {
+    if (!fname) return nullptr;
+    const int fd = open(fname, O_RDONLY);
+    if (fd < 0) return nullptr;
+    struct stat st;
+    if (fstat(fd, &st) || st.st_size <= 0) { close(fd); return nullptr; }
+    void *p = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return nullptr;
+    Stream *s = (Stream *)grk_stream_create((size_t)st.st_size, true);
+    MemBuf *m = new MemBuf();
+    m->buf = (uint8_t *)p;
+    m->len = (size_t)st.st_size;
+    m->map = p;
+    s->mem = m;
+    s->user = m;
+    s->free_user = mem_free;
+    s->read = mem_read;
+    s->seek = mem_seek;
+    s->user_len = m->len;
+    return (grk_stream *)s;
+}
+
+// ---------------------------------------------------------------------------
+// messages
+// ---------------------------------------------------------------------------
+GRK_EXPORT bool grk_set_info_handler(grk_msg_callback cb, void *u) { g_info = {cb, u}; return true; }
+GRK_EXPORT bool grk_set_warning_handler(grk_msg_callback cb, void *u) { g_warn = {cb, u}; return true; }
+GRK_EXPORT bool grk_set_error_handler(grk_msg_callback cb, void *u) { g_err = {cb, u}; return true; }
+
+// ---------------------------------------------------------------------------
+// decompression
+// ---------------------------------------------------------------------------
+GRK_EXPORT grk_codec *grk_create_decompress(GRK_CODEC_FORMAT format, grk_stream *stream) {
+    if (format != GRK_CODEC_J2K) { GRK_ERROR("only raw J2K codestreams are supported (no JP2)"); return nullptr; }
+    if (!stream) return nullptr;
+    Codec *c = new Codec();
+    c->decompressor = true;
+    c->stream = (Stream *)stream;
+    grk_set_default_decoder_parameters(&c->dparams);
+    return (grk_codec *)c;
+}
+
+GRK_EXPORT void grk_destroy_codec(grk_codec *codec) { delete (Codec *)codec; }
+
+GRK_EXPORT void grk_set_default_decoder_parameters(grk_dparameters *p) {
+    if (p) memset(p, 0, sizeof(*p));
+}
+
+GRK_EXPORT bool grk_setup_decoder(grk_codec *codec, grk_dparameters *p) {
+    Codec *c = (Codec *)codec;
+    if (!c || !p) return false;
+    if (!c->decompressor) { GRK_ERROR("Codec provided to grk_setup_decoder is not a decompressor handler."); return false; }
+    c->dparams = *p;
+    return true;
+}
+
+// j2k_read_header: the image from SIZ (grid coordinates, one component per
+// SIZ entry, no sample buffers yet) + the main header's coding parameters
+GRK_EXPORT bool grk_read_header(grk_codec *codec, grk_header_info *hi, grk_image **image) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !image) return false;
+    if (!c->have_header) {
+        if (!c->stream->read_all(c->cs) || c->cs.empty()) { GRK_ERROR("empty stream"); return false; }
+        if (grkgpu_read_header(c->cs.data(), c->cs.size(), &c->desc) ||
+            grkgpu_read_header_info(c->cs.data(), c->cs.size(), &c->hinfo)) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
+        c->have_header = true;
+    }
+    if (c->dparams.cp_reduce >= c->hinfo.numresolutions) {  // j2k.cpp:6994
+        GRK_ERROR("Error decoding component: the number of resolutions to remove is higher than the number of "
+                  "resolutions of this component");
+        return false;
+    }
+    const grkgpu_image_desc &d = c->desc;
+    grk_image *img = (grk_image *)calloc(1, sizeof(grk_image));
+    img->comps = (grk_image_comp *)calloc(d.numcomps, sizeof(grk_image_comp));
+    img->numcomps = d.numcomps;
+    img->x0 = d.x0; img->y0 = d.y0; img->x1 = d.x1; img->y1 = d.y1;
+    img->color_space = GRK_CLRSPC_UNKNOWN;  // a raw codestream carries none (JP2 colr box)
+    const uint32_t r = c->dparams.cp_reduce;
+    for (uint32_t k = 0; k < d.numcomps; ++k) {
+        grk_image_comp &cp = img->comps[k];
+        cp.dx = cp.dy = 1;
+        cp.prec = d.prec[k];
+        cp.sgnd = (uint32_t)d.sgnd[k];
+        cp.x0 = cdivpow2(d.x0, r);
+        cp.y0 = cdivpow2(d.y0, r);
+        cp.w = cdivpow2(d.x1, r) - cp.x0;
+        cp.h = cdivpow2(d.y1, r) - cp.y0;
+    }
+    *image = img;
+    if (hi) {
+        memset(hi, 0, sizeof(*hi));
+        const grkgpu_header_info &h = c->hinfo;
+        hi->cblockw_init = h.cblockw_init;
+        hi->cblockh_init = h.cblockh_init;
+        hi->irreversible = h.irreversible != 0;
+        hi->mct = h.mct;
+        hi->rsiz = (uint16_t)h.rsiz;
+        hi->numresolutions = h.numresolutions;
+        hi->csty = (uint8_t)h.csty;
+        hi->cblk_sty = (uint8_t)h.cblk_sty;
+        for (int i = 0; i < 33; ++i) { hi->prcw_init[i] = h.prcw_init[i]; hi->prch_init[i] = h.prch_init[i]; }
+        hi->cp_tx0 = h.tx0; hi->cp_ty0 = h.ty0; hi->cp_tdx = h.tdx; hi->cp_tdy = h.tdy;
+        hi->cp_tw = h.tw; hi->cp_th = h.th;
+        hi->tcp_numlayers = h.numlayers;
+    }
+    return true;
+}
+
+// j2k_set_decode_area: all zero = the whole image; else the area clipped to
+// the image becomes the image (and component) bounds
+GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t x0, uint32_t y0, uint32_t x1,
+                                    uint32_t y1) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header || !image) return false;
+    if (!x0 && !y0 && !x1 && !y1) {
+        c->window = false;
+        return true;
+    }
+    const grkgpu_image_desc &d = c->desc;
+    if (x0 >= d.x1 || y0 >= d.y1 || x1 <= d.x0 || y1 <= d.y0 || x1 <= x0 || y1 <= y0) {
+        GRK_ERROR("decode area (%u,%u,%u,%u) outside the image", x0, y0, x1, y1);
+        return false;
+    }
+    if (c->dparams.cp_reduce) {
+        GRK_ERROR("a decode area at a reduced resolution is not supported");
+        return false;
+    }
+    c->window = true;
+    c->win[0] = std::max(x0, d.x0); c->win[1] = std::max(y0, d.y0);
+    c->win[2] = std::min(x1, d.x1); c->win[3] = std::min(y1, d.y1);
+    image->x0 = c->win[0]; image->y0 = c->win[1]; image->x1 = c->win[2]; image->y1 = c->win[3];
+    for (uint32_t k = 0; k < image->numcomps; ++k) {
+        grk_image_comp &cp = image->comps[k];
+        cp.x0 = c->win[0]; cp.y0 = c->win[1];
+        cp.w = c->win[2] - c->win[0];
+        cp.h = c->win[3] - c->win[1];
+    }
+    return true;
+}
+
+GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header || !image || image->numcomps != c->desc.numcomps) return false;
+    grkgpu_ctx *ctx = ctx_for(0);
+    if (!ctx) return false;
+    std::vector<int32_t *> planes(image->numcomps);
+    for (uint32_t k = 0; k < image->numcomps; ++k) {
+        if (!grk_image_single_component_data_alloc(&image->comps[k])) return false;
+        planes[k] = image->comps[k].data;
+    }
+    grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
+    if (c->window) { dp.DA_x0 = c->win[0]; dp.DA_y0 = c->win[1]; dp.DA_x1 = c->win[2]; dp.DA_y1 = c->win[3]; }
+    if (grkgpu_decompress_ex(ctx, c->cs.data(), c->cs.size(), &dp, nullptr, planes.data(), 0)) {
+        GRK_ERROR("%s", grkgpu_last_error());
+        return false;
+    }
+    for (uint32_t k = 0; k < image->numcomps; ++k)
+        image->comps[k].resno_decoded = c->hinfo.numresolutions - 1 - c->dparams.cp_reduce;
+    return true;
+}
+
+// one tile (j2k_get_tile): the tile's rectangle decoded as a window
+GRK_EXPORT bool grk_get_decoded_tile(grk_codec *codec, grk_image *image, uint16_t tile_index) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header || !image) return false;
+    const grkgpu_header_info &h = c->hinfo;
+    if (tile_index >= h.tw * h.th) { GRK_ERROR("tile index %u out of range", tile_index); return false; }
+    const grkgpu_image_desc &d = c->desc;
+    const uint32_t p = tile_index % h.tw, q = tile_index / h.tw;
+    const uint32_t x0 = std::max(d.x0, h.tx0 + p * h.tdx), y0 = std::max(d.y0, h.ty0 + q * h.tdy);
+    const uint32_t x1 = std::min(d.x1, h.tx0 + (p + 1) * h.tdx), y1 = std::min(d.y1, h.ty0 + (q + 1) * h.tdy);
+    return grk_set_decode_area(codec, image, x0, y0, x1, y1) && grk_decode(codec, nullptr, image);
+}
+
+GRK_EXPORT bool grk_end_decompress(grk_codec *codec) { return codec && ((Codec *)codec)->decompressor; }
+
+GRK_EXPORT bool grk_read_tile_header(grk_codec *, uint16_t *, uint64_t *, uint32_t *, uint32_t *, uint32_t *,
+                                     uint32_t *, uint32_t *, bool *) {
+    GRK_ERROR("tile-by-tile decoding (grk_read_tile_header) is not provided; use grk_decode or grk_get_decoded_tile");
+    return false;
+}
+GRK_EXPORT bool grk_decode_tile_data(grk_codec *, uint16_t, uint8_t *, uint64_t) {
+    GRK_ERROR("tile-by-tile decoding (grk_decode_tile_data) is not provided");
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// compression
+// ---------------------------------------------------------------------------
+GRK_EXPORT grk_codec *grk_create_compress(GRK_CODEC_FORMAT format, grk_stream *stream) {
+    if (format != GRK_CODEC_J2K) { GRK_ERROR("only raw J2K codestreams are supported (no JP2)"); return nullptr; }
+    if (!stream) return nullptr;
+    Codec *c = new Codec();
+    c->stream = (Stream *)stream;
+    return (grk_codec *)c;
+}
+
+GRK_EXPORT void grk_set_default_encoder_parameters(grk_cparameters *p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->numresolution = 6;       // GRK_COMP_PARAM_DEFAULT_NUMRESOLUTION
+    p->cblockw_init = 64;       // GRK_COMP_PARAM_DEFAULT_CBLOCKW / H
+    p->cblockh_init = 64;
+    p->prog_order = 0;          // GRK_LRCP
+    p->roi_compno = -1;
+    p->subsampling_dx = 1;
+    p->subsampling_dy = 1;
+    p->numThreads = (uint32_t)std::max<long>(1, sysconf(_SC_NPROCESSORS_ONLN));
+    p->deviceId = 0;
+    p->repeats = 1;
+}
+
+GRK_EXPORT bool grk_setup_encoder(grk_codec *codec, grk_cparameters *p, grk_image *image) {
+    Codec *c = (Codec *)codec;
+    if (!c || c->decompressor || !p || !image) return false;
+    grkgpu_cparams tmp;
+    if (!map_cparams(p, image->numcomps, &tmp)) return false;
+    c->cparams = *p;
+    c->image = image;
+    c->setup = true;
+    return true;
+}
+
+GRK_EXPORT bool grk_start_compress(grk_codec *codec, grk_image *image) {
+    Codec *c = (Codec *)codec;
+    if (!c || c->decompressor || !c->setup) return false;
+    if (image) c->image = image;
+    return c->image != nullptr;
+}
+
+GRK_EXPORT bool grk_encode_with_plugin(grk_codec *codec, grk_plugin_tile *tile) {
+    Codec *c = (Codec *)codec;
+    if (!c || c->decompressor || !c->setup || !c->image) return false;
+    if (tile) { GRK_ERROR("plugin tiles are not taken by this library"); return false; }
+    grkgpu_image_desc d;
+    grkgpu_cparams p;
+    if (!image_desc(c->image, &d) || !map_cparams(&c->cparams, d.numcomps, &p)) return false;
+    grkgpu_ctx *ctx = ctx_for(c->cparams.deviceId);
+    if (!ctx) return false;
+    std::vector<const int32_t *> planes(d.numcomps);
+    for (uint32_t k = 0; k < d.numcomps; ++k) planes[k] = c->image->comps[k].data;
+    const uint8_t *out = nullptr;
+    size_t len = 0;
+    if (grkgpu_compress_view(ctx, &d, &p, planes.data(), 0, &out, &len)) {
+        GRK_ERROR("%s", grkgpu_last_error());
+        return false;
+    }
+    if (!c->stream->write_all(out, len)) { GRK_ERROR("stream write failed"); return false; }
+    return true;
+}
+
+GRK_EXPORT bool grk_encode(grk_codec *codec) { return grk_encode_with_plugin(codec, nullptr); }
+
+GRK_EXPORT bool grk_end_compress(grk_codec *codec) { return codec && !((Codec *)codec)->decompressor; }
+
+GRK_EXPORT bool grk_write_tile(grk_codec *, uint16_t, uint8_t *, uint64_t) {
+    GRK_ERROR("tile-by-tile encoding (grk_write_tile) is not provided; use grk_encode");
+    return false;
+}
+
+GRK_EXPORT bool grk_set_MCT(grk_cparameters *, float *, int32_t *, uint32_t) {
+    GRK_ERROR("custom MCT is not supported");
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// codestream information
+// ---------------------------------------------------------------------------
+GRK_EXPORT void grk_dump_codec(grk_codec *codec, int32_t, FILE *out) {
+    Codec *c = (Codec *)codec;
+    if (!c || !out || !c->have_header) return;
+    const grkgpu_header_info &h = c->hinfo;
+    const grkgpu_image_desc &d = c->desc;
+    fprintf(out, "Image info {\n\t x0=%u, y0=%u\n\t x1=%u, y1=%u\n\t numcomps=%u\n", d.x0, d.y0, d.x1, d.y1, d.numcomps);
+    for (uint32_t k = 0; k < d.numcomps; ++k) fprintf(out, "\t component %u: prec=%u sgnd=%d\n", k, d.prec[k], d.sgnd[k]);
+    fprintf(out, "}\nCodestream info from main header: {\n\t tx0=%u, ty0=%u\n\t tdx=%u, tdy=%u\n\t tw=%u, th=%u\n",
+            h.tx0, h.ty0, h.tdx, h.tdy, h.tw, h.th);
+    fprintf(out, "\t numlayers=%u progression=%u numresolutions=%u cblk=%ux%u csty=%u cblksty=%u qmfbid=%u mct=%u\n}\n",
+            h.numlayers, h.prog, h.numresolutions, h.cblockw_init, h.cblockh_init, h.csty, h.cblk_sty,
+            h.irreversible ? 0 : 1, h.mct);
+}
+GRK_EXPORT grk_codestream_info_v2 *grk_get_cstr_info(grk_codec *) { return nullptr; }
+GRK_EXPORT void grk_destroy_cstr_info(grk_codestream_info_v2 **p) { if (p) *p = nullptr; }
+GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *) { return nullptr; }
+GRK_EXPORT void grk_destroy_cstr_index(grk_codestream_index **p) { if (p) *p = nullptr; }
+
+// ---------------------------------------------------------------------------
+// plugin management: this library is the accelerated path, no plugin loads
+// (grok.cpp:834-1100 return conventions: false / -1 / no-op)
+// ---------------------------------------------------------------------------
+GRK_EXPORT bool grk_plugin_load(grk_plugin_load_info) { return false; }
+GRK_EXPORT void grk_plugin_cleanup(void) {}
+GRK_EXPORT bool grk_plugin_init(grk_plugin_init_info) { return false; }
+GRK_EXPORT uint32_t grk_plugin_get_debug_state(void) { return GRK_PLUGIN_STATE_NO_DEBUG; }
+GRK_EXPORT int32_t grk_plugin_encode(grk_cparameters *, GRK_PLUGIN_ENCODE_USER_CALLBACK) { return -1; }
+GRK_EXPORT int32_t grk_plugin_batch_encode(const char *, const char *, grk_cparameters *,
+                                           GRK_PLUGIN_ENCODE_USER_CALLBACK) {
+    return -1;
+}
+GRK_EXPORT bool grk_plugin_is_batch_complete(void) { return true; }
+GRK_EXPORT void grk_plugin_stop_batch_encode(void) {}
+GRK_EXPORT int32_t grk_plugin_decode(grk_decompress_parameters *, grk_plugin_decode_callback) { return -1; }
+GRK_EXPORT int32_t grk_plugin_init_batch_decode(const char *, const char *, grk_decompress_parameters *,
+                                                grk_plugin_decode_callback) {
+    return -1;
+}
+GRK_EXPORT int32_t grk_plugin_batch_decode(void) { return -1; }
+GRK_EXPORT void grk_plugin_stop_batch_decode(void) {}

@@ -193,6 +193,14 @@ int grkgpu_encode_blocks(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const gr
 
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
+/* The coding parameters of the main header (grk_header_info, grok.h:620-689). */
+typedef struct {
+    uint32_t cblockw_init, cblockh_init, irreversible, mct, rsiz, numresolutions, csty, cblk_sty;
+    uint32_t prcw_init[33], prch_init[33];  /* precinct size per resolution (samples) */
+    uint32_t tx0, ty0, tdx, tdy, tw, th;   /* tile grid */
+    uint32_t numlayers, prog;
+} grkgpu_header_info;
+int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_header_info *info);
 
 /* Whole-codestream decode into caller-provided planes (device or host). */
 int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_image_desc *img,

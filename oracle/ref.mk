@@ -45,7 +45,7 @@ LIBSRCS := util/BufferedStream.cpp util/logger.cpp util/mem_stream.cpp util/grok
   t1/t1_part1/t1.cpp t1/t1_part1/mqc_enc.cpp t1/t1_part1/mqc_dec.cpp t1/t1_part1/T1Part1.cpp
 OBJS := $(LIBSRCS:%.cpp=$(OUT)/obj/%.o)
 
-all: $(OUT)/libgrok.so $(OUT)/ref_driver $(OUT)/abi_check
+all: $(OUT)/libgrok.so $(OUT)/ref_driver $(OUT)/abi_check $(OUT)/ref_driver_mi355x
 
 $(GEN)/grk_config.h: $(SRC)/grk_config.h.cmake.in
 	@mkdir -p $(GEN)
@@ -88,3 +88,10 @@ clean:
 # layout check of include/grk_plugin_abi.h against the reference headers
 $(OUT)/abi_check: oracle/abi/abi_check.cpp oracle/abi/abi_ref.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_fields.h include/grk_plugin_abi.h $(GEN)/grk_config.h
 	$(CXX) -std=c++17 -O0 -w $(INC) -o $@ oracle/abi/abi_check.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_ref.cpp
+
+# the same driver linked against OUR grk_* library (grokimagecompression_amd/
+# lib/libgrok.so, include/grk_api.h) instead of the reference's: the grk_* ABI
+# drop-in test (tests/test_gpu_grk_api.py)
+MILIB := grokimagecompression_amd/lib
+$(OUT)/ref_driver_mi355x: oracle/ref_driver.cpp $(MILIB)/libgrok.so $(GEN)/grk_config.h
+	$(CXX) -std=c++17 -O2 -I$(SRC) -I$(GEN) -o $@ oracle/ref_driver.cpp -L$(MILIB) -lgrok -Wl,-rpath,'$$ORIGIN/../../$(MILIB)' -lpthread

@@ -1,0 +1,114 @@
+"""The grk_* C API drop-in (include/grk_api.h): the SAME
+driver source that regenerates the golden fixtures with the reference's
+libgrok (oracle/ref_driver.cpp: grk_compress's / grk_decompress's calls and
+option mapping), compiled against the reference's grok.h and linked against
+OUR grokimagecompression_amd/lib/libgrok.so instead (oracle/_ref/
+ref_driver_mi355x, oracle/ref.mk).  Every golden case must come out
+byte-identical on encode and sample-identical on decode -- including -r
+(reduce) and -l (layers) decodes -- i.e. an application written against Grok's
+API gets the reference's results from the MI355X path by relinking.
+
+CPU part: the library exports the reference's whole grk_* function set.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import synth
+from conftest import GOLD, ROOT, load_manifest
+
+MAN = load_manifest()
+DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver_mi355x")
+LIB = os.path.join(ROOT, "grokimagecompression_amd", "lib", "libgrok.so")
+
+# every GRK_API function of the reference's grok.h (v5.1.0)
+REFERENCE_API = """grk_buffer_delete grk_buffer_new grk_create_compress grk_create_decompress grk_decode
+grk_decode_tile_data grk_deinitialize grk_destroy_codec grk_destroy_cstr_index grk_destroy_cstr_info grk_dump_codec
+grk_encode grk_encode_with_plugin grk_end_compress grk_end_decompress grk_get_cstr_index grk_get_cstr_info
+grk_get_decoded_tile grk_image_all_components_data_free grk_image_create grk_image_destroy
+grk_image_single_component_data_alloc grk_image_single_component_data_free grk_initialize grk_plugin_batch_decode
+grk_plugin_batch_encode grk_plugin_cleanup grk_plugin_decode grk_plugin_encode grk_plugin_get_debug_state
+grk_plugin_init grk_plugin_init_batch_decode grk_plugin_is_batch_complete grk_plugin_load grk_plugin_stop_batch_decode
+grk_plugin_stop_batch_encode grk_read_header grk_read_tile_header grk_set_decode_area
+grk_set_default_decoder_parameters grk_set_default_encoder_parameters grk_set_error_handler grk_set_info_handler
+grk_set_warning_handler grk_setup_decoder grk_setup_encoder grk_start_compress grk_stream_create
+grk_stream_create_file_stream grk_stream_create_mapped_file_read_stream grk_stream_create_mem_stream
+grk_stream_destroy grk_stream_get_write_mem_stream_length grk_stream_set_read_function grk_stream_set_seek_function
+grk_stream_set_user_data grk_stream_set_user_data_length grk_stream_set_write_function
+grk_stream_set_zero_copy_read_function grk_version grk_write_tile grk_set_MCT""".split()
+
+
+def test_library_exports_reference_api():
+    if not os.path.exists(LIB):
+        pytest.skip("libgrok.so not built")
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [f for f in REFERENCE_API if f not in syms]
+    assert not missing, missing
+
+
+def _need_driver():
+    if not os.path.exists(DRIVER):
+        pytest.skip("oracle/_ref/ref_driver_mi355x not built (needs /root/reference at build time)")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(MAN))
+def test_grk_api_encode_matches_reference(name, tmp_path):
+    _need_driver()
+    m = MAN[name]
+    h, w, c, bits = m["shape"]
+    img = synth.synth_image(h, w, c, bits, m["seed"], m["kind"])
+    src, out = tmp_path / "in.i32", tmp_path / "out.j2k"
+    np.ascontiguousarray(img, dtype="<i4").tofile(src)
+    r = subprocess.run([DRIVER, "enc", str(src), str(out), str(w), str(h), str(c), str(bits), "0"] + m["args"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == open(f"{GOLD}/{name}.j2k", "rb").read()
+
+
+def _dec(name, tmp_path, extra=()):
+    out = tmp_path / "out.i32"
+    r = subprocess.run([DRIVER, "dec", f"{GOLD}/{name}.j2k", str(out)] + list(extra), capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.split())
+    return np.fromfile(out, dtype="<i4").reshape(nc, ch, cw), (x0, y0, x1, y1, prec, sgnd)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(MAN))
+def test_grk_api_decode_matches_reference(name, tmp_path):
+    _need_driver()
+    d, hdr = _dec(name, tmp_path)
+    ref = np.load(f"{GOLD}/{name}.dec.npy")
+    assert d.shape == ref.shape and np.array_equal(d, ref)
+    m = MAN[name]
+    h, w, c, bits = m["shape"]
+    ox, oy = map(int, m["args"][m["args"].index("-d") + 1].split(",")) if "-d" in m["args"] else (0, 0)
+    assert hdr == (ox, oy, ox + w, oy + h, bits, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,tag", sorted((n, t) for n in MAN for t in MAN[n].get("variants", {})))
+def test_grk_api_decode_options_match_reference(name, tag, tmp_path):
+    """cp_reduce / cp_layer through grk_setup_decoder: the reference's own
+    decode with those options, samples and image header."""
+    _need_driver()
+    v = MAN[name]["variants"][tag]
+    d, hdr = _dec(name, tmp_path, v["args"])
+    ref = np.load(f"{GOLD}/{name}.{tag}.dec.npy")
+    assert d.shape == ref.shape and np.array_equal(d, ref)
+    assert list(hdr) == v["header"]
+
+
+@pytest.mark.gpu
+def test_grk_api_decode_area(tmp_path):
+    """grk_set_decode_area: the window of the reference's full decode."""
+    _need_driver()
+    d, hdr = _dec("rgb12_I", tmp_path, ["-d", "10,7,60,50"])
+    ref = np.load(f"{GOLD}/rgb12_I.dec.npy")
+    assert np.array_equal(d, ref[:, 7:50, 10:60])
+    assert hdr[:4] == (10, 7, 60, 50)
