@@ -64,7 +64,8 @@ class CParams(ctypes.Structure):
                 ("csty", ctypes.c_uint32), ("res_spec", ctypes.c_uint32), ("prcw_init", ctypes.c_uint32 * 33),
                 ("prch_init", ctypes.c_uint32 * 33), ("prog_order", ctypes.c_int32), ("numpocs", ctypes.c_uint32),
                 ("POC", Poc * 32), ("tp_on", ctypes.c_int32), ("tp_flag", ctypes.c_int32), ("rsiz", ctypes.c_uint32),
-                ("framerate", ctypes.c_uint32), ("max_cs_size", ctypes.c_uint64), ("max_comp_size", ctypes.c_uint64)]
+                ("framerate", ctypes.c_uint32), ("max_cs_size", ctypes.c_uint64), ("max_comp_size", ctypes.c_uint64),
+                ("cblk_sty", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]
 
     @classmethod
     def make(cls, numresolution=6, cblk=(64, 64), irreversible=False, mct=-1, tiles=None, tile_offset=(0, 0)):
@@ -113,6 +114,8 @@ class CParams(ctypes.Structure):
                     off = tuple(int(x) for x in v.split(","))
                 elif a == "-p":
                     p.prog_order = PROGS[v[:4]]
+                elif a == "-M":  # code-block mode switches (grk_compress.cpp:1132)
+                    p.cblk_sty = int(v) & 0x7F
                 elif a == "-A":
                     p.rate_control_algorithm = int(v)
                 elif a == "-u":

@@ -84,8 +84,8 @@ struct grkgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf;
-    HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs;
+    DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf, segs;
+    HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs, h_segs;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
     // grkgpu_encode_blocks output (valid until the next call on the context)
@@ -256,6 +256,11 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     for (uint32_t k = 0; k < img->numcomps; ++k)
         if (img->prec[k] < 1 || img->prec[k] > 16) return set_err(GRKGPU_EUNSUPPORTED, "precision must be 1..16");
     if (p->tcp_numlayers > 100) return set_err(GRKGPU_EINVAL, "at most 100 quality layers");
+    // code-block mode switches (COD SPcod style, j2k.cpp j2k_setup_encoder): RESET,
+    // TERMALL, VSC, PTERM, SEGSYM; not BYPASS (0x01) nor HT (0x40)
+    if (p->cblk_sty & ~(uint32_t)(CBLKSTY_RESET | CBLKSTY_TERMALL | CBLKSTY_VSC | CBLKSTY_PTERM | CBLKSTY_SEGSYM))
+        return set_err(GRKGPU_EUNSUPPORTED, "code-block style (BYPASS / HT) not supported");
+    cp.cblksty = p->cblk_sty;
     if (p->tcp_numlayers == 0) {
         p->tcp_rates[0] = 0;
         p->tcp_numlayers = 1;
@@ -765,7 +770,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
-                            c->results.as<EncResult>(), s));
+                            c->results.as<EncResult>(), s, cp.cblksty));
     // per-pass distortion only when some layer is rate-controlled
     // (TileProcessor::needs_rate_control, TileProcessor.cpp:260-266)
     bool need_rc = force_dist != 0;
@@ -818,7 +823,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             EncPass ps;
             ps.rate = r.rate[k];
             ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
-            ps.term = k == np - 1;  // cblksty 0: only the last pass is terminated (t1_enc_is_term_pass)
+            // t1_enc_is_term_pass (t1.cpp:1131-1151): the last pass, or every one under TERMALL
+            ps.term = k == np - 1 || (cp.cblksty & CBLKSTY_TERMALL) != 0;
             ps.slope = 0;
             if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
                 const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
@@ -1270,6 +1276,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     uint64_t arena = 0, llarena = 0;
     std::vector<uint64_t> lloff(nsh * nc);
     std::vector<DecBlock> db;
+    std::vector<DecSeg> dsegs;        // codeword segments of all blocks
+    std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     std::vector<uint8_t> tilebuf;
     for (uint32_t lt = 0; lt < nsh; ++lt) {
@@ -1316,7 +1324,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
             const bool skip = max_layers && pk.layno >= max_layers;
             int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
-                                         base + off, tcp.csty, &packno, skip);
+                                         base + off, tcp.csty, &packno, skip, tcp.cblksty);
             if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
             off += (size_t)used;
         }
@@ -1337,17 +1345,29 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 d.numpasses = std::min<uint32_t>(cb.numpasses, cb.numbps ? 3 * cb.numbps - 2 : 0);
                 d.numbps = cb.numbps;
                 d.len = cb.seglen;
-                if (cb.chunks.size() == 1 && contiguous) {
-                    d.data_off = cb.chunks[0].first;
-                } else if (!cb.chunks.empty()) {
-                    d.data_off = (uint64_t)len + extra.size();  // placed after the codestream
-                    for (auto &ch : cb.chunks) {
-                        const uint8_t *srcp = contiguous ? csb + ch.first : tilebuf.data() + ch.first;
-                        extra.insert(extra.end(), srcp, srcp + ch.second);
+                // codeword segments (one unless TERMALL): each points at its
+                // bytes in place when they are one contiguous chunk, else at
+                // a copy appended after the codestream
+                seg_first.push_back((uint32_t)dsegs.size());
+                for (const auto &sg : cb.segs) {
+                    DecSeg ds{};
+                    ds.len = sg.len;
+                    ds.npasses = sg.numpasses;
+                    if (sg.chunks.size() == 1 && contiguous) {
+                        ds.data_off = sg.chunks[0].first;
+                    } else if (!sg.chunks.empty()) {
+                        ds.data_off = (uint64_t)len + extra.size();  // placed after the codestream
+                        for (auto &ch : sg.chunks) {
+                            const uint8_t *srcp = contiguous ? csb + ch.first : tilebuf.data() + ch.first;
+                            extra.insert(extra.end(), srcp, srcp + ch.second);
+                        }
+                    } else {
+                        ds.data_off = 0;
+                        ds.len = 0;
                     }
-                } else {
-                    d.len = 0;
+                    dsegs.push_back(ds);
                 }
+                d.data_off = cb.segs.empty() ? 0 : dsegs[seg_first.back()].data_off;
                 // no bytes: the block stays zero (T1Part1::decode returns before
                 // t1_decode_cblk when the block has no data, T1Part1.cpp:139-140)
                 if (!d.len) d.numpasses = 0;
@@ -1356,19 +1376,25 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         }
     }
     const uint32_t nblk = (uint32_t)db.size();
+    seg_first.push_back((uint32_t)dsegs.size());
     double t_t2 = now_ms();
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
-    // per-block unstuffed-stream regions (16-byte units in pad)
+    // per-segment unstuffed-stream regions (16-byte units)
     uint64_t uwords = 0;
-    for (auto &d : db) {
-        d.pad = (uint32_t)(uwords / 4);
-        uwords += t1_unstuff_region_words(d.len);
+    for (auto &sg : dsegs) {
+        sg.ub_off = (uint32_t)(uwords / 4);
+        uwords += t1_unstuff_region_words(sg.len);
     }
     if (uwords / 4 > 0xffffffffull) return set_err(GRKGPU_EUNSUPPORTED, "codestream too large for one call");
+    const size_t segbytes = dsegs.size() * sizeof(DecSeg), sfbytes = seg_first.size() * 4;
+    HIPCHK(c->segs.ensure(segbytes + sfbytes + 256));
+    HIPCHK(c->h_segs.ensure(segbytes + sfbytes + 256));
+    memcpy(c->h_segs.p, dsegs.data(), segbytes);
+    memcpy((uint8_t *)c->h_segs.p + segbytes, seg_first.data(), sfbytes);
     HIPCHK(c->ubuf.ensure(uwords * 4 + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
@@ -1382,6 +1408,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         HIPCHK(hipMemcpyAsync(c->cs.as<uint8_t>() + len, c->h_packed.p, extra.size(), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.p, segbytes + sfbytes, hipMemcpyHostToDevice, s));
     DwtPlan dplan;
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < tile.comps.size(); ++k) {
@@ -1396,7 +1423,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (win && arena) HIPCHK(hipMemsetAsync(c->coef.p, 0, arena * 4, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
-                            c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(), 0));
+                            c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(), 0, c->segs.as<DecSeg>(),
+                            (const uint32_t *)(c->segs.as<uint8_t>() + segbytes), cp.cblksty));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
     HIPCHK(hipEventRecord(c->ev[3], s));

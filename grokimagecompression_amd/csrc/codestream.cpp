@@ -295,7 +295,10 @@ struct BitReader {
 }  // namespace
 
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data) {
+                      uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data, uint32_t cblksty) {
+    // passes per codeword segment (T2::init_seg, T2.cpp:821-850): 1 when every
+    // pass is terminated, else 109 (a longer block is cut there, T2.cpp:566-577)
+    const uint32_t maxpasses = (cblksty & 0x04) ? 1u : 109u;
     Resolution &res = tc.res[resno];
     if (layno == 0) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
@@ -304,7 +307,7 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
             Precinct &pr = b.precs[precno];
             if (pr.cblks.empty()) continue;
             pr.incl.reset(); pr.imsb.reset();
-            for (auto &c : pr.cblks) { c.included = false; c.numpasses = 0; c.chunks.clear(); c.seglen = 0; }
+            for (auto &c : pr.cblks) { c.included = false; c.numpasses = 0; c.segs.clear(); c.seglen = 0; }
         }
     }
     size_t hstart = 0;
@@ -321,8 +324,8 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
         }
     }
     BitReader r(p + hstart, n - hstart);
-    struct Seg { Cblk *c; uint32_t len; };
-    std::vector<Seg> segs;
+    struct Part { Cblk *c; uint32_t seg, passes, len; };  // one segment's share of this packet
+    std::vector<Part> parts;
     if (n > hstart && r.read(1)) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
             Band &b = res.bands[bandno];
@@ -346,15 +349,24 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                 }
                 uint32_t np = r.numpasses();
                 c.numlenbits += r.comma();
-                // one segment per block (cblksty 0): at most 109 passes per
-                // segment, larger counts are truncated (T2.cpp:566-577)
-                if (np > 109) np = 109;
-                const uint32_t bits = c.numlenbits + (uint32_t)floorlog2((int32_t)np);
-                if (bits > 32) return -1;  // "too many bits in segment length", T2.cpp:590-593
-                uint32_t L = r.read(bits);
+                if (maxpasses > 1 && np > maxpasses) np = maxpasses;  // single segment: truncated (T2.cpp:566-577)
+                // the packet's passes fill the open segment, then new ones
+                // (T2::read_packet_header, T2.cpp:560-605)
+                if (c.segs.empty() || c.segs.back().numpasses == maxpasses) c.segs.emplace_back();
+                uint32_t left = np;
+                while (left) {
+                    const uint32_t si = (uint32_t)c.segs.size() - 1;
+                    const uint32_t take = std::min(left, maxpasses - c.segs[si].numpasses);
+                    const uint32_t bits = c.numlenbits + (uint32_t)floorlog2((int32_t)take);
+                    if (bits > 32) return -1;  // "too many bits in segment length", T2.cpp:590-593
+                    const uint32_t L = r.read(bits);
+                    if (r.err) return -1;
+                    parts.push_back({&c, si, take, L});
+                    c.segs[si].numpasses += take;
+                    left -= take;
+                    if (left) c.segs.emplace_back();
+                }
                 c.numpasses += np;
-                segs.push_back({&c, L});
-                if (r.err) return -1;
             }
         }
     }
@@ -363,18 +375,20 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
     size_t off = hstart + r.off;
     // EPH (T2.cpp:405-418 / 640-652): skipped when present
     if ((csty & CSTY_EPH) && off + 2 <= n && p[off] == 0xFF && p[off + 1] == 0x92) off += 2;
-    for (auto &sg : segs) {
+    for (auto &pt : parts) {
         // T2::read_packet_data (T2.cpp:686-698): a segment running past the
         // tile data is truncated to what is there (the decoder reads the
         // missing tail as the 0xFF fill), not an error
-        if (off + sg.len > n) sg.len = (uint32_t)(n - off);
+        if (off + pt.len > n) pt.len = (uint32_t)(n - off);
         // a layer beyond the decoded ones (T2::skip_packet_data, T2.cpp:
         // 758-819): its passes still count, its bytes are stepped over
         if (!skip_data) {
-            if (sg.len) sg.c->chunks.push_back({base_off + off, sg.len});
-            sg.c->seglen += sg.len;
+            Cblk::Seg &sg = pt.c->segs[pt.seg];
+            if (pt.len) sg.chunks.push_back({base_off + off, pt.len});
+            sg.len += pt.len;
+            pt.c->seglen += pt.len;
         }
-        off += sg.len;
+        off += pt.len;
     }
     return (int64_t)off;
 }
@@ -489,7 +503,8 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
     if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
     // j2k_read_header stops at the first SOT; a stream that ends before it is truncated
     if (first_sot == 0) { err = "truncated main header (no SOT)"; return false; }
-    if (cp.cblksty != 0) { err = "code-block mode switches not supported"; return false; }
+    // mode switches: RESET, TERMALL, VSC, PTERM, SEGSYM; not BYPASS (0x01) nor HT (0x40)
+    if (cp.cblksty & ~0x3Eu) { err = "code-block mode switches BYPASS / HT not supported"; return false; }
     if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
     for (uint32_t k = 0; k < cp.numcomps; ++k) cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
     return true;

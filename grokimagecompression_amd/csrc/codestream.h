@@ -86,9 +86,15 @@ struct Cblk {
     // T2 state
     uint32_t numbps = 0, numpasses = 0, numlenbits = 0;
     bool included = false;
-    // decoder: segment chunks (offset into codestream, length)
-    std::vector<std::pair<uint64_t, uint32_t>> chunks;
-    uint32_t seglen = 0;
+    // decoder: codeword segments (grk_tcd_seg): passes, bytes and the chunks
+    // (offset into the codestream, length) holding them.  One segment unless
+    // the code-block style terminates passes (TERMALL: one per pass).
+    struct Seg {
+        uint32_t numpasses = 0, len = 0;
+        std::vector<std::pair<uint64_t, uint32_t>> chunks;
+    };
+    std::vector<Seg> segs;
+    uint32_t seglen = 0;  // bytes over all segments
 };
 
 struct Precinct {
@@ -208,8 +214,10 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
 bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp);
 // returns bytes consumed or -1 (T2::read_packet_header / read_packet_data,
 // T2.cpp:314-725); csty: SOP / EPH markers; packno: SOP packet counter;
-// skip_data: a layer beyond the decoded ones (T2::skip_packet)
+// skip_data: a layer beyond the decoded ones (T2::skip_packet); cblksty: the
+// code-block style (segment boundaries)
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr, bool skip_data = false);
+                      uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr, bool skip_data = false,
+                      uint32_t cblksty = 0);
 
 }  // namespace grkgpu

@@ -88,9 +88,10 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.
+// cblksty: the CBLKSTY_* mode switches of the codestream (t1_lane.h), 0 = none
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s);
+                            hipStream_t s, uint32_t cblksty = 0);
 // Per-pass distortion sums of the blocks k_t1_model coded (same sym /
 // sym_off layout): nmsedec[pass] of every block, in the pass order of
 // t1_encode_cblk (t1.cpp:1222-1260).
@@ -99,8 +100,13 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 // ubuf: unstuffed-stream arena; block i's region at ubuf + i * fixed_words
 // words, or (fixed_words == 0) at blocks[i].pad * 16 bytes
 // (t1_unstuff_region_words words each).
+// segs / seg_first: the codeword segments of every block (block i's are
+// segs[seg_first[i] .. seg_first[i+1]), each with its own unstuffed region at
+// ubuf + ub_off * 16 bytes); null: one segment per block at blocks[i].data_off.
+// cblksty: CBLKSTY_* mode switches.
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
-                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words);
+                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words,
+                            const DecSeg *segs = nullptr, const uint32_t *seg_first = nullptr, uint32_t cblksty = 0);
 // 32-bit words of a block's unstuffed-stream region (header + words + carries)
 inline uint32_t t1_unstuff_region_words(uint32_t len) { return 4 + unstuff_word_cap(len) + unstuff_carry_cap(len); }
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,

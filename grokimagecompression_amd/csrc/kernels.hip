@@ -180,7 +180,8 @@ __device__ __forceinline__ uint64_t sym_block_off(const uint64_t *sym_off, uint3
 
 __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth,
                                                  T1Scratch *__restrict__ scr, uint8_t *__restrict__ sym,
-                                                 const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res) {
+                                                 const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res,
+                                                 uint32_t cblksty) {
     __shared__ uint8_t s_sc[256];
     for (uint32_t k = threadIdx.x; k < 256; k += 64) s_sc[k] = sc_lut_entry(k);
     __syncthreads();
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
     T1Scratch &S = scr[i];
     uint8_t *base = sym + off + (uint64_t)p * slot;
     t1_model_plane(b.w, b.h, b.orient, S.pa + p * 64, S.pb + p * 64, p + 1 < numbps ? S.pb + (p + 1) * 64 : nullptr,
-                   S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4);
+                   S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4,
+                   cblksty);
 }
 
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
@@ -212,7 +214,8 @@ template <int LANES, int MINW = 1>
 __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
                                                  const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
-                                                 EncResult *__restrict__ res, const uint32_t *__restrict__ perm) {
+                                                 EncResult *__restrict__ res, const uint32_t *__restrict__ perm,
+                                                 uint32_t cblksty) {
     __shared__ uint32_t s_mq[48];
     // 19 context words per lane at an odd stride (no bank conflicts).  The
     // read-ahead of the symbol after a pass's last one may index up to 31
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     const uint64_t off = sym_block_off(sym_off, i, &cap);
     uint32_t len;
     uint32_t np = t1_mq_block(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
-                              s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len);
+                              s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len, cblksty);
     r.numpasses = np;
     r.len = len;
     uint32_t nsym = 0;
@@ -318,22 +321,18 @@ __device__ __forceinline__ size_t ub_region(const DecBlock &b, uint32_t i, uint3
     return fixed_words ? (size_t)i * fixed_words : (size_t)b.pad * 4;
 }
 
-__global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                   const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf,
-                                                   uint32_t fixed_words) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= n) return;
-    const DecBlock b = blocks[i];
-    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
-    uint32_t *region = ubuf + ub_region(b, i, fixed_words);
-    uint32_t *words = region + 4, *carries = words + unstuff_word_cap(b.len);
-    const uintptr_t pa = (uintptr_t)(data + b.data_off);
+// unstuff one segment (len bytes at data + data_off) into region: header
+// {nwords, ncarry}, words, carries
+__device__ __forceinline__ void unstuff_segment(const uint8_t *__restrict__ data, uint64_t data_off, uint32_t len,
+                                                uint32_t *__restrict__ region) {
+    uint32_t *words = region + 4, *carries = words + unstuff_word_cap(len);
+    const uintptr_t pa = (uintptr_t)(data + data_off);
     const uint4 *src = (const uint4 *)(pa & ~(uintptr_t)15);
-    const uint32_t skip = (uint32_t)(pa & 15), end = skip + b.len;
+    const uint32_t skip = (uint32_t)(pa & 15), end = skip + len;
     const uint32_t nch = (end + 15) >> 4;
     Unstuff u;
     uint32_t nw = 0, nc = 0;
-    uint4 nxt = src[0];
+    uint4 nxt = nch ? src[0] : uint4{0, 0, 0, 0};
     for (uint32_t ch = 0; ch < nch; ++ch) {
         const uint4 cur = nxt;
         if (ch + 1 < nch) nxt = src[ch + 1];
@@ -355,10 +354,32 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     region[1] = nc;
 }
 
+// segs / seg_first (codestream decode): block i's segments are
+// segs[seg_first[i] .. seg_first[i+1]); null: one segment per block at
+// blocks[i].data_off (the stage entry point)
+__global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                   const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf,
+                                                   uint32_t fixed_words, const DecSeg *__restrict__ segs,
+                                                   const uint32_t *__restrict__ seg_first) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    if (segs) {
+        for (uint32_t q = seg_first[i]; q < seg_first[i + 1]; ++q) {
+            const DecSeg sg = segs[q];
+            unstuff_segment(data, sg.data_off, sg.len, ubuf + (size_t)sg.ub_off * 4);
+        }
+        return;
+    }
+    unstuff_segment(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words));
+}
+
 template <int LANES>
 __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
-                                                        T1Scratch *__restrict__ scr) {
+                                                        T1Scratch *__restrict__ scr, const DecSeg *__restrict__ segs,
+                                                        const uint32_t *__restrict__ seg_first, uint32_t sty) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
@@ -373,9 +394,22 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
     T1Scratch &S = scr[i];
+    uint32_t *cxw = s_cx + threadIdx.x * 21;
+    if (segs) {
+        const uint32_t q0 = seg_first[i], nseg = seg_first[i + 1] - q0;
+        const DecSeg s0 = segs[q0];
+        const uint32_t *region = ubuf + (size_t)s0.ub_off * 4;
+        for (uint32_t y = 0; y < b.h + 2; ++y) { S.st.sig[y] = 0; S.st.neg[y] = 0; S.st.vis[y] = 0; S.st.ref[y] = 0; }
+        mq_reset_words(cxw, T.mq);
+        BitDec d;
+        d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
+        SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
+        t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, S.st, T, cxw, S.pa, S.pb, sty, cur);
+        return;
+    }
     const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
     t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, S.st, T,
-                 s_cx + threadIdx.x * 21, S.pa, S.pb);
+                 cxw, S.pa, S.pb);
 }
 
 // One workgroup per block, lane = column: values from the bit-plane rows
@@ -473,15 +507,15 @@ constexpr int DEC_LANES = 64;
 
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t cblksty) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
     if (maxdepth > 32) maxdepth = 32;
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
-                       scratch, sym, sym_off, res);
+                       scratch, sym, sym_off, res, cblksty);
     hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s, blocks, n,
-                       scratch, sym, sym_off, out, res, (const uint32_t *)nullptr);
+                       scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
     return hipGetLastError();
 }
 
@@ -514,11 +548,13 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 }
 
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
-                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words) {
+                            int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words, const DecSeg *segs,
+                            const uint32_t *seg_first, uint32_t cblksty) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words);
+    hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
+                       seg_first);
     hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0, s,
-                       blocks, n, (const uint32_t *)ubuf, fixed_words, scratch);
+                       blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
     hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
     return hipGetLastError();
 }

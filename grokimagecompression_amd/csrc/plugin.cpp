@@ -112,7 +112,11 @@ bool map_params(const grkp_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     // tcp_mct 255 = "decide from the image" (grk_compress.cpp:1997-1998)
     p->tcp_mct = g->tcp_mct == 255 ? -1 : g->tcp_mct;
     if (g->tcp_mct == 2 || g->mct_data) return false;  // custom MCT
-    if (g->cblk_sty || g->isHT || g->roi_compno >= 0) return false;
+    // mode switches: the host's plugin path writes one codeword segment per
+    // block (encode_synch_with_plugin never sets pass->term), so only the
+    // single-segment ones travel: RESET, VSC, PTERM, SEGSYM -- not TERMALL,
+    // BYPASS or HT
+    if ((g->cblk_sty & ~0x3Au) || g->isHT || g->roi_compno >= 0) return false;
     if (g->subsampling_dx != 1 || g->subsampling_dy != 1) return false;
     if (g->tile_size_on) return false;  // the host hands ONE plugin tile to every tile (j2k.cpp:2059-2069)
     p->cp_tx0 = g->cp_tx0;
@@ -142,6 +146,7 @@ bool map_params(const grkp_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     p->framerate = (uint32_t)g->framerate;
     p->max_cs_size = g->max_cs_size;
     p->max_comp_size = g->max_comp_size;
+    p->cblk_sty = g->cblk_sty;
     (void)numcomps;
     return true;
 }

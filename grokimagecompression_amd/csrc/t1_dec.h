@@ -238,15 +238,29 @@ GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, ui
     setcol4(s.bit, x, bits);
 }
 
+// Codeword segments of a block: a single one (NoSegs) or a cursor that
+// re-initialises the decoder at each segment's first pass (t1_decode_cblk's
+// per-segment mqc_init_dec, t1.cpp:1066-1113).
+struct NoSegs {
+    template <class D> GRK_HD void at_pass(D &, uint32_t) {}
+};
+
 // The pass / stripe / column walk shared by v3 (byte-level MQ input, Dec3)
-// and v5 (unstuffed bit stream, BitDec in t1_flat.h).
-template <class D>
+// and v5 (unstuffed bit stream, BitDec in t1_flat.h).  Mode switches
+// (cblksty): VSC -- row k+4 reads as insignificant for row k+3 (the flags
+// update of t1.cpp:168-190 skips the north neighbours of a stripe's first
+// row); RESET -- contexts re-initialised after every pass (t1.cpp:1104-1105);
+// SEGSYM -- four uniform-context symbols end every cleanup pass (t1.cpp:873-889).
+template <class D, class S = NoSegs>
 GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, BlockState &st,
-                             const DecTables &T, uint32_t *cxw, uint64_t *sigafter, uint64_t *refbit) {
+                             const DecTables &T, uint32_t *cxw, uint64_t *sigafter, uint64_t *refbit,
+                             uint32_t sty = 0, S segs = S()) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
+    const bool vsc = (sty & CBLKSTY_VSC) != 0;
     int32_t bpno = (int32_t)numbps - 1;
     int passtype = 2;
     for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
+        segs.at_pass(d, passno);
         uint64_t *sa = sigafter + (uint32_t)bpno * 64;
         uint64_t *rb = refbit + (uint32_t)bpno * 64;
         // Each pass type loads and stores only the state rows it reads or
@@ -258,6 +272,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
             Stripe s;
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.sig[i] = st.sig[k + i];
+            if (vsc) s.sig[5] = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) s.vis[i] = st.vis[k + 1 + i];
             if (passtype == 1) {
@@ -281,6 +296,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
             }
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.neg[i] = st.neg[k + i];
+            if (vsc) s.neg[5] = 0;
             if (passtype == 0) {
                 uint64_t cand = spp_candidates(s, nr) & wm;
                 while (cand) {
@@ -314,6 +330,9 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                 if ((uint32_t)i < nr) sa[k + i] = s.sig[i + 1];
             }
         }
+        if (passtype == 2 && (sty & CBLKSTY_SEGSYM))
+            for (int q = 0; q < 4; ++q) d.decode(cxw, T.mq, CX_UNI);
+        if (sty & CBLKSTY_RESET) mq_reset_words(cxw, T.mq);
         if (++passtype == 3) { passtype = 0; bpno--; }
     }
 }

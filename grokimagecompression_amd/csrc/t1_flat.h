@@ -182,6 +182,29 @@ struct BitDec {
     }
 };
 
+// One codeword segment of a code-block (grk_tcd_seg): its bytes in the data
+// buffer, its passes, and where its unstuffed stream lives (16-byte units).
+struct DecSeg {
+    uint64_t data_off;
+    uint32_t len, npasses, ub_off, pad;
+};
+
+// Segment cursor for t1_decode_passes: BitDec moves to segment j+1's stream
+// at that segment's first pass (t1_decode_cblk's mqc_init_dec per segment,
+// t1.cpp:1066-1081; contexts carry over unless RESET).
+struct SegCursor {
+    const DecSeg *seg;
+    const uint32_t *ubuf;
+    uint32_t nseg, cur, next;
+    template <class D> GRK_HD void at_pass(D &d, uint32_t passno) {
+        if (passno != next || cur + 1 >= nseg) return;
+        ++cur;
+        const uint32_t *region = ubuf + (size_t)seg[cur].ub_off * 4;
+        d.init(region + 4, region[0], region + 4 + unstuff_word_cap(seg[cur].len));
+        next += seg[cur].npasses;
+    }
+};
+
 // v5: the nested pass / stripe / column walk of v3 (lanes of a wavefront stay
 // converged on the pass structure) fed by the unstuffed bit stream.
 GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,

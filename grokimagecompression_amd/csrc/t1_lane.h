@@ -85,6 +85,11 @@ GRK_HD uint32_t clz32(uint32_t v) { return (uint32_t)__builtin_clz(v); }
 GRK_HD uint32_t ctz64(uint64_t v) { return (uint32_t)__builtin_ctzll(v); }
 GRK_HD uint64_t dil(uint64_t m) { return m | (m << 1) | (m >> 1); }
 
+// code-block style bits (COD SPcod, grok.h GRK_CBLKSTY_*): the mode switches
+// this coder takes (BYPASS 0x01 and HT 0x40 are rejected by the host)
+constexpr uint32_t CBLKSTY_RESET = 0x02, CBLKSTY_TERMALL = 0x04, CBLKSTY_VSC = 0x08, CBLKSTY_PTERM = 0x10,
+                   CBLKSTY_SEGSYM = 0x20;
+
 // MQ context registers are 32-bit words: the packed table entry of the
 // current state (Qe | NMPS<<16 | NLPS<<22 | SWITCH<<28) | MPS<<31, so one LDS
 // read per symbol yields Qe; the next-state lookup is off the critical path.
@@ -167,6 +172,41 @@ GRK_HD void mqel_flush(MqEncLane &e) {
     e.c <<= e.ct; mqel_byteout(e);
     e.c <<= e.ct; mqel_byteout(e);
     if (e.cur != 0xff) mqel_emit(e, 0);  // "if (*bp != 0xff) bp++"
+}
+
+// ERTERM, predictable termination (mqc_erterm_enc, mqc_enc.cpp:384-395)
+GRK_HD void mqel_erterm(MqEncLane &e) {
+    int32_t k = (int32_t)(11 - e.ct + 1);
+    while (k > 0) {
+        e.c <<= e.ct;
+        e.ct = 0;
+        mqel_byteout(e);
+        k -= (int32_t)e.ct;
+    }
+    if (e.cur != 0xff) mqel_byteout(e);
+}
+
+// Restart after a terminated pass (mqc_restart_init_enc, mqc_enc.cpp:366-382):
+// INITENC again with bp stepped back onto the segment's last counted byte,
+// which becomes the carry target again.  That byte is already committed: in
+// `acc` when it shares bp's dword, else in `out` (reloaded into acc).
+GRK_HD void mqel_restart(MqEncLane &e) {
+    const int32_t nb = e.bp - 1;
+    uint32_t byte;
+    if (nb < 0) {  // the zero pad byte before the block (a first pass that wrote nothing counted)
+        byte = 0;
+        e.acc = 0;
+    } else if ((nb >> 2) == (e.bp >> 2)) {
+        byte = (e.acc >> ((nb & 3) * 8)) & 0xffu;
+    } else {  // nb is the last byte of the previous dword, already stored
+        e.acc = e.out[nb >> 2];
+        byte = e.acc >> 24;
+    }
+    e.bp = nb;
+    e.cur = byte;
+    e.a = 0x8000;
+    e.c = 0;
+    e.ct = byte == 0xff ? 13u : 12u;
 }
 
 GRK_HD void mqel_finish(MqEncLane &e, uint32_t len) {
@@ -411,17 +451,26 @@ struct LaneEncoder {
     const uint32_t *tab;
     const uint64_t *planes, *pl;
     uint32_t *rate;
+    uint32_t sty = 0;  // CBLKSTY_* mode switches
     GRK_HD void begin_pass(int32_t bpno) { pl = planes + (uint32_t)bpno * 64; }
     GRK_HD uint64_t stripe_bits(uint32_t y, uint32_t h) const { return y < h ? pl[y] : 0; }
     GRK_HD uint32_t code(uint32_t cx, uint32_t v) { mqel_encode(e, cxw, tab, cx, v); return v; }
     GRK_HD void end_stripe(uint32_t, uint32_t, int, const Stripe &) {}
+    // t1_encode_cblk's pass end (t1.cpp:1256-1298): a terminated pass (the
+    // last one; every one under TERMALL) is flushed -- ERTERM under PTERM --
+    // and the coder restarts for the next; else the rate gets the
+    // rate_extra_bytes correction.  RESET re-initialises the contexts.
     GRK_HD void end_pass(uint32_t passno, int passtype, int32_t bpno) {
-        if (passtype == 2 && bpno == 0) {  // the last cleanup pass is terminated
-            mqel_flush(e);
+        const bool last = passtype == 2 && bpno == 0;
+        if (last || (sty & CBLKSTY_TERMALL)) {
+            if (sty & CBLKSTY_PTERM) mqel_erterm(e);
+            else mqel_flush(e);
             rate[passno] = (uint32_t)e.bp;
-        } else {  // rate_extra_bytes (t1.cpp:1278-1288)
+            if (!last) mqel_restart(e);
+        } else {
             rate[passno] = (uint32_t)e.bp + 5 + (e.ct < 5 ? 1 : 0);
         }
+        if (sty & CBLKSTY_RESET) mq_reset_words(cxw, tab);
     }
 };
 
@@ -506,8 +555,9 @@ GRK_HD void t1_decode_lane(const uint8_t *data, uint32_t len, uint32_t numpasses
 //                   recording Grok's pass rates.
 // ===========================================================================
 GRK_HD uint32_t sym_stream_bytes(uint32_t w, uint32_t h) {
-    // per plane: <= 1 ZC/MAG + 1 sign per sample, <= 2 extra (AGG/UNI) per stripe column
-    return (w * h * 2 + ((h + 3) / 4) * w * 2 + 15) & ~15u;
+    // per plane: <= 1 ZC/MAG + 1 sign per sample, <= 2 extra (AGG/UNI) per
+    // stripe column, 4 segmentation symbols (SEGSYM)
+    return (w * h * 2 + ((h + 3) / 4) * w * 2 + 4 + 15) & ~15u;
 }
 GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h) + 2 * 64 * 8; }
 
@@ -580,10 +630,17 @@ GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0
 // rows (index y+1), tmp = 128 rows of scratch.  Writes the plane's stream and
 // cnt[0..2] = symbols of its SPP / MRP / CUP (SPP and MRP are empty for the
 // top plane).  Semantics: t1.cpp:197-338 (SPP), 443-555 (MRP), 639-782 (CUP).
+//
+// Mode switches (cblksty): VSC -- the contexts of a stripe's last row never
+// see the row below it (t1_update_flags_macro skips the north update from a
+// stripe's first row, t1.cpp:168-190), i.e. row k+4 reads as insignificant
+// for row k+3; SEGSYM -- the cleanup pass ends with the segmentation symbols
+// 1 0 1 0 in the uniform context (mqc_segmark_enc, t1.cpp:1244-1245).
 GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64_t *bitp, const uint64_t *above,
                            const uint64_t *ref, const uint64_t *negr, uint64_t *tmp, const uint8_t *sc,
-                           uint32_t *out, uint32_t *cnt) {
+                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
+    const bool vsc = (cblksty & CBLKSTY_VSC) != 0;
     uint64_t *postS = tmp, *visS = tmp + 64;
     SymOut so{out, 0, 0};
     // ---- significance propagation ----
@@ -600,7 +657,8 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
-        const uint64_t D = ldrow(above, (int32_t)(k + 4), h);
+        if (vsc) ng[5] = 0;
+        const uint64_t D = vsc ? 0 : ldrow(above, (int32_t)(k + 4), h);
         // fixed point of the causal significance recurrence; the W->E chain
         // inside a row is resolved with one carry-propagating add
         for (int it = 0; it < 300; ++it) {
@@ -655,6 +713,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
         uint64_t m[4], rf[4], bit[4], sS[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) sS[i] = ldrow(postS, (int32_t)(k + i) - 1, h);
+        if (vsc) sS[5] = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             m[r] = ldrow(above, (int32_t)(k + r), h);
@@ -689,7 +748,8 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
-        const uint64_t D = ldrow(postS, (int32_t)(k + 4), h);
+        if (vsc) ng[5] = 0;
+        const uint64_t D = vsc ? 0 : ldrow(postS, (int32_t)(k + 4), h);
         uint64_t agg = 0;
         if (nr == 4) {
             agg = cand[0] & cand[1] & cand[2] & cand[3];
@@ -734,6 +794,12 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             }
         }
         U = pc[3];
+    }
+    if (cblksty & CBLKSTY_SEGSYM) {
+        so.put(CX_UNI | 1u << 5);
+        so.put(CX_UNI);
+        so.put(CX_UNI | 1u << 5);
+        so.put(CX_UNI);
     }
     cnt[2] = so.n - cnt[0] - cnt[1];
     so.flush();
@@ -792,10 +858,12 @@ GRK_HD uint32_t mqel_step(MqEncLane &e, const uint32_t *tab, uint32_t w, uint32_
 }
 
 GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_words, const uint32_t *cnt,
-                            const uint32_t *tab, uint32_t *cxw, uint32_t *out, uint32_t *rate, uint32_t *len_out) {
+                            const uint32_t *tab, uint32_t *cxw, uint32_t *out, uint32_t *rate, uint32_t *len_out,
+                            uint32_t cblksty = 0) {
     *len_out = 0;
     if (numbps == 0) return 0;
     LaneEncoder cd;
+    cd.sty = cblksty;
     mq_reset_words(cxw, tab);
     cd.e.a = 0x8000; cd.e.c = 0; cd.e.ct = 12; cd.e.bp = -1; cd.e.cur = 0; cd.e.acc = 0; cd.e.out = out;
     cd.cxw = cxw; cd.tab = tab; cd.rate = rate;
@@ -834,6 +902,7 @@ GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_
                 ++t;                                                      \
                 bnd = t == 1 ? b1 : total;                                \
             } while (t < 3 && i == bnd);                                  \
+            w = cxw[cur & 31]; /* RESET may have re-initialised it */     \
         }                                                                 \
     }
         while (total - i >= 16) {  // full chunks

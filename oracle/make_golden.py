@@ -105,6 +105,19 @@ CASES = [
                                                           "-b", "32,32"]),
     ("rgb8_poc_r15_I", (96, 128, 3, 8), "smooth", 81, ["-I", "-r", "15,4",
                                                        "-P", "T1=0,0,2,3,3,CPRL/T1=3,0,2,6,3,LRCP"]),
+    # code-block mode switches (-M: 2 RESET, 4 RESTART = terminate every pass,
+    # 8 VSC, 16 PTERM = predictable termination, 32 SEGSYM)
+    ("g8_M2_reset", (96, 128, 1, 8), "smooth", 90, ["-M", "2"]),
+    ("g8_M8_vsc", (96, 128, 1, 8), "smooth", 91, ["-M", "8"]),
+    ("g8_M32_segsym", (96, 128, 1, 8), "smooth", 92, ["-M", "32"]),
+    ("g8_M4_termall", (96, 128, 1, 8), "smooth", 93, ["-M", "4"]),
+    ("g8_M16_pterm", (96, 128, 1, 8), "smooth", 94, ["-M", "16"]),
+    ("g8_M20_termall_pterm", (96, 128, 1, 8), "uniform", 95, ["-M", "20"]),
+    ("g8_M8_vsc_odd", (77, 100, 1, 8), "uniform", 98, ["-M", "8"]),
+    ("rgb8_M62_I_r", (96, 128, 3, 8), "smooth", 96, ["-M", "62", "-I", "-r", "20,5"]),
+    ("rgb12_M46_tiles", (150, 200, 3, 12), "smooth", 97, ["-M", "46", "-t", "64,64"]),
+    ("g12_M4_layers", (70, 90, 1, 12), "smooth", 99, ["-M", "4", "-r", "16,4,1"]),
+    ("g8_M42_b16", (100, 130, 1, 8), "smooth", 100, ["-M", "42", "-b", "16,16", "-r", "12,3"]),
 ]
 
 # Reference decodes with grk_decompress options (-l layers, -r reduce), per
@@ -129,6 +142,8 @@ DEC_VARIANTS = {
     "rgb12_cinema4k": [["-r", "1"]],
     "rgb8_prec_cprl": [["-r", "1"]],
     "g16_I": [["-r", "3"]],
+    "g12_M4_layers": [["-l", "1"], ["-l", "2"]],
+    "rgb8_M62_I_r": [["-l", "1"], ["-r", "1"]],
 }
 
 

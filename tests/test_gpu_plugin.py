@@ -43,6 +43,8 @@ def _handled(args):
     """Does the plugin take this grk_compress argument list?"""
     if "-t" in args:
         return False
+    if "-M" in args and int(args[args.index("-M") + 1]) & 0x45:  # TERMALL / BYPASS / HT: multi-segment blocks
+        return False
     if "-cinema2K" in args or "-cinema4K" in args:
         return True
     if "-q" in args:
