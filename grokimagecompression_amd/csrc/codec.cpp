@@ -256,10 +256,9 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     for (uint32_t k = 0; k < img->numcomps; ++k)
         if (img->prec[k] < 1 || img->prec[k] > 16) return set_err(GRKGPU_EUNSUPPORTED, "precision must be 1..16");
     if (p->tcp_numlayers > 100) return set_err(GRKGPU_EINVAL, "at most 100 quality layers");
-    // code-block mode switches (COD SPcod style, j2k.cpp j2k_setup_encoder): RESET,
-    // TERMALL, VSC, PTERM, SEGSYM; not BYPASS (0x01) nor HT (0x40)
-    if (p->cblk_sty & ~(uint32_t)(CBLKSTY_RESET | CBLKSTY_TERMALL | CBLKSTY_VSC | CBLKSTY_PTERM | CBLKSTY_SEGSYM))
-        return set_err(GRKGPU_EUNSUPPORTED, "code-block style (BYPASS / HT) not supported");
+    // code-block mode switches (COD SPcod style, j2k.cpp j2k_setup_encoder):
+    // BYPASS, RESET, TERMALL, VSC, PTERM, SEGSYM; not HT (0x40)
+    if (p->cblk_sty & ~0x3Fu) return set_err(GRKGPU_EUNSUPPORTED, "HT code-block style not supported");
     cp.cblksty = p->cblk_sty;
     if (p->tcp_numlayers == 0) {
         p->tcp_rates[0] = 0;
@@ -823,8 +822,12 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             EncPass ps;
             ps.rate = r.rate[k];
             ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
-            // t1_enc_is_term_pass (t1.cpp:1131-1151): the last pass, or every one under TERMALL
-            ps.term = k == np - 1 || (cp.cblksty & CBLKSTY_TERMALL) != 0;
+            // t1_enc_is_term_pass (t1.cpp:1131-1151)
+            {
+                const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
+                ps.term = t1_pass_term(cp.cblksty, bp, pt, r.numbps);
+            }
             ps.slope = 0;
             if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
                 const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);

@@ -297,8 +297,18 @@ struct BitReader {
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
                       uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data, uint32_t cblksty) {
     // passes per codeword segment (T2::init_seg, T2.cpp:821-850): 1 when every
-    // pass is terminated, else 109 (a longer block is cut there, T2.cpp:566-577)
-    const uint32_t maxpasses = (cblksty & 0x04) ? 1u : 109u;
+    // pass is terminated; BYPASS: 10 for the first, then 2 (raw) and 1 (MQ)
+    // alternately; else 109 (a longer block is cut there, T2.cpp:566-577)
+    auto seg_max = [cblksty](const Cblk &c) -> uint32_t {
+        if (cblksty & 0x04) return 1;
+        if (cblksty & 0x01) {
+            if (c.segs.empty()) return 10;
+            const uint32_t pm = c.segs.back().maxpasses;
+            return (pm == 1 || pm == 10) ? 2 : 1;
+        }
+        return 109;
+    };
+    const bool single = !(cblksty & 0x05);
     Resolution &res = tc.res[resno];
     if (layno == 0) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
@@ -349,14 +359,19 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                 }
                 uint32_t np = r.numpasses();
                 c.numlenbits += r.comma();
-                if (maxpasses > 1 && np > maxpasses) np = maxpasses;  // single segment: truncated (T2.cpp:566-577)
+                if (single && np > 109) np = 109;  // single segment: truncated (T2.cpp:566-577)
                 // the packet's passes fill the open segment, then new ones
                 // (T2::read_packet_header, T2.cpp:560-605)
-                if (c.segs.empty() || c.segs.back().numpasses == maxpasses) c.segs.emplace_back();
+                auto open_seg = [&]() {
+                    const uint32_t m = seg_max(c);
+                    c.segs.emplace_back();
+                    c.segs.back().maxpasses = m;
+                };
+                if (c.segs.empty() || c.segs.back().numpasses == c.segs.back().maxpasses) open_seg();
                 uint32_t left = np;
                 while (left) {
                     const uint32_t si = (uint32_t)c.segs.size() - 1;
-                    const uint32_t take = std::min(left, maxpasses - c.segs[si].numpasses);
+                    const uint32_t take = std::min(left, c.segs[si].maxpasses - c.segs[si].numpasses);
                     const uint32_t bits = c.numlenbits + (uint32_t)floorlog2((int32_t)take);
                     if (bits > 32) return -1;  // "too many bits in segment length", T2.cpp:590-593
                     const uint32_t L = r.read(bits);
@@ -364,7 +379,7 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                     parts.push_back({&c, si, take, L});
                     c.segs[si].numpasses += take;
                     left -= take;
-                    if (left) c.segs.emplace_back();
+                    if (left) open_seg();
                 }
                 c.numpasses += np;
             }
@@ -503,8 +518,8 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
     if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
     // j2k_read_header stops at the first SOT; a stream that ends before it is truncated
     if (first_sot == 0) { err = "truncated main header (no SOT)"; return false; }
-    // mode switches: RESET, TERMALL, VSC, PTERM, SEGSYM; not BYPASS (0x01) nor HT (0x40)
-    if (cp.cblksty & ~0x3Eu) { err = "code-block mode switches BYPASS / HT not supported"; return false; }
+    // mode switches: BYPASS, RESET, TERMALL, VSC, PTERM, SEGSYM; not HT (0x40)
+    if (cp.cblksty & ~0x3Fu) { err = "HT code-block style not supported"; return false; }
     if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
     for (uint32_t k = 0; k < cp.numcomps; ++k) cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
     return true;

@@ -88,9 +88,10 @@ struct Cblk {
     bool included = false;
     // decoder: codeword segments (grk_tcd_seg): passes, bytes and the chunks
     // (offset into the codestream, length) holding them.  One segment unless
-    // the code-block style terminates passes (TERMALL: one per pass).
+    // the code-block style terminates passes (TERMALL: one per pass; BYPASS:
+    // 10 passes, then raw / MQ segments of 2 and 1).
     struct Seg {
-        uint32_t numpasses = 0, len = 0;
+        uint32_t numpasses = 0, len = 0, maxpasses = 109;
         std::vector<std::pair<uint64_t, uint32_t>> chunks;
     };
     std::vector<Seg> segs;

@@ -171,7 +171,7 @@ uint32_t cdivpow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + (1u
 // codestream/j2k.cpp:1609-2050); false for options outside grk_mi355x.h
 bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p) {
     grkgpu_default_cparams(p);
-    if (g->cblk_sty & ~0x3Eu) { GRK_ERROR("code-block style 0x%x: BYPASS / HT are not supported", g->cblk_sty); return false; }
+    if (g->cblk_sty & ~0x3Fu) { GRK_ERROR("code-block style 0x%x: HT is not supported", g->cblk_sty); return false; }
     if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
     if (g->roi_compno >= 0) { GRK_ERROR("ROI is not supported"); return false; }
     if (g->tcp_mct == 2 || g->mct_data) { GRK_ERROR("custom MCT is not supported"); return false; }

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
     uint8_t *base = sym + off + (uint64_t)p * slot;
     t1_model_plane(b.w, b.h, b.orient, S.pa + p * 64, S.pb + p * 64, p + 1 < numbps ? S.pb + (p + 1) * 64 : nullptr,
                    S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4,
-                   cblksty);
+                   cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps));
 }
 
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words

@@ -133,7 +133,32 @@ struct BitDec {
     FlatBits bits;
     uint32_t A, C, consumed, cq;
     const uint32_t *cp;
+    bool raw;  // the current segment is raw (BYPASS): bits straight from the stream
+    // raw segment (mqc_raw_init_dec / mqc_raw_decode, mqc_dec.cpp:195-200,
+    // mqc_dec_inl.h:90-112): the unstuffed stream IS the raw bit sequence --
+    // 7 bits from the byte after a 0xFF, 1-bits from a marker on
+    GRK_HD void init_raw(const uint32_t *words, uint32_t nwords) {
+        bits.base = (const uint4 *)words;
+        bits.nchunks = (nwords + 3) >> 2;
+        bits.cur = fb_load(bits, 0);
+        bits.chunk = 0;
+        bits.wi = 0;
+        const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
+        bits.W = (w0 << 32) | w1;
+        bits.NB = 64;
+        raw = true;
+    }
+    GRK_HD uint32_t rawbit() {
+        const uint32_t b = (uint32_t)(bits.W >> 63);
+        bits.W <<= 1;
+        if (--bits.NB < 32) {
+            bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
+            bits.NB += 32;
+        }
+        return b;
+    }
     GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
+        raw = false;
         bits.base = (const uint4 *)words;
         bits.nchunks = (nwords + 3) >> 2;
         bits.cur = fb_load(bits, 0);
@@ -151,6 +176,7 @@ struct BitDec {
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
     }
     GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
+        if (raw) return rawbit();
         const uint32_t wd = cxw[cx];
         const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
         uint32_t a = A - qe;
@@ -196,11 +222,13 @@ struct SegCursor {
     const DecSeg *seg;
     const uint32_t *ubuf;
     uint32_t nseg, cur, next;
-    template <class D> GRK_HD void at_pass(D &d, uint32_t passno) {
+    // raw: the segment starting here is a BYPASS (raw) one (t1.cpp:1070-1080)
+    template <class D> GRK_HD void at_pass(D &d, uint32_t passno, bool raw) {
         if (passno != next || cur + 1 >= nseg) return;
         ++cur;
         const uint32_t *region = ubuf + (size_t)seg[cur].ub_off * 4;
-        d.init(region + 4, region[0], region + 4 + unstuff_word_cap(seg[cur].len));
+        if (raw) d.init_raw(region + 4, region[0]);
+        else d.init(region + 4, region[0], region + 4 + unstuff_word_cap(seg[cur].len));
         next += seg[cur].npasses;
     }
 };

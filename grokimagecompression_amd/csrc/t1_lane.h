@@ -87,8 +87,26 @@ GRK_HD uint64_t dil(uint64_t m) { return m | (m << 1) | (m >> 1); }
 
 // code-block style bits (COD SPcod, grok.h GRK_CBLKSTY_*): the mode switches
 // this coder takes (BYPASS 0x01 and HT 0x40 are rejected by the host)
-constexpr uint32_t CBLKSTY_RESET = 0x02, CBLKSTY_TERMALL = 0x04, CBLKSTY_VSC = 0x08, CBLKSTY_PTERM = 0x10,
-                   CBLKSTY_SEGSYM = 0x20;
+constexpr uint32_t CBLKSTY_LAZY = 0x01, CBLKSTY_RESET = 0x02, CBLKSTY_TERMALL = 0x04, CBLKSTY_VSC = 0x08,
+                   CBLKSTY_PTERM = 0x10, CBLKSTY_SEGSYM = 0x20;
+
+// Pass classification of t1_encode_cblk / t1_decode_cblk: BYPASS (LAZY)
+// codes the significance and refinement passes below the four most
+// significant bit-planes raw (t1.cpp:1223-1225, 1070-1072), and
+// t1_enc_is_term_pass (t1.cpp:1131-1151) decides which passes end a codeword
+// segment.
+GRK_HD bool t1_pass_raw(uint32_t sty, int32_t bpno, int passtype, uint32_t numbps) {
+    return (sty & CBLKSTY_LAZY) && bpno < (int32_t)numbps - 4 && passtype < 2;
+}
+GRK_HD bool t1_pass_term(uint32_t sty, int32_t bpno, int passtype, uint32_t numbps) {
+    if (passtype == 2 && bpno == 0) return true;
+    if (sty & CBLKSTY_TERMALL) return true;
+    if (sty & CBLKSTY_LAZY) {
+        if (bpno == (int32_t)numbps - 4 && passtype == 2) return true;
+        if (bpno < (int32_t)numbps - 4 && passtype > 0) return true;
+    }
+    return false;
+}
 
 // MQ context registers are 32-bit words: the packed table entry of the
 // current state (Qe | NMPS<<16 | NLPS<<22 | SWITCH<<28) | MPS<<31, so one LDS
@@ -186,27 +204,80 @@ GRK_HD void mqel_erterm(MqEncLane &e) {
     if (e.cur != 0xff) mqel_byteout(e);
 }
 
-// Restart after a terminated pass (mqc_restart_init_enc, mqc_enc.cpp:366-382):
-// INITENC again with bp stepped back onto the segment's last counted byte,
-// which becomes the carry target again.  That byte is already committed: in
-// `acc` when it shares bp's dword, else in `out` (reloaded into acc).
-GRK_HD void mqel_restart(MqEncLane &e) {
+// The byte at position pos (< bp): committed, in `acc` when it shares bp's
+// dword, else in `out`.
+GRK_HD uint32_t mqel_byte_at(const MqEncLane &e, int32_t pos) {
+    if (pos < 0) return 0;  // the zero pad byte before the block
+    if ((pos >> 2) == (e.bp >> 2)) return (e.acc >> ((pos & 3) * 8)) & 0xffu;
+    return (e.out[pos >> 2] >> ((pos & 3) * 8)) & 0xffu;
+}
+
+// bp-- (the reference steps its byte pointer back in a few terminations):
+// the byte there becomes `cur` again, and acc is reloaded when bp crosses
+// back into the previous (already stored) dword.
+GRK_HD void mqel_step_back(MqEncLane &e) {
     const int32_t nb = e.bp - 1;
-    uint32_t byte;
-    if (nb < 0) {  // the zero pad byte before the block (a first pass that wrote nothing counted)
-        byte = 0;
+    if (nb < 0) {
+        e.cur = 0;
         e.acc = 0;
-    } else if ((nb >> 2) == (e.bp >> 2)) {
-        byte = (e.acc >> ((nb & 3) * 8)) & 0xffu;
-    } else {  // nb is the last byte of the previous dword, already stored
-        e.acc = e.out[nb >> 2];
-        byte = e.acc >> 24;
+    } else {
+        if ((nb >> 2) != (e.bp >> 2)) e.acc = e.out[nb >> 2];
+        e.cur = (e.acc >> ((nb & 3) * 8)) & 0xffu;
     }
     e.bp = nb;
-    e.cur = byte;
+}
+
+// Restart after a terminated pass (mqc_restart_init_enc, mqc_enc.cpp:366-382):
+// INITENC again with bp stepped back onto the segment's last counted byte,
+// which becomes the carry target again.
+GRK_HD void mqel_restart(MqEncLane &e) {
+    mqel_step_back(e);
     e.a = 0x8000;
     e.c = 0;
-    e.ct = byte == 0xff ? 13u : 12u;
+    e.ct = e.cur == 0xff ? 13u : 12u;
+}
+
+// ---- raw (BYPASS) coding, mqc_enc.cpp:264-364 ----
+constexpr uint32_t BYPASS_CT_INIT = 0xDEADBEEFu;  // "no raw bit coded yet"
+
+GRK_HD void mqel_bypass_init(MqEncLane &e) {  // mqc_bypass_init_enc: bp stays
+    e.c = 0;
+    e.ct = BYPASS_CT_INIT;
+}
+
+GRK_HD void mqel_bypass(MqEncLane &e, uint32_t d) {  // mqc_bypass_enc
+    if (e.ct == BYPASS_CT_INIT) e.ct = 8;
+    e.ct--;
+    e.c += d << e.ct;
+    if (e.ct == 0) {
+        e.cur = e.c & 0xffu;  // *bp = c
+        e.ct = e.cur == 0xff ? 7u : 8u;
+        mqel_emit(e, 0);      // bp++
+        e.c = 0;
+    }
+}
+
+GRK_HD uint32_t mqel_bypass_extra(const MqEncLane &e, bool erterm) {  // mqc_bypass_get_extra_bytes_enc
+    return (e.ct < 7 || (e.ct == 7 && (erterm || mqel_byte_at(e, e.bp - 1) != 0xff))) ? 2u : 1u;
+}
+
+GRK_HD void mqel_bypass_flush(MqEncLane &e, bool erterm) {  // mqc_bypass_flush_enc
+    const uint32_t prev = mqel_byte_at(e, e.bp - 1);
+    if (e.ct < 7 || (e.ct == 7 && (erterm || prev != 0xff))) {
+        uint32_t bit = 0;  // fill the remaining bits with 0 1 0 1 ...
+        while (e.ct > 0) {
+            e.ct--;
+            e.c += bit << e.ct;
+            bit = 1u - bit;
+        }
+        e.cur = e.c & 0xffu;
+        mqel_emit(e, 0);
+    } else if (e.ct == 7 && prev == 0xff) {  // discard the last 0xFF
+        mqel_step_back(e);
+    } else if (e.ct == 8 && !erterm && prev == 0x7f && mqel_byte_at(e, e.bp - 2) == 0xff) {
+        mqel_step_back(e);  // discard a terminating 0xFF 0x7F
+        mqel_step_back(e);
+    }
 }
 
 GRK_HD void mqel_finish(MqEncLane &e, uint32_t len) {
@@ -451,26 +522,39 @@ struct LaneEncoder {
     const uint32_t *tab;
     const uint64_t *planes, *pl;
     uint32_t *rate;
-    uint32_t sty = 0;  // CBLKSTY_* mode switches
+    uint32_t sty = 0;     // CBLKSTY_* mode switches
+    uint32_t numbps = 0;
+    bool raw = false;     // the current pass is coded raw (BYPASS)
     GRK_HD void begin_pass(int32_t bpno) { pl = planes + (uint32_t)bpno * 64; }
     GRK_HD uint64_t stripe_bits(uint32_t y, uint32_t h) const { return y < h ? pl[y] : 0; }
     GRK_HD uint32_t code(uint32_t cx, uint32_t v) { mqel_encode(e, cxw, tab, cx, v); return v; }
     GRK_HD void end_stripe(uint32_t, uint32_t, int, const Stripe &) {}
-    // t1_encode_cblk's pass end (t1.cpp:1256-1298): a terminated pass (the
-    // last one; every one under TERMALL) is flushed -- ERTERM under PTERM --
-    // and the coder restarts for the next; else the rate gets the
+    // t1_encode_cblk's pass end (t1.cpp:1256-1298) and the next pass's start
+    // (:1222-1233): a terminated pass is flushed -- ERTERM under PTERM, the
+    // raw flush for a raw pass -- and the coder restarts (MQ) or re-enters
+    // raw mode for the next pass; a pass that is not terminated gets the
     // rate_extra_bytes correction.  RESET re-initialises the contexts.
     GRK_HD void end_pass(uint32_t passno, int passtype, int32_t bpno) {
         const bool last = passtype == 2 && bpno == 0;
-        if (last || (sty & CBLKSTY_TERMALL)) {
-            if (sty & CBLKSTY_PTERM) mqel_erterm(e);
+        int nt = passtype + 1;
+        int32_t nb = bpno;
+        if (nt == 3) { nt = 0; nb--; }
+        const bool next_raw = t1_pass_raw(sty, nb, nt, numbps);
+        const bool pterm = (sty & CBLKSTY_PTERM) != 0;
+        if (t1_pass_term(sty, bpno, passtype, numbps)) {
+            if (raw) mqel_bypass_flush(e, pterm);
+            else if (pterm) mqel_erterm(e);
             else mqel_flush(e);
             rate[passno] = (uint32_t)e.bp;
-            if (!last) mqel_restart(e);
+            if (!last) {
+                if (next_raw) mqel_bypass_init(e);
+                else mqel_restart(e);
+            }
         } else {
-            rate[passno] = (uint32_t)e.bp + 5 + (e.ct < 5 ? 1 : 0);
+            rate[passno] = (uint32_t)e.bp + (raw ? mqel_bypass_extra(e, pterm) : 5u + (e.ct < 5 ? 1u : 0u));
         }
         if (sty & CBLKSTY_RESET) mq_reset_words(cxw, tab);
+        raw = next_raw;
     }
 };
 
@@ -615,12 +699,13 @@ GRK_HD uint32_t ctx_at(const Ctx4 &c, uint32_t x) {
 
 // sign symbol for sample x: W/E/N/S significance masks already aligned to x
 GRK_HD uint32_t sc_symbol(const uint8_t *sc, uint64_t sW, uint64_t nW, uint64_t sE, uint64_t nE, uint64_t sN,
-                          uint64_t nN, uint64_t sS, uint64_t nS, uint64_t neg, uint32_t x) {
+                          uint64_t nN, uint64_t sS, uint64_t nS, uint64_t neg, uint32_t x, bool raw = false) {
     uint32_t i = (uint32_t)((sW >> x) & 1) | (uint32_t)((nW >> x) & 1) << 1 | (uint32_t)((sE >> x) & 1) << 2 |
                  (uint32_t)((nE >> x) & 1) << 3 | (uint32_t)((sN >> x) & 1) << 4 | (uint32_t)((nN >> x) & 1) << 5 |
                  (uint32_t)((sS >> x) & 1) << 6 | (uint32_t)((nS >> x) & 1) << 7;
     uint32_t si = sc[i];
-    return (si & 0x7f) | ((((uint32_t)(neg >> x) & 1u) ^ (si >> 7)) << 5);
+    // a raw (BYPASS) pass codes the sign itself, not its XOR with the prediction (t1.cpp:221-222)
+    return (si & 0x7f) | ((((uint32_t)(neg >> x) & 1u) ^ (raw ? 0u : (si >> 7))) << 5);
 }
 
 GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0 && (uint32_t)y < h) ? a[y] : 0; }
@@ -638,7 +723,7 @@ GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0
 // 1 0 1 0 in the uniform context (mqc_segmark_enc, t1.cpp:1244-1245).
 GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64_t *bitp, const uint64_t *above,
                            const uint64_t *ref, const uint64_t *negr, uint64_t *tmp, const uint8_t *sc,
-                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0) {
+                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0, bool raw_spp = false) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     const bool vsc = (cblksty & CBLKSTY_VSC) != 0;
     uint64_t *postS = tmp, *visS = tmp + 64;
@@ -701,7 +786,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
                 if (s) {
                     const uint64_t up = r == 0 ? U : post[r - 1], dn = r == 3 ? D : pre[r + 1];
                     so.put(sc_symbol(sc, post[r] << 1, ng[r + 1] << 1, pre[r] >> 1, ng[r + 1] >> 1, up, ng[r], dn,
-                                     ng[r + 2], ng[r + 1], x));
+                                     ng[r + 2], ng[r + 1], x, raw_spp));
                 }
             }
         }
@@ -864,6 +949,7 @@ GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_
     if (numbps == 0) return 0;
     LaneEncoder cd;
     cd.sty = cblksty;
+    cd.numbps = numbps;
     mq_reset_words(cxw, tab);
     cd.e.a = 0x8000; cd.e.c = 0; cd.e.ct = 12; cd.e.bp = -1; cd.e.cur = 0; cd.e.acc = 0; cd.e.out = out;
     cd.cxw = cxw; cd.tab = tab; cd.rate = rate;
@@ -892,10 +978,14 @@ GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_
         const uint32_t b = cur & 0xff;                                    \
         cur >>= 8;                                                        \
         ++i;                                                              \
-        const uint32_t wn = cxw[cur & 31];                                \
-        const uint32_t nw = mqel_step(cd.e, tab, w, b >> 5);              \
-        cxw[b & 31] = nw;                                                 \
-        w = (((cur ^ b) & 31) == 0) ? nw : wn;                            \
+        if (cd.raw) {                                                     \
+            mqel_bypass(cd.e, b >> 5);                                    \
+        } else {                                                          \
+            const uint32_t wn = cxw[cur & 31];                            \
+            const uint32_t nw = mqel_step(cd.e, tab, w, b >> 5);          \
+            cxw[b & 31] = nw;                                             \
+            w = (((cur ^ b) & 31) == 0) ? nw : wn;                        \
+        }                                                                 \
         if (i == bnd) {                                                   \
             do {                                                          \
                 cd.end_pass(passno++, t, p);                              \

@@ -112,8 +112,8 @@ typedef struct {
     uint32_t rsiz;
     uint32_t framerate;
     uint64_t max_cs_size, max_comp_size;
-    /* code-block style (-M): 0x02 RESET, 0x04 TERMALL (restart), 0x08 VSC,
-     * 0x10 PTERM (ERTERM), 0x20 SEGSYM; BYPASS (0x01) is not supported */
+    /* code-block style (-M): 0x01 BYPASS (lazy), 0x02 RESET, 0x04 TERMALL
+     * (restart), 0x08 VSC, 0x10 PTERM (ERTERM), 0x20 SEGSYM */
     uint32_t cblk_sty;
     uint32_t pad_;
 } grkgpu_cparams;

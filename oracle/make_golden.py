@@ -118,6 +118,14 @@ CASES = [
     ("rgb12_M46_tiles", (150, 200, 3, 12), "smooth", 97, ["-M", "46", "-t", "64,64"]),
     ("g12_M4_layers", (70, 90, 1, 12), "smooth", 99, ["-M", "4", "-r", "16,4,1"]),
     ("g8_M42_b16", (100, 130, 1, 8), "smooth", 100, ["-M", "42", "-b", "16,16", "-r", "12,3"]),
+    # BYPASS (-M 1): raw significance / refinement passes below the top four bit-planes
+    ("g8_M1_lazy", (96, 128, 1, 8), "smooth", 101, ["-M", "1"]),
+    ("g12_M1_lazy", (70, 90, 1, 12), "uniform", 102, ["-M", "1"]),
+    ("rgb8_M1_I_r", (96, 128, 3, 8), "smooth", 103, ["-M", "1", "-I", "-r", "20,5"]),
+    ("g16_M5_lazy_termall", (64, 64, 1, 16), "smooth", 104, ["-M", "5"]),
+    ("g12_M17_lazy_pterm", (70, 90, 1, 12), "uniform", 105, ["-M", "17"]),
+    ("g12_M63", (70, 90, 1, 12), "smooth", 106, ["-M", "63"]),
+    ("g16_M3_lazy_reset", (64, 64, 1, 16), "uniform", 107, ["-M", "3", "-r", "8,2,1"]),
 ]
 
 # Reference decodes with grk_decompress options (-l layers, -r reduce), per
@@ -144,6 +152,8 @@ DEC_VARIANTS = {
     "g16_I": [["-r", "3"]],
     "g12_M4_layers": [["-l", "1"], ["-l", "2"]],
     "rgb8_M62_I_r": [["-l", "1"], ["-r", "1"]],
+    "g16_M3_lazy_reset": [["-l", "1"], ["-l", "2"]],
+    "rgb8_M1_I_r": [["-l", "1"]],
 }
 
 

@@ -90,7 +90,7 @@ def test_cod_qcd_field_checks():
     _rejects(_patch(cs, p + 2, ">H", 0))              # zero layers
     _rejects(_patch(cs, p + 5, ">B", 33))             # 34 resolutions
     _rejects(_patch(cs, p + 6, ">B", 9))              # 2^11-wide code-blocks
-    _rejects(_patch(cs, p + 8, ">B", 1))              # BYPASS mode switch
+    _rejects(_patch(cs, p + 8, ">B", 0x40))           # HT code-block style
     _rejects(_patch(cs, p + 9, ">B", 2))              # qmfbid 2
     _rejects(_patch(cs, p, ">B", 1))                  # Scod: user precincts, but no precinct sizes
     _rejects(_patch(cs, p, ">B", 8))                  # unknown Scod bit
