@@ -210,7 +210,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
 
 // MQ coding, one lane per block (lane j codes block perm[j], or j).
-template <int LANES, int MINW = 1>
+template <int LANES, int MINW = 1, bool LAZY = false>
 __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
                                                  const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     uint32_t cap;
     const uint64_t off = sym_block_off(sym_off, i, &cap);
     uint32_t len;
-    uint32_t np = t1_mq_block(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
+    uint32_t np = t1_mq_block<LAZY>(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
                               s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len, cblksty);
     r.numpasses = np;
     r.len = len;
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     unstuff_segment(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words));
 }
 
-template <int LANES>
+template <int LANES, bool LAZY = false>
 __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
                                                         T1Scratch *__restrict__ scr, const DecSeg *__restrict__ segs,
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
         const uint32_t *region = ubuf + (size_t)s0.ub_off * 4;
         for (uint32_t y = 0; y < b.h + 2; ++y) { S.st.sig[y] = 0; S.st.neg[y] = 0; S.st.vis[y] = 0; S.st.ref[y] = 0; }
         mq_reset_words(cxw, T.mq);
-        BitDec d;
+        BitDecT<LAZY> d;
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
         SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
         t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, S.st, T, cxw, S.pa, S.pb, sty, cur);
@@ -514,8 +514,12 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res, cblksty);
-    hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s, blocks, n,
-                       scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
+    if (cblksty & CBLKSTY_LAZY)
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s,
+                           blocks, n, scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
+    else
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s,
+                           blocks, n, scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
     return hipGetLastError();
 }
 
@@ -553,8 +557,12 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
                        seg_first);
-    hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0, s,
-                       blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
+    if (cblksty & CBLKSTY_LAZY)
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
+                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
+    else
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
+                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
     hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
     return hipGetLastError();
 }

@@ -37,7 +37,7 @@ struct Dec3;
 GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx);
 
 struct Dec3 {
-    static constexpr bool raw = false;  // byte-level decoder: MQ segments only
+    static constexpr bool kLazy = false, raw = false;  // byte-level decoder: MQ segments only
     uint32_t a, c, ct;
     uint32_t cur, nxt;  // code bytes at bp and bp + 1
     const uint4 *p;     // next chunk to load
@@ -191,7 +191,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;
         if (!CUP) newvis |= k0 ? 1u << r : 0u;
         // SC: the sample is significant with sign sg
-        const uint32_t sg = bit ^ (d.raw ? 0u : (si >> 7));  // a raw sign is the sign itself
+        const uint32_t sg = bit ^ ((D::kLazy && d.raw) ? 0u : (si >> 7));  // a raw sign is the sign itself
         P |= k1 ? 1u << (sh + 4) : 0u;
         Q |= k1 ? sg << (sh + 4) : 0u;
         newsig |= k1 ? 1u << r : 0u;
@@ -333,7 +333,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
         }
         if (passtype == 2 && (sty & CBLKSTY_SEGSYM))
             for (int q = 0; q < 4; ++q) d.decode(cxw, T.mq, CX_UNI);
-        if ((sty & CBLKSTY_RESET) && !d.raw) mq_reset_words(cxw, T.mq);  // after MQ passes (t1.cpp:1104-1105)
+        if ((sty & CBLKSTY_RESET) && !(D::kLazy && d.raw)) mq_reset_words(cxw, T.mq);  // after MQ passes (t1.cpp:1104-1105)
         if (++passtype == 3) { passtype = 0; bpno--; }
     }
 }

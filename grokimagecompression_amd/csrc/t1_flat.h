@@ -129,7 +129,11 @@ GRK_HD uint32_t fb_word(FlatBits &b) {
 // MQ decoder over the unstuffed stream (used by the nested-loop decoder v5
 // in t1_dec.h and by t1_decode_flat): branch-free renormalisation.
 // ---------------------------------------------------------------------------
-struct BitDec {
+// LAZY: the decoder may meet raw (BYPASS) segments; compiled out otherwise,
+// so the common case keeps its per-symbol path branch-free.
+template <bool LAZY>
+struct BitDecT {
+    static constexpr bool kLazy = LAZY;
     FlatBits bits;
     uint32_t A, C, consumed, cq;
     const uint32_t *cp;
@@ -176,7 +180,9 @@ struct BitDec {
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
     }
     GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
-        if (raw) return rawbit();
+        if constexpr (LAZY) {
+            if (raw) return rawbit();
+        }
         const uint32_t wd = cxw[cx];
         const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
         uint32_t a = A - qe;
@@ -207,6 +213,7 @@ struct BitDec {
         return mps ^ (uint32_t)lps;
     }
 };
+using BitDec = BitDecT<false>;
 
 // One codeword segment of a code-block (grk_tcd_seg): its bytes in the data
 // buffer, its passes, and where its unstuffed stream lives (16-byte units).

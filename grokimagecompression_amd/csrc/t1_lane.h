@@ -942,6 +942,7 @@ GRK_HD uint32_t mqel_step(MqEncLane &e, const uint32_t *tab, uint32_t w, uint32_
     return keep ? w : (tw | (nmps << 31));
 }
 
+template <bool LAZY = false>
 GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_words, const uint32_t *cnt,
                             const uint32_t *tab, uint32_t *cxw, uint32_t *out, uint32_t *rate, uint32_t *len_out,
                             uint32_t cblksty = 0) {
@@ -978,7 +979,7 @@ GRK_HD uint32_t t1_mq_block(uint32_t numbps, const uint32_t *sym, uint32_t slot_
         const uint32_t b = cur & 0xff;                                    \
         cur >>= 8;                                                        \
         ++i;                                                              \
-        if (cd.raw) {                                                     \
+        if (LAZY && cd.raw) {                                             \
             mqel_bypass(cd.e, b >> 5);                                    \
         } else {                                                          \
             const uint32_t wn = cxw[cur & 31];                            \
