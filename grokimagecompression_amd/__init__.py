@@ -65,7 +65,8 @@ class CParams(ctypes.Structure):
                 ("prch_init", ctypes.c_uint32 * 33), ("prog_order", ctypes.c_int32), ("numpocs", ctypes.c_uint32),
                 ("POC", Poc * 32), ("tp_on", ctypes.c_int32), ("tp_flag", ctypes.c_int32), ("rsiz", ctypes.c_uint32),
                 ("framerate", ctypes.c_uint32), ("max_cs_size", ctypes.c_uint64), ("max_comp_size", ctypes.c_uint64),
-                ("cblk_sty", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]
+                ("cblk_sty", ctypes.c_uint32), ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
+                ("pad_", ctypes.c_uint32)]
 
     @classmethod
     def make(cls, numresolution=6, cblk=(64, 64), irreversible=False, mct=-1, tiles=None, tile_offset=(0, 0)):
@@ -114,6 +115,9 @@ class CParams(ctypes.Structure):
                     off = tuple(int(x) for x in v.split(","))
                 elif a == "-p":
                     p.prog_order = PROGS[v[:4]]
+                elif a in ("-R", "-ROI"):  # c=<comp>,U=<shift> (grk_compress.cpp:1470-1476)
+                    kv = dict(x.split("=") for x in v.split(","))
+                    p.roi_compno, p.roi_shift = int(kv["c"]), int(kv["U"])
                 elif a == "-M":  # code-block mode switches (grk_compress.cpp:1132)
                     p.cblk_sty = int(v) & 0x7F
                 elif a == "-A":

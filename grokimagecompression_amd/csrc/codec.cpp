@@ -260,6 +260,12 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     // BYPASS, RESET, TERMALL, VSC, PTERM, SEGSYM; not HT (0x40)
     if (p->cblk_sty & ~0x3Fu) return set_err(GRKGPU_EUNSUPPORTED, "HT code-block style not supported");
     cp.cblksty = p->cblk_sty;
+    if (p->roi_shift) {  // j2k_setup_encoder (j2k.cpp:1997-2001)
+        if (p->roi_compno < 0 || (uint32_t)p->roi_compno >= img->numcomps)
+            return set_err(GRKGPU_EINVAL, "ROI component out of range");
+        if (p->roi_shift > 255) return set_err(GRKGPU_EINVAL, "ROI shift must fit a byte");
+        cp.roishift[p->roi_compno] = (uint8_t)p->roi_shift;
+    }
     if (p->tcp_numlayers == 0) {
         p->tcp_rates[0] = 0;
         p->tcp_numlayers = 1;
@@ -1280,6 +1286,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     std::vector<uint64_t> lloff(nsh * nc);
     std::vector<DecBlock> db;
     std::vector<DecSeg> dsegs;        // codeword segments of all blocks
+    std::vector<uint8_t> droi;        // per-block ROI shift (empty: no ROI)
+    bool any_roi = false;
+    for (uint32_t k = 0; k < cp.numcomps; ++k) any_roi = any_roi || cp.roishift[k];
     std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     std::vector<uint8_t> tilebuf;
@@ -1371,6 +1380,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     dsegs.push_back(ds);
                 }
                 d.data_off = cb.segs.empty() ? 0 : dsegs[seg_first.back()].data_off;
+                if (any_roi) droi.push_back(cp.roishift[k]);
                 // no bytes: the block stays zero (T1Part1::decode returns before
                 // t1_decode_cblk when the block has no data, T1Part1.cpp:139-140)
                 if (!d.len) d.numpasses = 0;
@@ -1393,11 +1403,12 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         uwords += t1_unstuff_region_words(sg.len);
     }
     if (uwords / 4 > 0xffffffffull) return set_err(GRKGPU_EUNSUPPORTED, "codestream too large for one call");
-    const size_t segbytes = dsegs.size() * sizeof(DecSeg), sfbytes = seg_first.size() * 4;
-    HIPCHK(c->segs.ensure(segbytes + sfbytes + 256));
-    HIPCHK(c->h_segs.ensure(segbytes + sfbytes + 256));
+    const size_t segbytes = dsegs.size() * sizeof(DecSeg), sfbytes = seg_first.size() * 4, roibytes = droi.size();
+    HIPCHK(c->segs.ensure(segbytes + sfbytes + roibytes + 256));
+    HIPCHK(c->h_segs.ensure(segbytes + sfbytes + roibytes + 256));
     memcpy(c->h_segs.p, dsegs.data(), segbytes);
     memcpy((uint8_t *)c->h_segs.p + segbytes, seg_first.data(), sfbytes);
+    if (roibytes) memcpy((uint8_t *)c->h_segs.p + segbytes + sfbytes, droi.data(), roibytes);
     HIPCHK(c->ubuf.ensure(uwords * 4 + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
     HIPCHK(c->h_blocks.ensure((size_t)nblk * sizeof(DecBlock) + 256));
@@ -1411,7 +1422,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         HIPCHK(hipMemcpyAsync(c->cs.as<uint8_t>() + len, c->h_packed.p, extra.size(), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.p, segbytes + sfbytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.p, segbytes + sfbytes + roibytes, hipMemcpyHostToDevice, s));
     DwtPlan dplan;
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < tile.comps.size(); ++k) {
@@ -1427,7 +1438,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
                             c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(), 0, c->segs.as<DecSeg>(),
-                            (const uint32_t *)(c->segs.as<uint8_t>() + segbytes), cp.cblksty));
+                            (const uint32_t *)(c->segs.as<uint8_t>() + segbytes), cp.cblksty,
+                            roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes : nullptr));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
     HIPCHK(hipEventRecord(c->ev[3], s));

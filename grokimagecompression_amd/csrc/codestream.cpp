@@ -159,7 +159,7 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
             const StepSize &st = cp.ss[off + bandno];
             b.stepsize = (float)((1.0 + st.mant / 2048.0) * std::pow(2.0, (int32_t)(numbps - st.expn))) *
                          (encoder ? 1.0f : 0.5f);
-            b.numbps = st.expn + 2 - 1;  // guard bits 2 (j2k.cpp:1834)
+            b.numbps = cp.roishift[compno] + st.expn + 2 - 1;  // guard bits 2 (j2k.cpp:1834), + ROI (Quantizer.cpp:90-93)
             b.inv_step = (uint32_t)((8192.0 / b.stepsize) + 0.5f);
             uint32_t np = res.pw * res.ph;
             b.precs.assign(np, Precinct());
@@ -239,6 +239,15 @@ void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at, uint
         if (tlm_at) *tlm_at = cs.size();
         for (uint32_t i = 0; i < 5 * total_tile_parts; ++i) cs.put8(0);
         if (cp.rsiz == RSIZ_CINEMA_4K) write_poc(cs, cp);  // main-header POC (j2k.cpp:2353-2356)
+    }
+    // RGN per ROI component (j2k_write_regions / j2k_write_rgn, j2k.cpp:5482-5531, 5687-5706):
+    // Crgn (1 or 2 bytes), Srgn 0, SPrgn = roishift
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        if (!cp.roishift[k]) continue;
+        const uint32_t room = cp.numcomps <= 256 ? 1 : 2;
+        cs.put16(0xFF5E); cs.put16(4 + room);
+        if (room == 2) cs.put16(k); else cs.put8(k);
+        cs.put8(0); cs.put8(cp.roishift[k]);
     }
     static const char kCom[] = "Created by Grok     version 5.1.0";  // j2k.cpp:1798
     cs.put16(0xFF64); cs.put16(4 + (uint32_t)strlen(kCom)); cs.put16(1);
@@ -509,8 +518,15 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             have_qcd = true;
         } else if (m == 0xFF5F) {
             if (!parse_poc(p, L - 2, cp)) { err = "Error reading POC marker"; return false; }
-        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF5E || m == 0xFF60) {
-            err = "COC/QCC/RGN/PPM markers not supported";
+        } else if (m == 0xFF5E) {  // RGN (j2k_read_rgn, j2k.cpp:5555-5604)
+            if (!have_siz) { err = "RGN before SIZ"; return false; }
+            const uint32_t room = cp.numcomps <= 256 ? 1 : 2;
+            if (L - 2 != 2 + room) { err = "Error reading RGN marker"; return false; }
+            const uint32_t comp = room == 2 ? rd16(p) : p[0];
+            if (comp >= cp.numcomps) { err = "bad component number in RGN"; return false; }
+            cp.roishift[comp] = p[room + 1];  // Srgn != 0 is only a warning there
+        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF60) {
+            err = "COC/QCC/PPM markers not supported";
             return false;
         }
         pos += 2 + L;

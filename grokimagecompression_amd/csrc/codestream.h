@@ -65,6 +65,10 @@ struct CodingParams {
     double distoratio[100] = {};
     uint64_t max_cs_size = 0, max_comp_size = 0;
     uint32_t nb_tile_parts = 1;  // per tile (tcp->m_nb_tile_parts)
+    // ROI up-shift per component (tccp->roishift: grk_compress -ROI, the RGN
+    // marker, j2k.cpp:1997-2001 / 5482-5604): adds to every band's bit-plane
+    // count, and the decoder shifts decoded magnitudes >= 2^roishift down
+    uint8_t roishift[16] = {};
     CodingParams() {
         for (int i = 0; i < 33; ++i) prcw[i] = prch[i] = 15;
     }

@@ -103,10 +103,11 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 // segs / seg_first: the codeword segments of every block (block i's are
 // segs[seg_first[i] .. seg_first[i+1]), each with its own unstuffed region at
 // ubuf + ub_off * 16 bytes); null: one segment per block at blocks[i].data_off.
-// cblksty: CBLKSTY_* mode switches.
+// cblksty: CBLKSTY_* mode switches; roi: per-block ROI shift (null: none).
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words,
-                            const DecSeg *segs = nullptr, const uint32_t *seg_first = nullptr, uint32_t cblksty = 0);
+                            const DecSeg *segs = nullptr, const uint32_t *seg_first = nullptr, uint32_t cblksty = 0,
+                            const uint8_t *roi = nullptr);
 // 32-bit words of a block's unstuffed-stream region (header + words + carries)
 inline uint32_t t1_unstuff_region_words(uint32_t len) { return 4 + unstuff_word_cap(len) + unstuff_carry_cap(len); }
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,

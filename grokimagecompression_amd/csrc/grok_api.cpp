@@ -173,7 +173,6 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     grkgpu_default_cparams(p);
     if (g->cblk_sty & ~0x3Fu) { GRK_ERROR("code-block style 0x%x: HT is not supported", g->cblk_sty); return false; }
     if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
-    if (g->roi_compno >= 0) { GRK_ERROR("ROI is not supported"); return false; }
     if (g->tcp_mct == 2 || g->mct_data) { GRK_ERROR("custom MCT is not supported"); return false; }
     if (g->subsampling_dx != 1 || g->subsampling_dy != 1) { GRK_ERROR("subsampling is not supported"); return false; }
     p->numresolution = g->numresolution;
@@ -213,6 +212,10 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     p->max_cs_size = g->max_cs_size;
     p->max_comp_size = g->max_comp_size;
     p->cblk_sty = g->cblk_sty;
+    if (g->roi_compno >= 0) {
+        p->roi_compno = g->roi_compno;
+        p->roi_shift = g->roi_shift;
+    }
     return true;
 }
 

@@ -379,7 +379,8 @@ template <int LANES, bool LAZY = false>
 __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
                                                         T1Scratch *__restrict__ scr, const DecSeg *__restrict__ segs,
-                                                        const uint32_t *__restrict__ seg_first, uint32_t sty) {
+                                                        const uint32_t *__restrict__ seg_first, uint32_t sty,
+                                                        const uint8_t *__restrict__ roi) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
         BitDecT<LAZY> d;
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
         SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
-        t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, S.st, T, cxw, S.pa, S.pb, sty, cur);
+        t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, S.st, T, cxw, S.pa, S.pb, sty, cur, roi ? roi[i] : 0u);
         return;
     }
     const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
@@ -415,8 +416,12 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
 // One workgroup per block, lane = column: values from the bit-plane rows
 // (staged in LDS, broadcast reads), then T1Part1::postDecode scaling
 // (5/3: v/2, 9/7: float(v) * step) and a coalesced row store.
+// roi (null: none): per-block ROI up-shift -- T1Part1::post_decode
+// (T1Part1.cpp:230-250) shifts magnitudes >= 2^roishift down by roishift
+// (and zeroes the block for a shift >= 31) before the scaling.
 __global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ blocks,
-                                                   const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles) {
+                                                   const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles,
+                                                   const uint8_t *__restrict__ roi) {
     __shared__ uint64_t s_sig[32 * 64];
     __shared__ uint64_t s_ref[32 * 64];
     __shared__ uint64_t s_neg[64];
@@ -424,6 +429,7 @@ __global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ 
     const DecBlock b = blocks[i];
     const DecodedPlanes dp = decoded_planes(b.len ? b.numpasses : 0, b.numbps);
     const T1Scratch &S = scr[i];
+    const uint32_t rs = roi ? roi[i] : 0u;
     const uint32_t h = b.h;
     for (int32_t q = dp.low; q <= dp.top; ++q)
         if (x < h) s_sig[q * 64 + x] = S.pa[q * 64 + x];
@@ -445,6 +451,7 @@ __global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ 
                 for (int32_t q = p - 1; q >= ql; --q) cr = (cr << 1) | (uint32_t)((s_ref[q * 64 + y] >> x) & 1u);
                 uint32_t bits = (1u << (p - ql)) | cr;
                 int32_t mag = (int32_t)((bits << (ql + 1)) | (1u << ql));
+                if (rs) mag = rs >= 31 ? 0 : (mag >= (1 << rs) ? mag >> rs : mag);
                 v = ((s_neg[y] >> x) & 1u) ? -mag : mag;
             }
         }
@@ -553,17 +560,18 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words, const DecSeg *segs,
-                            const uint32_t *seg_first, uint32_t cblksty) {
+                            const uint32_t *seg_first, uint32_t cblksty, const uint8_t *roi) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
                        seg_first);
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
-                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
+                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi);
     else
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
-                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty);
-    hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles);
+                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
+                           nullptr);  // the ROI shift only moves BYPASS pass boundaries
+    hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles, roi);
     return hipGetLastError();
 }
 

@@ -116,7 +116,7 @@ bool map_params(const grkp_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     // block (encode_synch_with_plugin never sets pass->term), so only the
     // single-segment ones travel: RESET, VSC, PTERM, SEGSYM -- not TERMALL,
     // BYPASS or HT
-    if ((g->cblk_sty & ~0x3Au) || g->isHT || g->roi_compno >= 0) return false;
+    if ((g->cblk_sty & ~0x3Au) || g->isHT) return false;
     if (g->subsampling_dx != 1 || g->subsampling_dy != 1) return false;
     if (g->tile_size_on) return false;  // the host hands ONE plugin tile to every tile (j2k.cpp:2059-2069)
     p->cp_tx0 = g->cp_tx0;
@@ -147,6 +147,10 @@ bool map_params(const grkp_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     p->max_cs_size = g->max_cs_size;
     p->max_comp_size = g->max_comp_size;
     p->cblk_sty = g->cblk_sty;
+    if (g->roi_compno >= 0) {
+        p->roi_compno = g->roi_compno;
+        p->roi_shift = g->roi_shift;
+    }
     (void)numcomps;
     return true;
 }

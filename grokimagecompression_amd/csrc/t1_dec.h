@@ -255,13 +255,17 @@ struct NoSegs {
 template <class D, class S = NoSegs>
 GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, BlockState &st,
                              const DecTables &T, uint32_t *cxw, uint64_t *sigafter, uint64_t *refbit,
-                             uint32_t sty = 0, S segs = S()) {
+                             uint32_t sty = 0, S segs = S(), uint32_t roishift = 0) {
+    // BYPASS pass types are classified against the block's bit-planes less
+    // the ROI shift (t1_decode_cblk gets numbps - roishift, T1Part1.cpp:186,
+    // while its bit-plane counter starts at numbps, t1.cpp:1055 / 1070-1072)
+    const uint32_t rawbps = numbps - roishift;
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     const bool vsc = (sty & CBLKSTY_VSC) != 0;
     int32_t bpno = (int32_t)numbps - 1;
     int passtype = 2;
     for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
-        segs.at_pass(d, passno, t1_pass_raw(sty, bpno, passtype, numbps));
+        segs.at_pass(d, passno, t1_pass_raw(sty, bpno, passtype, rawbps));
         uint64_t *sa = sigafter + (uint32_t)bpno * 64;
         uint64_t *rb = refbit + (uint32_t)bpno * 64;
         // Each pass type loads and stores only the state rows it reads or

@@ -115,6 +115,9 @@ typedef struct {
     /* code-block style (-M): 0x01 BYPASS (lazy), 0x02 RESET, 0x04 TERMALL
      * (restart), 0x08 VSC, 0x10 PTERM (ERTERM), 0x20 SEGSYM */
     uint32_t cblk_sty;
+    /* ROI up-shift (-ROI c=compno,U=shift; the RGN marker): roi_shift 0 = none */
+    int32_t roi_compno;
+    uint32_t roi_shift;
     uint32_t pad_;
 } grkgpu_cparams;
 

@@ -126,6 +126,12 @@ CASES = [
     ("g12_M17_lazy_pterm", (70, 90, 1, 12), "uniform", 105, ["-M", "17"]),
     ("g12_M63", (70, 90, 1, 12), "smooth", 106, ["-M", "63"]),
     ("g16_M3_lazy_reset", (64, 64, 1, 16), "uniform", 107, ["-M", "3", "-r", "8,2,1"]),
+    # region of interest (-R c=<comp>,U=<shift>): RGN marker, band bit-planes
+    # raised by the shift, decoder scales magnitudes >= 2^shift back down
+    ("g8_roi_U5", (96, 128, 1, 8), "smooth", 110, ["-R", "c=0,U=5"]),
+    ("rgb8_roi_c1_I_r", (96, 128, 3, 8), "smooth", 111, ["-R", "c=1,U=7", "-I", "-r", "20,5"]),
+    ("g12_roi_M1_tiles", (130, 170, 1, 12), "uniform", 112, ["-R", "c=0,U=3", "-M", "1", "-t", "64,64"]),
+    ("rgb12_roi_c2_U12", (70, 90, 3, 12), "smooth", 113, ["-R", "c=2,U=12"]),
 ]
 
 # Reference decodes with grk_decompress options (-l layers, -r reduce), per
@@ -154,6 +160,8 @@ DEC_VARIANTS = {
     "rgb8_M62_I_r": [["-l", "1"], ["-r", "1"]],
     "g16_M3_lazy_reset": [["-l", "1"], ["-l", "2"]],
     "rgb8_M1_I_r": [["-l", "1"]],
+    "rgb8_roi_c1_I_r": [["-l", "1"], ["-r", "1"]],
+    "g8_roi_U5": [["-r", "2"]],
 }
 
 

@@ -103,6 +103,9 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
         else if (a == "-M") p->cblk_sty = (uint8_t)(atoi(v) & 0x7f);
         else if (a == "-u") { p->tp_flag = (uint8_t)v[0]; p->tp_on = 1; }
         else if (a == "-A") p->rateControlAlgorithm = (uint32_t)atoi(v);
+        else if (a == "-R") {  // grk_compress.cpp:1470-1476
+            if (sscanf(v, "c=%d,U=%u", &p->roi_compno, &p->roi_shift) != 2) return false;
+        }
         else if (a == "-r" || a == "-q") {
             double *dst = a == "-r" ? p->tcp_rates : p->tcp_distoratio;
             p->tcp_numlayers = 0;
