@@ -206,6 +206,88 @@ __device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], in
     }
 }
 
+// Vertical lifting of a window (position = window row; even rows are low pass).
+template <bool IRREV, int R>
+__device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R], int rh, int casy) {
+    if (rh > 1) {
+        if constexpr (!IRREV) {
+            vstep<0, 1>(lo); vstep<0, 1>(hi);
+            vstep<1, 0>(lo); vstep<1, 0>(hi);
+        } else {
+            vstep<2, 1>(lo); vstep<2, 1>(hi);
+            vstep<3, 0>(lo); vstep<3, 0>(hi);
+            vstep<4, 1>(lo); vstep<4, 1>(hi);
+            vstep<5, 0>(lo); vstep<5, 0>(hi);
+        }
+    } else if (!IRREV && casy) {  // single row, odd origin: S0 <<= 1 (dwt53.cpp:161)
+#pragma unroll
+        for (int r = 0; r < R; ++r) { lo[r] = (int32_t)((uint32_t)lo[r] << 1); hi[r] = (int32_t)((uint32_t)hi[r] << 1); }
+    }
+}
+
+// Horizontal lifting of the window's core rows, then the stores into the
+// LL buffer and the Mallat bands.
+template <bool IRREV, int TH, bool NOCOMP = false, int BAUX = 0>
+__device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&lo)[DwtGeo<IRREV, TH>::R],
+                                                     int32_t (&hi)[DwtGeo<IRREV, TH>::R], int ty, int yw, int gx0,
+                                                     int lane) {
+    using G = DwtGeo<IRREV, TH>;
+    const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
+    const int gx1 = gx0 + 1;
+    const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
+    const bool lane_core = lane >= corel && lane < coreh;
+    const bool okx0 = lane_core && gx0 >= 0 && gx0 < rw, okx1 = lane_core && gx1 >= 0 && gx1 < rw;
+    const int vl = okx0 ? ((gx0 - casx) >> 1) * 4 : OOB;                  // low-pass column -> L bands
+    const int vh = okx1 ? (J.snx + ((gx1 - 1 + casx) >> 1)) * 4 : OOB;     // high-pass column -> H bands
+    const rsrc_t outb = mkbuf(J.out, J.out_bytes), bandb = mkbuf(J.bands, J.bands_bytes);
+    const int ost = (int)J.out_stride * 4, bst = (int)J.bands_stride * 4;
+    // Output rows: window row r (even: low pass) of gy = yw + r goes to row
+    // lbase + r/2 of the L bands (LL | HL), odd r to row hbase + (r-1)/2 of the
+    // H bands (LH | HH); both bases are scalars (ty * TH, HALO even).
+    const int lbase = ty * (G::TH / 2) - casy - G::HALO / 2;
+    const int hbase = J.sny + ty * (G::TH / 2) - G::HALO / 2;
+    const int ylo = yw + G::HALO, yhi = ylo + G::TH;  // core rows [ylo, yhi)
+    const bool rows_all = ylo >= 0 && yhi <= rh;      // wave-uniform: no per-row checks
+#pragma unroll
+    for (int r = G::HALO; r < G::HALO + G::TH; ++r) {
+        int32_t L = lo[r], H = hi[r];
+        if (IRREV && rh > 1 && !NOCOMP) {
+            const int32_t k = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
+            L = fixmul13(L, k); H = fixmul13(H, k);
+        }
+        if (NOCOMP) {
+        } else if (rw > 1) {
+            if constexpr (!IRREV) {
+                H = lift<0>(H, L, from_next(L));
+                L = lift<1>(L, from_prev(H), H);
+            } else {
+                H = lift<2>(H, L, from_next(L));
+                L = lift<3>(L, from_prev(H), H);
+                H = lift<4>(H, L, from_next(L));
+                L = lift<5>(L, from_prev(H), H);
+                H = fixmul13(H, 5039);
+                L = fixmul13(L, 6659);
+            }
+        } else if (!IRREV && casx) {
+            L = (int32_t)((uint32_t)L << 1);
+            H = (int32_t)((uint32_t)H << 1);
+        }
+        if (!rows_all) {
+            const int gy = yw + r;
+            if (gy < 0 || gy >= rh) continue;
+        }
+        if ((r & 1) == 0) {  // low row -> LL | HL
+            const int iy = lbase + r / 2;
+            st32(L, outb, vl, iy * ost);
+            st32<BAUX>(H, bandb, vh, iy * bst);
+        } else {             // high row -> LH | HH
+            const int so = (hbase + (r - 1) / 2) * bst;
+            st32<BAUX>(L, bandb, vl, so);
+            st32<BAUX>(H, bandb, vh, so);
+        }
+    }
+}
+
 // FUSED: 0 = reads `in`; 1 = DC shift fused into the loads (fused_load);
 // 2 = the three MCT components of one window in one workgroup of 3
 // wavefronts (wavefront w = component w): each loads its own image plane,
@@ -287,82 +369,99 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
             hi[r] = mct_px<IRREV>(J, xs[0][r][2 * lane + 1], xs[1][r][2 * lane + 1], xs[2][r][2 * lane + 1]);
         }
     }
-    // vertical (position = window row; even rows are low pass)
-    if (NOCOMP) {
-    } else if (rh > 1) {
-        if constexpr (!IRREV) {
-            vstep<0, 1>(lo); vstep<0, 1>(hi);
-            vstep<1, 0>(lo); vstep<1, 0>(hi);
-        } else {
-            vstep<2, 1>(lo); vstep<2, 1>(hi);
-            vstep<3, 0>(lo); vstep<3, 0>(hi);
-            vstep<4, 1>(lo); vstep<4, 1>(hi);
-            vstep<5, 0>(lo); vstep<5, 0>(hi);
-        }
-    } else if (!IRREV && casy) {  // single row, odd origin: S0 <<= 1 (dwt53.cpp:161)
-#pragma unroll
-        for (int r = 0; r < R; ++r) { lo[r] = (int32_t)((uint32_t)lo[r] << 1); hi[r] = (int32_t)((uint32_t)hi[r] << 1); }
-    }
-    // horizontal on the core rows, then store
-    const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
-    const bool lane_core = lane >= corel && lane < coreh;
-    const bool okx0 = lane_core && gx0 >= 0 && gx0 < rw, okx1 = lane_core && gx1 >= 0 && gx1 < rw;
-    const int vl = okx0 ? ((gx0 - casx) >> 1) * 4 : OOB;                  // low-pass column -> L bands
-    const int vh = okx1 ? (J.snx + ((gx1 - 1 + casx) >> 1)) * 4 : OOB;     // high-pass column -> H bands
-    const rsrc_t outb = mkbuf(J.out, J.out_bytes), bandb = mkbuf(J.bands, J.bands_bytes);
-    const int ost = (int)J.out_stride * 4, bst = (int)J.bands_stride * 4;
-    // Output rows: window row r (even: low pass) of gy = yw + r goes to row
-    // lbase + r/2 of the L bands (LL | HL), odd r to row hbase + (r-1)/2 of the
-    // H bands (LH | HH); both bases are scalars (ty * TH, HALO even).
-    const int lbase = ty * (G::TH / 2) - casy - G::HALO / 2;
-    const int hbase = J.sny + ty * (G::TH / 2) - G::HALO / 2;
-    const int ylo = yw + G::HALO, yhi = ylo + G::TH;  // core rows [ylo, yhi)
-    const bool rows_all = ylo >= 0 && yhi <= rh;      // wave-uniform: no per-row checks
+    if (!NOCOMP) fwd_vertical<IRREV, R>(lo, hi, rh, casy);
     if (XM == 2) {
         int32_t acc = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) acc += lo[r] ^ hi[r];
-        if (acc == 0x12345678) st32(acc, outb, vl, 0);
+        if (acc == 0x12345678) st32(acc, mkbuf(J.out, J.out_bytes), 0, 0);
         return;
     }
+    fwd_horizontal_store<IRREV, TH, NOCOMP, BAUX>(J, lo, hi, ty, yw, gx0, lane);
+}
+
+// Forward level 0 of an MCT component triple in ONE wavefront per window:
+// the three image planes are read once (8-byte loads), the DC shift + RCT /
+// ICT forms all three components in registers (mct_px), and each component
+// is lifted and stored in turn.  jobs = component triples (blockIdx.y).
+template <bool IRREV, int TH>
+__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *__restrict__ jobs, int lay) {
+    using G = DwtGeo<IRREV, TH>;
+    constexpr int R = G::R;
+    const int gx = gridDim.x;
+    int L = blockIdx.y * gx + blockIdx.x;
+    if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+    const int wg = L % gx, trip = L / gx;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const DwtJob &J0 = jobs[trip * 3];
+    const int tile = wg * DWT_WAVES + w;
+    const int tx = tile % J0.tiles_x, ty = tile / J0.tiles_x;
+    const int rw = J0.rw, rh = J0.rh, casx = J0.casx, casy = J0.casy;
+    if (ty >= (rh + casy + TH - 1) / TH) return;
+    const int lane = threadIdx.x & 63;
+    const int xw = tx * G::CW - casx - G::HALO;
+    const int yw = ty * G::TH - casy - G::HALO;
+    const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
+    int32_t a0[R], a1[R], b0[R], b1[R], c0[R], c1[R];
+    {
+        const int st = (int)J0.src_stride * 4;
+        const rsrc_t p0 = mkbuf(J0.src[0], J0.src_bytes), p1 = mkbuf(J0.src[1], J0.src_bytes),
+                     p2 = mkbuf(J0.src[2], J0.src_bytes);
+        const bool vec = J0.src_vec && casx == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
+        const bool rows_in = yw >= 0 && yw + R <= rh;
+        if (vec) {
 #pragma unroll
-    for (int r = G::HALO; r < G::HALO + G::TH; ++r) {
-        int32_t L = lo[r], H = hi[r];
-        if (IRREV && rh > 1 && !NOCOMP) {
-            const int32_t k = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
-            L = fixmul13(L, k); H = fixmul13(H, k);
-        }
-        if (NOCOMP) {
-        } else if (rw > 1) {
-            if constexpr (!IRREV) {
-                H = lift<0>(H, L, from_next(L));
-                L = lift<1>(L, from_prev(H), H);
-            } else {
-                H = lift<2>(H, L, from_next(L));
-                L = lift<3>(L, from_prev(H), H);
-                H = lift<4>(H, L, from_next(L));
-                L = lift<5>(L, from_prev(H), H);
-                H = fixmul13(H, 5039);
-                L = fixmul13(L, 6659);
+            for (int r = 0; r < R; ++r) {
+                const int so = (rows_in ? yw + r : mirror_idx(yw + r, rh)) * st;
+                const auto a = __builtin_amdgcn_raw_buffer_load_b64(p0, gx0 * 4, so, 0);
+                const auto b = __builtin_amdgcn_raw_buffer_load_b64(p1, gx0 * 4, so, 0);
+                const auto c = __builtin_amdgcn_raw_buffer_load_b64(p2, gx0 * 4, so, 0);
+                a0[r] = (int32_t)a[0]; a1[r] = (int32_t)a[1];
+                b0[r] = (int32_t)b[0]; b1[r] = (int32_t)b[1];
+                c0[r] = (int32_t)c[0]; c1[r] = (int32_t)c[1];
             }
-        } else if (!IRREV && casx) {
-            L = (int32_t)((uint32_t)L << 1);
-            H = (int32_t)((uint32_t)H << 1);
-        }
-        if (!rows_all) {
-            const int gy = yw + r;
-            if (gy < 0 || gy >= rh) continue;
-        }
-        if ((r & 1) == 0) {  // low row -> LL | HL
-            const int iy = lbase + r / 2;
-            st32(L, outb, vl, iy * ost);
-            st32<BAUX>(H, bandb, vh, iy * bst);
-        } else {             // high row -> LH | HH
-            const int so = (hbase + (r - 1) / 2) * bst;
-            st32<BAUX>(L, bandb, vl, so);
-            st32<BAUX>(H, bandb, vh, so);
+        } else {
+            const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int so = mirror_idx(yw + r, rh) * st;
+                a0[r] = ld32(p0, o0, so); a1[r] = ld32(p0, o1, so);
+                b0[r] = ld32(p1, o0, so); b1[r] = ld32(p1, o1, so);
+                c0[r] = ld32(p2, o0, so); c1[r] = ld32(p2, o1, so);
+            }
         }
     }
+    // DC shift + forward MCT in place: a = component 0, b = 1, c = 2
+    const int32_t s0 = J0.shift[0], s1 = J0.shift[1], s2 = J0.shift[2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int32_t rr = (h ? a1[r] : a0[r]) - s0, gg = (h ? b1[r] : b0[r]) - s1, bb = (h ? c1[r] : c0[r]) - s2;
+            int32_t y, u, v;
+            if constexpr (!IRREV) {
+                y = (rr + (gg * 2) + bb) >> 2; u = bb - gg; v = rr - gg;
+            } else {
+                rr = (int32_t)((uint32_t)rr << 11); gg = (int32_t)((uint32_t)gg << 11); bb = (int32_t)((uint32_t)bb << 11);
+                y = fixmul13(rr, 2449) + fixmul13(gg, 4809) + fixmul13(bb, 934);
+                u = -fixmul13(rr, 1382) - fixmul13(gg, 2714) + fixmul13(bb, 4096);
+                v = fixmul13(rr, 4096) - fixmul13(gg, 3430) - fixmul13(bb, 666);
+            }
+            if (h) { a1[r] = y; b1[r] = u; c1[r] = v; } else { a0[r] = y; b0[r] = u; c0[r] = v; }
+        }
+        if (IRREV) __builtin_amdgcn_sched_barrier(0);
+    }
+    // scheduling fences between the components keep the live set at the
+    // three windows (6 R registers) instead of interleaved lifting chains
+    __builtin_amdgcn_sched_barrier(0);
+    fwd_vertical<IRREV, R>(a0, a1, rh, casy);
+    fwd_horizontal_store<IRREV, TH>(jobs[trip * 3 + 0], a0, a1, ty, yw, gx0, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    fwd_vertical<IRREV, R>(b0, b1, rh, casy);
+    fwd_horizontal_store<IRREV, TH>(jobs[trip * 3 + 1], b0, b1, ty, yw, gx0, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    fwd_vertical<IRREV, R>(c0, c1, rh, casy);
+    fwd_horizontal_store<IRREV, TH>(jobs[trip * 3 + 2], c0, c1, ty, yw, gx0, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -826,6 +925,12 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         else hipLaunchKernelGGL((k_dwt_fwd<true, TH, 2>), grid, block, 0, s, jobs, lay);
         return;
     }
+    if (fused == 3) {  // forward level 0, MCT triples: one wavefront = the 3 components of one window
+        const dim3 g3(grid.x, grid.y / 3);
+        if (irrev) hipLaunchKernelGGL((k_dwt_fwd_mct3<true, TH>), g3, block, 0, s, jobs, lay);
+        else hipLaunchKernelGGL((k_dwt_fwd_mct3<false, TH>), g3, block, 0, s, jobs, lay);
+        return;
+    }
     if (fused == 2) {  // forward level 0, MCT triples: workgroup = the 3 components of one window
         const dim3 g3(grid.x * DWT_WAVES, grid.y / 3), b3(192);
         if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 2>), g3, b3, 0, s, jobs, lay);
@@ -856,7 +961,9 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
     if (!njobs || !max_tiles) return hipSuccess;
     dim3 grid((max_tiles + DWT_WAVES - 1) / DWT_WAVES, njobs), block(64 * DWT_WAVES);
     const int nch = (code >> 8) & 0xff;
-    const int fused = inverse || nch ? 0 : (code & DWT_FUSED_MCT3) ? 2 : (code & DWT_FUSED) ? 1 : 0;
+    const int fused = inverse || nch ? 0
+                      : (code & DWT_FUSED_MCT3) ? (env_int("GRKGPU_DWT_MCT3", 3) == 2 ? 2 : 3)
+                      : (code & DWT_FUSED) ? 1 : 0;
     switch (code & 0xff) {
         case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
         case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
