@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgrk_mi355x.so")
+# GRKGPU_LIB: another build of the library (A/B experiments)
+LIB_PATH = os.environ.get("GRKGPU_LIB") or os.path.join(_HERE, "lib", "libgrk_mi355x.so")
 MAXC = 16
 
 __all__ = ["Codec", "CParams", "GrkGpuError", "lib", "build", "read_header"]

@@ -155,21 +155,24 @@ struct DecTables {
 
 // significance propagation (CUP = false) or cleanup (CUP = true) of one
 // column; returns true if a sample became significant.
-template <bool CUP, class D>
-GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+// CUP < 0: the pass type is the runtime flag `cup` (one instantiation for
+// both passes, so lanes of a wavefront in an SPP and in a cleanup pass share
+// the column code and its decode site).
+template <int CUP_, class D>
+GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr, bool cup_rt = false) {
+    const bool CUP = CUP_ < 0 ? cup_rt : CUP_ != 0;
     uint32_t P = win18(s.sig, x);
     const uint32_t vis4 = col4(s.vis, x);
     const uint32_t rows = (1u << nr) - 1;
     const uint32_t sig4 = win_self4(P);
-    uint32_t todo;
-    if (!CUP) {
-        uint32_t nz = 0;
+    uint32_t nz = 0xF;  // SPP: rows with a significant neighbour
+    if (CUP_ <= 0) {
+        uint32_t z = 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) nz |= (((P >> (3 * r)) & 0x1EF) != 0 ? 1u : 0u) << r;
-        todo = nz & ~sig4 & ~vis4 & rows;
-    } else {
-        todo = ~sig4 & ~vis4 & rows;
+        for (int r = 0; r < 4; ++r) z |= (((P >> (3 * r)) & 0x1EF) != 0 ? 1u : 0u) << r;
+        nz = CUP ? 0xFu : z;
     }
+    uint32_t todo = nz & ~sig4 & ~vis4 & rows;
     uint32_t kind = 0, r = 0;  // 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo)
     if (CUP && nr == 4 && P == 0 && vis4 == 0) {
         kind = 2;
@@ -189,7 +192,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const uint32_t bit = d.decode(cxw, T.mq, cx);
         if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
         const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;
-        if (!CUP) newvis |= k0 ? 1u << r : 0u;
+        newvis |= (!CUP && k0) ? 1u << r : 0u;
         // SC: the sample is significant with sign sg
         const uint32_t sg = bit ^ ((D::kLazy && d.raw) ? 0u : (si >> 7));  // a raw sign is the sign itself
         P |= k1 ? 1u << (sh + 4) : 0u;
@@ -197,7 +200,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         newsig |= k1 ? 1u << r : 0u;
         newneg |= k1 ? sg << r : 0u;
         // the sample below now has a significant neighbour (SPP)
-        if (!CUP) todo |= k1 ? (rows & ~(sig4 | vis4)) & (2u << r) : 0u;
+        todo |= (!CUP && k1) ? (rows & ~(sig4 | vis4)) & (2u << r) : 0u;
         // UNI, UNI: the run position; the rows after it are plain ZC
         r = k3 ? bit << 1 : k4 ? (r | bit) : r;
         todo = k4 ? rows & ~((2u << r) - 1) : todo;
@@ -302,12 +305,43 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.neg[i] = st.neg[k + i];
             if (vsc) s.neg[5] = 0;
+#ifdef GRK_T1_UNIFY_SPP_CUP
+            // SPP and cleanup sharing one column loop (runtime pass type):
+            // measured 3-15 % SLOWER (lone 8K decode 52.0 -> 54.5 ms, bench
+            // 2431-2472 -> 2262-2409 Mpix/s): the union of both passes' work
+            // per column costs more than the divergence it removes
+            {
+                const bool cup = passtype == 2;
+                uint64_t cand = 0;
+                if (cup) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if ((uint32_t)r < nr) cand |= ~(s.sig[r + 1] | s.vis[r]);
+                } else {
+                    cand = spp_candidates(s, nr);
+                }
+                cand &= wm;
+                while (cand) {
+                    const uint32_t x = ctz64(cand);
+                    const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
+                    const bool grew = d3_column<-1>(d, cxw, T, s, x, nr, cup);
+                    cand &= ~done;
+                    // SPP: a new significant sample in column x can only make
+                    // column x + 1 a candidate (x - 1 is behind the scan)
+                    if (grew && !cup) cand |= ((uint64_t)2 << x) & wm;
+                }
+                if (cup) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s.vis[r] = 0;
+                }
+            }
+#else
             if (passtype == 0) {
                 uint64_t cand = spp_candidates(s, nr) & wm;
                 while (cand) {
                     const uint32_t x = ctz64(cand);
                     const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
-                    const bool grew = d3_column<false>(d, cxw, T, s, x, nr);
+                    const bool grew = d3_column<0>(d, cxw, T, s, x, nr);
                     cand &= ~done;
                     // a new significant sample in column x can only make
                     // column x + 1 a candidate (x - 1 is behind the scan)
@@ -322,11 +356,12 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                 while (cand) {
                     const uint32_t x = ctz64(cand);
                     cand &= cand - 1;
-                    d3_column<true>(d, cxw, T, s, x, nr);
+                    d3_column<1>(d, cxw, T, s, x, nr);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) s.vis[r] = 0;
             }
+#endif
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 st.sig[k + 1 + i] = s.sig[i + 1];
