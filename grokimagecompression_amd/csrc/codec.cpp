@@ -1395,7 +1395,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
-    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
+    // the decoder's lane-interleaved groups span 64 records each (t1_lane.h)
+    HIPCHK(c->scratch.ensure((size_t)t1_scratch_records(nblk) * sizeof(T1Scratch) + 256));
     // per-segment unstuffed-stream regions (16-byte units)
     uint64_t uwords = 0;
     for (auto &sg : dsegs) {
@@ -1659,9 +1660,10 @@ extern "C" int grkgpu_t1_decode_blocks(const grkgpu_dec_block *blocks, uint32_t 
     if (!blocks || !data || !scratch || !dst) return set_err(GRKGPU_EINVAL, "null argument");
     int rc = check_device(-1);
     if (rc) return rc;
-    // scratch layout: nblocks T1Scratch records, then one fixed-size
+    // scratch layout: nblocks rounded up to a multiple of 64 T1Scratch
+    // records (the decoder's lane-interleaved groups), then one fixed-size
     // unstuffed-stream region per block
-    uint32_t *ubuf = (uint32_t *)((uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch));
+    uint32_t *ubuf = (uint32_t *)((uint8_t *)scratch + (size_t)t1_scratch_records(nblocks) * sizeof(T1Scratch));
     HIPCHK(launch_t1_decode((const DecBlock *)blocks, nblocks, data, (T1Scratch *)scratch, dst, (hipStream_t)stream,
                             ubuf, t1_stage_dec_words()));
     return GRKGPU_OK;

@@ -164,10 +164,9 @@ __device__ __forceinline__ int32_t mct_px(const DwtJob &J, int32_t a, int32_t b,
     if constexpr (!IRREV) {
         return J.comp == 0 ? (r + (g * 2) + bl) >> 2 : J.comp == 1 ? bl - g : r - g;
     } else {
-        r = (int32_t)((uint32_t)r << 11); g = (int32_t)((uint32_t)g << 11); bl = (int32_t)((uint32_t)bl << 11);
-        if (J.comp == 0) return fixmul13(r, 2449) + fixmul13(g, 4809) + fixmul13(bl, 934);
-        if (J.comp == 1) return -fixmul13(r, 1382) - fixmul13(g, 2714) + fixmul13(bl, 4096);
-        return fixmul13(r, 4096) - fixmul13(g, 3430) - fixmul13(bl, 666);
+        if (J.comp == 0) return ict_term(r, 2449) + ict_term(g, 4809) + ict_term(bl, 934);
+        if (J.comp == 1) return -ict_term(r, 1382) - ict_term(g, 2714) + ict_term(bl, 4096);
+        return ict_term(r, 4096) - ict_term(g, 3430) - ict_term(bl, 666);
     }
 }
 
@@ -442,10 +441,9 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *_
             if constexpr (!IRREV) {
                 y = (rr + (gg * 2) + bb) >> 2; u = bb - gg; v = rr - gg;
             } else {
-                rr = (int32_t)((uint32_t)rr << 11); gg = (int32_t)((uint32_t)gg << 11); bb = (int32_t)((uint32_t)bb << 11);
-                y = fixmul13(rr, 2449) + fixmul13(gg, 4809) + fixmul13(bb, 934);
-                u = -fixmul13(rr, 1382) - fixmul13(gg, 2714) + fixmul13(bb, 4096);
-                v = fixmul13(rr, 4096) - fixmul13(gg, 3430) - fixmul13(bb, 666);
+                y = ict_term(rr, 2449) + ict_term(gg, 4809) + ict_term(bb, 934);
+                u = -ict_term(rr, 1382) - ict_term(gg, 2714) + ict_term(bb, 4096);
+                v = ict_term(rr, 4096) - ict_term(gg, 3430) - ict_term(bb, 666);
             }
             if (h) { a1[r] = y; b1[r] = u; c1[r] = v; } else { a0[r] = y; b0[r] = u; c0[r] = v; }
         }

@@ -113,4 +113,10 @@ inline uint32_t t1_unstuff_region_words(uint32_t len) { return 4 + unstuff_word_
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,
                          hipStream_t s);
 
+// One product of the forward ICT (mct.cpp:195-350), int_fix_mul(r << 11, c)
+// = (2048 r c + 4096) >> 13 with the 64-bit product, for a DC-shifted sample
+// r (|r| <= 2^16, precision <= 16 bits): 2048 (r c + 2) / 8192 = (r c + 2) / 4,
+// so the same value is floor((r c + 2) / 4) in 32-bit arithmetic (|r c| < 2^30).
+__device__ __forceinline__ int32_t ict_term(int32_t r, int32_t c) { return (r * c + 2) >> 2; }
+
 }  // namespace grkgpu

@@ -54,10 +54,9 @@ __global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst
             o1 = b - g;
             o2 = r - g;
         } else {
-            r = (int32_t)((uint32_t)r << 11); g = (int32_t)((uint32_t)g << 11); b = (int32_t)((uint32_t)b << 11);
-            o0 = fix_mul13(r, 2449) + fix_mul13(g, 4809) + fix_mul13(b, 934);
-            o1 = -fix_mul13(r, 1382) - fix_mul13(g, 2714) + fix_mul13(b, 4096);
-            o2 = fix_mul13(r, 4096) - fix_mul13(g, 3430) - fix_mul13(b, 666);
+            o0 = ict_term(r, 2449) + ict_term(g, 4809) + ict_term(b, 934);
+            o1 = -ict_term(r, 1382) - ict_term(g, 2714) + ict_term(b, 4096);
+            o2 = ict_term(r, 4096) - ict_term(g, 3430) - ict_term(b, 666);
         }
         put<NT>(&dst.p[0][di], o0); put<NT>(&dst.p[1][di], o1); put<NT>(&dst.p[2][di], o2);
         c0 = 3;
@@ -375,6 +374,34 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     unstuff_segment(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words));
 }
 
+// Lane-interleaved rows (t1_lane.h) through buffer instructions: the group's
+// region is one buffer resource (wave-uniform, SGPRs) and a row access is a
+// 32-bit lane offset, so the decoder keeps one offset VGPR per row index
+// instead of a 64-bit pointer per state array.
+struct LRef {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t so, vo;
+    __device__ operator uint64_t() const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
+        return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+    }
+    __device__ const LRef &operator=(uint64_t v) const {
+        const __attribute__((ext_vector_type(2))) uint32_t p = {(uint32_t)v, (uint32_t)(v >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(p, r, vo, so, 0);
+        return *this;
+    }
+};
+// so: the field's byte offset (scalar); vo: the lane's byte offset + rows
+struct LRow {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t so, vo;
+    __device__ LRef operator[](uint32_t y) const { return LRef{r, so, vo + y * 512u}; }
+    __device__ LRow operator+(uint32_t n) const { return LRow{r, so, vo + n * 512u}; }
+};
+struct LState {
+    LRow sig, neg, vis, ref;
+};
+
 template <int LANES, bool LAZY = false>
 __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
@@ -394,71 +421,80 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     const DecBlock b = blocks[i];
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
-    T1Scratch &S = scr[i];
+    // lane-interleaved state and bit-plane rows of this block (t1_lane.h T1Group)
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        t1_group_base(scr, i >> 6, sizeof(T1Scratch)), 0, (int)(64 * sizeof(T1Scratch)), 0x00020000);
+    const uint32_t lo = (i & 63) * 8;
+    LState st{LRow{gr, T1R_SIG * 512, lo}, LRow{gr, T1R_NEG * 512, lo}, LRow{gr, T1R_VIS * 512, lo},
+              LRow{gr, T1R_REF * 512, lo}};
+    const LRow pa{gr, T1R_PA * 512, lo}, pb{gr, T1R_PB * 512, lo};
     uint32_t *cxw = s_cx + threadIdx.x * 21;
     if (segs) {
         const uint32_t q0 = seg_first[i], nseg = seg_first[i + 1] - q0;
         const DecSeg s0 = segs[q0];
         const uint32_t *region = ubuf + (size_t)s0.ub_off * 4;
-        for (uint32_t y = 0; y < b.h + 2; ++y) { S.st.sig[y] = 0; S.st.neg[y] = 0; S.st.vis[y] = 0; S.st.ref[y] = 0; }
+        for (uint32_t y = 0; y < b.h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
         mq_reset_words(cxw, T.mq);
         BitDecT<LAZY> d;
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
         SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
-        t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, S.st, T, cxw, S.pa, S.pb, sty, cur, roi ? roi[i] : 0u);
+        t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, st, T, cxw, pa, pb, sty, cur, roi ? roi[i] : 0u);
         return;
     }
     const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
-    t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, S.st, T,
-                 cxw, S.pa, S.pb);
+    t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, st, T,
+                 cxw, pa, pb);
 }
 
-// One workgroup per block, lane = column: values from the bit-plane rows
-// (staged in LDS, broadcast reads), then T1Part1::postDecode scaling
-// (5/3: v/2, 9/7: float(v) * step) and a coalesced row store.
-// roi (null: none): per-block ROI up-shift -- T1Part1::post_decode
-// (T1Part1.cpp:230-250) shifts magnitudes >= 2^roishift down by roishift
-// (and zeroes the block for a shift >= 31) before the scaling.
-__global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ blocks,
+// Rebuild of the decoded values from the lane-interleaved bit-plane rows:
+// one wavefront per (64-block group, RB_ROWS rows), lane = column.  The
+// per-(block, row, plane) row words are wave-uniform, so they come through
+// scalar loads (a group's rows are contiguous per plane row, so consecutive
+// blocks share scalar-cache lines); the coefficient rows are stored
+// coalesced.  Then T1Part1::postDecode scaling (5/3: v/2, 9/7:
+// float(v) * step).  roi (null: none): per-block ROI up-shift --
+// T1Part1::post_decode (T1Part1.cpp:230-250) shifts magnitudes >= 2^roishift
+// down by roishift (and zeroes the block for a shift >= 31) before the
+// scaling.
+constexpr uint32_t RB_ROWS = 8;
+__global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ blocks, uint32_t n,
                                                    const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles,
                                                    const uint8_t *__restrict__ roi) {
-    __shared__ uint64_t s_sig[32 * 64];
-    __shared__ uint64_t s_ref[32 * 64];
-    __shared__ uint64_t s_neg[64];
-    const uint32_t i = blockIdx.x, x = threadIdx.x;
-    const DecBlock b = blocks[i];
-    const DecodedPlanes dp = decoded_planes(b.len ? b.numpasses : 0, b.numbps);
-    const T1Scratch &S = scr[i];
-    const uint32_t rs = roi ? roi[i] : 0u;
-    const uint32_t h = b.h;
-    for (int32_t q = dp.low; q <= dp.top; ++q)
-        if (x < h) s_sig[q * 64 + x] = S.pa[q * 64 + x];
-    for (int32_t q = dp.qlow; q < dp.top; ++q)
-        if (x < h) s_ref[q * 64 + x] = S.pb[q * 64 + x];
-    if (dp.top >= 0 && x < h) s_neg[x] = S.st.neg[x + 1];
-    __syncthreads();
-    if (x >= b.w) return;
-    int32_t *dst = tiles + b.dst_off + x;
-    for (uint32_t y = 0; y < h; ++y) {
-        int32_t v = 0;
-        if (dp.top >= 0) {
-            uint32_t cs = 0;  // bit (q - low): significant after plane q
-            for (int32_t q = dp.top; q >= dp.low; --q) cs = (cs << 1) | (uint32_t)((s_sig[q * 64 + y] >> x) & 1u);
-            if (cs) {
-                int32_t p = dp.low + 31 - (int32_t)__clz(cs);
-                int32_t ql = p < dp.qlow ? p : dp.qlow;
-                uint32_t cr = 0;  // bit (q - ql): refinement bit at plane q, q in [ql, p)
-                for (int32_t q = p - 1; q >= ql; --q) cr = (cr << 1) | (uint32_t)((s_ref[q * 64 + y] >> x) & 1u);
-                uint32_t bits = (1u << (p - ql)) | cr;
-                int32_t mag = (int32_t)((bits << (ql + 1)) | (1u << ql));
-                if (rs) mag = rs >= 31 ? 0 : (mag >= (1 << rs) ? mag >> rs : mag);
-                v = ((s_neg[y] >> x) & 1u) ? -mag : mag;
+    const uint32_t g = blockIdx.x, x = threadIdx.x;
+    const uint32_t y0 = blockIdx.y * RB_ROWS;
+    const uint64_t *gb = t1_group_base(const_cast<T1Scratch *>(scr), g, sizeof(T1Scratch));
+    const uint32_t nb = n - g * 64 < 64 ? n - g * 64 : 64;
+    for (uint32_t l = 0; l < nb; ++l) {
+        const DecBlock b = blocks[g * 64 + l];
+        if (y0 >= b.h) continue;
+        const DecodedPlanes dp = decoded_planes(b.len ? b.numpasses : 0, b.numbps);
+        const uint32_t rs = roi ? roi[g * 64 + l] : 0u;
+        const uint32_t y1 = b.h < y0 + RB_ROWS ? b.h : y0 + RB_ROWS;
+        const bool col = x < b.w;
+        int32_t *dst = tiles + b.dst_off + x;
+        const uint64_t *pa = gb + (size_t)T1R_PA * 64 + l, *pb = gb + (size_t)T1R_PB * 64 + l;
+        const uint64_t *ng = gb + (size_t)T1R_NEG * 64 + l;
+        for (uint32_t y = y0; y < y1; ++y) {
+            int32_t v = 0;
+            if (dp.top >= 0) {
+                uint32_t cs = 0;  // bit (q - low): significant after plane q
+                for (int32_t q = dp.top; q >= dp.low; --q)
+                    cs = (cs << 1) | (uint32_t)((pa[(size_t)((uint32_t)q * 64 + y) * 64] >> x) & 1u);
+                if (cs) {
+                    const int32_t p = dp.low + 31 - (int32_t)__clz(cs);
+                    const int32_t ql = p < dp.qlow ? p : dp.qlow;
+                    uint32_t cr = 0;  // bit (q - ql): refinement bit at plane q, q in [ql, p)
+                    for (int32_t q = p - 1; q >= ql; --q)
+                        cr = (cr << 1) | (uint32_t)((pb[(size_t)((uint32_t)q * 64 + y) * 64] >> x) & 1u);
+                    const uint32_t bits = (1u << (p - ql)) | cr;
+                    int32_t mag = (int32_t)((bits << (ql + 1)) | (1u << ql));
+                    if (rs) mag = rs >= 31 ? 0 : (mag >= (1 << rs) ? mag >> rs : mag);
+                    v = ((ng[(size_t)(y + 1) * 64] >> x) & 1u) ? -mag : mag;
+                }
             }
+            const int32_t o = !b.irrev ? v / 2 : __float_as_int(__fmul_rn((float)v, b.step));
+            if (col) dst[(size_t)y * b.dstride] = o;
         }
-        int32_t o;
-        if (!b.irrev) o = v / 2;
-        else o = __float_as_int(__fmul_rn((float)v, b.step));
-        dst[(size_t)y * b.dstride] = o;
     }
 }
 
@@ -571,7 +607,8 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
                            s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
                            nullptr);  // the ROI shift only moves BYPASS pass boundaries
-    hipLaunchKernelGGL(k_t1_rebuild, dim3(n), dim3(64), 0, s, blocks, scratch, tiles, roi);
+    hipLaunchKernelGGL(k_t1_rebuild, dim3((n + 63) / 64, 64 / RB_ROWS), dim3(64), 0, s, blocks, n, scratch, tiles,
+                       roi);
     return hipGetLastError();
 }
 

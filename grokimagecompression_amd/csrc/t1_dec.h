@@ -255,9 +255,12 @@ struct NoSegs {
 // update of t1.cpp:168-190 skips the north neighbours of a stripe's first
 // row); RESET -- contexts re-initialised after every pass (t1.cpp:1104-1105);
 // SEGSYM -- four uniform-context symbols end every cleanup pass (t1.cpp:873-889).
-template <class D, class S = NoSegs>
-GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, BlockState &st,
-                             const DecTables &T, uint32_t *cxw, uint64_t *sigafter, uint64_t *refbit,
+// ST / RP: the block state and the bit-plane row pointers -- plain arrays
+// (BlockState, uint64_t *: host tests) or the GPU decoder's lane-interleaved
+// rows (kernels.hip LState / LRow, t1_lane.h).
+template <class D, class S = NoSegs, class ST = BlockState, class RP = uint64_t *>
+GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, ST &st,
+                             const DecTables &T, uint32_t *cxw, RP sigafter, RP refbit,
                              uint32_t sty = 0, S segs = S(), uint32_t roishift = 0) {
     // BYPASS pass types are classified against the block's bit-planes less
     // the ROI shift (t1_decode_cblk gets numbps - roishift, T1Part1.cpp:186,
@@ -269,8 +272,8 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
     int passtype = 2;
     for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
         segs.at_pass(d, passno, t1_pass_raw(sty, bpno, passtype, rawbps));
-        uint64_t *sa = sigafter + (uint32_t)bpno * 64;
-        uint64_t *rb = refbit + (uint32_t)bpno * 64;
+        const RP sa = sigafter + (uint32_t)bpno * 64;
+        const RP rb = refbit + (uint32_t)bpno * 64;
         // Each pass type loads and stores only the state rows it reads or
         // changes (SPP / CUP: sig, neg, vis; MRP: sig, vis, ref + the
         // refinement bits), so no row is live across the three branches:

@@ -242,9 +242,10 @@ struct SegCursor {
 
 // v5: the nested pass / stripe / column walk of v3 (lanes of a wavefront stay
 // converged on the pass structure) fed by the unstuffed bit stream.
+template <class ST = BlockState, class RP = uint64_t *>
 GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
-                         uint32_t numbps, uint32_t w, uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw,
-                         uint64_t *sa, uint64_t *rb) {
+                         uint32_t numbps, uint32_t w, uint32_t h, ST &st, const DecTables &T, uint32_t *cxw,
+                         RP sa, RP rb) {
     for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
     mq_reset_words(cxw, T.mq);
     BitDec d;

@@ -1084,6 +1084,21 @@ struct T1Scratch {
     uint32_t cnt[32 * 4];  // encoder: symbols per (plane, pass type)
 };
 
+// ---- lane-interleaved scratch (decoder) ----
+// The 64 blocks of a decoder wavefront (a "group") share one region of
+// 64 * sizeof(T1Scratch) bytes in which row R of the T1Scratch fields of
+// lane l lives at word R * 64 + l.  A row access of the wavefront is then one
+// 512-byte contiguous run (4 cache lines) instead of 64 lines 35 KB apart,
+// and the rows a lane writes fill whole lines together with its neighbours'.
+// The last group also spans 64 records: scratch holds the block count
+// rounded up to a multiple of 64 (t1_scratch_records).
+// row offsets of the T1Scratch fields (in 8-byte rows)
+constexpr uint32_t T1R_SIG = 0, T1R_NEG = 66, T1R_VIS = 132, T1R_REF = 198, T1R_PA = 264, T1R_PB = 264 + 2048;
+GRK_HD uint64_t *t1_group_base(void *scr, uint32_t g, size_t rec_bytes) {
+    return (uint64_t *)((uint8_t *)scr + (size_t)g * 64 * rec_bytes);
+}
+GRK_HD constexpr uint32_t t1_scratch_records(uint32_t n) { return (n + 63) & ~63u; }
+
 // Serial restatement of the encoder prep kernel (quantise, sign rows,
 // numbps, magnitude bit-planes): T1Part1::preEncode (T1Part1.cpp:58-94).
 GRK_HD uint32_t t1_prep_serial(const int32_t *coef, uint32_t stride, uint32_t w, uint32_t h, int32_t qmfbid,

@@ -31,7 +31,7 @@ def run(n, scale, reps=3):
     eb["qmfbid"] = 1
     deb = torch.from_numpy(eb.view(np.uint8)).cuda()
     out = torch.zeros(n * (4096 * 4 + 128) + 256, dtype=torch.uint8, device="cuda")
-    scr = torch.empty(n * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device="cuda")
+    scr = torch.empty(((n + 63) // 64 * 64) * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device="cuda")
     res = torch.zeros(n * RES_WORDS, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     ts = []

@@ -127,7 +127,8 @@ def _gpu_decode(items):
     t_data = torch.from_numpy(np.frombuffer(bytes(blob) + bytes(64), np.uint8).copy()).to(dev)
     t_blocks = torch.from_numpy(db.view(np.uint8)).to(dev)
     t_dst = torch.full((dst_off + 16,), 0x5A5A5A5A, dtype=torch.int32, device=dev)
-    t_scr = torch.empty(n * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
+    nrec = (n + 63) // 64 * 64  # decode: whole 64-block groups (grk_mi355x.h)
+    t_scr = torch.empty(nrec * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream(0).cuda_stream)
     grk._check(L.grkgpu_t1_decode_blocks(t_blocks.data_ptr(), n, t_data.data_ptr(), t_scr.data_ptr(),
                                          t_dst.data_ptr(), s))

@@ -52,3 +52,15 @@ def test_t1_core_host_matches_oracle(oracle, tmp_path):
                     "-L" + ob, "-lgrk_oracle", "-Wl,-rpath," + ob], check=True)
     r = subprocess.run([str(exe), "800"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:]
+
+
+def test_ict_term_identity():
+    """grk_device.h ict_term: the forward ICT's int_fix_mul(r << 11, c)
+    (mct.cpp:195-350, 64-bit product) equals floor((r c + 2) / 4) in 32-bit
+    arithmetic for every DC-shifted sample of up to 16 bits."""
+    import numpy as np
+    r = np.arange(-(1 << 16), (1 << 16) + 1, dtype=np.int64)
+    for c in (2449, 4809, 934, 1382, 2714, 4096, 3430, 666):
+        ref = ((r << 11) * c + 4096) >> 13
+        assert np.array_equal(ref, (r * c + 2) >> 2)
+        assert np.abs(r * c).max() < 2 ** 31
