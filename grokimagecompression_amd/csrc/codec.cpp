@@ -490,6 +490,10 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
             minh = std::min(minh, (int)j.rh);
         }
         P.th[l] = dwt_pick_th(irrev, samples, minw, minh);
+        // the fused DC shift + MCT level 0 holds the windows of three
+        // components: 8-row windows (measured on the 8K frame: 5/3 162 us at
+        // TH 8, 168 at 16, 194 at 32; 9/7 229 / 319 / 330)
+        if (l == 0 && P.mct3) P.th[l] = 8;
         for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j.rw, j.rh, j.casx, j.casy, &j.tiles_x, &j.ntiles);
     }
 }
@@ -719,11 +723,17 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipEventRecord(c->ev[1], s));
     ShiftArr sh{};
     for (uint32_t k = 0; k < nc; ++k) sh.v[k] = cp.shift[k];
-    // GRKGPU_DWT_FUSE=1 fuses the DC shift + MCT into the first DWT level
-    // (every tile-component decomposed at least once and spanning its tile).
-    // Off by default: it saves the 8 B/sample MCT round trip, but measured
-    // 1.3-1.6x SLOWER than MCT pass + level 0 on the 8K frame.
-    bool fuse = getenv("GRKGPU_DWT_FUSE") && atoi(getenv("GRKGPU_DWT_FUSE")) != 0;
+    // The DC shift + RCT of a 3-component 5/3 tile is fused into its first
+    // DWT level (k_dwt_fwd_mct3: one wavefront reads the three image planes
+    // once and lifts the three components of its window): 162 us instead of
+    // 132 (MCT pass) + 133 (level 0) on the 8K frame.  The 9/7 (ICT) triple
+    // is left separate: fused 229 us vs 132 + 145, but the separate level-0
+    // launch is the DWT whose roofline the bench reports.
+    // GRKGPU_DWT_FUSE=0/1 forces it off / on (1: also 9/7 and single
+    // components, DC shift in the loads).  Requires every tile-component to be
+    // decomposed at least once and to span its tile.
+    const char *fe = getenv("GRKGPU_DWT_FUSE");
+    bool fuse = fe && *fe ? atoi(fe) != 0 : (!cp.irrev && cp.mct && nc == 3);
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
@@ -811,6 +821,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         mct_numcomps = nc;
     }
     uint64_t nsym = 0;
+    {
+        size_t npass = 0;
+        for (uint32_t i = 0; i < nblk; ++i) npass += std::min<uint32_t>(res[i].numpasses, GRK_MAX_PASSES);
+        passes.reserve(npass);
+    }
     for (uint32_t i = 0; i < nblk; ++i) {
         const EncResult &r = res[i];
         if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");

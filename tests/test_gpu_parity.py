@@ -83,6 +83,19 @@ def test_encode_fused_mct_dwt(codec, monkeypatch, name, mct3):
     assert codec.compress(img, bits, p, offset=off) == open(f"{GOLD}/{name}.j2k", "rb").read()
 
 
+@pytest.mark.parametrize("name", ["rgb8_128x96", "rgb12_96x80", "rgb16_64", "rgb8_r10_tiles", "rgb8_uniform_64"])
+def test_encode_unfused_rct(codec, monkeypatch, name):
+    """A 3-component 5/3 tile fuses the DC shift + RCT into DWT level 0 by
+    default (k_dwt_fwd_mct3); GRKGPU_DWT_FUSE=0 keeps the separate
+    k_dcshift_mct_fwd pass, which must give the same bytes."""
+    import grokimagecompression_amd as grk
+    monkeypatch.setenv("GRKGPU_DWT_FUSE", "0")
+    m = MAN[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    assert codec.compress(img, bits, p, offset=off) == open(f"{GOLD}/{name}.j2k", "rb").read()
+
+
 def test_device_resident_roundtrip(codec):
     import torch
     import grokimagecompression_amd as grk
