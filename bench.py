@@ -242,7 +242,8 @@ def main():
     # region on one context (HIP events on the codec stream around the level
     # launches): per-launch algorithmic bytes / mean launch duration.
     bdwt = dwt_bytes(H, W, C)
-    nlaunch = 5
+    fused01 = os.environ.get("GRKGPU_DWT_F01", "4") != "0"  # levels 0 + 1 in one launch (dwt.hip k_dwt_fwd01)
+    nlaunch = 4 if fused01 else 5
     torch.cuda.synchronize()
     iso = []
     p97 = grk.CParams.make(irreversible=True)
@@ -257,9 +258,12 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
-        tot = sum(e["bytes"] for k, v in d["kernels"].items() if "k_dwt_fwd<true" in k for e in v)
+        tot = sum(e["bytes"] for k, v in d["kernels"].items()
+                  if ("k_dwt_fwd<true" in k or "k_dwt_fwd01<true" in k) for e in v)
         traffic = round(tot / nlaunch)
-    roofline = {"bound": "hbm", "kernel": "k_dwt_fwd<9/7> (5 level launches x 3 comps, dwt.hip)",
+    kname = ("k_dwt_fwd01<9/7> (levels 0+1, LL0 kept in LDS) + k_dwt_fwd<9/7> x 3 (levels 2-4), 3 comps per launch"
+             if fused01 else "k_dwt_fwd<9/7> (5 level launches x 3 comps, dwt.hip)")
+    roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": bdwt // nlaunch, "launches": nlaunch,

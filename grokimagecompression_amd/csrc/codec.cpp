@@ -515,6 +515,51 @@ static hipError_t dwt_upload(DwtPlan &P, DevBuf &djobs, HostBuf &hjobs, int irre
 }
 
 // Run the levels (job table already uploaded by dwt_upload on the same stream).
+// Forward 9/7 levels 0 and 1 fused into one launch (dwt.hip k_dwt_fwd01)
+// when every tile-component has both levels, level 0 is not the fused
+// DC shift + MCT one, and the resolutions are big enough (>= 16 samples each
+// way) for the fused windows; GRKGPU_DWT_F01=0 keeps two launches.  Returns
+// the workgroups per job, 0 = not fused.
+static uint32_t dwt_f01_tiles(const DwtPlan &P, int irrev, bool inverse) {
+    const char *e = getenv("GRKGPU_DWT_F01"), *strip = getenv("GRKGPU_DWT_STRIP");
+    if (inverse || !irrev || P.fused0 || P.levels.size() < 2 || (e && *e && !atoi(e))) return 0;
+    if (strip && *strip && atoi(strip)) return 0;  // the strip kernels' experiment keeps every level separate
+    const auto &l0 = P.levels[0], &l1 = P.levels[1];
+    if (l0.empty() || l0.size() != l1.size()) return 0;
+    uint32_t maxt = 0;
+    for (size_t i = 0; i < l0.size(); ++i) {
+        const DwtJob &a = l0[i], &b = l1[i];
+        if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
+        int tx;
+        const int n = dwt01_tiles(irrev, b.rw, b.rh, b.casx, b.casy, &tx);
+        if (n <= 0) return 0;
+        maxt = std::max<uint32_t>(maxt, (uint32_t)n);
+    }
+    return maxt;
+}
+
+// All levels of an uploaded plan (job table at djobs, levels back to back).
+static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, bool inverse, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    size_t k = 0, li = 0;
+    if (const uint32_t t01 = dwt_f01_tiles(P, irrev, inverse)) {
+        e = launch_dwt_fwd01(djobs, djobs + P.levels[0].size(), (uint32_t)P.levels[0].size(), t01, irrev, s);
+        if (e != hipSuccess) return e;
+        k = P.levels[0].size() + P.levels[1].size();
+        li = 2;
+    }
+    for (; li < P.levels.size(); ++li) {
+        const auto &l = P.levels[li];
+        uint32_t maxt = 0;
+        for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
+        const int code = P.th[li] | (li == 0 && P.fused0 && !inverse ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) : 0);
+        e = launch_dwt_jobs(djobs + k, (uint32_t)l.size(), maxt, code, irrev, inverse ? 1 : 0, s);
+        if (e != hipSuccess) return e;
+        k += l.size();
+    }
+    return hipSuccess;
+}
+
 static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse, hipStream_t s) {
     for (auto &cp : P.copies) {
         hipError_t e = hipMemcpyAsync(cp.first, cp.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s);
@@ -525,18 +570,7 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
                                         cp.h, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
-    hipError_t e = hipSuccess;
-    size_t k = 0;
-    for (size_t li = 0; li < P.levels.size(); ++li) {
-        const auto &l = P.levels[li];
-        uint32_t maxt = 0;
-        for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
-        const int code = P.th[li] | (li == 0 && P.fused0 && !inverse ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) : 0);
-        e = launch_dwt_jobs(djobs.as<DwtJob>() + k, (uint32_t)l.size(), maxt, code, irrev, inverse ? 1 : 0, s);
-        if (e != hipSuccess) return e;
-        k += l.size();
-    }
-    return hipSuccess;
+    return dwt_run_levels(P, djobs.as<DwtJob>(), irrev, inverse, s);
 }
 
 static bool overlap(const Rect &a, const Rect &b) { return a.x0 < b.x1 && b.x0 < a.x1 && a.y0 < b.y1 && b.y0 < a.y1; }
@@ -1629,14 +1663,7 @@ static int dwt_common(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, 
         HIPCHK(hipStreamSynchronize(s));
     }
     for (auto &cpy : P.copies) HIPCHK(hipMemcpyAsync(cpy.first, cpy.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s));
-    size_t k = 0;
-    for (size_t li = 0; li < P.levels.size(); ++li) {
-        const auto &l = P.levels[li];
-        uint32_t maxt = 0;
-        for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
-        HIPCHK(launch_dwt_jobs(djobs + k, (uint32_t)l.size(), maxt, P.th[li], irrev, inverse ? 1 : 0, s));
-        k += l.size();
-    }
+    HIPCHK(dwt_run_levels(P, djobs, irrev, inverse, s));
     return GRKGPU_OK;
 }
 

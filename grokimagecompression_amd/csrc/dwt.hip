@@ -37,10 +37,10 @@ namespace grkgpu {
 constexpr int DWT_WIN = 128;   // window columns per wavefront (64 lanes x 2)
 constexpr int DWT_WAVES = 4;   // wavefronts (independent windows) per workgroup
 
-template <bool IRREV, int TH_>
+template <bool IRREV, int TH_, int WIN = DWT_WIN>
 struct DwtGeo {
     static constexpr int HALO = IRREV ? 4 : 2;
-    static constexpr int CW = DWT_WIN - 2 * HALO;  // core columns per window
+    static constexpr int CW = WIN - 2 * HALO;      // core columns per window
     static constexpr int TH = TH_;                 // core rows per window
     static constexpr int R = TH + 2 * HALO;        // window rows
 };
@@ -226,11 +226,11 @@ __device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R],
 
 // Horizontal lifting of the window's core rows, then the stores into the
 // LL buffer and the Mallat bands.
-template <bool IRREV, int TH, bool NOCOMP = false, int BAUX = 0>
+template <bool IRREV, int TH, bool NOCOMP = false, int BAUX = 0, int WIN = DWT_WIN>
 __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&lo)[DwtGeo<IRREV, TH>::R],
                                                      int32_t (&hi)[DwtGeo<IRREV, TH>::R], int ty, int yw, int gx0,
                                                      int lane) {
-    using G = DwtGeo<IRREV, TH>;
+    using G = DwtGeo<IRREV, TH, WIN>;
     const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
     const int gx1 = gx0 + 1;
     const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
@@ -852,6 +852,174 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv_stream(const DwtJob 
 }
 
 // ---------------------------------------------------------------------------
+// Forward levels 0 and 1 in one launch (9/7).  Level 1 reads level 0's LL
+// band, which the separate launches write to HBM and read back (2 x 4 B per
+// LL sample, a quarter of level 0's bytes); here a workgroup computes the LL
+// samples its level-1 window needs into LDS and lifts level 1 from there, so
+// LL0 never leaves the chip.
+//   * Level-1 window (LL0 coordinates): W1 = 120 columns x R1 = 12 NY rows,
+//     core CW1 = 112 x TH1 = R1 - 8, origin (xw1, yw1) as in k_dwt_fwd.
+//   * Level-0 stage: the LL0 samples of that window (extended coordinates,
+//     left / top edges included) come from 2 x NY level-0 windows of 128
+//     columns x (24 + 8) rows (60 x 12 LL0 samples each), NY / 2 per
+//     wavefront.  Their LL samples go to LDS; their HL / LH / HH samples go to
+//     HBM for the level-0 pairs this workgroup owns (those under its level-1
+//     core; the first / last workgroup of a row or column also owns the pairs
+//     before / after it), so every band sample is written once.
+//   * Level-1 stage: each wavefront lifts TH1 / 4 core rows (+ 2 x 4 halo) of
+//     the window from LDS, with whole-sample symmetric extension of LL0
+//     applied to the LDS indices (the level-0 stage computed every real LL0
+//     sample the mirrored window reaches), then stores as k_dwt_fwd.
+// Level-0 windows overlap (halo re-reads hit in L2) and the LL0 halo of the
+// level-1 windows is computed twice; in exchange 8 B per LL0 sample of HBM
+// traffic and one launch disappear.  (A variant walking 4 consecutive
+// 16-row windows per wavefront with the overlap rows carried in registers,
+// as k_dwt_fwd_stream, measured 189 us against 182 for NY = 4.)
+// ---------------------------------------------------------------------------
+constexpr int F01_TH0 = 24;  // level-0 window rows
+template <bool IRREV, int NY>
+struct F01Geo {
+    static constexpr int H = IRREV ? 4 : 2;
+    static constexpr int PW = (DWT_WIN - 2 * H) / 2;  // LL0 columns per level-0 window
+    static constexpr int W1 = 2 * PW;                 // level-1 window columns
+    static constexpr int CW1 = W1 - 2 * H;
+    static constexpr int R1 = NY * F01_TH0 / 2;       // level-1 window rows
+    static constexpr int TH1 = R1 - 2 * H;
+    static constexpr int THW = TH1 / 4;               // level-1 core rows per wavefront
+    static_assert(THW * 4 == TH1 && THW % 2 == 0, "level-1 rows split into even per-wavefront windows");
+};
+
+static int env_int(const char *name, int dflt);
+// level-0 row windows per workgroup (GRKGPU_DWT_F01 = 2 / 4 / 6; 0 disables
+// the fusion on the host side)
+int dwt01_ny() {
+    const int v = env_int("GRKGPU_DWT_F01", 4);
+    return v == 2 || v == 6 ? v : 4;
+}
+
+int dwt01_tiles(int irrev, int rw1, int rh1, int casx1, int casy1, int *tiles_x) {
+    if (!irrev) return 0;  // 9/7 only
+    const int ny = dwt01_ny();
+    const int cw = F01Geo<true, 4>::CW1;
+    const int th = ny == 2 ? F01Geo<true, 2>::TH1 : ny == 6 ? F01Geo<true, 6>::TH1 : F01Geo<true, 4>::TH1;
+    *tiles_x = (rw1 + casx1 + cw - 1) / cw;
+    return *tiles_x * ((rh1 + casy1 + th - 1) / th);
+}
+
+template <bool IRREV, int NY>
+__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__restrict__ jobs0,
+                                                             const DwtJob *__restrict__ jobs1, int lay) {
+    using F = F01Geo<IRREV, NY>;
+    using G0 = DwtGeo<IRREV, F01_TH0>;
+    constexpr int H = F::H, R0 = G0::R;
+    __shared__ int32_t ll[F::R1][F::W1];
+    const int gx = gridDim.x;
+    int L = blockIdx.y * gx + blockIdx.x;
+    if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+    const int job = L / gx, wg = L % gx;
+    const DwtJob &J0 = jobs0[job];
+    const DwtJob &J1 = jobs1[job];
+    const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
+    const int ntx = (rw1 + casx1 + F::CW1 - 1) / F::CW1, nty = (rh1 + casy1 + F::TH1 - 1) / F::TH1;
+    if (wg >= ntx * nty) return;  // uniform over the workgroup
+    const int tx1 = wg % ntx, ty1 = wg / ntx;
+    const int xw1 = tx1 * F::CW1 - casx1 - H, yw1 = ty1 * F::TH1 - casy1 - H;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // level-0 pairs (LL0 coordinates) whose bands this workgroup stores
+    const int P0 = tx1 == 0 ? INT32_MIN : xw1 + H, P1 = tx1 == ntx - 1 ? INT32_MAX : xw1 + H + F::CW1;
+    const int Q0 = ty1 == 0 ? INT32_MIN : yw1 + H, Q1 = ty1 == nty - 1 ? INT32_MAX : yw1 + H + F::TH1;
+
+    // ---- level 0: 2 column windows x NY row windows ----
+    {
+        const int rw = J0.rw, rh = J0.rh, casx = J0.casx, casy = J0.casy;
+        const int k = w & 1;
+        const int xw = 2 * (xw1 + F::PW * k) + casx - H;
+        const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
+        const rsrc_t in = mkbuf(J0.in, J0.in_bytes);
+        const int st = (int)J0.in_stride * 4;
+        const bool vec = (casx | (J0.in_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
+        const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+        const int corel = H / 2, coreh = corel + F::PW;
+        const bool lane_core = lane >= corel && lane < coreh;
+        const int pc = (gx0 - casx) >> 1;  // this lane's pair column (LL0 coordinates)
+        const bool own_c = lane_core && pc >= P0 && pc < P1;
+        const bool okx0 = own_c && gx0 >= 0 && gx0 < rw, okx1 = own_c && gx1 >= 0 && gx1 < rw;
+        const int vl = okx0 ? pc * 4 : OOB;
+        const int vh = okx1 ? (J0.snx + pc + casx) * 4 : OOB;
+        const rsrc_t bandb = mkbuf(J0.bands, J0.bands_bytes);
+        const int bst = (int)J0.bands_stride * 4;
+        const int lcol = lane_core ? pc - xw1 : 0;  // LDS column of this lane's LL sample
+        for (int jy = w >> 1; jy < NY; jy += DWT_WAVES / 2) {
+            const int yw = 2 * (yw1 + (F01_TH0 / 2) * jy) + casy - H;
+            int32_t lo[R0], hi[R0];
+            const bool rows_in = yw >= 0 && yw + R0 <= rh;  // wave-uniform
+            if (vec && rows_in) {
+                const int base = yw * st;
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, base + r * st, 0);
+                    lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int so = mirror_idx(yw + r, rh) * st;
+                    lo[r] = ld32(in, o0, so); hi[r] = ld32(in, o1, so);
+                }
+            }
+            fwd_vertical<IRREV, R0>(lo, hi, rh, casy);
+            const int prow0 = yw1 + (F01_TH0 / 2) * jy;  // pair row of window row H
+#pragma unroll
+            for (int r = H; r < H + F01_TH0; ++r) {
+                int32_t Lv = lo[r], Hv = hi[r];
+                if constexpr (IRREV) {
+                    const int32_t kk = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
+                    Lv = fixmul13(Lv, kk); Hv = fixmul13(Hv, kk);
+                    Hv = lift<2>(Hv, Lv, from_next(Lv));
+                    Lv = lift<3>(Lv, from_prev(Hv), Hv);
+                    Hv = lift<4>(Hv, Lv, from_next(Lv));
+                    Lv = lift<5>(Lv, from_prev(Hv), Hv);
+                    Hv = fixmul13(Hv, 5039);
+                    Lv = fixmul13(Lv, 6659);
+                } else {
+                    Hv = lift<0>(Hv, Lv, from_next(Lv));
+                    Lv = lift<1>(Lv, from_prev(Hv), Hv);
+                }
+                const int prow = prow0 + ((r - H) >> 1);
+                const int gy = yw + r;
+                const bool rok = prow >= Q0 && prow < Q1 && gy >= 0 && gy < rh;  // wave-uniform
+                if ((r & 1) == 0) {
+                    if (lane_core) ll[prow - yw1][lcol] = Lv;
+                    if (rok) st32(Hv, bandb, vh, prow * bst);  // HL
+                } else if (rok) {
+                    const int so = (J0.sny + prow + casy) * bst;  // LH | HH row (pair row + casy)
+                    st32(Lv, bandb, vl, so);
+                    st32(Hv, bandb, vh, so);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- level 1 from LDS: wavefront w lifts core rows [w THW, (w + 1) THW) ----
+    {
+        constexpr int RW = F::THW + 2 * H;
+        const int yw = yw1 + F::THW * w;
+        const int gx0 = xw1 + 2 * lane;
+        const int c0 = min(max(mirror_idx(gx0, rw1) - xw1, 0), F::W1 - 1);
+        const int c1 = min(max(mirror_idx(gx0 + 1, rw1) - xw1, 0), F::W1 - 1);
+        int32_t lo[RW], hi[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int rr = min(max(mirror_idx(yw + r, rh1) - yw1, 0), F::R1 - 1);
+            lo[r] = ll[rr][c0];
+            hi[r] = ll[rr][c1];
+        }
+        fwd_vertical<IRREV, RW>(lo, hi, rh1, casy1);
+        fwd_horizontal_store<IRREV, F::THW, false, 0, F::W1>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 // Rows per window: tall windows for big levels (less halo re-read), short
@@ -952,6 +1120,21 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         if (irrev) hipLaunchKernelGGL((k_dwt_inv<true, TH>), grid, block, 0, s, jobs, lay);
         else hipLaunchKernelGGL((k_dwt_inv<false, TH>), grid, block, 0, s, jobs, lay);
     }
+}
+
+// Forward levels 0 + 1 of a 9/7 plan in one launch (k_dwt_fwd01); jobs1[i]
+// is level 1 of the tile-component of jobs0[i].
+hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
+                            hipStream_t s) {
+    if (!njobs || !max_tiles || !irrev) return hipErrorInvalidValue;
+    const int lay = env_int("GRKGPU_DWT_LAY", 1);
+    const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
+    switch (dwt01_ny()) {
+        case 2: hipLaunchKernelGGL((k_dwt_fwd01<true, 2>), g, b, 0, s, jobs0, jobs1, lay); break;
+        case 6: hipLaunchKernelGGL((k_dwt_fwd01<true, 6>), g, b, 0, s, jobs0, jobs1, lay); break;
+        default: hipLaunchKernelGGL((k_dwt_fwd01<true, 4>), g, b, 0, s, jobs0, jobs1, lay); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int code, int irrev,

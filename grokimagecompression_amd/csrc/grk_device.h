@@ -85,6 +85,11 @@ constexpr int DWT_FUSED_MCT3 = 1 << 17;  // ... with fused DC shift + MCT (jobs 
 void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
                            int inverse, hipStream_t s);
+// forward 9/7 levels 0 and 1 in one launch (dwt.hip k_dwt_fwd01): workgroups
+// per job from dwt01_tiles (level-1 geometry), 0 if unsupported
+int dwt01_tiles(int irrev, int rw1, int rh1, int casx1, int casy1, int *tiles_x);
+hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
+                            hipStream_t s);
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.

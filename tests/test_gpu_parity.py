@@ -142,6 +142,29 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
         assert np.array_equal(t.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("ny", ["2", "4", "6", "0"])
+@pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
+                                       ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
+                                       ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
+@pytest.mark.parametrize("numres", [3, 6])
+def test_dwt_fused01_stage_vs_oracle(oracle, monkeypatch, ny, shape_off, numres):
+    """9/7 levels 0 + 1 in one launch (k_dwt_fwd01, LL0 in LDS; default when
+    both resolutions are >= 16 x 16), at each workgroup height
+    (GRKGPU_DWT_F01 = 2 / 4 / 6 level-0 row windows; 0 = two launches), on
+    odd sizes and offsets (every cas parity, image edges inside the windows)."""
+    import torch
+    import grokimagecompression_amd as grk
+    monkeypatch.setenv("GRKGPU_DWT_F01", ny)
+    (h, w), (x0, y0) = shape_off
+    rng = np.random.default_rng(h * 31 + w + numres)
+    a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
+    ref = oracle.dwt_fwd(a, x0, y0, numres, True)
+    t = torch.from_numpy(a).cuda()
+    grk.dwt_fwd(t, x0, y0, numres, True)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("irrev", [False, True])
 @pytest.mark.parametrize("shape_off", [((64, 64), (0, 0)), ((77, 100), (3, 5)), ((129, 200), (1, 1)),
                                        ((513, 257), (0, 3)), ((300, 497), (2, 2)), ((37, 260), (1, 1)),
