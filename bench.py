@@ -243,7 +243,7 @@ def main():
     # launches): per-launch algorithmic bytes / mean launch duration.
     bdwt = dwt_bytes(H, W, C)
     fused01 = os.environ.get("GRKGPU_DWT_F01", "4") != "0"  # levels 0 + 1 in one launch (dwt.hip k_dwt_fwd01)
-    nlaunch = 4 if fused01 else 5
+    nlaunch = 4 if fused01 else 5  # fused: levels 0+1, then 2, 3, 4
     torch.cuda.synchronize()
     iso = []
     p97 = grk.CParams.make(irreversible=True)

@@ -408,6 +408,8 @@ struct DwtPlan {
     std::vector<Copy2D> copies2d;  // reduced decode at resolution 0: LL band -> compact output
     bool fused0 = false;  // forward level 0 reads the image planes (DC shift + MCT fused, dwt.hip)
     bool mct3 = false;    // ... and its jobs are MCT component triples (tile-major, component-minor)
+    bool inverse = false;
+    std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
 };
 
 // inverse with numres_dec < tc.numres (reduced-resolution decode): only the
@@ -416,6 +418,7 @@ struct DwtPlan {
 static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *coef, int32_t *llbase, int irrev,
                         bool inverse, uint32_t numres_dec = 0) {
     const uint32_t stride = tc.r.w(), rows = tc.r.h();
+    P.inverse = inverse;
     if (!inverse || numres_dec == 0 || numres_dec > tc.numres) numres_dec = tc.numres;
     if (inverse && numres_dec == 1 && tc.numres > 1) {
         const Rect &r0 = tc.res[0].r;
@@ -478,6 +481,38 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
     }
 }
 
+// Forward 9/7 levels l and l + 1 fused into one launch (dwt.hip
+// k_dwt_fwd01: level l + 1 lifted from level l's LL band kept in LDS) when
+// every tile-component has both levels, level l is not the fused DC shift +
+// MCT one, and the resolutions are big enough (>= 16 samples each way) for
+// the fused windows; GRKGPU_DWT_F01=0 keeps one launch per level.  Returns
+// the workgroups per job, 0 = not fused.
+static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev) {
+    const char *e = getenv("GRKGPU_DWT_F01"), *strip = getenv("GRKGPU_DWT_STRIP");
+    if (P.inverse || !irrev || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || (e && *e && !atoi(e))) return 0;
+    if (strip && *strip && atoi(strip)) return 0;  // the strip kernels' experiment keeps every level separate
+    const auto &l0 = P.levels[li], &l1 = P.levels[li + 1];
+    if (l0.empty() || l0.size() != l1.size()) return 0;
+    // only where the pair still fills the chip (GRKGPU_DWT_F01_MIN samples,
+    // default 2^23): the 8K frame's levels 2 + 3 fused took 26 us against
+    // 14 + 7 apart (378 workgroups)
+    const char *mn = getenv("GRKGPU_DWT_F01_MIN");
+    uint64_t samples = 0;
+    for (auto &j : l0) samples += (uint64_t)j.rw * j.rh;
+    if (samples < (mn && *mn ? (uint64_t)atoll(mn) : (uint64_t)1 << 23)) return 0;
+    uint32_t maxt = 0;
+    for (size_t i = 0; i < l0.size(); ++i) {
+        const DwtJob &a = l0[i], &b = l1[i];
+        if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
+        if (a.out != b.in) return 0;  // level l + 1 must read level l's LL
+        int tx;
+        const int n = dwt01_tiles(irrev, b.rw, b.rh, b.casx, b.casy, &tx);
+        if (n <= 0) return 0;
+        maxt = std::max<uint32_t>(maxt, (uint32_t)n);
+    }
+    return maxt;
+}
+
 // Pick each level's window height from the level's total size; tile counts.
 static void dwt_finalize(DwtPlan &P, int irrev) {
     P.th.assign(P.levels.size(), 8);
@@ -495,6 +530,39 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
         // TH 8, 168 at 16, 194 at 32; 9/7 229 / 319 / 330)
         if (l == 0 && P.mct3) P.th[l] = 8;
         for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j.rw, j.rh, j.casx, j.casy, &j.tiles_x, &j.ntiles);
+    }
+    // Fused level pairs (k_dwt_fwd01).  A fused pair never writes its first
+    // level's LL band, so the LL ping-pong is re-dealt: every level reads the
+    // last LL band written and writes into the slot that is not the one its
+    // launch reads (for a fused pair: the pair's input), so no launch reads
+    // and writes one buffer.  Without fused pairs this is the plan's own
+    // alternation.
+    P.f01.assign(P.levels.size(), 0);
+    bool any = false;
+    for (size_t l = 0; l + 1 < P.levels.size(); ++l)
+        if ((P.f01[l] = dwt_f01_tiles(P, l, irrev))) { any = true; ++l; }
+    // the re-deal below pairs job i of every level (one tile-component)
+    for (auto &l : P.levels) any = any && l.size() == P.levels[0].size();
+    if (!any) {
+        P.f01.assign(P.levels.size(), 0);
+        return;
+    }
+    struct Slot { int32_t *p; uint32_t stride, bytes; };
+    for (size_t i = 0; i < P.levels[0].size(); ++i) {
+        Slot slot[2] = {{P.levels[0][i].out, P.levels[0][i].out_stride, P.levels[0][i].out_bytes}, {nullptr, 0, 0}};
+        if (P.levels.size() > 2) slot[1] = {P.levels[1][i].out, P.levels[1][i].out_stride, P.levels[1][i].out_bytes};
+        Slot prev{const_cast<int32_t *>(P.levels[0][i].in), P.levels[0][i].in_stride, P.levels[0][i].in_bytes};
+        for (size_t l = 0; l < P.levels.size(); ++l) {
+            DwtJob &j = P.levels[l][i];
+            const bool second = l > 0 && P.f01[l - 1];
+            if (!second) { j.in = prev.p; j.in_stride = prev.stride; j.in_bytes = prev.bytes; }
+            if (j.out != j.bands) {  // not the last level (that one writes its LL into the Mallat buffer)
+                const int32_t *rd = second ? P.levels[l - 1][i].in : j.in;
+                const Slot &o = slot[0].p != rd ? slot[0] : slot[1];
+                j.out = o.p; j.out_stride = o.stride; j.out_bytes = o.bytes;
+            }
+            prev = {j.out, j.out_stride, j.out_bytes};
+        }
     }
 }
 
@@ -515,41 +583,20 @@ static hipError_t dwt_upload(DwtPlan &P, DevBuf &djobs, HostBuf &hjobs, int irre
 }
 
 // Run the levels (job table already uploaded by dwt_upload on the same stream).
-// Forward 9/7 levels 0 and 1 fused into one launch (dwt.hip k_dwt_fwd01)
-// when every tile-component has both levels, level 0 is not the fused
-// DC shift + MCT one, and the resolutions are big enough (>= 16 samples each
-// way) for the fused windows; GRKGPU_DWT_F01=0 keeps two launches.  Returns
-// the workgroups per job, 0 = not fused.
-static uint32_t dwt_f01_tiles(const DwtPlan &P, int irrev, bool inverse) {
-    const char *e = getenv("GRKGPU_DWT_F01"), *strip = getenv("GRKGPU_DWT_STRIP");
-    if (inverse || !irrev || P.fused0 || P.levels.size() < 2 || (e && *e && !atoi(e))) return 0;
-    if (strip && *strip && atoi(strip)) return 0;  // the strip kernels' experiment keeps every level separate
-    const auto &l0 = P.levels[0], &l1 = P.levels[1];
-    if (l0.empty() || l0.size() != l1.size()) return 0;
-    uint32_t maxt = 0;
-    for (size_t i = 0; i < l0.size(); ++i) {
-        const DwtJob &a = l0[i], &b = l1[i];
-        if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
-        int tx;
-        const int n = dwt01_tiles(irrev, b.rw, b.rh, b.casx, b.casy, &tx);
-        if (n <= 0) return 0;
-        maxt = std::max<uint32_t>(maxt, (uint32_t)n);
-    }
-    return maxt;
-}
-
-// All levels of an uploaded plan (job table at djobs, levels back to back).
+// All levels of an uploaded plan (job table at djobs, levels back to back);
+// fused 9/7 level pairs (P.f01) as one launch (8K frame: 0+1, then 2, 3, 4).
 static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, bool inverse, hipStream_t s) {
     hipError_t e = hipSuccess;
-    size_t k = 0, li = 0;
-    if (const uint32_t t01 = dwt_f01_tiles(P, irrev, inverse)) {
-        e = launch_dwt_fwd01(djobs, djobs + P.levels[0].size(), (uint32_t)P.levels[0].size(), t01, irrev, s);
-        if (e != hipSuccess) return e;
-        k = P.levels[0].size() + P.levels[1].size();
-        li = 2;
-    }
-    for (; li < P.levels.size(); ++li) {
+    size_t k = 0;
+    for (size_t li = 0; li < P.levels.size(); ++li) {
         const auto &l = P.levels[li];
+        if (li < P.f01.size() && P.f01[li]) {
+            e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, s);
+            if (e != hipSuccess) return e;
+            k += l.size() + P.levels[li + 1].size();
+            ++li;
+            continue;
+        }
         uint32_t maxt = 0;
         for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
         const int code = P.th[li] | (li == 0 && P.fused0 && !inverse ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) : 0);

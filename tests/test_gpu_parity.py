@@ -148,13 +148,15 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
 @pytest.mark.parametrize("numres", [3, 6])
 def test_dwt_fused01_stage_vs_oracle(oracle, monkeypatch, ny, shape_off, numres):
-    """9/7 levels 0 + 1 in one launch (k_dwt_fwd01, LL0 in LDS; default when
-    both resolutions are >= 16 x 16), at each workgroup height
+    """9/7 level pairs in one launch (k_dwt_fwd01, LL in LDS; default for
+    pairs of >= 2^23 samples whose resolutions are >= 16 x 16, here forced
+    onto every qualifying pair: 0+1, 2+3, ...), at each workgroup height
     (GRKGPU_DWT_F01 = 2 / 4 / 6 level-0 row windows; 0 = two launches), on
     odd sizes and offsets (every cas parity, image edges inside the windows)."""
     import torch
     import grokimagecompression_amd as grk
     monkeypatch.setenv("GRKGPU_DWT_F01", ny)
+    monkeypatch.setenv("GRKGPU_DWT_F01_MIN", "0")  # fuse every qualifying pair, not only chip-filling ones
     (h, w), (x0, y0) = shape_off
     rng = np.random.default_rng(h * 31 + w + numres)
     a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
