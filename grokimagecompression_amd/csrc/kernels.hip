@@ -447,54 +447,83 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
 }
 
 // Rebuild of the decoded values from the lane-interleaved bit-plane rows:
-// one wavefront per (64-block group, RB_ROWS rows), lane = column.  The
-// per-(block, row, plane) row words are wave-uniform, so they come through
-// scalar loads (a group's rows are contiguous per plane row, so consecutive
-// blocks share scalar-cache lines); the coefficient rows are stored
-// coalesced.  Then T1Part1::postDecode scaling (5/3: v/2, 9/7:
-// float(v) * step).  roi (null: none): per-block ROI up-shift --
-// T1Part1::post_decode (T1Part1.cpp:230-250) shifts magnitudes >= 2^roishift
-// down by roishift (and zeroes the block for a shift >= 31) before the
-// scaling.
+// one workgroup of 4 wavefronts per (64-block group, RB_ROWS rows).  For
+// each row, lane l of every wavefront stages its block's plane words of that
+// row into LDS (wavefront w takes the planes q = w mod 4; one 512-byte run
+// per plane); then wavefront w takes blocks b = w mod 4, and lane x forms
+// coefficient (y, x) from the LDS words (broadcast reads; the block's
+// parameters by readlane) and the row is stored coalesced.  Then
+// T1Part1::postDecode scaling (5/3: v/2, 9/7: float(v) * step).  roi (null:
+// none): per-block ROI up-shift -- T1Part1::post_decode (T1Part1.cpp:230-250)
+// shifts magnitudes >= 2^roishift down by roishift (and zeroes the block for
+// a shift >= 31) before the scaling.
 constexpr uint32_t RB_ROWS = 8;
-__global__ __launch_bounds__(64) void k_t1_rebuild(const DecBlock *__restrict__ blocks, uint32_t n,
-                                                   const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles,
-                                                   const uint8_t *__restrict__ roi) {
-    const uint32_t g = blockIdx.x, x = threadIdx.x;
+__global__ __launch_bounds__(256) void k_t1_rebuild(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                    const T1Scratch *__restrict__ scr, int32_t *__restrict__ tiles,
+                                                    const uint8_t *__restrict__ roi) {
+    __shared__ uint64_t s_sig[32][64];  // [plane][block]
+    __shared__ uint64_t s_ref[32][64];
+    __shared__ uint64_t s_neg[64];
+    const uint32_t g = blockIdx.x, l = threadIdx.x & 63;
+    const int32_t w = (int32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t y0 = blockIdx.y * RB_ROWS;
     const uint64_t *gb = t1_group_base(const_cast<T1Scratch *>(scr), g, sizeof(T1Scratch));
     const uint32_t nb = n - g * 64 < 64 ? n - g * 64 : 64;
-    for (uint32_t l = 0; l < nb; ++l) {
-        const DecBlock b = blocks[g * 64 + l];
-        if (y0 >= b.h) continue;
-        const DecodedPlanes dp = decoded_planes(b.len ? b.numpasses : 0, b.numbps);
-        const uint32_t rs = roi ? roi[g * 64 + l] : 0u;
-        const uint32_t y1 = b.h < y0 + RB_ROWS ? b.h : y0 + RB_ROWS;
-        const bool col = x < b.w;
-        int32_t *dst = tiles + b.dst_off + x;
-        const uint64_t *pa = gb + (size_t)T1R_PA * 64 + l, *pb = gb + (size_t)T1R_PB * 64 + l;
-        const uint64_t *ng = gb + (size_t)T1R_NEG * 64 + l;
-        for (uint32_t y = y0; y < y1; ++y) {
+    // this lane's block (lane l < nb)
+    DecBlock mb{};
+    DecodedPlanes dp{-1, 0, 32};
+    uint32_t rs = 0;
+    if (l < nb) {
+        mb = blocks[g * 64 + l];
+        dp = decoded_planes(mb.len ? mb.numpasses : 0, mb.numbps);
+        rs = roi ? roi[g * 64 + l] : 0u;
+    }
+    // packed per-block parameters for the readlane broadcasts
+    const uint32_t pk = (uint32_t)(dp.top & 0xff) | ((uint32_t)dp.low & 0xff) << 8 | ((uint32_t)dp.qlow & 0xff) << 16 |
+                        (rs & 0xff) << 24;
+    const uint32_t wh = mb.w | mb.h << 8 | (mb.irrev ? 1u << 16 : 0u);
+    const uint64_t *pa = gb + (size_t)T1R_PA * 64 + l, *pb = gb + (size_t)T1R_PB * 64 + l;
+    const uint64_t *ng = gb + (size_t)T1R_NEG * 64 + l;
+    for (uint32_t y = y0; y < y0 + RB_ROWS; ++y) {
+        if (y < mb.h && dp.top >= 0) {
+            for (int32_t q = dp.low + ((w - dp.low) & 3); q <= dp.top; q += 4)
+                s_sig[q][l] = pa[(size_t)((uint32_t)q * 64 + y) * 64];
+            for (int32_t q = dp.qlow + ((w - dp.qlow) & 3); q < dp.top; q += 4)
+                s_ref[q][l] = pb[(size_t)((uint32_t)q * 64 + y) * 64];
+            if (w == 0) s_neg[l] = ng[(size_t)(y + 1) * 64];
+        }
+        __syncthreads();
+        for (uint32_t b = (uint32_t)w; b < nb; b += 4) {
+            const uint32_t bwh = __builtin_amdgcn_readlane(wh, b);
+            const uint32_t bh = (bwh >> 8) & 0xff, bw = bwh & 0xff;
+            if (y >= bh) continue;  // uniform
+            const uint32_t bpk = __builtin_amdgcn_readlane(pk, b);
+            const int32_t top = (int8_t)(bpk & 0xff), low = (int32_t)((bpk >> 8) & 0xff);
+            const int32_t qlow = (int32_t)((bpk >> 16) & 0xff);
+            const uint32_t brs = bpk >> 24;
             int32_t v = 0;
-            if (dp.top >= 0) {
+            if (top >= 0) {
                 uint32_t cs = 0;  // bit (q - low): significant after plane q
-                for (int32_t q = dp.top; q >= dp.low; --q)
-                    cs = (cs << 1) | (uint32_t)((pa[(size_t)((uint32_t)q * 64 + y) * 64] >> x) & 1u);
+                for (int32_t q = top; q >= low; --q) cs = (cs << 1) | (uint32_t)((s_sig[q][b] >> l) & 1u);
                 if (cs) {
-                    const int32_t p = dp.low + 31 - (int32_t)__clz(cs);
-                    const int32_t ql = p < dp.qlow ? p : dp.qlow;
+                    const int32_t p = low + 31 - (int32_t)__clz(cs);
+                    const int32_t ql = p < qlow ? p : qlow;
                     uint32_t cr = 0;  // bit (q - ql): refinement bit at plane q, q in [ql, p)
-                    for (int32_t q = p - 1; q >= ql; --q)
-                        cr = (cr << 1) | (uint32_t)((pb[(size_t)((uint32_t)q * 64 + y) * 64] >> x) & 1u);
+                    for (int32_t q = p - 1; q >= ql; --q) cr = (cr << 1) | (uint32_t)((s_ref[q][b] >> l) & 1u);
                     const uint32_t bits = (1u << (p - ql)) | cr;
                     int32_t mag = (int32_t)((bits << (ql + 1)) | (1u << ql));
-                    if (rs) mag = rs >= 31 ? 0 : (mag >= (1 << rs) ? mag >> rs : mag);
-                    v = ((ng[(size_t)(y + 1) * 64] >> x) & 1u) ? -mag : mag;
+                    if (brs) mag = brs >= 31 ? 0 : (mag >= (1 << brs) ? mag >> brs : mag);
+                    v = ((s_neg[b] >> l) & 1u) ? -mag : mag;
                 }
             }
-            const int32_t o = !b.irrev ? v / 2 : __float_as_int(__fmul_rn((float)v, b.step));
-            if (col) dst[(size_t)y * b.dstride] = o;
+            const float step = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mb.step), b));
+            const int32_t o = (bwh >> 16) ? __float_as_int(__fmul_rn((float)v, step)) : v / 2;
+            const uint32_t off_lo = __builtin_amdgcn_readlane((uint32_t)mb.dst_off, b);
+            const uint32_t off_hi = __builtin_amdgcn_readlane((uint32_t)(mb.dst_off >> 32), b);
+            const uint32_t stride = __builtin_amdgcn_readlane(mb.dstride, b);
+            if (l < bw) tiles[(((uint64_t)off_hi << 32) | off_lo) + (size_t)y * stride + l] = o;
         }
+        __syncthreads();
     }
 }
 
@@ -607,7 +636,7 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
                            s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
                            nullptr);  // the ROI shift only moves BYPASS pass boundaries
-    hipLaunchKernelGGL(k_t1_rebuild, dim3((n + 63) / 64, 64 / RB_ROWS), dim3(64), 0, s, blocks, n, scratch, tiles,
+    hipLaunchKernelGGL(k_t1_rebuild, dim3((n + 63) / 64, 64 / RB_ROWS), dim3(256), 0, s, blocks, n, scratch, tiles,
                        roi);
     return hipGetLastError();
 }

@@ -284,8 +284,10 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.sig[i] = st.sig[k + i];
             if (vsc) s.sig[5] = 0;
+            // vis (visited by this plane's SPP) is reset by every cleanup
+            // pass, so an SPP starts from zero and only the SPP stores it
 #pragma unroll
-            for (int i = 0; i < 4; ++i) s.vis[i] = st.vis[k + 1 + i];
+            for (int i = 0; i < 4; ++i) s.vis[i] = passtype == 0 ? 0 : (uint64_t)st.vis[k + 1 + i];
             if (passtype == 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) { s.ref[i] = st.ref[k + 1 + i]; s.bit[i] = 0; }
@@ -308,37 +310,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.neg[i] = st.neg[k + i];
             if (vsc) s.neg[5] = 0;
-#ifdef GRK_T1_UNIFY_SPP_CUP
-            // SPP and cleanup sharing one column loop (runtime pass type):
-            // measured 3-15 % SLOWER (lone 8K decode 52.0 -> 54.5 ms, bench
-            // 2431-2472 -> 2262-2409 Mpix/s): the union of both passes' work
-            // per column costs more than the divergence it removes
-            {
-                const bool cup = passtype == 2;
-                uint64_t cand = 0;
-                if (cup) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if ((uint32_t)r < nr) cand |= ~(s.sig[r + 1] | s.vis[r]);
-                } else {
-                    cand = spp_candidates(s, nr);
-                }
-                cand &= wm;
-                while (cand) {
-                    const uint32_t x = ctz64(cand);
-                    const uint64_t done = ((uint64_t)2 << x) - 1;  // x = 63 wraps to all ones
-                    const bool grew = d3_column<-1>(d, cxw, T, s, x, nr, cup);
-                    cand &= ~done;
-                    // SPP: a new significant sample in column x can only make
-                    // column x + 1 a candidate (x - 1 is behind the scan)
-                    if (grew && !cup) cand |= ((uint64_t)2 << x) & wm;
-                }
-                if (cup) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s.vis[r] = 0;
-                }
-            }
-#else
+            bool chg = false;  // a sample of the stripe became significant
             if (passtype == 0) {
                 uint64_t cand = spp_candidates(s, nr) & wm;
                 while (cand) {
@@ -349,6 +321,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                     // a new significant sample in column x can only make
                     // column x + 1 a candidate (x - 1 is behind the scan)
                     if (grew) cand |= ((uint64_t)2 << x) & wm;
+                    chg = chg || grew;
                 }
             } else {
                 uint64_t cand = 0;
@@ -359,18 +332,22 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                 while (cand) {
                     const uint32_t x = ctz64(cand);
                     cand &= cand - 1;
-                    d3_column<1>(d, cxw, T, s, x, nr);
+                    chg = d3_column<1>(d, cxw, T, s, x, nr) || chg;
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s.vis[r] = 0;
             }
-#endif
+            // write back only what changed: sig / neg if the stripe grew, vis
+            // after an SPP, and the significance-after-plane rows after the
+            // cleanup pass -- or after the SPP when this plane's cleanup is
+            // not decoded (truncated pass count)
+            const bool wsa = passtype == 2 || passno + 2 >= numpasses;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                st.sig[k + 1 + i] = s.sig[i + 1];
-                st.neg[k + 1 + i] = s.neg[i + 1];
-                st.vis[k + 1 + i] = s.vis[i];
-                if ((uint32_t)i < nr) sa[k + i] = s.sig[i + 1];
+                if (chg) {
+                    st.sig[k + 1 + i] = s.sig[i + 1];
+                    st.neg[k + 1 + i] = s.neg[i + 1];
+                }
+                if (passtype == 0) st.vis[k + 1 + i] = s.vis[i];
+                if (wsa && (uint32_t)i < nr) sa[k + i] = s.sig[i + 1];
             }
         }
         if (passtype == 2 && (sty & CBLKSTY_SEGSYM))
