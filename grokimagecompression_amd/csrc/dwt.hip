@@ -226,7 +226,7 @@ __device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R],
 
 // Horizontal lifting of the window's core rows, then the stores into the
 // LL buffer and the Mallat bands.
-template <bool IRREV, int TH, bool NOCOMP = false, int BAUX = 0, int WIN = DWT_WIN>
+template <bool IRREV, int TH, int WIN = DWT_WIN>
 __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&lo)[DwtGeo<IRREV, TH>::R],
                                                      int32_t (&hi)[DwtGeo<IRREV, TH>::R], int ty, int yw, int gx0,
                                                      int lane) {
@@ -250,12 +250,11 @@ __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&
 #pragma unroll
     for (int r = G::HALO; r < G::HALO + G::TH; ++r) {
         int32_t L = lo[r], H = hi[r];
-        if (IRREV && rh > 1 && !NOCOMP) {
+        if (IRREV && rh > 1) {
             const int32_t k = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
             L = fixmul13(L, k); H = fixmul13(H, k);
         }
-        if (NOCOMP) {
-        } else if (rw > 1) {
+        if (rw > 1) {
             if constexpr (!IRREV) {
                 H = lift<0>(H, L, from_next(L));
                 L = lift<1>(L, from_prev(H), H);
@@ -278,39 +277,24 @@ __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&
         if ((r & 1) == 0) {  // low row -> LL | HL
             const int iy = lbase + r / 2;
             st32(L, outb, vl, iy * ost);
-            st32<BAUX>(H, bandb, vh, iy * bst);
+            st32(H, bandb, vh, iy * bst);
         } else {             // high row -> LH | HH
             const int so = (hbase + (r - 1) / 2) * bst;
-            st32<BAUX>(L, bandb, vl, so);
-            st32<BAUX>(H, bandb, vh, so);
+            st32(L, bandb, vl, so);
+            st32(H, bandb, vh, so);
         }
     }
 }
 
-// FUSED: 0 = reads `in`; 1 = DC shift fused into the loads (fused_load);
-// 2 = the three MCT components of one window in one workgroup of 3
-// wavefronts (wavefront w = component w): each loads its own image plane,
-// the raw rows are exchanged through LDS, and each wavefront forms its MCT
-// component -- every image sample is read from HBM once.
-template <bool IRREV, int TH, int XM = 0, int FUSED = 0, int BAUX = 0>
+// FUSED: 0 = reads `in`; 1 = DC shift (+ MCT for a component of an MCT
+// triple) fused into the loads (fused_load: 3 planes per MCT component).
+template <bool IRREV, int TH, int FUSED = 0>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__restrict__ jobs, int lay) {
-    constexpr bool NOCOMP = XM != 0;  // timing probes: 1 no lifting, 2 loads only, 3 stores only
     using G = DwtGeo<IRREV, TH>;
     constexpr int R = G::R;
     DwtJob J;
     int tx, ty;
-    if constexpr (FUSED == 2) {
-        const int gx = gridDim.x;
-        int L = blockIdx.y * gx + blockIdx.x;
-        if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
-        const int wg = L % gx, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        J = jobs[(L / gx) * 3 + w];
-        tx = wg % J.tiles_x;
-        ty = wg / J.tiles_x;
-        if (ty >= (J.rh + J.casy + TH - 1) / TH) return;  // same for the 3 wavefronts
-    } else {
-        if (!dwt_window(jobs, lay, TH, J, tx, ty)) return;
-    }
+    if (!dwt_window(jobs, lay, TH, J, tx, ty)) return;
     const int lane = threadIdx.x & 63;
     const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
     const int xw = tx * G::CW - casx - G::HALO;  // window column origin (parity of casx)
@@ -318,18 +302,12 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
     const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
 
     int32_t lo[R], hi[R];  // column 2l (low pass) and 2l+1 (high pass)
-    if (XM == 3) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) { lo[r] = lane + r; hi[r] = lane - r; }
-    } else if (FUSED == 1) {
+    if (FUSED == 1) {
         fused_load<IRREV, R>(J, lo, hi, xw, yw, gx0, gx1);
     } else {
-        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int32_t *sp = w == 0 ? J.src[0] : w == 1 ? J.src[1] : J.src[2];  // no dynamic struct index
-        const rsrc_t in = FUSED == 2 ? mkbuf(sp, J.src_bytes) : mkbuf(J.in, J.in_bytes);
-        const int st = (int)(FUSED == 2 ? J.src_stride : J.in_stride) * 4;
-        const bool vec = (FUSED == 2 ? J.src_vec && !casx : (casx | (J.in_stride & 1)) == 0) && xw >= 0 &&
-                         xw + DWT_WIN <= rw;  // wave-uniform
+        const rsrc_t in = mkbuf(J.in, J.in_bytes);
+        const int st = (int)J.in_stride * 4;
+        const bool vec = (casx | (J.in_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
         const bool rows_in = yw >= 0 && yw + R <= rh;  // no row mirroring: offsets are base + r * stride
         if (vec && rows_in) {
             const int base = yw * st;
@@ -353,30 +331,8 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
             }
         }
     }
-    if constexpr (FUSED == 2) {  // exchange the raw planes, form this wavefront's MCT component
-        __shared__ int32_t xs[3][R][DWT_WIN];
-        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            xs[w][r][2 * lane] = lo[r];
-            xs[w][r][2 * lane + 1] = hi[r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            lo[r] = mct_px<IRREV>(J, xs[0][r][2 * lane], xs[1][r][2 * lane], xs[2][r][2 * lane]);
-            hi[r] = mct_px<IRREV>(J, xs[0][r][2 * lane + 1], xs[1][r][2 * lane + 1], xs[2][r][2 * lane + 1]);
-        }
-    }
-    if (!NOCOMP) fwd_vertical<IRREV, R>(lo, hi, rh, casy);
-    if (XM == 2) {
-        int32_t acc = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc += lo[r] ^ hi[r];
-        if (acc == 0x12345678) st32(acc, mkbuf(J.out, J.out_bytes), 0, 0);
-        return;
-    }
-    fwd_horizontal_store<IRREV, TH, NOCOMP, BAUX>(J, lo, hi, ty, yw, gx0, lane);
+    fwd_vertical<IRREV, R>(lo, hi, rh, casy);
+    fwd_horizontal_store<IRREV, TH>(J, lo, hi, ty, yw, gx0, lane);
 }
 
 // Forward level 0 of an MCT component triple in ONE wavefront per window:
@@ -1015,7 +971,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
             hi[r] = ll[rr][c1];
         }
         fwd_vertical<IRREV, RW>(lo, hi, rh1, casy1);
-        fwd_horizontal_store<IRREV, F::THW, false, 0, F::W1>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
+        fwd_horizontal_store<IRREV, F::THW, F::W1>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
     }
 }
 
@@ -1086,34 +1042,18 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         }
         return;
     }
-    if (!inverse && TH == 24 && irrev && env_int("GRKGPU_DWT_X", 0)) {  // timing probes: 1 no lifting, 2 loads only
-        if (env_int("GRKGPU_DWT_X", 0) == 1) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1>), grid, block, 0, s, jobs, lay);
-        else hipLaunchKernelGGL((k_dwt_fwd<true, TH, 2>), grid, block, 0, s, jobs, lay);
-        return;
-    }
     if (fused == 3) {  // forward level 0, MCT triples: one wavefront = the 3 components of one window
         const dim3 g3(grid.x, grid.y / 3);
         if (irrev) hipLaunchKernelGGL((k_dwt_fwd_mct3<true, TH>), g3, block, 0, s, jobs, lay);
         else hipLaunchKernelGGL((k_dwt_fwd_mct3<false, TH>), g3, block, 0, s, jobs, lay);
         return;
     }
-    if (fused == 2) {  // forward level 0, MCT triples: workgroup = the 3 components of one window
-        const dim3 g3(grid.x * DWT_WAVES, grid.y / 3), b3(192);
-        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 2>), g3, b3, 0, s, jobs, lay);
-        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 2>), g3, b3, 0, s, jobs, lay);
-        return;
-    }
     if (fused == 1) {  // forward level 0 with the DC shift in the loads
-        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 1>), grid, block, 0, s, jobs, lay);
-        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 1>), grid, block, 0, s, jobs, lay);
+        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1>), grid, block, 0, s, jobs, lay);
+        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 1>), grid, block, 0, s, jobs, lay);
         return;
     }
     if (!inverse) {
-        if (env_int("GRKGPU_DWT_BNT", 0)) {  // probe: band stores non-temporal (LL stays cached)
-            if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, 0, 2>), grid, block, 0, s, jobs, lay);
-            else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 0, 0, 2>), grid, block, 0, s, jobs, lay);
-            return;
-        }
         if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH>), grid, block, 0, s, jobs, lay);
         else hipLaunchKernelGGL((k_dwt_fwd<false, TH>), grid, block, 0, s, jobs, lay);
     } else {
@@ -1143,7 +1083,7 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
     dim3 grid((max_tiles + DWT_WAVES - 1) / DWT_WAVES, njobs), block(64 * DWT_WAVES);
     const int nch = (code >> 8) & 0xff;
     const int fused = inverse || nch ? 0
-                      : (code & DWT_FUSED_MCT3) ? (env_int("GRKGPU_DWT_MCT3", 3) == 2 ? 2 : 3)
+                      : (code & DWT_FUSED_MCT3) ? 3
                       : (code & DWT_FUSED) ? 1 : 0;
     switch (code & 0xff) {
         case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;

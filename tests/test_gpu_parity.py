@@ -69,14 +69,12 @@ def test_decode_options_match_reference(codec, name, tag):
 
 @pytest.mark.parametrize("name", ["g8_off35", "rgb12_I", "rgb8_128x96", "rgb12_tiles_I", "g16_I", "rgb8_nomct",
                                   "g8_off_tiles"])
-@pytest.mark.parametrize("mct3", ["3", "2"])
-def test_encode_fused_mct_dwt(codec, monkeypatch, name, mct3):
-    """Opt-in fused level 0 (DC shift + MCT in the first DWT level's loads,
-    GRKGPU_DWT_FUSE=1; MCT triples in one wavefront (GRKGPU_DWT_MCT3=3) or
-    three exchanging through LDS (2)): same bytes as the reference."""
+def test_encode_fused_mct_dwt(codec, monkeypatch, name):
+    """Fused level 0 forced on (GRKGPU_DWT_FUSE=1: the DC shift in the first
+    DWT level's loads; MCT triples -- 9/7 included -- in one wavefront,
+    k_dwt_fwd_mct3): same bytes as the reference."""
     import grokimagecompression_amd as grk
     monkeypatch.setenv("GRKGPU_DWT_FUSE", "1")
-    monkeypatch.setenv("GRKGPU_DWT_MCT3", mct3)
     m = MAN[name]
     img, bits = _img(m)
     p, off = grk.CParams.from_cli(m["args"])
