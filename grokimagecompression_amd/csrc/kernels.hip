@@ -214,7 +214,7 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
                                                  const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
                                                  EncResult *__restrict__ res, const uint32_t *__restrict__ perm,
-                                                 uint32_t cblksty) {
+                                                 uint32_t cblksty, uint32_t bpw) {
     __shared__ uint32_t s_mq[48];
     // 19 context words per lane at an odd stride (no bank conflicts).  The
     // read-ahead of the symbol after a pass's last one may index up to 31
@@ -224,7 +224,8 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     __shared__ uint32_t s_cx[LANES * MQ_CX_STRIDE + 32];
     for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
-    const uint32_t j = blockIdx.x * LANES + threadIdx.x;
+    if (threadIdx.x >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
+    const uint32_t j = blockIdx.x * bpw + threadIdx.x;
     if (j >= n) return;
     const uint32_t i = perm ? perm[j] : j;
     const EncBlock b = blocks[i];
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
                                                         T1Scratch *__restrict__ scr, const DecSeg *__restrict__ segs,
                                                         const uint32_t *__restrict__ seg_first, uint32_t sty,
-                                                        const uint8_t *__restrict__ roi) {
+                                                        const uint8_t *__restrict__ roi, uint32_t bpw) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
@@ -416,7 +417,8 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
     for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
-    const uint32_t i = blockIdx.x * LANES + threadIdx.x;
+    if (threadIdx.x >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
+    const uint32_t i = blockIdx.x * bpw + threadIdx.x;
     if (i >= n) return;
     const DecBlock b = blocks[i];
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
@@ -577,6 +579,18 @@ constexpr int MQ_LANES = 64;
 // ~10% faster with 16).
 constexpr int DEC_LANES = 64;
 
+// Blocks per wavefront of the lane coders: 64 keeps the most blocks resident
+// per wave slot, which is what the throughput of many frames in flight
+// needs; a launch of few blocks (a small image) is bound by its longest
+// block's chain instead, and the 64 blocks of a wavefront execute the union of
+// their paths -- there one block per wavefront (n <= 1024: at most one
+// wavefront per SIMD), then 2, 4, ... up to 64 from 4096 blocks on.
+static uint32_t t1_blocks_per_wave(uint32_t n) {
+    uint32_t b = 1;
+    while (b < 64 && (uint64_t)n > 1024ull * b) b <<= 1;
+    return n >= 4096 ? 64 : b;
+}
+
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
                             hipStream_t s, uint32_t cblksty) {
@@ -586,12 +600,13 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res, cblksty);
+    const uint32_t bpw = t1_blocks_per_wave(n);
     if (cblksty & CBLKSTY_LAZY)
-        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s,
-                           blocks, n, scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
+                           scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty, bpw);
     else
-        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + MQ_LANES - 1) / MQ_LANES), dim3(MQ_LANES), 0, s,
-                           blocks, n, scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty);
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
+                           scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty, bpw);
     return hipGetLastError();
 }
 
@@ -629,13 +644,14 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
                        seg_first);
+    const uint32_t bpw = t1_blocks_per_wave(n);
     if (cblksty & CBLKSTY_LAZY)
-        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
-                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi);
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
+                           n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi, bpw);
     else
-        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + DEC_LANES - 1) / DEC_LANES), dim3(DEC_LANES), 0,
-                           s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
-                           nullptr);  // the ROI shift only moves BYPASS pass boundaries
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
+                           n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
+                           nullptr, bpw);  // the ROI shift only moves BYPASS pass boundaries
     hipLaunchKernelGGL(k_t1_rebuild, dim3((n + 63) / 64, 64 / RB_ROWS), dim3(256), 0, s, blocks, n, scratch, tiles,
                        roi);
     return hipGetLastError();
