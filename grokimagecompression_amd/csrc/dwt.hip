@@ -830,7 +830,8 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv_stream(const DwtJob 
 // level-1 windows is computed twice; in exchange 8 B per LL0 sample of HBM
 // traffic and one launch disappear.  (A variant walking 4 consecutive
 // 16-row windows per wavefront with the overlap rows carried in registers,
-// as k_dwt_fwd_stream, measured 189 us against 182 for NY = 4.)
+// as k_dwt_fwd_stream, measured 189 us against 182 for NY = 4; non-temporal
+// band stores 203 us.)
 // ---------------------------------------------------------------------------
 constexpr int F01_TH0 = 24;  // level-0 window rows
 template <bool IRREV, int NY>
