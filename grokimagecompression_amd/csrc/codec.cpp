@@ -533,10 +533,9 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
     }
     // Fused level pairs (k_dwt_fwd01).  A fused pair never writes its first
     // level's LL band, so the LL ping-pong is re-dealt: every level reads the
-    // last LL band written and writes into the slot that is not the one its
-    // launch reads (for a fused pair: the pair's input), so no launch reads
-    // and writes one buffer.  Without fused pairs this is the plan's own
-    // alternation.
+    // last LL band written and keeps its own output slot unless its launch
+    // reads that slot (for a fused pair: the pair's input), in which case it
+    // takes the other one -- no launch reads and writes one buffer.
     P.f01.assign(P.levels.size(), 0);
     bool any = false;
     for (size_t l = 0; l + 1 < P.levels.size(); ++l)
@@ -557,9 +556,12 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
             const bool second = l > 0 && P.f01[l - 1];
             if (!second) { j.in = prev.p; j.in_stride = prev.stride; j.in_bytes = prev.bytes; }
             if (j.out != j.bands) {  // not the last level (that one writes its LL into the Mallat buffer)
+                // the plan's own slot unless the launch reads it
                 const int32_t *rd = second ? P.levels[l - 1][i].in : j.in;
-                const Slot &o = slot[0].p != rd ? slot[0] : slot[1];
-                j.out = o.p; j.out_stride = o.stride; j.out_bytes = o.bytes;
+                if (j.out == rd) {
+                    const Slot &o = slot[0].p != rd ? slot[0] : slot[1];
+                    j.out = o.p; j.out_stride = o.stride; j.out_bytes = o.bytes;
+                }
             }
             prev = {j.out, j.out_stride, j.out_bytes};
         }
