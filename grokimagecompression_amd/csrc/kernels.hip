@@ -424,8 +424,11 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
     // lane-interleaved state and bit-plane rows of this block (t1_lane.h T1Group)
+    // bpw is a power of two <= 64, so the wavefront's blocks share one group:
+    // the group (and the buffer resource) stays wave-uniform, in SGPRs
+    const uint32_t grp = __builtin_amdgcn_readfirstlane((blockIdx.x * bpw) >> 6);
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-        t1_group_base(scr, i >> 6, sizeof(T1Scratch)), 0, (int)(64 * sizeof(T1Scratch)), 0x00020000);
+        t1_group_base(scr, grp, sizeof(T1Scratch)), 0, (int)(64 * sizeof(T1Scratch)), 0x00020000);
     const uint32_t lo = (i & 63) * 8;
     LState st{LRow{gr, T1R_SIG * 512, lo}, LRow{gr, T1R_NEG * 512, lo}, LRow{gr, T1R_VIS * 512, lo},
               LRow{gr, T1R_REF * 512, lo}};

@@ -645,42 +645,15 @@ GRK_HD uint32_t sym_stream_bytes(uint32_t w, uint32_t h) {
 }
 GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h) + 2 * 64 * 8; }
 
-// Symbol stream writer: bytes packed into words, words into 16-byte chunks,
-// one 16-byte store per 16 symbols (the lanes of a wavefront write different
-// streams, so each store is its own memory segment: 4x fewer partial-line
-// writes than dword stores).  out is 16-byte aligned (slot offsets are
-// multiples of 16) and the stream area is a multiple of 16 bytes.
 struct SymOut {
     uint32_t *out;
     uint32_t acc, n;
-    uint32_t p0 = 0, p1 = 0, p2 = 0;  // completed words of the current chunk
     GRK_HD void put(uint32_t b) {
         acc |= b << ((n & 3) * 8);
         ++n;
-        if ((n & 3) == 0) {
-            const uint32_t k = ((n >> 2) - 1) & 3;
-            if (k == 3) {
-                uint4 v;
-                v.x = p0; v.y = p1; v.z = p2; v.w = acc;
-                *(uint4 *)(out + (n >> 2) - 4) = v;
-            } else {
-                p0 = k == 0 ? acc : p0;
-                p1 = k == 1 ? acc : p1;
-                p2 = k == 2 ? acc : p2;
-            }
-            acc = 0;
-        }
+        if ((n & 3) == 0) { out[(n >> 2) - 1] = acc; acc = 0; }
     }
-    GRK_HD void flush() {
-        if (!(n & 15)) return;
-        const uint32_t cw = (n >> 2) & 3;  // completed words of the last chunk; acc = the partial one
-        uint4 v;
-        v.x = cw > 0 ? p0 : acc;
-        v.y = cw > 1 ? p1 : (cw == 1 ? acc : 0u);
-        v.z = cw > 2 ? p2 : (cw == 2 ? acc : 0u);
-        v.w = cw == 3 ? acc : 0u;
-        *(uint4 *)(out + (n >> 4) * 4) = v;
-    }
+    GRK_HD void flush() { if (n & 3) out[n >> 2] = acc; }
 };
 
 // Bit-sliced zero-coding context (t1_generate_luts.cpp:63-140) for 64
