@@ -324,3 +324,21 @@ def test_window_decode_16k_tiles(codec):
     win = (1000, 3000, 1100, 3100)
     d = codec.decompress(b, window=win, device_out=True)
     assert torch.equal(d.cpu(), torch.from_numpy(img[:, 3000:3100, 1000:1100].copy()))
+
+
+@pytest.mark.parametrize("hw", [(1024, 1536), (1536, 2048), (1100, 1700)])
+@pytest.mark.parametrize("irrev", [False, True])
+def test_mid_size_blocks_per_wave(codec, oracle, hw, irrev):
+    """Images of 1,000-4,000 code-blocks: the T1 lane coders run 2-32 blocks
+    per wavefront there (kernels.hip t1_blocks_per_wave; the goldens have
+    fewer than 1,024 blocks -- one per wavefront -- and the full-size configs
+    more than 4,096 -- 64).  Codestream == the oracle's, decode == the
+    oracle's decode."""
+    import grokimagecompression_amd as grk
+    h, w = hw
+    img = synth.synth_image(h, w, 3, 10, h + w)
+    b = codec.compress(img, 10, grk.CParams.make(irreversible=irrev))
+    ref = oracle.encode(img, 10, oracle.params(irreversible=irrev, nthreads=8))
+    assert b == ref
+    d = codec.decompress(b)
+    assert np.array_equal(d, oracle.decode(ref, nthreads=8))
