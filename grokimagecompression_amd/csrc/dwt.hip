@@ -152,56 +152,31 @@ __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int 
 // forward level
 // ---------------------------------------------------------------------------
 
-// DC shift + forward MCT of one sample (k_dcshift_mct_fwd, kernels.hip;
-// TileProcessor.cpp:1449-1471, mct.cpp:85-139 RCT, :195-350 ICT).
-template <bool IRREV>
-__device__ __forceinline__ int32_t mct_px(const DwtJob &J, int32_t a, int32_t b, int32_t c) {
-    if (J.mct_mode == 1) {
-        const int32_t v = a - J.shift[0];
-        return IRREV ? (int32_t)((uint32_t)v << 11) : v;
-    }
-    int32_t r = a - J.shift[0], g = b - J.shift[1], bl = c - J.shift[2];
-    if constexpr (!IRREV) {
-        return J.comp == 0 ? (r + (g * 2) + bl) >> 2 : J.comp == 1 ? bl - g : r - g;
-    } else {
-        if (J.comp == 0) return ict_term(r, 2449) + ict_term(g, 4809) + ict_term(bl, 934);
-        if (J.comp == 1) return -ict_term(r, 1382) - ict_term(g, 2714) + ict_term(bl, 4096);
-        return ict_term(r, 4096) - ict_term(g, 3430) - ict_term(bl, 666);
-    }
-}
-
-// Window rows of a fused level 0: DC shift + MCT applied as the image planes
-// are read (3 planes for an MCT component, 1 otherwise).
+// Window rows of a fused level 0 for a component outside an MCT triple: the
+// DC shift (TileProcessor.cpp:1449-1471; 9/7: then << 11) applied as the
+// image plane is read.  (MCT triples take k_dwt_fwd_mct3.)
 template <bool IRREV, int R>
 __device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], int32_t (&hi)[R], int xw, int yw,
                                            int gx0, int gx1) {
     const int rw = J.rw, rh = J.rh;
     const int st = (int)J.src_stride * 4;
-    const bool three = J.mct_mode >= 2;
     const rsrc_t p0 = mkbuf(J.src[0], J.src_bytes);
-    const rsrc_t p1 = mkbuf(three ? J.src[1] : J.src[0], J.src_bytes);
-    const rsrc_t p2 = mkbuf(three ? J.src[2] : J.src[0], J.src_bytes);
     const bool vec = J.src_vec && J.casx == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
     const bool rows_in = yw >= 0 && yw + R <= rh;
     const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+    const int32_t sh = J.shift[0];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int so = (rows_in ? yw + r : mirror_idx(yw + r, rh)) * st;
-        int32_t a0, a1, b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+        int32_t a0, a1;
         if (vec) {
             const auto a = __builtin_amdgcn_raw_buffer_load_b64(p0, gx0 * 4, so, 0);
             a0 = (int32_t)a[0]; a1 = (int32_t)a[1];
-            if (three) {
-                const auto b = __builtin_amdgcn_raw_buffer_load_b64(p1, gx0 * 4, so, 0);
-                const auto c = __builtin_amdgcn_raw_buffer_load_b64(p2, gx0 * 4, so, 0);
-                b0 = (int32_t)b[0]; b1 = (int32_t)b[1]; c0 = (int32_t)c[0]; c1 = (int32_t)c[1];
-            }
         } else {
             a0 = ld32(p0, o0, so); a1 = ld32(p0, o1, so);
-            if (three) { b0 = ld32(p1, o0, so); b1 = ld32(p1, o1, so); c0 = ld32(p2, o0, so); c1 = ld32(p2, o1, so); }
         }
-        lo[r] = mct_px<IRREV>(J, a0, b0, c0);
-        hi[r] = mct_px<IRREV>(J, a1, b1, c1);
+        lo[r] = IRREV ? (int32_t)((uint32_t)(a0 - sh) << 11) : a0 - sh;
+        hi[r] = IRREV ? (int32_t)((uint32_t)(a1 - sh) << 11) : a1 - sh;
     }
 }
 
@@ -337,7 +312,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
 
 // Forward level 0 of an MCT component triple in ONE wavefront per window:
 // the three image planes are read once (8-byte loads), the DC shift + RCT /
-// ICT forms all three components in registers (mct_px), and each component
+// ICT forms all three components in registers, and each component
 // is lifted and stored in turn.  jobs = component triples (blockIdx.y).
 template <bool IRREV, int TH>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *__restrict__ jobs, int lay) {

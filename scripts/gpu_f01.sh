@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.txt; exit 1; }
 tail -1 $OUT/pytest_gpu.txt
-for spec in "GRKGPU_DWT_F01=4" "GRKGPU_DWT_F01=0"; do
+for spec in ${SPECS:-"GRKGPU_DWT_F01=4" "GRKGPU_DWT_F01=0"}; do
   n=$(echo $spec | tr ',=' '__')
   bash scripts/dwt_levels.sh $TAG/$n $(echo $spec | tr ',' ' ') > /dev/null || { echo "levels $spec failed"; exit 1; }
   echo "== $spec"; grep -E "dwt_fwd|dcshift" $OUT/$n/levels.txt
