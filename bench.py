@@ -366,7 +366,7 @@ def bench_c4(args, grk, synth, dist, world, rank, local):
     codec = grk.Codec(local)
 
     def step():
-        cs = codec.compress_tiles(frame, BITS, p, b, e, parts=grk.PART_ALL, row0=r0, height=H)
+        cs = codec.compress_tiles(frame, BITS, p, b, e, parts=grk.PART_ALL, row0=r0, height=H, view=True)
         codec.decompress_tiles(cs, b, e, out)
         return cs, None
 

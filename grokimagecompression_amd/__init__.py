@@ -384,9 +384,11 @@ class Codec:
         return b
 
     def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False,
-                       row0=None, height=None):
+                       row0=None, height=None, view=False):
         """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
-        (plus the main header / EOC when `parts` asks for them) as bytes.
+        (plus the main header / EOC when `parts` asks for them) as bytes, or
+        (view=True) as a numpy uint8 array over the library's result buffer
+        (no copy; the buffer is released with the array).
         row0 / height: img holds only image rows [row0, row0 + img rows) of an
         image `height` rows tall (a tile-row shard, grkgpu_compress_tile_rows)."""
         if row0 is None:
@@ -405,6 +407,11 @@ class Codec:
         args = (self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0) + extra + \
             (tile_begin, tile_end, parts, ctypes.byref(out), ctypes.byref(n))
         _check(fn(*args))
+        if view and n.value:
+            import weakref
+            a = np.ctypeslib.as_array(out, shape=(n.value,))
+            weakref.finalize(a, lib().grkgpu_free, out)
+            return a
         b = ctypes.string_at(out, n.value)
         lib().grkgpu_free(out)
         return b

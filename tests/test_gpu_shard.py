@@ -150,3 +150,18 @@ def test_row_slab_shards_match_reference(codec, name):
     with pytest.raises(grk.GrkGpuError):
         codec.compress_tiles(np.ascontiguousarray(img[:, 1:3]), bits, p, 0, 1, grk.PART_ALL, offset=off, row0=1,
                              height=img.shape[1])
+
+
+def test_compress_tiles_view(codec):
+    """compress_tiles(view=True): the same bytes as a numpy view over the
+    library's result buffer (no copy), usable as decompress_tiles input."""
+    import torch
+    import grokimagecompression_amd as grk
+    img = synth.synth_image(300, 500, 1, 12, 9)
+    p, _ = grk.CParams.from_cli(["-t", "128,128"])
+    ref = codec.compress_tiles(img, 12, p, 0, 12, grk.PART_ALL)
+    v = codec.compress_tiles(img, 12, p, 0, 12, grk.PART_ALL, view=True)
+    assert isinstance(v, np.ndarray) and v.dtype == np.uint8 and v.tobytes() == ref
+    out = torch.zeros((1, 300, 500), dtype=torch.int32, device="cuda:0")
+    codec.decompress_tiles(v, 0, 12, out)
+    assert np.array_equal(out.cpu().numpy(), img.astype(np.int32))
