@@ -261,6 +261,22 @@ def _buf_ptr(buf):
 PART_TILES, PART_HEADER, PART_EOC, PART_ALL = 0, 1, 2, 3
 
 
+class _LibBuffer:
+    """Owner of a result buffer the library allocated (released with
+    grkgpu_free when the last numpy view of it goes).  numpy arrays made from
+    its __array_interface__ keep this object as their base, and every view or
+    slice of them keeps that base alive, so no view can outlive the memory."""
+
+    def __init__(self, ptr, n):
+        self._ptr = ctypes.cast(ptr, ctypes.c_void_p).value
+        self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (self._ptr, False), "version": 3}
+
+    def __del__(self):
+        if self._ptr:
+            lib().grkgpu_free(ctypes.c_void_p(self._ptr))
+            self._ptr = None
+
+
 def num_tiles(shape, prec, params, offset=(0, 0)):
     """Tile count of a (c,h,w) image under `params` (grkgpu_num_tiles)."""
     c, h, w = shape
@@ -408,10 +424,7 @@ class Codec:
             (tile_begin, tile_end, parts, ctypes.byref(out), ctypes.byref(n))
         _check(fn(*args))
         if view and n.value:
-            import weakref
-            a = np.ctypeslib.as_array(out, shape=(n.value,))
-            weakref.finalize(a, lib().grkgpu_free, out)
-            return a
+            return np.asarray(_LibBuffer(out, n.value))
         b = ctypes.string_at(out, n.value)
         lib().grkgpu_free(out)
         return b

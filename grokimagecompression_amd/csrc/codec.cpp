@@ -1390,6 +1390,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     std::vector<uint8_t> tilebuf;
+    bool too_deep = false;
     for (uint32_t lt = 0; lt < nsh; ++lt) {
         const uint32_t t = tb + lt;
         Tile &tile = tiles[lt];
@@ -1482,10 +1483,16 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 // no bytes: the block stays zero (T1Part1::decode returns before
                 // t1_decode_cblk when the block has no data, T1Part1.cpp:139-140)
                 if (!d.len) d.numpasses = 0;
+                // t1_decode_cblk refuses bpno_plus_one = roishift + numbps >= 31
+                // (t1.cpp:1055-1060; our numbps already holds the ROI shift, as
+                // T1Part1.cpp:186 subtracts it before the call); the decoder's
+                // scratch holds 32 planes
+                if (d.numpasses && d.numbps >= 31) too_deep = true;
                 db.push_back(d);
             }, numres_dec, win ? &need : nullptr);
         }
     }
+    if (too_deep) return set_err(GRKGPU_ECORRUPT, "unsupported bpno_plus_one >= 31 (code-block bit-planes + ROI shift)");
     const uint32_t nblk = (uint32_t)db.size();
     seg_first.push_back((uint32_t)dsegs.size());
     double t_t2 = now_ms();

@@ -47,20 +47,47 @@ void emit(const Handler &h, const char *fmt, ...) {
 }
 #define GRK_ERROR(...) emit(g_err, __VA_ARGS__)
 
-// ---- the GPU context: one per device, created on first use ----
+// ---- GPU contexts: a pool per device ----
+// A grkgpu_ctx (its stream, arenas and pinned result buffer) serves one call
+// at a time.  The reference allows one codec per caller thread
+// (SURVEY 8(b1)), so each grk_encode / grk_decode leases a context from its
+// device's pool for the whole call -- the GPU work and the copy of the result
+// out of the context's buffer -- and returns it; concurrent codecs get
+// different contexts, and a context is created only when all are leased.
 std::mutex g_mu;
-std::vector<grkgpu_ctx *> g_ctx;
+std::vector<std::vector<grkgpu_ctx *>> g_free;  // [device] idle contexts
+std::vector<grkgpu_ctx *> g_all;                // every context created (grk_deinitialize)
 
-grkgpu_ctx *ctx_for(int device) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (device < 0) device = 0;
-    if ((size_t)device >= g_ctx.size()) g_ctx.resize(device + 1, nullptr);
-    if (!g_ctx[device] && grkgpu_create(device, &g_ctx[device]) != GRKGPU_OK) {
-        GRK_ERROR("MI355X context on device %d: %s", device, grkgpu_last_error());
-        g_ctx[device] = nullptr;
+struct Lease {
+    grkgpu_ctx *ctx = nullptr;
+    int device = 0;
+    explicit Lease(int dev) : device(dev < 0 ? 0 : dev) {
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            if ((size_t)device >= g_free.size()) g_free.resize(device + 1);
+            if (!g_free[device].empty()) {
+                ctx = g_free[device].back();
+                g_free[device].pop_back();
+                return;
+            }
+        }
+        grkgpu_ctx *c = nullptr;
+        if (grkgpu_create(device, &c) != GRKGPU_OK) {
+            GRK_ERROR("MI355X context on device %d: %s", device, grkgpu_last_error());
+            return;
+        }
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_all.push_back(c);
+        ctx = c;
     }
-    return g_ctx[device];
-}
+    ~Lease() {
+        if (!ctx) return;
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_free[device].push_back(ctx);
+    }
+    Lease(const Lease &) = delete;
+    Lease &operator=(const Lease &) = delete;
+};
 
 // ---- streams (BufferedStream semantics for the calls the codec makes:
 // sequential read to the end, sequential write) ----
@@ -252,8 +279,9 @@ GRK_EXPORT bool grk_initialize(const char *, uint32_t) { return false; }  // "pl
 
 GRK_EXPORT void grk_deinitialize(void) {
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &c : g_ctx)
-        if (c) { grkgpu_destroy(c); c = nullptr; }
+    for (auto *c : g_all) grkgpu_destroy(c);  // callers must have finished their codec calls
+    g_all.clear();
+    g_free.clear();
 }
 
 // ---------------------------------------------------------------------------
@@ -545,7 +573,9 @@ GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t
 GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image) {
     Codec *c = (Codec *)codec;
     if (!c || !c->decompressor || !c->have_header || !image || image->numcomps != c->desc.numcomps) return false;
-    grkgpu_ctx *ctx = ctx_for(0);
+    // grk_dparameters carries no device (grok.h:693-738): device 0
+    Lease lease(0);
+    grkgpu_ctx *ctx = lease.ctx;
     if (!ctx) return false;
     std::vector<int32_t *> planes(image->numcomps);
     for (uint32_t k = 0; k < image->numcomps; ++k) {
@@ -639,7 +669,8 @@ GRK_EXPORT bool grk_encode_with_plugin(grk_codec *codec, grk_plugin_tile *tile) 
     grkgpu_image_desc d;
     grkgpu_cparams p;
     if (!image_desc(c->image, &d) || !map_cparams(&c->cparams, d.numcomps, &p)) return false;
-    grkgpu_ctx *ctx = ctx_for(c->cparams.deviceId);
+    Lease lease(c->cparams.deviceId);  // held until the codestream is written out of the context's buffer
+    grkgpu_ctx *ctx = lease.ctx;
     if (!ctx) return false;
     std::vector<const int32_t *> planes(d.numcomps);
     for (uint32_t k = 0; k < d.numcomps; ++k) planes[k] = c->image->comps[k].data;

@@ -364,7 +364,7 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
     const DecBlock b = blocks[i];
-    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0 || b.numbps > T1_MAX_DEC_BPS) return;
     if (segs) {
         for (uint32_t q = seg_first[i]; q < seg_first[i + 1]; ++q) {
             const DecSeg sg = segs[q];
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     const uint32_t i = blockIdx.x * bpw + threadIdx.x;
     if (i >= n) return;
     const DecBlock b = blocks[i];
-    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0) return;
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0 || b.numbps > T1_MAX_DEC_BPS) return;
     const DecTables T{s_zc + b.orient * 512, s_sc, s_mq};
     // lane-interleaved state and bit-plane rows of this block (t1_lane.h T1Group)
     // bpw is a power of two <= 64, so the wavefront's blocks share one group:
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void k_t1_rebuild(const DecBlock *__restrict__
     uint32_t rs = 0;
     if (l < nb) {
         mb = blocks[g * 64 + l];
-        dp = decoded_planes(mb.len ? mb.numpasses : 0, mb.numbps);
+        dp = decoded_planes(mb.len && mb.numbps <= T1_MAX_DEC_BPS ? mb.numpasses : 0, mb.numbps);
         rs = roi ? roi[g * 64 + l] : 0u;
     }
     // packed per-block parameters for the readlane broadcasts

@@ -1,5 +1,6 @@
-// t1_dec.h -- EBCOT Tier-1 decoder, v3: one lane per code-block, built for a
-// lone serial lane on CDNA4.
+// t1_dec.h -- the EBCOT Tier-1 decoder's pass / stripe / column walk: one
+// lane per code-block (the decoder "v5", fed by t1_flat.h's unstuffed bit
+// stream; kernels.hip k_t1_decode_ub).
 //
 //   * block state = 64-bit row masks in HBM, one 4-row stripe held in
 //     registers (Stripe); each lane visits only the columns of a stripe that
@@ -11,14 +12,12 @@
 //   * the symbols of a column go through ONE decode site (a small state
 //     machine: ZC -> SC, AGG -> UNI -> UNI -> SC), so lanes of a wavefront
 //     that sit in different rows / symbol kinds still share the MQ code
-//   * the MQ decoder is select-based; only a renormalisation that needs a new
-//     byte branches.  Bytes arrive through a 16-byte-chunk ring refilled one
-//     chunk ahead.
 //   * outputs are write-only bit-plane rows (sigafter / refbit, t1_lane.h)
 //     rebuilt into coefficients by k_t1_rebuild.
 //
 // Semantics: Grok v5.1.0 t1/t1_part1/t1.cpp t1_decode_cblk (:1038) with
-// dec_sigpass / dec_refpass / dec_clnpass, mqc_dec_inl.h; cblksty 0.
+// dec_sigpass / dec_refpass / dec_clnpass, mqc_dec_inl.h, and the mode
+// switches (see t1_decode_passes).
 #pragma once
 #include "t1_lane.h"
 
@@ -31,96 +30,6 @@ GRK_HD uint8_t sc_win_entry(uint32_t i) {
     int cx = sc_ctx((i >> 2) & 1, (i >> 4) & 1, i & 1, (i >> 6) & 1, (i >> 3) & 1, (i >> 5) & 1, (i >> 1) & 1,
                     (i >> 7) & 1, &xr);
     return (uint8_t)(cx | (xr << 7));
-}
-
-struct Dec3;
-GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx);
-
-struct Dec3 {
-    static constexpr bool kLazy = false, raw = false;  // byte-level decoder: MQ segments only
-    uint32_t a, c, ct;
-    uint32_t cur, nxt;  // code bytes at bp and bp + 1
-    const uint4 *p;     // next chunk to load
-    uint4 c0, c1, c2;   // c0.x = current word (consumed low byte first)
-    uint32_t wleft, wq; // bytes left in c0.x, words left in c0
-    uint32_t idx, len;  // bytes handed out so far, segment length
-    GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) { return d3_decode(*this, cxw, tab, cx); }
-};
-
-GRK_HD uint32_t d3_byte(Dec3 &d) {
-    const uint32_t b = d.c0.x & 0xff;
-    d.c0.x >>= 8;
-    if (--d.wleft == 0) {
-        d.wleft = 4;
-        if (--d.wq == 0) {
-            d.wq = 4;
-            d.c0 = d.c1; d.c1 = d.c2; d.c2 = *d.p++;
-        } else {
-            d.c0.x = d.c0.y; d.c0.y = d.c0.z; d.c0.z = d.c0.w;
-        }
-    }
-    return d.idx++ < d.len ? b : 0xffu;
-}
-
-// BYTEIN (mqc_dec_inl.h): a 0xFF followed by a byte > 0x8F is a marker and
-// feeds 1-bits from then on
-GRK_HD void d3_bytein(Dec3 &d) {
-    const bool ff = d.cur == 0xff;
-    const bool marker = ff && d.nxt > 0x8f;
-    d.c += marker ? 0xff00u : (d.nxt << (ff ? 9 : 8));
-    d.ct = (ff && !marker) ? 7u : 8u;
-    if (!marker) {
-        d.cur = d.nxt;
-        d.nxt = d3_byte(d);
-    }
-}
-
-GRK_HD void d3_init(Dec3 &d, const uint8_t *data, uint32_t len) {
-    const uintptr_t pa = (uintptr_t)data;
-    d.p = (const uint4 *)(pa & ~(uintptr_t)15);
-    d.c0 = d.p[0]; d.c1 = d.p[1]; d.c2 = d.p[2];
-    d.p += 3;
-    d.wleft = 4; d.wq = 4;
-    d.idx = 0; d.len = 0;  // skip the bytes before the segment start
-    for (uint32_t s = (uint32_t)(pa & 15); s > 0; --s) { d3_byte(d); }
-    d.idx = 0; d.len = len;
-    d.cur = d3_byte(d);
-    d.nxt = d3_byte(d);
-    d.c = d.cur << 16;  // len == 0 reads 0xFF, as Grok's padded buffer does
-    d3_bytein(d);
-    d.c <<= 7; d.ct -= 7; d.a = 0x8000;
-}
-
-// MQ decode of one symbol in context cx (mqc_dec_inl.h DECODE_SYMBOL).
-GRK_HD uint32_t d3_decode(Dec3 &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
-    const uint32_t w = cxw[cx];
-    const uint32_t qe = w & 0xffff, mps = w >> 31;
-    uint32_t a = d.a - qe;
-    const uint32_t qe16 = qe << 16;
-    const bool lo = d.c < qe16;
-    const bool lps = lo ? (a >= qe) : (a < qe);
-    const bool keep = !lo && (a & 0x8000);
-    d.c = lo ? d.c : d.c - qe16;
-    a = lo ? qe : a;
-    const uint32_t nidx = (w >> (lps ? 22 : 16)) & 63;
-    const uint32_t nmps = mps ^ (lps ? (w >> 28) & 1u : 0u);
-    const uint32_t tw = tab[nidx];
-    uint32_t n = clz32(a) - 16;
-    if (n <= d.ct) {
-        a <<= n; d.c <<= n; d.ct -= n;
-    } else {
-        do {
-            if (d.ct == 0) d3_bytein(d);
-            const uint32_t sh = n < d.ct ? n : d.ct;
-            a <<= sh; d.c <<= sh; d.ct -= sh; n -= sh;
-        } while (n);
-    }
-    d.a = a;
-    if (!keep) cxw[cx] = tw | (nmps << 31);
-#ifdef T1_TRACE
-    T1_TRACE(cx, mps ^ (uint32_t)lps, d.a, d.c >> 16);
-#endif
-    return mps ^ (uint32_t)lps;
 }
 
 // 18-bit 3x6 window of column x: bits 3i..3i+2 = row i (k-1+i), columns x-1..x+1
@@ -249,8 +158,8 @@ struct NoSegs {
     template <class D> GRK_HD void at_pass(D &, uint32_t, bool) {}
 };
 
-// The pass / stripe / column walk shared by v3 (byte-level MQ input, Dec3)
-// and v5 (unstuffed bit stream, BitDec in t1_flat.h).  Mode switches
+// The pass / stripe / column walk over an MQ / raw bit source D (BitDecT,
+// t1_flat.h).  Mode switches
 // (cblksty): VSC -- row k+4 reads as insignificant for row k+3 (the flags
 // update of t1.cpp:168-190 skips the north neighbours of a stripe's first
 // row); RESET -- contexts re-initialised after every pass (t1.cpp:1104-1105);
@@ -355,17 +264,6 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
         if ((sty & CBLKSTY_RESET) && !(D::kLazy && d.raw)) mq_reset_words(cxw, T.mq);  // after MQ passes (t1.cpp:1104-1105)
         if (++passtype == 3) { passtype = 0; bpno--; }
     }
-}
-
-// Decode one block into write-only bit-plane rows (see t1_decode_lane).
-GRK_HD void t1_decode_v3(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
-                         uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw, uint64_t *sigafter,
-                         uint64_t *refbit) {
-    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    mq_reset_words(cxw, T.mq);
-    Dec3 d;
-    d3_init(d, data, len);
-    t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sigafter, refbit);
 }
 
 }  // namespace grkgpu

@@ -1,17 +1,10 @@
-// t1_flat.h -- EBCOT Tier-1 decoder, v4 ("flat"): one lane per code-block,
-// ONE MQ decision per loop iteration.
+// t1_flat.h -- the T1 decoder's input side: byte-stuffing removal (the
+// k_t1_unstuff pre-pass) and the MQ / raw bit decoder over the unstuffed
+// stream (BitDecT), driven by t1_dec.h's pass walk (t1_decode_v5 /
+// t1_decode_passes).
 //
-// Why: with nested pass / stripe / column loops (v3), the lanes of a
-// wavefront re-converge at every loop exit, so a wavefront pays, for every
-// (pass, stripe), the slowest of its blocks.  Here the whole decoder is a
-// single loop whose body (1) forms the context of the pending decision,
-// (2) runs the MQ decoder, (3) applies the decision and (4) moves the
-// cursor to the next decision.  Lanes advance independently; a lane only
-// leaves the common path for a stripe switch (row-mask load/store), a chunk
-// refill of its bit stream, or the end of its block.
-//
-//   * The MQ byte stuffing is removed beforehand (t1_unstuff, one pass per
-//     block): the decoder reads a plain bit stream, so renormalisation is
+//   * The MQ byte stuffing is removed beforehand (one pass per block): the
+//     decoder reads a plain bit stream, so renormalisation is
 //     C = C << n | next n bits, with no per-byte branches.  Equivalence with
 //     the ct / BYTEIN formulation of mqc_dec_inl.h: the comparisons only use
 //     C[31:16], subtractions never borrow into it, and BYTEIN always supplies
@@ -19,17 +12,9 @@
 //     byte contributes its low 7 bits (its top bit is the stuffed 0), and a
 //     0xFF followed by a byte > 0x8F (a marker), or the end of the segment
 //     (Grok pads with 0xFF 0xFF), turns the stream into 1-bits forever.
-//   * Block state = 64-bit row masks (t1_lane.h BlockState) in HBM; the
-//     current 4-row stripe lives in registers.  Stripes that cannot hold
-//     work for a significance / refinement pass are skipped using a 16-bit
-//     "stripe has a significant sample" mask, so the significance-after-plane
-//     rows (sa) are zero-filled up front and written only for visited
-//     stripes.
 //
-// Semantics: Grok v5.1.0 t1/t1_part1/t1.cpp t1_decode_cblk (:1038),
-// dec_sigpass / dec_refpass / dec_clnpass, mqc_dec_inl.h; cblksty 0.
-// Outputs are those of v3 (t1_dec.h): sa / rb bit-plane rows + st.neg,
-// consumed by k_t1_rebuild.
+// Semantics: Grok v5.1.0 t1/t1_part1/mqc_dec_inl.h (decode_macro :148,
+// bytein), mqc_dec.cpp:178-193 (mqc_init_dec), t1.cpp:1038 t1_decode_cblk.
 #pragma once
 #include "t1_dec.h"
 
@@ -43,7 +28,7 @@ namespace grkgpu {
 // its top bit at the position of the 0xFF's last bit -- an arithmetic carry
 // into the code register that BYTEIN applies at the moment that bit sits at
 // C[16].  The event is recorded as q = (stream index of that bit) + 17 (the
-// decoder's consumed-bit count at that moment, see t1_decode_flat).
+// decoder's consumed-bit count at that moment, see BitDecT).
 // Returns the word count; *ncarry = events written to carries[].
 // ---------------------------------------------------------------------------
 struct Unstuff {
@@ -126,8 +111,8 @@ GRK_HD uint32_t fb_word(FlatBits &b) {
 }
 
 // ---------------------------------------------------------------------------
-// MQ decoder over the unstuffed stream (used by the nested-loop decoder v5
-// in t1_dec.h and by t1_decode_flat): branch-free renormalisation.
+// MQ decoder over the unstuffed stream (used by the pass walk of t1_dec.h):
+// branch-free renormalisation.
 // ---------------------------------------------------------------------------
 // LAZY: the decoder may meet raw (BYPASS) segments; compiled out otherwise,
 // so the common case keeps its per-symbol path branch-free.
@@ -240,7 +225,7 @@ struct SegCursor {
     }
 };
 
-// v5: the nested pass / stripe / column walk of v3 (lanes of a wavefront stay
+// v5: the nested pass / stripe / column walk (lanes of a wavefront stay
 // converged on the pass structure) fed by the unstuffed bit stream.
 template <class ST = BlockState, class RP = uint64_t *>
 GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
@@ -251,255 +236,6 @@ GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t 
     BitDec d;
     d.init(words, nwords, carries);
     t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sa, rb);
-}
-
-// ---------------------------------------------------------------------------
-// the flat decoder
-// ---------------------------------------------------------------------------
-enum FlatKind : uint32_t { FK_ZC = 0, FK_SC = 1, FK_MAG = 2, FK_AGG = 3, FK_UNI1 = 4, FK_UNI2 = 5 };
-
-struct FlatStripe {
-    uint64_t s[6], n[6];  // sig / neg rows k-1 .. k+4
-    uint64_t v[4], f[4];  // vis / ref rows k .. k+3
-    uint64_t b[4];        // refinement bits out (MRP)
-};
-
-// words / carries: t1_unstuff output (words 16-byte aligned; carries end
-// with a ~0 sentinel).
-GRK_HD void t1_decode_flat(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
-                           uint32_t numbps, uint32_t w, uint32_t h, BlockState &st, const DecTables &T, uint32_t *cxw,
-                           uint64_t *sa, uint64_t *rb) {
-    if (numpasses == 0 || numbps == 0) return;
-    const uint32_t maxp = 3 * numbps - 2;
-    if (numpasses > maxp) numpasses = maxp;
-    for (uint32_t y = 0; y < 66; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    // significance-after-plane rows of skipped stripes stay zero
-    {
-        int32_t lowp; int ty;
-        pass_info(numpasses - 1, numbps, &lowp, &ty);
-        for (int32_t p = lowp; p < (int32_t)numbps; ++p)
-            for (uint32_t y = 0; y < h; ++y) sa[(uint32_t)p * 64 + y] = 0;
-    }
-    mq_reset_words(cxw, T.mq);
-    const uint64_t wmask = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
-    const uint32_t nstripes = (h + 3) >> 2;
-
-    BitDec md;
-    md.init(words, nwords, carries);
-
-    // pass / stripe / column cursor
-    uint32_t ptype = 2;                 // first pass: cleanup of the top plane
-    int32_t bpno = (int32_t)numbps - 1;
-    uint32_t passno = 0;
-    uint32_t sigstr = 0;                // stripes holding a significant sample
-    uint32_t k = 0, nr = 0, si = 0;     // stripe start row, rows, stripe index
-    FlatStripe S;
-    uint64_t cand = 0;                  // columns of this stripe still to visit
-    uint32_t x = 0, r = 0, kind = FK_ZC, todo = 0, rows = 0;
-    uint32_t P = 0, Q = 0, sig4 = 0, vis4 = 0, ref4 = 0;
-    bool grew = false;                  // SPP: a sample became significant in this column
-    bool need_stripe = true;            // enter the first stripe of the pass
-    si = 0;
-
-    for (;;) {
-        // ---------------- stripe / pass switch (rare path) ----------------
-        if (need_stripe) {
-            bool found = false;
-            while (!found) {
-                // find the next stripe of this pass that can hold work
-                uint32_t pot;
-                if (ptype == 2) pot = 0xffffu;
-                else if (ptype == 0) pot = sigstr | (sigstr << 1) | (sigstr >> 1);
-                else pot = sigstr;
-                pot &= ((1u << nstripes) - 1) & ~((1u << si) - 1);
-                if (!pot) {
-                    // next pass
-                    if (++passno >= numpasses) return;
-                    if (++ptype == 3) { ptype = 0; --bpno; }
-                    si = 0;
-                    continue;
-                }
-                si = (uint32_t)__builtin_ctz(pot);
-                k = si << 2;
-                nr = h - k < 4 ? h - k : 4;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) { S.s[i] = st.sig[k + i]; S.n[i] = st.neg[k + i]; }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) { S.v[i] = st.vis[k + 1 + i]; S.f[i] = st.ref[k + 1 + i]; S.b[i] = 0; }
-                Stripe tmp;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) tmp.sig[i] = S.s[i];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tmp.vis[i] = S.v[i];
-                if (ptype == 0) {
-                    cand = spp_candidates(tmp, nr) & wmask;
-                } else if (ptype == 1) {
-                    cand = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) cand |= S.s[i + 1] & ~S.v[i];
-                    cand &= wmask;
-                } else {
-                    cand = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) cand |= ~(S.s[i + 1] | S.v[i]);
-                    cand &= wmask;
-                }
-                if (cand) { found = true; break; }
-                // nothing to decode here: finish the stripe as the pass would
-                if (ptype == 2) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) st.vis[k + 1 + i] = 0;
-                }
-                if (ptype != 1) {
-                    uint64_t *sap = sa + (uint32_t)bpno * 64;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) sap[k + i] = S.s[i + 1];
-                } else {
-                    uint64_t *rbp = rb + (uint32_t)bpno * 64;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) rbp[k + i] = 0;
-                }
-                ++si;
-            }
-            need_stripe = false;
-            // enter the first column
-            x = ctz64(cand);
-            goto column_entry;
-        }
-
-        {
-            // ---------------- one decision ----------------
-            const uint32_t nb9 = (P >> (3 * r)) & 0x1FFu;
-            uint32_t cx;
-            const uint32_t scw = T.sc[((nb9 & 0xAAu) >> 1) | ((Q >> (3 * r)) & 0xAAu)];
-            if (kind == FK_ZC) cx = T.zc[nb9];
-            else if (kind == FK_SC) cx = scw & 0x7fu;
-            else if (kind == FK_MAG) cx = ((ref4 >> r) & 1u) ? CX_MAG + 2 : CX_MAG + ((nb9 & 0x1EFu) ? 1u : 0u);
-            else cx = kind == FK_AGG ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
-
-            const uint32_t d = md.decode(cxw, T.mq, cx);
-
-            // ---------------- apply ----------------
-            bool advance = true;
-            if (kind == FK_ZC) {
-                if (ptype == 0) S.v[r] |= (uint64_t)1 << x;
-                if (d) { kind = FK_SC; advance = false; }
-            } else if (kind == FK_SC) {
-                const uint32_t sg = d ^ (scw >> 7);
-                P |= 1u << (3 * r + 4);
-                Q |= sg << (3 * r + 4);
-                sig4 |= 1u << r;
-                S.s[r + 1] |= (uint64_t)1 << x;
-                S.n[r + 1] |= (uint64_t)sg << x;
-                if (ptype == 0) {
-                    grew = true;
-                    vis4 |= 1u << r;
-                    todo |= rows & ~(sig4 | vis4) & (2u << r);  // the sample below gains a neighbour
-                }
-                kind = FK_ZC;
-            } else if (kind == FK_MAG) {
-                S.f[r] |= (uint64_t)1 << x;
-                S.b[r] |= (uint64_t)d << x;
-            } else if (kind == FK_AGG) {
-                if (d) { kind = FK_UNI1; advance = false; }
-                else todo = 0;  // four zeros: column done
-            } else if (kind == FK_UNI1) {
-                r = d << 1;
-                kind = FK_UNI2;
-                advance = false;
-            } else {
-                r |= d;
-                todo = rows & ~((2u << r) - 1);  // rows after the run are plain ZC
-                kind = FK_SC;
-                advance = false;
-            }
-            if (!advance) continue;
-            todo &= ~((2u << r) - 1);
-            if (todo) {
-                r = (uint32_t)__builtin_ctz(todo);
-                kind = ptype == 1 ? FK_MAG : FK_ZC;
-                continue;
-            }
-            // ---------------- next column ----------------
-            const uint64_t done = (x >= 63) ? ~(uint64_t)0 : (((uint64_t)2 << x) - 1);
-            cand &= ~done;
-            if (ptype == 0 && grew) {
-                Stripe tmp;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) tmp.sig[i] = S.s[i];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tmp.vis[i] = S.v[i];
-                cand = spp_candidates(tmp, nr) & wmask & ~done;
-            }
-            if (!cand) {
-                // ---------------- stripe end: write back ----------------
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    st.sig[k + 1 + i] = S.s[i + 1];
-                    st.neg[k + 1 + i] = S.n[i + 1];
-                    st.vis[k + 1 + i] = ptype == 2 ? 0 : S.v[i];
-                    st.ref[k + 1 + i] = S.f[i];
-                }
-                if (ptype != 1) {
-                    uint64_t *sap = sa + (uint32_t)bpno * 64;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) sap[k + i] = S.s[i + 1];
-                } else {
-                    uint64_t *rbp = rb + (uint32_t)bpno * 64;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((uint32_t)i < nr) rbp[k + i] = S.b[i];
-                }
-                if (S.s[1] | S.s[2] | S.s[3] | S.s[4]) sigstr |= 1u << si;
-                ++si;
-                need_stripe = true;
-                continue;
-            }
-            x = ctz64(cand);
-        }
-    column_entry:
-        // ---------------- column entry ----------------
-        {
-            uint32_t pp = 0, qq = 0;
-            const uint32_t s1 = x ? x - 1 : 0, m = x ? 7u : 3u, s2 = x ? 0u : 1u;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                pp |= ((((uint32_t)(S.s[i] >> s1)) & m) << s2) << (3 * i);
-                qq |= ((((uint32_t)(S.n[i] >> s1)) & m) << s2) << (3 * i);
-            }
-            P = pp;
-            Q = qq;
-        }
-        vis4 = 0;
-        ref4 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            vis4 |= (uint32_t)((S.v[i] >> x) & 1u) << i;
-            ref4 |= (uint32_t)((S.f[i] >> x) & 1u) << i;
-        }
-        sig4 = win_self4(P);
-        rows = (1u << nr) - 1;
-        grew = false;
-        if (ptype == 0) {
-            uint32_t nz = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) nz |= (((P >> (3 * i)) & 0x1EFu) != 0 ? 1u : 0u) << i;
-            todo = nz & ~sig4 & ~vis4 & rows;
-            kind = FK_ZC;
-        } else if (ptype == 1) {
-            todo = sig4 & ~vis4 & rows;
-            kind = FK_MAG;
-        } else {
-            todo = ~sig4 & ~vis4 & rows;
-            kind = (nr == 4 && P == 0 && vis4 == 0) ? (uint32_t)FK_AGG : (uint32_t)FK_ZC;
-        }
-        r = kind == FK_AGG ? 0u : (uint32_t)__builtin_ctz(todo | 16u);
-    }
 }
 
 }  // namespace grkgpu

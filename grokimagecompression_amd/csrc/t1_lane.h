@@ -1,16 +1,21 @@
-// t1_lane.h -- lane-per-code-block EBCOT Tier-1 coder, v2 (MI355X layout).
+// t1_lane.h -- lane-per-code-block EBCOT Tier-1 encoder (MI355X layout) and
+// the block state shared with the decoder.
 //
-// One GPU lane owns one code-block (w, h <= 64).  All per-block state lives in
-// HBM as 64-bit ROW MASKS (bit x = column x) and is streamed through
-// registers one 4-row stripe at a time (Stripe), so the serial MQ loop only
-// touches registers and three small LDS tables (zero-coding LUT, sign LUT,
-// MQ state table).  Decoded magnitudes are never read back: the decoder
-// writes write-only bit-plane rows (significance after each plane, refinement
-// bits per plane) and a separate, fully parallel kernel rebuilds the values
+// All per-block state lives in HBM as 64-bit ROW MASKS (bit x = column x).
+// The encoder is split in two kernels (kernels.hip):
+//   * k_t1_model: the context modelling of one bit-plane of one block per
+//     lane (t1_model_plane): significance / refinement / cleanup passes formed
+//     with row-mask arithmetic, one byte per MQ symbol (context | decision)
+//     into the block's symbol stream;
+//   * k_t1_mq: the serial MQ coder per block (t1_mq_block) over those symbols,
+//     with Grok's rate bookkeeping, pass terminations and BYPASS raw coding.
+// Decoded magnitudes are never read back by the decoder (t1_dec.h): it writes
+// write-only bit-plane rows (significance after each plane, refinement bits
+// per plane) and a separate, fully parallel kernel rebuilds the values
 // (t1_rebuild).  Same source compiles for the host (tests/cpp) and gfx950.
 //
 // Semantics: Grok v5.1.0 t1/t1_part1/t1.cpp (t1_encode_cblk :1182,
-// t1_decode_cblk :1038), mqc_enc.cpp, mqc_dec_inl.h; cblksty 0.
+// t1_decode_cblk :1038), mqc_enc.cpp, mqc_dec_inl.h.
 #pragma once
 #include "t1_core.h"
 
@@ -286,84 +291,6 @@ GRK_HD void mqel_finish(MqEncLane &e, uint32_t len) {
 }
 
 // ---------------------------------------------------------------------------
-// MQ decoder (mqc_dec_inl.h) with a register byte window over an 8-byte
-// aligned stream; bytes past the segment read as 0xFF.
-// ---------------------------------------------------------------------------
-struct MqDecLane {
-    uint32_t a, c, ct;
-    uint32_t bp, len;
-    uint32_t cur, nxt;     // bytes at bp and bp+1
-    const uint64_t *src;   // aligned base
-    uint32_t s0;           // byte offset of the segment start within src
-    uint64_t w0, w1;       // window: chunks wk and wk+1
-    uint32_t wk;
-};
-
-GRK_HD uint32_t mqdl_fetch(MqDecLane &d, uint32_t i) {  // byte i; requests are non-decreasing
-    if (i >= d.len) return 0xFF;
-    uint32_t a = d.s0 + i, k = a >> 3;
-    while (k > d.wk) { d.w0 = d.w1; d.w1 = d.src[d.wk + 2]; d.wk++; }
-    return (uint32_t)(d.w0 >> ((a & 7) * 8)) & 0xFF;
-}
-
-GRK_HD void mqdl_bytein(MqDecLane &d) {
-    if (d.cur == 0xff) {
-        if (d.nxt > 0x8f) { d.c += 0xff00; d.ct = 8; return; }
-        d.bp++; d.c += d.nxt << 9; d.ct = 7;
-    } else {
-        d.bp++; d.c += d.nxt << 8; d.ct = 8;
-    }
-    d.cur = d.nxt;
-    d.nxt = mqdl_fetch(d, d.bp + 1);
-}
-
-GRK_HD void mqdl_init(MqDecLane &d, const uint8_t *data, uint32_t len) {
-    uintptr_t p = (uintptr_t)data;
-    d.src = (const uint64_t *)(p & ~(uintptr_t)7);
-    d.s0 = (uint32_t)(p & 7);
-    d.len = len;
-    d.wk = 0;
-    d.w0 = d.src[0];
-    d.w1 = d.src[1];
-    d.bp = 0;
-    d.cur = mqdl_fetch(d, 0);
-    d.nxt = mqdl_fetch(d, 1);
-    d.c = (len == 0 ? 0xffu : d.cur) << 16;
-    mqdl_bytein(d);
-    d.c <<= 7; d.ct -= 7; d.a = 0x8000;
-}
-
-GRK_HD uint32_t mqdl_decode(MqDecLane &d, uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
-    const uint32_t w = cxw[cx];
-    const uint32_t qe = w & 0xffff, mps = w >> 31;
-    uint32_t r;
-    bool lps_state;
-    d.a -= qe;
-    if (d.c < (qe << 16)) {
-        lps_state = d.a >= qe;
-        d.a = qe;
-    } else {
-        d.c -= qe << 16;
-        if (d.a & 0x8000) return mps;
-        lps_state = d.a < qe;
-    }
-    if (lps_state) {
-        r = mps ^ 1;
-        cxw[cx] = tab[(w >> 22) & 63] | ((mps ^ ((w >> 28) & 1)) << 31);
-    } else {
-        r = mps;
-        cxw[cx] = tab[(w >> 16) & 63] | (mps << 31);
-    }
-    uint32_t n = clz32(d.a) - 16;
-    while (n) {
-        if (d.ct == 0) mqdl_bytein(d);
-        uint32_t sh = n < d.ct ? n : d.ct;
-        d.a <<= sh; d.c <<= sh; d.ct -= sh; n -= sh;
-    }
-    return r;
-}
-
-// ---------------------------------------------------------------------------
 // Coding passes, shared by encoder and decoder.  A 4-row stripe of the block
 // state is held in registers; each lane walks only the columns that hold
 // work for the pass (bit-scan over candidate masks), which keeps SIMT
@@ -384,135 +311,6 @@ GRK_HD uint64_t spp_candidates(const Stripe &s, uint32_t nr) {
         c |= nb & ~(s.sig[r + 1] | s.vis[r]);
     }
     return c;
-}
-
-// Coder: code(cx, v) encodes v / decodes and returns the bit.
-template <class Coder>
-GRK_HD void t1_passes(Coder &cd, uint32_t w, uint32_t h, uint32_t numbps, uint32_t maxpasses, BlockState &st,
-                      const uint8_t *zc, const uint8_t *sc) {
-    const uint64_t wmask = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
-    int32_t bpno = (int32_t)numbps - 1;
-    int passtype = 2;
-    for (uint32_t passno = 0; passno < maxpasses && bpno >= 0; ++passno) {
-        cd.begin_pass(bpno);
-        for (uint32_t k = 0; k < h; k += 4) {
-            Stripe s;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) { s.sig[i] = st.sig[k + i]; s.neg[i] = st.neg[k + i]; }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                s.vis[i] = st.vis[k + 1 + i];
-                s.ref[i] = st.ref[k + 1 + i];
-                s.bit[i] = cd.stripe_bits(k + i, h);
-            }
-            const uint32_t nr = h - k < 4 ? h - k : 4;
-            if (passtype == 0) {  // significance propagation (t1.cpp:197-338)
-                uint64_t cand = spp_candidates(s, nr) & wmask;
-                while (cand) {
-                    const uint32_t x = ctz64(cand);
-                    const uint64_t bx = (uint64_t)1 << x;
-                    const uint64_t done = bx | (bx - 1);
-                    bool grew = false;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        if ((uint32_t)r >= nr) break;
-                        if ((s.sig[r + 1] | s.vis[r]) & bx) continue;
-                        uint32_t nb = nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x);
-                        if (!nb) continue;
-                        if (cd.code(zc[nb], (uint32_t)(s.bit[r] >> x) & 1u)) {
-                            uint32_t si = sc[sc_index(s.sig[r], s.sig[r + 1], s.sig[r + 2], s.neg[r], s.neg[r + 1],
-                                                      s.neg[r + 2], x)];
-                            uint32_t xr = si >> 7;
-                            uint32_t sg = cd.code(si & 0x7f, ((uint32_t)(s.neg[r + 1] >> x) & 1u) ^ xr) ^ xr;
-                            s.sig[r + 1] |= bx;
-                            if (sg) s.neg[r + 1] |= bx;
-                            grew = true;
-                        }
-                        s.vis[r] |= bx;
-                    }
-                    cand &= ~done;
-                    if (grew) cand = spp_candidates(s, nr) & wmask & ~done;
-                }
-            } else if (passtype == 1) {  // magnitude refinement (t1.cpp:443-555)
-                uint64_t mem = 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if ((uint32_t)r < nr) mem |= s.sig[r + 1] & ~s.vis[r];
-                while (mem) {
-                    const uint32_t x = ctz64(mem);
-                    const uint64_t bx = (uint64_t)1 << x;
-                    mem &= mem - 1;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        if ((uint32_t)r >= nr) break;
-                        if (!(s.sig[r + 1] & bx) || (s.vis[r] & bx)) continue;
-                        uint32_t cx;
-                        if (s.ref[r] & bx) cx = CX_MAG + 2;
-                        else cx = CX_MAG + (nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x) ? 1 : 0);
-                        if (cd.code(cx, (uint32_t)(s.bit[r] >> x) & 1u)) s.bit[r] |= bx;
-                        s.ref[r] |= bx;
-                    }
-                }
-            } else {  // cleanup + run-length (t1.cpp:639-782)
-                uint64_t cand = 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if ((uint32_t)r < nr) cand |= ~(s.sig[r + 1] | s.vis[r]);
-                cand &= wmask;
-                while (cand) {
-                    const uint32_t x = ctz64(cand);
-                    const uint64_t bx = (uint64_t)1 << x;
-                    cand &= cand - 1;
-                    int r0 = 0;
-                    bool partial = false;
-                    if (nr == 4) {
-                        uint64_t wn = s.sig[0] | s.sig[1] | s.sig[2] | s.sig[3] | s.sig[4] | s.sig[5];
-                        uint64_t vs = s.vis[0] | s.vis[1] | s.vis[2] | s.vis[3];
-                        if (b3(wn, x) == 0 && !(vs & bx)) {
-                            uint32_t rl = 4;  // encoder: first row with a 1 bit
-#pragma unroll
-                            for (int r = 3; r >= 0; --r)
-                                if ((s.bit[r] >> x) & 1u) rl = (uint32_t)r;
-                            if (!cd.code(CX_AGG, rl != 4)) continue;
-                            uint32_t r1 = cd.code(CX_UNI, rl >> 1);
-                            uint32_t r2 = cd.code(CX_UNI, rl & 1);
-                            r0 = (int)(r1 * 2 + r2);
-                            partial = true;
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        if ((uint32_t)r >= nr || r < r0) continue;
-                        uint32_t code_sign = 0;
-                        if (partial && r == r0) code_sign = 1;
-                        else if (!((s.sig[r + 1] | s.vis[r]) & bx))
-                            code_sign = cd.code(zc[nb9(s.sig[r], s.sig[r + 1], s.sig[r + 2], x)],
-                                                (uint32_t)(s.bit[r] >> x) & 1u);
-                        if (code_sign) {
-                            uint32_t si = sc[sc_index(s.sig[r], s.sig[r + 1], s.sig[r + 2], s.neg[r], s.neg[r + 1],
-                                                      s.neg[r + 2], x)];
-                            uint32_t xr = si >> 7;
-                            uint32_t sg = cd.code(si & 0x7f, ((uint32_t)(s.neg[r + 1] >> x) & 1u) ^ xr) ^ xr;
-                            s.sig[r + 1] |= bx;
-                            if (sg) s.neg[r + 1] |= bx;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s.vis[r] = 0;  // the cleanup pass clears every PI flag
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                st.sig[k + 1 + i] = s.sig[i + 1];
-                if (Coder::kDecoder) st.neg[k + 1 + i] = s.neg[i + 1];
-                st.vis[k + 1 + i] = s.vis[i];
-                st.ref[k + 1 + i] = s.ref[i];
-            }
-            cd.end_stripe(k, nr, passtype, s);
-        }
-        cd.end_pass(passno, passtype, bpno);
-        if (++passtype == 3) { passtype = 0; bpno--; }
-    }
 }
 
 struct LaneEncoder {
@@ -557,75 +355,6 @@ struct LaneEncoder {
         raw = next_raw;
     }
 };
-
-struct LaneDecoder {
-    static constexpr bool kDecoder = true;
-    MqDecLane d;
-    uint32_t *cxw;
-    const uint32_t *tab;
-    uint64_t *sigafter, *refbit, *sa, *rb;
-    GRK_HD void begin_pass(int32_t bpno) {
-        sa = sigafter + (uint32_t)bpno * 64;
-        rb = refbit + (uint32_t)bpno * 64;
-    }
-    GRK_HD uint64_t stripe_bits(uint32_t, uint32_t) const { return 0; }
-    GRK_HD uint32_t code(uint32_t cx, uint32_t) { return mqdl_decode(d, cxw, tab, cx); }
-    GRK_HD void end_stripe(uint32_t k, uint32_t nr, int passtype, const Stripe &s) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if ((uint32_t)i < nr) {
-                if (passtype == 1) rb[k + i] = s.bit[i];
-                else sa[k + i] = s.sig[i + 1];
-            }
-    }
-    GRK_HD void end_pass(uint32_t, int, int32_t) {}
-};
-
-// ENCODER: magnitude bit-plane rows planes[p*64 + y] and sign rows st.neg
-// come from the prep step.  Output bytes to out (4-byte aligned), cumulative
-// pass rates (after Grok's fix-ups) to rate[].  Returns the pass count.
-GRK_HD uint32_t t1_encode_lane(uint32_t w, uint32_t h, uint32_t numbps, const uint64_t *planes, BlockState &st,
-                               const T1Tables &T, uint32_t orient, uint32_t *cxw, uint32_t *out, uint32_t *rate,
-                               uint32_t *len_out) {
-    *len_out = 0;
-    if (numbps == 0) return 0;
-    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    LaneEncoder cd;
-    mq_reset_words(cxw, T.mq);
-    cd.e.a = 0x8000; cd.e.c = 0; cd.e.ct = 12; cd.e.bp = -1; cd.e.cur = 0; cd.e.acc = 0; cd.e.out = out;
-    cd.cxw = cxw; cd.tab = T.mq; cd.planes = planes; cd.pl = planes; cd.rate = rate;
-    const uint32_t total = 3 * numbps - 2;
-    t1_passes(cd, w, h, numbps, total, st, T.zc + orient * 512, T.sc);
-    const uint32_t len = (uint32_t)cd.e.bp;
-    mqel_finish(cd.e, len);
-    // non-increasing rates + no pass ends on 0xFF (t1.cpp:1303-1324)
-    uint32_t last = len;
-    for (uint32_t i = total; i > 0;) {
-        --i;
-        uint32_t r = rate[i];
-        if (r > last) r = last; else last = r;
-        rate[i] = r;
-    }
-    const uint8_t *ob = (const uint8_t *)out;
-    for (uint32_t i = 0; i < total; ++i)
-        if (rate[i] > 0 && ob[rate[i] - 1] == 0xFF) rate[i]--;
-    *len_out = len;
-    return total;
-}
-
-// DECODER: outputs per plane p: sigafter[p*64+y] = significance rows after
-// the last decoded pass of plane p; refbit[p*64+y] = refinement bits decoded
-// at plane p.  Final sign rows stay in st.neg.
-GRK_HD void t1_decode_lane(const uint8_t *data, uint32_t len, uint32_t numpasses, uint32_t numbps, uint32_t w,
-                           uint32_t h, uint32_t orient, BlockState &st, const T1Tables &T, uint32_t *cxw,
-                           uint64_t *sigafter, uint64_t *refbit) {
-    for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    LaneDecoder cd;
-    mq_reset_words(cxw, T.mq);
-    mqdl_init(cd.d, data, len);
-    cd.cxw = cxw; cd.tab = T.mq; cd.sigafter = sigafter; cd.refbit = refbit; cd.sa = sigafter; cd.rb = refbit;
-    t1_passes(cd, w, h, numbps, numpasses, st, T.zc + orient * 512, T.sc);
-}
 
 // ===========================================================================
 // Encoder, split form.  Because the encoder knows every magnitude up front,
@@ -1074,6 +803,11 @@ GRK_HD int32_t t1_rebuild(uint32_t x, uint32_t y, const DecodedPlanes &dp, const
     int32_t m = (int32_t)((bits << (ql + 1)) | (1u << ql));
     return ((negrow >> x) & 1u) ? -m : m;
 }
+
+// Deepest block the decoder accepts: t1_decode_cblk refuses roishift + numbps
+// >= 31 (t1.cpp:1055-1060); blocks deeper than this are left zero on the
+// device and rejected by the host (ECORRUPT) before the launch.
+constexpr uint32_t T1_MAX_DEC_BPS = 30;
 
 // Per-block HBM scratch: state rows + two 32-plane x 64-row bit-plane sets
 // (encoder: pa = magnitude bit-planes; decoder: pa = sigafter, pb = refbit).

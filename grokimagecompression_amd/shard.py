@@ -56,17 +56,32 @@ def assemble(parts):
     return b"".join(parts)
 
 
+def _group_geom(dist, group):
+    """(gather group, rank in it, its size, the global rank of its member 0).
+    Tile ranges follow the rank WITHIN the group, so a subset or reordered
+    group still splits the tiles among its members and gathers at its own
+    first member."""
+    if dist is None:
+        return None, 0, 1, 0
+    g = group if group is not None else data_group(dist)
+    rank, world = dist.get_rank(g), dist.get_world_size(g)
+    if rank < 0:
+        raise ValueError("this process is not a member of the shard group")
+    root = dist.get_global_rank(g, 0) if g is not None else 0
+    return g, rank, world, root
+
+
 def compress_sharded(codec, img, prec, params, ntiles, dist=None, group=None, offset=(0, 0), sgnd=False,
                      rows=None, height=None):
-    """Encode this rank's tile range; returns the full codestream on rank 0
-    (None elsewhere).  Without torch.distributed (dist=None) it is the
-    single-process path.
+    """Encode this rank's tile range; returns the full codestream on the
+    group's first member (None elsewhere).  Without torch.distributed
+    (dist=None) it is the single-process path.
 
     img: the whole image, or (rows given) only this rank's rows: rows = (r0, r1)
     of an image `height` rows tall, img holding rows [r0, r1)
-    (see tile_rows).  group: the group to gather over (default: data_group)."""
-    world = dist.get_world_size() if dist is not None else 1
-    rank = dist.get_rank() if dist is not None else 0
+    (see tile_rows).  group: the group that shares the tiles and gathers the
+    tile-parts (default: data_group, i.e. every rank); only its members call."""
+    g, rank, world, root = _group_geom(dist, group)
     b, e = tile_range(ntiles, rank, world)
     parts = PART_TILES | (PART_HEADER if rank == 0 else 0) | (PART_EOC if rank == world - 1 else 0)
     if rows is None:
@@ -76,17 +91,21 @@ def compress_sharded(codec, img, prec, params, ntiles, dist=None, group=None, of
                                     height=height)
     if dist is None:
         return mine
-    g = group if group is not None else data_group(dist)
     gathered = [None] * world if rank == 0 else None
-    dist.gather_object(mine, gathered, dst=0, group=g)
+    dist.gather_object(mine, gathered, dst=root, group=g)
     return assemble(gathered) if rank == 0 else None
+
+
+def shard_range(ntiles, dist=None, group=None):
+    """The [begin, end) tile range this process takes in compress_sharded /
+    decompress_sharded (by its rank within `group`)."""
+    _, rank, world, _ = _group_geom(dist, group)
+    return tile_range(ntiles, rank, world)
 
 
 def decompress_sharded(codec, buf, out, ntiles, dist=None, group=None):
     """Decode this rank's tile range of `buf` into `out` (other tiles are left
     untouched); returns the (begin, end) range decoded."""
-    world = dist.get_world_size() if dist is not None else 1
-    rank = dist.get_rank() if dist is not None else 0
-    b, e = tile_range(ntiles, rank, world)
+    b, e = shard_range(ntiles, dist, group)
     codec.decompress_tiles(buf, b, e, out)
     return b, e

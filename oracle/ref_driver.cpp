@@ -39,6 +39,11 @@
 //       grk_plugin_decode(params, decode_callback) with decode_callback /
 //       pre_decode / post_decode restated (:1336-1557) -- post_decode writes
 //       the planes as dec does.  Exit 0 iff the plugin decoded; 3 if declined.
+//   ref_driver mt IN.i32 EXPECT.j2k W H C BITS SGND THREADS REPS [options]
+//       THREADS caller threads, each with its own codecs (one codec per
+//       caller thread), encode + decode REPS times concurrently;
+//       exit 0 iff every encode equals EXPECT.j2k and every decode equals the
+//       first decode (lossless: the input).
 // IN.i32 / OUT.i32: planar int32 little-endian (c, h, w).  dec prints
 // "x0 y0 x1 y1 numcomps prec sgnd" of the decoded image on stdout.
 #include <grok.h>
@@ -46,8 +51,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 static void err_cb(const char *msg, void *) { fprintf(stderr, "[grk error] %s", msg); }
@@ -413,6 +420,61 @@ static int plugin_dec_mode(int argc, char **argv) {
     return rc ? 1 : 0;
 }
 
+// ---- concurrent codecs (thread-safety of the library) ----
+static int mt_mode(int argc, char **argv) {
+    if (argc < 12) return 2;
+    const uint32_t w = (uint32_t)atoi(argv[4]), h = (uint32_t)atoi(argv[5]), c = (uint32_t)atoi(argv[6]);
+    const uint32_t bits = (uint32_t)atoi(argv[7]), sgnd = (uint32_t)atoi(argv[8]);
+    const uint32_t threads = (uint32_t)atoi(argv[9]), reps = (uint32_t)atoi(argv[10]);
+    std::vector<uint8_t> in = read_file(argv[2]);
+    const std::vector<uint8_t> expect = read_file(argv[3]);
+    if (in.size() != (size_t)w * h * c * 4) { fprintf(stderr, "input size mismatch\n"); return 2; }
+    grk_initialize(nullptr, 0);
+    std::vector<int32_t> first;
+    {  // reference decode of the expected stream, single-threaded
+        grk_codec *codec;
+        grk_stream *st;
+        const uint32_t area[4] = {0, 0, 0, 0};
+        grk_image *img = decode(expect.data(), expect.size(), 0, 0, area, &codec, &st);
+        if (!img) { fprintf(stderr, "decode failed\n"); return 1; }
+        for (uint32_t k = 0; k < img->numcomps; ++k)
+            first.insert(first.end(), img->comps[k].data, img->comps[k].data + (size_t)img->comps[k].w * img->comps[k].h);
+        grk_destroy_codec(codec);
+        grk_stream_destroy(st);
+    }
+    std::atomic<int> bad{0};
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < threads; ++t)
+        pool.emplace_back([&]() {
+            for (uint32_t r = 0; r < reps; ++r) {
+                grk_cparameters p;
+                std::vector<uint8_t> cs;
+                if (!parse_enc_opts(&p, argc - 11, argv + 11) ||
+                    !encode(&p, (const int32_t *)in.data(), w, h, c, bits, sgnd, cs) || cs != expect) {
+                    bad++;
+                    continue;
+                }
+                grk_codec *codec;
+                grk_stream *st;
+                const uint32_t area[4] = {0, 0, 0, 0};
+                grk_image *img = decode(cs.data(), cs.size(), 0, 0, area, &codec, &st);
+                if (!img) { bad++; continue; }
+                size_t off = 0;
+                for (uint32_t k = 0; k < img->numcomps; ++k) {
+                    const size_t n = (size_t)img->comps[k].w * img->comps[k].h;
+                    if (off + n > first.size() || memcmp(img->comps[k].data, first.data() + off, n * 4)) bad++;
+                    off += n;
+                }
+                grk_destroy_codec(codec);
+                grk_stream_destroy(st);
+            }
+        });
+    for (auto &th : pool) th.join();
+    grk_deinitialize();
+    if (bad) fprintf(stderr, "%d mismatching results\n", bad.load());
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
@@ -421,6 +483,7 @@ int main(int argc, char **argv) {
     const std::string mode = argv[1];
     if (mode == "plugin") return plugin_mode(argc, argv);
     if (mode == "plugin-dec") return plugin_dec_mode(argc, argv);
+    if (mode == "mt") return mt_mode(argc, argv);
     if (mode == "enc" || mode == "bench") {
         const bool bench = mode == "bench";
         const int need = bench ? 10 : 9;

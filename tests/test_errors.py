@@ -218,3 +218,21 @@ def test_cut_stream_matches_oracle(codec, oracle, name):
         cut = cs[:-k]
         ref = oracle.decode(cut)
         assert np.array_equal(codec.decompress(cut), ref), k
+
+
+@pytest.mark.gpu
+def test_roi_shift_past_decoder_depth(codec):
+    """An RGN shift raised so far that a code-block's bit-planes + shift reach
+    31: the reference refuses the block (t1.cpp:1055-1060, "unsupported
+    bpno_plus_one >= 31"); the GPU decoder, whose scratch holds 32 planes,
+    must refuse it too -- a clean error, not a write past the block's
+    scratch -- and stay healthy."""
+    grk = _grk()
+    cs = _cs("g8_roi_U5")
+    rgn = _marker(cs, 0xFF5E)
+    assert cs[rgn + 6] == 5  # Crgn (1 byte), Srgn, SPrgn = the shift
+    for shift in (28, 40, 200):
+        with pytest.raises(grk.GrkGpuError):
+            codec.decompress(_patch(cs, rgn + 6, ">B", shift))
+    ref = np.load("%s/g8_roi_U5.dec.npy" % GOLD)
+    assert np.array_equal(codec.decompress(cs), ref)

@@ -112,3 +112,23 @@ def test_grk_api_decode_area(tmp_path):
     ref = np.load(f"{GOLD}/rgb12_I.dec.npy")
     assert np.array_equal(d, ref[:, 7:50, 10:60])
     assert hdr[:4] == (10, 7, 60, 50)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rgb12_I", "g8_256", "rgb8_r10_tiles"])
+def test_grk_api_concurrent_codecs(name, tmp_path):
+    """Four caller threads, each with its own grk_* codecs, encode and decode
+    at the same time (the reference allows one codec per caller thread): every
+    result equals the single-threaded one.  The library leases a GPU context
+    per call (grok_api.cpp), so no two calls share arenas or result buffers."""
+    _need_driver()
+    if name not in MAN:
+        pytest.skip("fixture %s absent" % name)
+    m = MAN[name]
+    h, w, c, bits = m["shape"]
+    img = synth.synth_image(h, w, c, bits, m["seed"], m["kind"])
+    src = tmp_path / "in.i32"
+    np.ascontiguousarray(img, dtype="<i4").tofile(src)
+    r = subprocess.run([DRIVER, "mt", str(src), f"{GOLD}/{name}.j2k", str(w), str(h), str(c), str(bits), "0", "4",
+                        "6"] + m["args"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr

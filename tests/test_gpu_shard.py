@@ -165,3 +165,13 @@ def test_compress_tiles_view(codec):
     out = torch.zeros((1, 300, 500), dtype=torch.int32, device="cuda:0")
     codec.decompress_tiles(v, 0, 12, out)
     assert np.array_equal(out.cpu().numpy(), img.astype(np.int32))
+    # only a slice of the view survives: it keeps the library buffer alive
+    import gc
+    head = v[:64]
+    tail = np.asarray(v[-2:])
+    del v
+    gc.collect()
+    for _ in range(3):
+        codec.compress_tiles(img, 12, p, 0, 12, grk.PART_ALL, view=True)  # churn the allocator
+    gc.collect()
+    assert head.tobytes() == ref[:64] and tail.tobytes() == ref[-2:]

@@ -143,3 +143,36 @@ def test_gloo_world2_sharded(ntiles, nccl_default):
     expect = b"H" + b"".join(b"T%d;" % t for t in range(ntiles)) + b"E"
     assert res[0][0] == expect and res[1][0] is None
     assert sorted(res[0][1] + res[1][1]) == list(range(ntiles))
+
+
+def _subgroup_worker(rank, world, port, ntiles, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    g = dist.new_group(ranks=[1, 2], backend="gloo")  # collective: every rank creates it
+    cs, dec = None, []
+    if rank in (1, 2):
+        cs = shard.compress_sharded(FakeCoder(), None, 8, None, ntiles, dist=dist, group=g)
+        shard.decompress_sharded(FakeCoder(), b"", dec, ntiles, dist=dist, group=g)
+    q.put((rank, cs, dec))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_subgroup_sharded():
+    """A shard group that is a subset of the job (global ranks 1 and 2 of 3):
+    tiles are split by the rank within the group, and the tile-parts are
+    gathered at the group's first member (global rank 1), not at rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000)
+    ntiles = 7
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, ntiles, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict((r, (cs, dec)) for r, cs, dec in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    expect = b"H" + b"".join(b"T%d;" % t for t in range(ntiles)) + b"E"
+    assert res[1][0] == expect and res[2][0] is None and res[0] == (None, [])
+    assert sorted(res[1][1] + res[2][1]) == list(range(ntiles))
