@@ -165,6 +165,17 @@ class CParams(ctypes.Structure):
         return p, off
 
 
+SAMPLE_I32, SAMPLE_U8, SAMPLE_I8, SAMPLE_U16, SAMPLE_I16 = 0, 1, 2, 3, 4
+_NP_FMT = {np.dtype(np.int32): SAMPLE_I32, np.dtype(np.uint8): SAMPLE_U8, np.dtype(np.int8): SAMPLE_I8,
+           np.dtype(np.uint16): SAMPLE_U16, np.dtype(np.int16): SAMPLE_I16}
+
+
+class Planes(ctypes.Structure):
+    """grkgpu_planes: the image planes of grkgpu_compress_ex."""
+    _fields_ = [("planes", ctypes.c_void_p * MAXC), ("sample_fmt", ctypes.c_uint32), ("on_device", ctypes.c_int32),
+                ("row0", ctypes.c_uint32), ("nrows", ctypes.c_uint32)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("h2d_ms", ctypes.c_float), ("dcshift_mct_ms", ctypes.c_float), ("dwt_ms", ctypes.c_float),
                 ("t1_ms", ctypes.c_float), ("gather_ms", ctypes.c_float), ("d2h_ms", ctypes.c_float),
@@ -212,6 +223,8 @@ def lib():
                                       P(ctypes.c_size_t)]
         L.grkgpu_compress_view.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int,
                                            P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
+        L.grkgpu_compress_ex.argtypes = [VP, P(ImageDesc), P(CParams), P(Planes), U32, U32, U32, P(P(ctypes.c_uint8)),
+                                         P(ctypes.c_size_t)]
         L.grkgpu_read_header.argtypes = [VP, ctypes.c_size_t, P(ImageDesc)]
         L.grkgpu_decompress.argtypes = [VP, VP, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_free.argtypes = [VP]
@@ -261,20 +274,17 @@ def _buf_ptr(buf):
 PART_TILES, PART_HEADER, PART_EOC, PART_ALL = 0, 1, 2, 3
 
 
-class _LibBuffer:
-    """Owner of a result buffer the library allocated (released with
-    grkgpu_free when the last numpy view of it goes).  numpy arrays made from
-    its __array_interface__ keep this object as their base, and every view or
-    slice of them keeps that base alive, so no view can outlive the memory."""
+class _CtxView:
+    """Owner of a numpy view of a context's pinned output buffer: it keeps the
+    Codec (and so the buffer) alive for as long as any view or slice of it
+    exists -- numpy arrays made from __array_interface__ keep this object as
+    their base, and every view of them keeps that base.  The bytes stay those
+    of the call that made the view until the next compress call on the Codec."""
 
-    def __init__(self, ptr, n):
-        self._ptr = ctypes.cast(ptr, ctypes.c_void_p).value
-        self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (self._ptr, False), "version": 3}
-
-    def __del__(self):
-        if self._ptr:
-            lib().grkgpu_free(ctypes.c_void_p(self._ptr))
-            self._ptr = None
+    def __init__(self, codec, ptr, n):
+        self.codec = codec
+        addr = ctypes.cast(ptr, ctypes.c_void_p).value
+        self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (addr, False), "version": 3}
 
 
 def num_tiles(shape, prec, params, offset=(0, 0)):
@@ -352,6 +362,9 @@ class Codec:
         return s.as_dict()
 
     def _image(self, img, prec, offset, sgnd):
+        """Image descriptor + grkgpu_planes of a (c,h,w) numpy array or torch
+        tensor of int32, uint16, int16, uint8 or int8 samples (host, pinned
+        host, or on this codec's device)."""
         c, h, w = img.shape
         d = ImageDesc()
         d.x0, d.y0 = offset
@@ -360,74 +373,69 @@ class Codec:
         for k in range(c):
             d.prec[k] = prec
             d.sgnd[k] = 1 if sgnd else 0
-        on_dev = not isinstance(img, np.ndarray)
-        if on_dev:
+        pl = Planes()
+        if isinstance(img, np.ndarray):
+            if img.dtype not in _NP_FMT:
+                img = img.astype(np.int32)
+            img = np.ascontiguousarray(img)
+            fmt = _NP_FMT[img.dtype]
+            for k in range(c):
+                pl.planes[k] = img[k].ctypes.data
+            on_dev = False
+        else:
             torch = _torch()
-            if img.dtype != torch.int32 or not img.is_contiguous():
-                raise GrkGpuError("image tensor must be contiguous int32")
-            if img.is_cuda:
+            tf = {torch.int32: SAMPLE_I32, torch.uint8: SAMPLE_U8, torch.int8: SAMPLE_I8, torch.int16: SAMPLE_I16}
+            if hasattr(torch, "uint16"):
+                tf[torch.uint16] = SAMPLE_U16
+            if img.dtype not in tf or not img.is_contiguous():
+                raise GrkGpuError("image tensor must be contiguous int32 / uint16 / int16 / uint8 / int8")
+            fmt = tf[img.dtype]
+            on_dev = img.is_cuda
+            if on_dev:
                 if img.device.index != self.device:
                     raise GrkGpuError("image tensor on %s, codec on cuda:%d" % (img.device, self.device))
                 lib().grkgpu_set_stream(self._ctx, _stream_handle(img.device))
             else:
                 # host tensor (pinned or not): the library copies it H2D on the
                 # caller's current stream
-                on_dev = False
                 lib().grkgpu_set_stream(self._ctx, _stream_handle(torch.device("cuda", self.device)))
-            ptrs = (ctypes.c_void_p * c)(*[img[k].data_ptr() for k in range(c)])
-        else:
-            img = np.ascontiguousarray(img, dtype=np.int32)
-            ptrs = (ctypes.c_void_p * c)(*[img[k].ctypes.data for k in range(c)])
-        return d, ptrs, on_dev, img
+            for k in range(c):
+                pl.planes[k] = img[k].data_ptr()
+        pl.sample_fmt = fmt
+        pl.on_device = 1 if on_dev else 0
+        return d, pl, img
 
     def compress(self, img, prec, params=None, offset=(0, 0), sgnd=False, view=False):
-        """img: (c,h,w) int32 numpy array (host) or torch tensor on cuda:<device>.
-        Returns the .j2k codestream as bytes, or (view=True) as a zero-copy numpy
-        uint8 view of the context's pinned output buffer, valid until the next
-        call on this Codec."""
-        params = params or CParams.make()
-        d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
-        out = ctypes.POINTER(ctypes.c_uint8)()
-        n = ctypes.c_size_t()
-        if view:
-            _check(lib().grkgpu_compress_view(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs,
-                                              1 if on_dev else 0, ctypes.byref(out), ctypes.byref(n)))
-            return np.ctypeslib.as_array(out, shape=(n.value,))
-        _check(lib().grkgpu_compress(self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0,
-                                     ctypes.byref(out), ctypes.byref(n)))
-        b = ctypes.string_at(out, n.value)
-        lib().grkgpu_free(out)
-        return b
+        """img: (c,h,w) numpy array or torch tensor (host, pinned host or
+        cuda:<device>) of int32 samples, or of the 8 / 16-bit samples of the
+        image file (uint8 / int8 / uint16 / int16: widened on the GPU, so a host
+        frame crosses PCIe at its own width).  Returns the .j2k codestream as
+        bytes, or (view=True) as a zero-copy numpy uint8 view of the context's
+        pinned output buffer, valid until the next call on this Codec."""
+        return self.compress_tiles(img, prec, params or CParams.make(), 0, 0xFFFFFFFF, PART_ALL, offset, sgnd,
+                                   view=view)
 
     def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False,
                        row0=None, height=None, view=False):
         """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
         (plus the main header / EOC when `parts` asks for them) as bytes, or
-        (view=True) as a numpy uint8 array over the library's result buffer
-        (no copy; the buffer is released with the array).
+        (view=True) as a numpy uint8 view of the context's pinned output
+        buffer (no copy), valid until the next compress call on this Codec.
         row0 / height: img holds only image rows [row0, row0 + img rows) of an
-        image `height` rows tall (a tile-row shard, grkgpu_compress_tile_rows)."""
-        if row0 is None:
-            d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
-            fn = lambda *a: lib().grkgpu_compress_tiles(*a)  # noqa: E731
-            extra = ()
-        else:
+        image `height` rows tall (a tile-row shard)."""
+        d, pl, keep = self._image(img, prec, offset, sgnd)
+        if row0 is not None:
             if height is None:
                 raise GrkGpuError("height (the full image height) is required with row0")
-            d, ptrs, on_dev, keep = self._image(img, prec, offset, sgnd)
             d.y1 = offset[1] + height
-            fn = lambda *a: lib().grkgpu_compress_tile_rows(*a)  # noqa: E731
-            extra = (row0, img.shape[1])
+            pl.row0, pl.nrows = row0, img.shape[1]
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
-        args = (self._ctx, ctypes.byref(d), ctypes.byref(params), ptrs, 1 if on_dev else 0) + extra + \
-            (tile_begin, tile_end, parts, ctypes.byref(out), ctypes.byref(n))
-        _check(fn(*args))
-        if view and n.value:
-            return np.asarray(_LibBuffer(out, n.value))
-        b = ctypes.string_at(out, n.value)
-        lib().grkgpu_free(out)
-        return b
+        _check(lib().grkgpu_compress_ex(self._ctx, ctypes.byref(d), ctypes.byref(params), ctypes.byref(pl), tile_begin,
+                                        tile_end, parts, ctypes.byref(out), ctypes.byref(n)))
+        if view:
+            return np.asarray(_CtxView(self, out, n.value)) if n.value else np.empty(0, np.uint8)
+        return ctypes.string_at(out, n.value)
 
     def decompress_tiles(self, buf, tile_begin, tile_end, out):
         """Decode tiles [tile_begin, tile_end) of a codestream into `out`

@@ -408,6 +408,7 @@ struct DwtPlan {
     std::vector<Copy2D> copies2d;  // reduced decode at resolution 0: LL band -> compact output
     bool fused0 = false;  // forward level 0 reads the image planes (DC shift + MCT fused, dwt.hip)
     bool mct3 = false;    // ... and its jobs are MCT component triples (tile-major, component-minor)
+    int32_t fmt = SMP_I32;  // ... reading image samples of this format
     bool inverse = false;
     std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
 };
@@ -601,7 +602,8 @@ static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, boo
         }
         uint32_t maxt = 0;
         for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
-        const int code = P.th[li] | (li == 0 && P.fused0 && !inverse ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) : 0);
+        const bool f0 = li == 0 && P.fused0 && !inverse;
+        const int code = P.th[li] | (f0 ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) | (P.fmt << DWT_FMT_SHIFT) : 0);
         e = launch_dwt_jobs(djobs + k, (uint32_t)l.size(), maxt, code, irrev, inverse ? 1 : 0, s);
         if (e != hipSuccess) return e;
         k += l.size();
@@ -684,13 +686,21 @@ static BandNeed window_need(const TileComp &tc, const Rect &win) {
 // row0 / nrows: the planes hold only image rows [row0, row0 + nrows) (a tile-
 // row shard: a rank loads just the rows of its tiles); nrows = 0: all rows.
 static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
-                         const int32_t *const *planes, int planes_on_device, const uint8_t **view, size_t *outlen,
+                         const void *const *planes, int planes_on_device, int32_t fmt, const uint8_t **view,
+                         size_t *outlen,
                          uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL,
                          bool export_blocks = false, int force_dist = 0, uint32_t row0 = 0, uint32_t nrows = 0) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
     if (rc) return rc;
+    if (fmt < SMP_I32 || fmt > SMP_I16) return set_err(GRKGPU_EINVAL, "unknown sample format");
+    for (uint32_t k = 0; fmt != SMP_I32 && k < img->numcomps; ++k) {
+        const bool sg = fmt == SMP_I8 || fmt == SMP_I16;
+        if ((img->sgnd[k] != 0) != sg || img->prec[k] > 8 * sample_bytes(fmt))
+            return set_err(GRKGPU_EINVAL, "sample format does not hold the component's precision / signedness");
+    }
+    const uint32_t sb = sample_bytes(fmt);  // bytes per input sample
     {
         const uint32_t nt = cp.tw * cp.th;
         if (te > nt) te = nt;
@@ -792,17 +802,19 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->h_symoff.ensure(symoff.size() * 8 + 256));
 
     HIPCHK(hipEventRecord(c->ev[0], s));
-    // input planes on the device
-    PlanePtrs src{};
+    // input planes on the device, as the caller's samples (widened to int32
+    // by the first kernel that reads them)
+    SrcPlanes src{};
     if (planes_on_device) {
-        for (uint32_t k = 0; k < nc; ++k) src.p[k] = (int32_t *)planes[k];
+        for (uint32_t k = 0; k < nc; ++k) src.p[k] = planes[k];
     } else {
-        HIPCHK(c->img.ensure(plane * nc * 4 + 256));
+        HIPCHK(c->img.ensure(plane * nc * sb + 256));
         for (uint32_t k = 0; k < nc; ++k) {
-            src.p[k] = c->img.as<int32_t>() + plane * k;
-            HIPCHK(hipMemcpyAsync(src.p[k], planes[k], plane * 4, hipMemcpyHostToDevice, s));
+            src.p[k] = c->img.as<uint8_t>() + plane * sb * k;
+            HIPCHK(hipMemcpyAsync((void *)src.p[k], planes[k], plane * sb, hipMemcpyHostToDevice, s));
         }
     }
+    auto src_at = [&](uint32_t k, uint64_t off) { return (const void *)((const uint8_t *)src.p[k] + off * sb); };
     HIPCHK(hipEventRecord(c->ev[1], s));
     ShiftArr sh{};
     for (uint32_t k = 0; k < nc; ++k) sh.v[k] = cp.shift[k];
@@ -823,6 +835,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             fuse = fuse && tc.numres >= 2 && tc.r.w() == tile.r.w() && tc.r.h() == tile.r.h();
         }
     if (cp.mct && nc != 3) fuse = false;  // MCT over more than 3 components: separate pass
+    if (fmt == SMP_I8 || fmt == SMP_I16) fuse = false;  // the fused loads read int32, u16 or u8 samples
     DwtPlan dplan;
     dplan.fused0 = fuse;
     dplan.mct3 = fuse && cp.mct && nc == 3;
@@ -838,26 +851,29 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             const bool mct3 = cp.mct && nc >= 3 && k < 3;
             for (uint32_t i = 0; i < 3; ++i) {
                 const uint32_t pk = mct3 ? i : k;
-                j.src[i] = src.p[pk] + org;
+                j.src[i] = src_at(pk, org);
                 j.shift[i] = cp.shift[pk];
             }
             j.src_stride = iw;
-            j.src_bytes = (uint32_t)std::min<uint64_t>((plane - org) * 4, 0xffffffffu);
+            j.src_bytes = (uint32_t)std::min<uint64_t>((plane - org) * sb, 0xffffffffu);
+            j.src_fmt = fmt;
             j.mct_mode = mct3 ? (cp.irrev ? 3 : 2) : 1;
             j.comp = (int32_t)k;
             bool al = (iw & 1) == 0;
-            for (uint32_t i = 0; i < 3; ++i) al = al && ((uintptr_t)j.src[i] & 7) == 0;
+            for (uint32_t i = 0; i < 3; ++i) al = al && ((uintptr_t)j.src[i] & (2 * sb - 1)) == 0;
             j.src_vec = al ? 1 : 0;
         }
+    dplan.fmt = fmt;
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
         if (fuse) break;
-        PlanePtrs tsrc{}, tdst{};
+        SrcPlanes tsrc{};
+        PlanePtrs tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
-            tsrc.p[k] = src.p[k] + (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0);
+            tsrc.p[k] = src_at(k, (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0));
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
-        HIPCHK(launch_dcshift_mct_fwd(tsrc, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+        HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, false, s));
@@ -1171,7 +1187,7 @@ extern "C" int grkgpu_compress_view(grkgpu_ctx *c, const grkgpu_image_desc *img,
                                     const int32_t *const *planes, int planes_on_device, const uint8_t **out,
                                     size_t *outlen) {
     if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
-    return compress_impl(c, img, p, planes, planes_on_device, out, outlen);
+    return compress_impl(c, img, p, (const void *const *)planes, planes_on_device, SMP_I32, out, outlen);
 }
 
 extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
@@ -1179,7 +1195,7 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
     const uint8_t *v = nullptr;
     size_t n = 0;
-    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n);
+    int rc = compress_impl(c, img, p, (const void *const *)planes, planes_on_device, SMP_I32, &v, &n);
     if (rc) return rc;
     uint8_t *o = (uint8_t *)malloc(n ? n : 1);
     if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
@@ -1189,12 +1205,21 @@ extern "C" int grkgpu_compress(grkgpu_ctx *c, const grkgpu_image_desc *img, cons
     return GRKGPU_OK;
 }
 
+extern "C" int grkgpu_compress_ex(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                                  const grkgpu_planes *in, uint32_t tile_begin, uint32_t tile_end, uint32_t parts,
+                                  const uint8_t **out, size_t *outlen) {
+    if (!in || !out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
+    if (in->nrows == 0 && in->row0) return set_err(GRKGPU_EINVAL, "row0 without nrows");
+    return compress_impl(c, img, p, in->planes, in->on_device, (int32_t)in->sample_fmt, out, outlen, tile_begin,
+                         tile_end, parts, false, 0, in->row0, in->nrows);
+}
+
 extern "C" int grkgpu_encode_blocks(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                                     const int32_t *const *planes, int planes_on_device, int with_distortion,
                                     const grkgpu_block_info **blocks, uint32_t *nblocks) {
     if (!blocks || !nblocks) return set_err(GRKGPU_EINVAL, "null argument");
-    int rc = compress_impl(c, img, p, planes, planes_on_device, nullptr, nullptr, 0, 0xffffffffu, GRKGPU_PART_ALL,
-                           true, with_distortion);
+    int rc = compress_impl(c, img, p, (const void *const *)planes, planes_on_device, SMP_I32, nullptr, nullptr, 0,
+                           0xffffffffu, GRKGPU_PART_ALL, true, with_distortion);
     if (rc) return rc;
     *blocks = c->bexp.data();
     *nblocks = (uint32_t)c->bexp.size();
@@ -1216,7 +1241,8 @@ extern "C" int grkgpu_compress_tiles(grkgpu_ctx *c, const grkgpu_image_desc *img
     if (!out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
     const uint8_t *v = nullptr;
     size_t n = 0;
-    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n, tile_begin, tile_end, parts);
+    int rc = compress_impl(c, img, p, (const void *const *)planes, planes_on_device, SMP_I32, &v, &n, tile_begin,
+                           tile_end, parts);
     if (rc) return rc;
     uint8_t *o = (uint8_t *)malloc(n ? n : 1);
     if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
@@ -1234,8 +1260,8 @@ extern "C" int grkgpu_compress_tile_rows(grkgpu_ctx *c, const grkgpu_image_desc 
     if (nrows == 0) return set_err(GRKGPU_EINVAL, "nrows must be > 0");
     const uint8_t *v = nullptr;
     size_t n = 0;
-    int rc = compress_impl(c, img, p, planes, planes_on_device, &v, &n, tile_begin, tile_end, parts, false, 0, row0,
-                           nrows);
+    int rc = compress_impl(c, img, p, (const void *const *)planes, planes_on_device, SMP_I32, &v, &n, tile_begin,
+                           tile_end, parts, false, 0, row0, nrows);
     if (rc) return rc;
     uint8_t *o = (uint8_t *)malloc(n ? n : 1);
     if (!o) return set_err(GRKGPU_EINVAL, "out of host memory");
@@ -1649,9 +1675,10 @@ extern "C" int grkgpu_dcshift_mct_fwd(int32_t *const *planes, uint32_t numcomps,
     int rc = check_device(-1);
     if (rc) return rc;
     PlanePtrs p{};
+    SrcPlanes ps{};
     ShiftArr sh{};
-    for (uint32_t k = 0; k < numcomps; ++k) { p.p[k] = planes[k]; sh.v[k] = shift[k]; }
-    HIPCHK(launch_dcshift_mct_fwd(p, stride, p, w, h, numcomps, sh, mct, irreversible, (hipStream_t)stream));
+    for (uint32_t k = 0; k < numcomps; ++k) { p.p[k] = planes[k]; ps.p[k] = planes[k]; sh.v[k] = shift[k]; }
+    HIPCHK(launch_dcshift_mct_fwd(ps, SMP_I32, stride, p, w, h, numcomps, sh, mct, irreversible, (hipStream_t)stream));
     return GRKGPU_OK;
 }
 

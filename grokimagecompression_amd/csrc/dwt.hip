@@ -152,28 +152,60 @@ __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int 
 // forward level
 // ---------------------------------------------------------------------------
 
+// Image samples of type S as the fused level 0 reads them: a column pair
+// (2 adjacent samples, one load: 8 / 4 / 2 bytes) or one sample, widened to
+// int32 (unsigned types zero-, signed types sign-extended).
+template <typename S> struct Smp;
+template <> struct Smp<int32_t> {
+    static constexpr int B = 4;
+    static __device__ __forceinline__ void pair(rsrc_t r, int vo, int so, int32_t &a, int32_t &b) {
+        const auto p = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
+        a = (int32_t)p[0]; b = (int32_t)p[1];
+    }
+    static __device__ __forceinline__ int32_t one(rsrc_t r, int vo, int so) { return ld32(r, vo, so); }
+};
+template <> struct Smp<uint16_t> {
+    static constexpr int B = 2;
+    static __device__ __forceinline__ void pair(rsrc_t r, int vo, int so, int32_t &a, int32_t &b) {
+        const uint32_t p = __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+        a = (int32_t)(p & 0xffffu); b = (int32_t)(p >> 16);
+    }
+    static __device__ __forceinline__ int32_t one(rsrc_t r, int vo, int so) {
+        return (int32_t)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0);
+    }
+};
+template <> struct Smp<uint8_t> {
+    static constexpr int B = 1;
+    static __device__ __forceinline__ void pair(rsrc_t r, int vo, int so, int32_t &a, int32_t &b) {
+        const uint32_t p = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0);
+        a = (int32_t)(p & 0xffu); b = (int32_t)(p >> 8);
+    }
+    static __device__ __forceinline__ int32_t one(rsrc_t r, int vo, int so) {
+        return (int32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, vo, so, 0);
+    }
+};
+
 // Window rows of a fused level 0 for a component outside an MCT triple: the
 // DC shift (TileProcessor.cpp:1449-1471; 9/7: then << 11) applied as the
 // image plane is read.  (MCT triples take k_dwt_fwd_mct3.)
-template <bool IRREV, int R>
+template <bool IRREV, int R, typename S>
 __device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], int32_t (&hi)[R], int xw, int yw,
                                            int gx0, int gx1) {
     const int rw = J.rw, rh = J.rh;
-    const int st = (int)J.src_stride * 4;
+    const int st = (int)J.src_stride * Smp<S>::B;
     const rsrc_t p0 = mkbuf(J.src[0], J.src_bytes);
     const bool vec = J.src_vec && J.casx == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
     const bool rows_in = yw >= 0 && yw + R <= rh;
-    const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+    const int o0 = mirror_idx(gx0, rw) * Smp<S>::B, o1 = mirror_idx(gx1, rw) * Smp<S>::B;
     const int32_t sh = J.shift[0];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int so = (rows_in ? yw + r : mirror_idx(yw + r, rh)) * st;
         int32_t a0, a1;
         if (vec) {
-            const auto a = __builtin_amdgcn_raw_buffer_load_b64(p0, gx0 * 4, so, 0);
-            a0 = (int32_t)a[0]; a1 = (int32_t)a[1];
+            Smp<S>::pair(p0, gx0 * Smp<S>::B, so, a0, a1);
         } else {
-            a0 = ld32(p0, o0, so); a1 = ld32(p0, o1, so);
+            a0 = Smp<S>::one(p0, o0, so); a1 = Smp<S>::one(p0, o1, so);
         }
         lo[r] = IRREV ? (int32_t)((uint32_t)(a0 - sh) << 11) : a0 - sh;
         hi[r] = IRREV ? (int32_t)((uint32_t)(a1 - sh) << 11) : a1 - sh;
@@ -263,7 +295,7 @@ __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&
 
 // FUSED: 0 = reads `in`; 1 = DC shift (+ MCT for a component of an MCT
 // triple) fused into the loads (fused_load: 3 planes per MCT component).
-template <bool IRREV, int TH, int FUSED = 0>
+template <bool IRREV, int TH, int FUSED = 0, typename S = int32_t>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__restrict__ jobs, int lay) {
     using G = DwtGeo<IRREV, TH>;
     constexpr int R = G::R;
@@ -278,7 +310,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
 
     int32_t lo[R], hi[R];  // column 2l (low pass) and 2l+1 (high pass)
     if (FUSED == 1) {
-        fused_load<IRREV, R>(J, lo, hi, xw, yw, gx0, gx1);
+        fused_load<IRREV, R, S>(J, lo, hi, xw, yw, gx0, gx1);
     } else {
         const rsrc_t in = mkbuf(J.in, J.in_bytes);
         const int st = (int)J.in_stride * 4;
@@ -314,7 +346,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
 // the three image planes are read once (8-byte loads), the DC shift + RCT /
 // ICT forms all three components in registers, and each component
 // is lifted and stored in turn.  jobs = component triples (blockIdx.y).
-template <bool IRREV, int TH>
+template <bool IRREV, int TH, typename S = int32_t>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *__restrict__ jobs, int lay) {
     using G = DwtGeo<IRREV, TH>;
     constexpr int R = G::R;
@@ -334,7 +366,8 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *_
     const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
     int32_t a0[R], a1[R], b0[R], b1[R], c0[R], c1[R];
     {
-        const int st = (int)J0.src_stride * 4;
+        constexpr int B = Smp<S>::B;
+        const int st = (int)J0.src_stride * B;
         const rsrc_t p0 = mkbuf(J0.src[0], J0.src_bytes), p1 = mkbuf(J0.src[1], J0.src_bytes),
                      p2 = mkbuf(J0.src[2], J0.src_bytes);
         const bool vec = J0.src_vec && casx == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
@@ -343,21 +376,18 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *_
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int so = (rows_in ? yw + r : mirror_idx(yw + r, rh)) * st;
-                const auto a = __builtin_amdgcn_raw_buffer_load_b64(p0, gx0 * 4, so, 0);
-                const auto b = __builtin_amdgcn_raw_buffer_load_b64(p1, gx0 * 4, so, 0);
-                const auto c = __builtin_amdgcn_raw_buffer_load_b64(p2, gx0 * 4, so, 0);
-                a0[r] = (int32_t)a[0]; a1[r] = (int32_t)a[1];
-                b0[r] = (int32_t)b[0]; b1[r] = (int32_t)b[1];
-                c0[r] = (int32_t)c[0]; c1[r] = (int32_t)c[1];
+                Smp<S>::pair(p0, gx0 * B, so, a0[r], a1[r]);
+                Smp<S>::pair(p1, gx0 * B, so, b0[r], b1[r]);
+                Smp<S>::pair(p2, gx0 * B, so, c0[r], c1[r]);
             }
         } else {
-            const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
+            const int o0 = mirror_idx(gx0, rw) * B, o1 = mirror_idx(gx1, rw) * B;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int so = mirror_idx(yw + r, rh) * st;
-                a0[r] = ld32(p0, o0, so); a1[r] = ld32(p0, o1, so);
-                b0[r] = ld32(p1, o0, so); b1[r] = ld32(p1, o1, so);
-                c0[r] = ld32(p2, o0, so); c1[r] = ld32(p2, o1, so);
+                a0[r] = Smp<S>::one(p0, o0, so); a1[r] = Smp<S>::one(p0, o1, so);
+                b0[r] = Smp<S>::one(p1, o0, so); b1[r] = Smp<S>::one(p1, o1, so);
+                c0[r] = Smp<S>::one(p2, o0, so); c1[r] = Smp<S>::one(p2, o1, so);
             }
         }
     }
@@ -1005,7 +1035,7 @@ void dwt_job_tiles(int irrev, int code, int rw, int rh, int casx, int casy, int3
 }
 
 template <int TH>
-static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int nch, int fused,
+static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int nch, int fused, int fmt,
                       hipStream_t s) {
     const int lay = env_int("GRKGPU_DWT_LAY", 1);
     if (nch) {
@@ -1020,13 +1050,19 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
     }
     if (fused == 3) {  // forward level 0, MCT triples: one wavefront = the 3 components of one window
         const dim3 g3(grid.x, grid.y / 3);
-        if (irrev) hipLaunchKernelGGL((k_dwt_fwd_mct3<true, TH>), g3, block, 0, s, jobs, lay);
-        else hipLaunchKernelGGL((k_dwt_fwd_mct3<false, TH>), g3, block, 0, s, jobs, lay);
+#define GRK_M3(S)                                                                         \
+    if (irrev) hipLaunchKernelGGL((k_dwt_fwd_mct3<true, TH, S>), g3, block, 0, s, jobs, lay); \
+    else hipLaunchKernelGGL((k_dwt_fwd_mct3<false, TH, S>), g3, block, 0, s, jobs, lay)
+        if (fmt == SMP_U16) { GRK_M3(uint16_t); } else if (fmt == SMP_U8) { GRK_M3(uint8_t); } else { GRK_M3(int32_t); }
+#undef GRK_M3
         return;
     }
     if (fused == 1) {  // forward level 0 with the DC shift in the loads
-        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1>), grid, block, 0, s, jobs, lay);
-        else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 1>), grid, block, 0, s, jobs, lay);
+#define GRK_F1(S)                                                                            \
+    if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH, 1, S>), grid, block, 0, s, jobs, lay); \
+    else hipLaunchKernelGGL((k_dwt_fwd<false, TH, 1, S>), grid, block, 0, s, jobs, lay)
+        if (fmt == SMP_U16) { GRK_F1(uint16_t); } else if (fmt == SMP_U8) { GRK_F1(uint8_t); } else { GRK_F1(int32_t); }
+#undef GRK_F1
         return;
     }
     if (!inverse) {
@@ -1061,11 +1097,12 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
     const int fused = inverse || nch ? 0
                       : (code & DWT_FUSED_MCT3) ? 3
                       : (code & DWT_FUSED) ? 1 : 0;
+    const int fmt = (code >> DWT_FMT_SHIFT) & 7;  // image sample format of a fused level 0
     switch (code & 0xff) {
-        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
-        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
-        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
-        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, nch, fused, s); break;
+        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
+        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
+        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
+        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

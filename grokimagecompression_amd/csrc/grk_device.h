@@ -11,6 +11,13 @@ constexpr int GRK_MAX_COMPS = 16;
 constexpr int GRK_MAX_PASSES = 96;  // 3 * 31 - 2 = 91 passes max for cblksty 0
 
 struct PlanePtrs { int32_t *p[GRK_MAX_COMPS]; };
+// Image planes as the caller holds them: int32 (grk_image) or the 8 / 16-bit
+// samples of the image file (GRKGPU_SAMPLE_*, include/grk_mi355x.h), widened
+// to int32 by the kernel that first reads them (DC shift + MCT, or the fused
+// DWT level 0) -- an 8K 12-bit frame crosses PCIe as 2 B/sample.
+struct SrcPlanes { const void *p[GRK_MAX_COMPS]; };
+enum SampleFmt : int32_t { SMP_I32 = 0, SMP_U8 = 1, SMP_I8 = 2, SMP_U16 = 3, SMP_I16 = 4 };
+constexpr uint32_t sample_bytes(int32_t fmt) { return fmt == SMP_I32 ? 4u : (fmt <= SMP_I8 ? 1u : 2u); }
 struct ShiftArr { int32_t v[GRK_MAX_COMPS]; };
 
 // One code-block to encode (T1Part1::preEncode + t1_encode_cblk inputs,
@@ -49,9 +56,9 @@ struct DecBlock {
 
 struct GatherItem { uint64_t src, dst; uint32_t len, pad; };  // pad: 0 = header blob, 1 = MQ slab
 
-hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const PlanePtrs &dst, uint32_t tw,
-                                  uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct, int32_t irrev,
-                                  hipStream_t s);
+hipError_t launch_dcshift_mct_fwd(const SrcPlanes &src, int32_t fmt, uint32_t sstride, const PlanePtrs &dst,
+                                  uint32_t tw, uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct,
+                                  int32_t irrev, hipStream_t s);
 // src rows at sstride elements (a window of a tile buffer), dst rows at dstride
 hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32_t tw, uint32_t th,
                                   const PlanePtrs &dst, uint32_t dstride, uint32_t ncomp, const ShiftArr &shift,
@@ -71,17 +78,19 @@ struct DwtJob {
     // (TileProcessor.cpp:1449-1471, mct.cpp:85-139 / 195-350): the window is
     // read from the image planes instead of `in`.  mct_mode 0: not fused;
     // 1: DC shift of src[0]; 2: RCT output component `comp` of src[0..2];
-    // 3: ICT output component `comp`.
-    const int32_t *src[3];      // image planes at the tile origin
+    // 3: ICT output component `comp`.  Samples in format src_fmt (SampleFmt).
+    const void *src[3];         // image planes at the tile origin
     uint32_t src_stride, src_bytes;  // elements; bytes from src[i] to its plane's end (min)
     int32_t shift[3];
-    int32_t mct_mode, comp, src_vec;  // src_vec: 8-byte loads allowed (aligned base, even stride)
+    int32_t mct_mode, comp, src_vec;  // src_vec: pair loads allowed (base aligned to 2 samples, even stride)
+    int32_t src_fmt, pad_;
 };
 // level geometry code (window rows | strip windows << 8) for a level of that
 // many samples whose smallest resolution is minw x minh
 int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh);
 constexpr int DWT_FUSED = 1 << 16;       // geometry-code flag: forward level with fused DC shift loads
 constexpr int DWT_FUSED_MCT3 = 1 << 17;  // ... with fused DC shift + MCT (jobs in component triples)
+constexpr int DWT_FMT_SHIFT = 18;        // bits 18-20: SampleFmt of the fused level's image planes (I32 / U8 / U16)
 void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
                            int inverse, hipStream_t s);

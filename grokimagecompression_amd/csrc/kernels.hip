@@ -28,26 +28,27 @@ __device__ __forceinline__ int32_t fix_mul13(int32_t a, int32_t b) {
     return (int32_t)(t >> 13);
 }
 
-// src: image planes (row stride sstride), dst: tile-component buffers
-// (row stride tw).  One thread per sample of the tile.
+// NT: non-temporal stores (the output is streamed to HBM instead of lingering
+// dirty in the caches for the next kernel to evict).
 template <bool NT>
 __device__ __forceinline__ void put(int32_t *p, int32_t v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
-// NT: non-temporal stores (the output is streamed to HBM instead of lingering
-// dirty in the caches for the next kernel to evict).
-template <bool NT>
-__global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst, uint32_t tw, uint32_t th,
+// src: image planes of samples S (row stride sstride), dst: tile-component
+// buffers (row stride tw).  One thread per sample of the tile.
+template <bool NT, typename S>
+__global__ void k_dcshift_mct_fwd(SrcPlanes src, uint32_t sstride, PlanePtrs dst, uint32_t tw, uint32_t th,
                                   uint32_t ncomp, ShiftArr shift, int32_t mct, int32_t irrev) {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
     if (x >= tw || y >= th) return;
     size_t si = (size_t)y * sstride + x, di = (size_t)y * tw + x;
+    auto smp = [&](uint32_t c) { return (int32_t)((const S *)src.p[c])[si]; };
     uint32_t c0 = 0;
     if (mct && ncomp >= 3) {
-        int32_t r = src.p[0][si] - shift.v[0], g = src.p[1][si] - shift.v[1], b = src.p[2][si] - shift.v[2];
+        int32_t r = smp(0) - shift.v[0], g = smp(1) - shift.v[1], b = smp(2) - shift.v[2];
         int32_t o0, o1, o2;
         if (!irrev) {
             o0 = (r + (g * 2) + b) >> 2;
@@ -62,7 +63,7 @@ __global__ void k_dcshift_mct_fwd(PlanePtrs src, uint32_t sstride, PlanePtrs dst
         c0 = 3;
     }
     for (uint32_t c = c0; c < ncomp; ++c) {
-        int32_t v = src.p[c][si] - shift.v[c];
+        int32_t v = smp(c) - shift.v[c];
         put<NT>(&dst.p[c][di], irrev ? (int32_t)((uint32_t)v << 11) : v);
     }
 }
@@ -546,21 +547,26 @@ __global__ void k_gather(const uint8_t *__restrict__ hdr, const uint8_t *__restr
 // ---------------------------------------------------------------------------
 // launchers (host side, used by codec.cpp)
 // ---------------------------------------------------------------------------
-hipError_t launch_dcshift_mct_fwd(const PlanePtrs &src, uint32_t sstride, const PlanePtrs &dst, uint32_t tw,
-                                  uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct, int32_t irrev,
-                                  hipStream_t s) {
+hipError_t launch_dcshift_mct_fwd(const SrcPlanes &src, int32_t fmt, uint32_t sstride, const PlanePtrs &dst,
+                                  uint32_t tw, uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct,
+                                  int32_t irrev, hipStream_t s) {
     dim3 grid((tw + 255) / 256, th);
-    // Non-temporal output stores by default (GRKGPU_MCT_NT=0: plain stores):
-    // with plain stores the 8 B/sample this pass writes sit dirty in L2 / MALL
-    // and are written back while the first DWT level runs, which then reads
-    // at ~4 TB/s instead of ~6 (scripts/probe/read_pattern.hip "dirty 1").
-    // Measured on the 8K frame: MCT 0.137 -> 0.150 ms, 9/7 DWT 0.255 -> 0.239.
-    if (!getenv("GRKGPU_MCT_NT") || atoi(getenv("GRKGPU_MCT_NT")))
-        hipLaunchKernelGGL(k_dcshift_mct_fwd<true>, grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, shift, mct,
-                           irrev);
-    else
-        hipLaunchKernelGGL(k_dcshift_mct_fwd<false>, grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, shift,
-                           mct, irrev);
+    // Non-temporal output stores: with plain stores the 8 B/sample this pass
+    // writes sit dirty in L2 / MALL and are written back while the first DWT
+    // level runs, which then reads at ~4 TB/s instead of ~6
+    // (scripts/probe/read_pattern.hip "dirty 1").  Measured on the 8K frame:
+    // MCT 0.137 -> 0.150 ms, 9/7 DWT 0.255 -> 0.239.
+#define GRK_DCS(S) hipLaunchKernelGGL((k_dcshift_mct_fwd<true, S>), grid, dim3(256), 0, s, src, sstride, dst, tw, th, \
+                                      ncomp, shift, mct, irrev)
+    switch (fmt) {
+        case SMP_I32: GRK_DCS(int32_t); break;
+        case SMP_U8: GRK_DCS(uint8_t); break;
+        case SMP_I8: GRK_DCS(int8_t); break;
+        case SMP_U16: GRK_DCS(uint16_t); break;
+        case SMP_I16: GRK_DCS(int16_t); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef GRK_DCS
     return hipGetLastError();
 }
 

@@ -176,6 +176,36 @@ int grkgpu_compress_tile_rows(grkgpu_ctx *ctx, const grkgpu_image_desc *img, con
                               const int32_t *const *planes, int planes_on_device, uint32_t row0, uint32_t nrows,
                               uint32_t tile_begin, uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
 
+/* The general encode entry point: image samples in the width the image file
+ * holds them (grk_image's planes are int32, grok.h:851-918; the PGM / PPM /
+ * raw files grk_compress and the plugin read are 1 or 2 bytes per sample,
+ * PNMFormat.cpp), widened to int32 on the GPU by the kernel that first reads
+ * them -- so a 12-bit frame crosses PCIe as 2 B/sample.  planes[c] holds
+ * rows [row0, row0 + nrows) of component c (nrows = 0: every row; a tile-row
+ * shard gives only its tiles' rows, see grkgpu_compress_tile_rows), on the
+ * device when on_device != 0.  Encodes tiles [tile_begin, tile_end) and
+ * emits the parts `parts` selects (GRKGPU_PART_*; 0, 0xffffffff, ALL = the
+ * whole codestream, as grkgpu_compress).  *out points into the context's
+ * pinned output buffer, valid until the next call on ctx (as
+ * grkgpu_compress_view).  A sample format must hold the component's
+ * precision and signedness (U16: unsigned, prec <= 16), else GRKGPU_EINVAL. */
+enum {
+    GRKGPU_SAMPLE_I32 = 0, /* int32_t (grk_image) */
+    GRKGPU_SAMPLE_U8 = 1,
+    GRKGPU_SAMPLE_I8 = 2,
+    GRKGPU_SAMPLE_U16 = 3,
+    GRKGPU_SAMPLE_I16 = 4
+};
+typedef struct {
+    const void *planes[GRKGPU_MAX_COMPS];
+    uint32_t sample_fmt;  /* GRKGPU_SAMPLE_* */
+    int32_t on_device;
+    uint32_t row0, nrows;
+} grkgpu_planes;
+int grkgpu_compress_ex(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                       const grkgpu_planes *planes, uint32_t tile_begin, uint32_t tile_end, uint32_t parts,
+                       const uint8_t **out, size_t *outlen);
+
 /* Tier-1 only (the tile hot path of TileProcessor::encode_tile up to and
  * including t1_encode, TileProcessor.cpp:994-1012; SURVEY 8(b)
  * "grkgpu_encode_tile"): DC shift + MCT + DWT + T1 of every tile on the GPU,

@@ -294,12 +294,106 @@ static inline int32_t fix_mul_t1(int32_t a, int32_t b) {
     return (int32_t)(t >> 18);
 }
 
+/* Normalised MSE decrease tables (t1_generate_luts.cpp:290-318, the
+ * generator of t1_luts.h lut_nmsedec_sig / sig0 / ref / ref0), restated:
+ * index i = the 7 magnitude bits from the coded bit-plane down (6 fraction
+ * bits), t = i / 2^6; sig: (t^2 - (t - 1.5)^2), sig0: t^2, ref: ((t - 1)^2 -
+ * (t - 1.5 or t - 0.5)^2) (by bit 6), ref0: (t - 1)^2, each rounded to 1/64
+ * and scaled by 8192, clamped at 0. */
+static int16_t NMSE_SIG[128], NMSE_SIG0[128], NMSE_REF[128], NMSE_REF0[128];
+static pthread_once_t nmse_once = PTHREAD_ONCE_INIT;
+static int nmse_q(double x) {
+    const int v = (int)(floor(x * 64.0 + 0.5) / 64.0 * 8192.0);
+    return v > 0 ? v : 0;
+}
+static void nmse_init(void) {
+    for (int i = 0; i < 128; ++i) {
+        const double t = i / 64.0;
+        double u = t, v = t - 1.5;
+        NMSE_SIG[i] = (int16_t)nmse_q(u * u - v * v);
+        NMSE_SIG0[i] = (int16_t)nmse_q(u * u);
+        u = t - 1.0;
+        v = (i & 64) ? t - 1.5 : t - 0.5;
+        NMSE_REF[i] = (int16_t)nmse_q(u * u - v * v);
+        NMSE_REF0[i] = (int16_t)nmse_q(u * u);
+    }
+}
+/* t1_getnmsedec_sig / _ref (t1.cpp:155-166): x = |quantised coefficient|
+ * (6 fraction bits), bitpos = the pass's bit-plane */
+static inline int32_t nmse_sig(uint32_t x, int32_t bitpos) {
+    return bitpos > 0 ? NMSE_SIG[(x >> bitpos) & 127] : NMSE_SIG0[x & 127];
+}
+static inline int32_t nmse_ref(uint32_t x, int32_t bitpos) {
+    return bitpos > 0 ? NMSE_REF[(x >> bitpos) & 127] : NMSE_REF0[x & 127];
+}
+
+void orc_nmse_tables(int16_t *out) {
+    pthread_once(&nmse_once, nmse_init);
+    memcpy(out, NMSE_SIG, sizeof NMSE_SIG);
+    memcpy(out + 128, NMSE_SIG0, sizeof NMSE_SIG0);
+    memcpy(out + 256, NMSE_REF, sizeof NMSE_REF);
+    memcpy(out + 384, NMSE_REF0, sizeof NMSE_REF0);
+}
+
+/* sqrt_energy_gains (HTParams.cpp:54-90): the 5/3 and 9/7 synthesis energy
+ * gains per decomposition level, as the reference stores them (float) */
+static const float SQE_53_L[34] = {1.0000e+00f, 1.2247e+00f, 1.3229e+00f, 1.5411e+00f, 1.7139e+00f, 1.9605e+00f,
+    2.2044e+00f, 2.5047e+00f, 2.8277e+00f, 3.2049e+00f, 3.6238e+00f, 4.1033e+00f, 4.6423e+00f, 5.2548e+00f,
+    5.9462e+00f, 6.7299e+00f, 7.6159e+00f, 8.6193e+00f, 9.7544e+00f, 1.1039e+01f, 1.2493e+01f, 1.4139e+01f,
+    1.6001e+01f, 1.8108e+01f, 2.0493e+01f, 2.3192e+01f, 2.6246e+01f, 2.9702e+01f, 3.3614e+01f, 3.8041e+01f,
+    4.3051e+01f, 4.8721e+01f, 5.5138e+01f, 6.2399e+01f};
+static const float SQE_53_H[34] = {1.0458e+00f, 1.3975e+00f, 1.4389e+00f, 1.7287e+00f, 1.8880e+00f, 2.1841e+00f,
+    2.4392e+00f, 2.7830e+00f, 3.1341e+00f, 3.5576e+00f, 4.0188e+00f, 4.5532e+00f, 5.1494e+00f, 5.8301e+00f,
+    6.5963e+00f, 7.4663e+00f, 8.4489e+00f, 9.5623e+00f, 1.0821e+01f, 1.2247e+01f, 1.3860e+01f, 1.5685e+01f,
+    1.7751e+01f, 2.0089e+01f, 2.2735e+01f, 2.5729e+01f, 2.9117e+01f, 3.2952e+01f, 3.7292e+01f, 4.2203e+01f,
+    4.7761e+01f, 5.4051e+01f, 6.1170e+01f, 6.9226e+01f};
+
+static const float SQE_97_L[34] = {1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f,
+    8.2388e+00f, 1.1652e+01f, 1.6479e+01f, 2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f,
+    1.3183e+02f, 1.8643e+02f, 2.6366e+02f, 3.7287e+02f, 5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f,
+    2.1093e+03f, 2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f, 1.1932e+04f, 1.6874e+04f, 2.3864e+04f,
+    3.3748e+04f, 4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
+static const float SQE_97_H[34] = {1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f,
+    1.1809e+01f, 1.6701e+01f, 2.3620e+01f, 3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f,
+    1.8896e+02f, 2.6723e+02f, 3.7792e+02f, 5.3446e+02f, 7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f,
+    3.0233e+03f, 4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f, 1.7103e+04f, 2.4187e+04f, 3.4205e+04f,
+    4.8373e+04f, 6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
+
+/* dwt_utils::getnorm (dwt_utils.cpp:143-166): products of two float gains,
+ * computed in float and widened */
+static double orc_getnorm(uint32_t level, uint32_t orient, int reversible) {
+    const float *L = reversible ? SQE_53_L : SQE_97_L, *H = reversible ? SQE_53_H : SQE_97_H;
+    float v = 0.0f;
+    if (orient == 0) v = L[level] * L[level];
+    else if (orient == 3) v = H[level] * H[level];
+    else v = L[level + 1] * H[level];
+    return (double)v;
+}
+
+/* t1_getwmsedec (t1.cpp:912-930): a pass's weighted MSE decrease from its
+ * normalised sum, the band's norm, step size and bit-plane, and the MCT
+ * component weight (mct_norms, TileProcessor.cpp:1535-1551). */
+double orc_t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno,
+                      uint32_t qmfbid, double stepsize, const double *mct_norms, uint32_t mct_numcomps) {
+    double w1 = 1, w2, wmsedec;
+    if (mct_norms && compno < mct_numcomps) w1 = mct_norms[compno];
+    w2 = orc_getnorm(level, orient, qmfbid == 1);
+    wmsedec = w1 * w2 * stepsize * (1 << bpno);
+    wmsedec *= wmsedec * nmsedec / 8192.0;
+    return wmsedec;
+}
+
 /* T1 encode of one code-block: T1Part1::preEncode (T1Part1.cpp:58-94) +
- * t1_encode_cblk (t1.cpp:1182-1326) for cblksty == 0. */
-int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t h,
-                       uint32_t orient, int32_t qmfbid, int32_t inv_step,
-                       uint8_t *out, uint32_t outcap, orc_pass *passes,
-                       uint32_t *numbps_out, uint32_t *outlen) {
+ * t1_encode_cblk (t1.cpp:1182-1326) for cblksty == 0.  nmsedec (optional):
+ * the per-pass normalised distortion decrease sums of the rate-controlled
+ * encode -- reset at each pass, incremented by t1_getnmsedec_sig when a
+ * sample becomes significant (significance / cleanup, t1.cpp:217, :684) and
+ * by t1_getnmsedec_ref for each refinement bit (:452). */
+int orc_t1_encode_cblk_nmse(const int32_t *src, uint32_t stride, uint32_t w, uint32_t h,
+                            uint32_t orient, int32_t qmfbid, int32_t inv_step,
+                            uint8_t *out, uint32_t outcap, orc_pass *passes,
+                            uint32_t *numbps_out, uint32_t *outlen, int32_t *nmsedec) {
+    pthread_once(&nmse_once, nmse_init);
     const int fs = (int)w + 2;
     uint32_t *mag = (uint32_t *)malloc(sizeof(uint32_t) * w * h);
     uint8_t *flags = (uint8_t *)calloc((size_t)fs * (h + 2), 1);
@@ -331,6 +425,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
     int passtype = 2;
     for (; bpno >= 0; ++passno) {
         const uint32_t one = 1u << (bpno + 6);
+        int32_t nm = 0;
         if (passtype == 0) {
             /* significance propagation (t1.cpp:197-231, 287-338) */
             for (uint32_t k = 0; k < h; k += 4) {
@@ -343,6 +438,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
                             if (bit) {
                                 int xr;
                                 int cx = sc_of(p, fs, &xr);
+                                nm += nmse_sig(mag[y * w + x], bpno);
                                 mqe_encode(&e, cx, ((*p & F_NEG) ? 1u : 0u) ^ (uint32_t)xr);
                                 *p |= F_SIG;
                             }
@@ -358,6 +454,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
                     for (uint32_t y = k; y < k + 4 && y < h; ++y) {
                         uint8_t *p = &flags[(y + 1) * fs + x + 1];
                         if ((*p & (F_SIG | F_VISIT)) == F_SIG) {
+                            nm += nmse_ref(mag[y * w + x], bpno);
                             mqe_encode(&e, mag_ctx(p, fs), (mag[y * w + x] & one) ? 1 : 0);
                             *p |= F_REF;
                         }
@@ -396,6 +493,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
                         if (partial && y == y0) {
                             int xr;
                             int cx = sc_of(p, fs, &xr);
+                            nm += nmse_sig(mag[y * w + x], bpno);
                             mqe_encode(&e, cx, ((*p & F_NEG) ? 1u : 0u) ^ (uint32_t)xr);
                             *p |= F_SIG;
                         } else if ((*p & (F_SIG | F_VISIT)) == 0) {
@@ -404,6 +502,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
                             if (bit) {
                                 int xr;
                                 int cx = sc_of(p, fs, &xr);
+                                nm += nmse_sig(mag[y * w + x], bpno);
                                 mqe_encode(&e, cx, ((*p & F_NEG) ? 1u : 0u) ^ (uint32_t)xr);
                                 *p |= F_SIG;
                             }
@@ -414,6 +513,7 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
             }
         }
         orc_pass *ps = &passes[passno];
+        if (nmsedec) nmsedec[passno] = nm;
         if (passtype == 2 && bpno == 0) {
             /* t1_enc_is_term_pass: last cleanup pass (t1.cpp:1131-1151) */
             mqe_flush(&e);
@@ -443,6 +543,14 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
     *outlen = mqe_numbytes(&e);
     free(mag); free(flags);
     return (int)total;
+}
+
+int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t h,
+                       uint32_t orient, int32_t qmfbid, int32_t inv_step,
+                       uint8_t *out, uint32_t outcap, orc_pass *passes,
+                       uint32_t *numbps_out, uint32_t *outlen) {
+    return orc_t1_encode_cblk_nmse(src, stride, w, h, orient, qmfbid, inv_step, out, outcap, passes, numbps_out,
+                                   outlen, NULL);
 }
 
 /* T1 decode of a single-segment code-block (t1.cpp:1038-1130, passes
@@ -811,17 +919,6 @@ static const float BIBO_53_H[34] = {2.0000e+00f, 2.5000e+00f, 2.7500e+00f, 2.804
     2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f,
     2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f,
     2.8671e+00f, 2.8671e+00f, 2.8671e+00f, 2.8671e+00f};
-static const float SQE_97_L[34] = {1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f,
-    8.2388e+00f, 1.1652e+01f, 1.6479e+01f, 2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f,
-    1.3183e+02f, 1.8643e+02f, 2.6366e+02f, 3.7287e+02f, 5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f,
-    2.1093e+03f, 2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f, 1.1932e+04f, 1.6874e+04f, 2.3864e+04f,
-    3.3748e+04f, 4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
-static const float SQE_97_H[34] = {1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f,
-    1.1809e+01f, 1.6701e+01f, 2.3620e+01f, 3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f,
-    1.8896e+02f, 2.6723e+02f, 3.7792e+02f, 5.3446e+02f, 7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f,
-    3.0233e+03f, 4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f, 1.7103e+04f, 2.4187e+04f, 3.4205e+04f,
-    4.8373e+04f, 6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
-
 typedef struct { uint32_t expn, mant; } stepsize_t;
 
 /* param_qcd::set_rev_quant (HTParams.cpp:187-207).  NB the RCT bit is never

@@ -88,6 +88,21 @@ int orc_t1_encode_cblk(const int32_t *src, uint32_t stride, uint32_t w, uint32_t
                        uint8_t *out, uint32_t outcap, orc_pass *passes,
                        uint32_t *numbps, uint32_t *outlen);
 
+/* The same, also returning the per-pass normalised distortion decrease
+ * sums of a rate-controlled encode in nmsedec[pass] (t1.cpp:217, :452, :684;
+ * LUTs of t1_generate_luts.cpp:290-318). */
+int orc_t1_encode_cblk_nmse(const int32_t *src, uint32_t stride, uint32_t w, uint32_t h,
+                            uint32_t orient, int32_t qmfbid, int32_t inv_step,
+                            uint8_t *out, uint32_t outcap, orc_pass *passes,
+                            uint32_t *numbps, uint32_t *outlen, int32_t *nmsedec);
+
+/* The four nmsedec tables (sig, sig0, ref, ref0; 128 entries each). */
+void orc_nmse_tables(int16_t *out512);
+
+/* t1_getwmsedec (t1.cpp:912-930): weighted distortion decrease of a pass. */
+double orc_t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno,
+                      uint32_t qmfbid, double stepsize, const double *mct_norms, uint32_t mct_numcomps);
+
 /* Tier-1 decode of one single-segment code-block (t1.cpp:1038-1130).
  * data must have 2 writable bytes after len.  Writes w*h raw decoded values
  * (one extra LSB of precision, as Grok's t1->data) into dst. */

@@ -59,6 +59,11 @@ def lib():
                                             ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                             ctypes.c_uint32, ctypes.POINTER(OrcPass), ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_uint32)]
+        _lib.orc_t1_encode_cblk_nmse.argtypes = _lib.orc_t1_encode_cblk.argtypes + [ctypes.c_void_p]
+        _lib.orc_t1_wmsedec.restype = ctypes.c_double
+        _lib.orc_t1_wmsedec.argtypes = [ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_int32, ctypes.c_uint32, ctypes.c_double, ctypes.c_void_p,
+                                        ctypes.c_uint32]
         _lib.orc_t1_decode_cblk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         _lib.orc_count_cblks.argtypes = [ctypes.c_uint32] * 7
@@ -174,7 +179,10 @@ def dcshift_mct_fwd(planes, shifts, mct, irreversible):
     return p
 
 
-def t1_encode_cblk(block, orient, qmfbid, inv_step=0):
+def t1_encode_cblk(block, orient, qmfbid, inv_step=0, nmse=False):
+    """T1 encode of one block (preEncode quantisation included): (bytes,
+    [(rate, len, term)] per pass, numbps) -- plus, with nmse=True, the
+    per-pass normalised distortion decrease sums (t1.cpp nmsedec)."""
     blk = np.ascontiguousarray(block, dtype=np.int32)
     h, w = blk.shape
     cap = w * h * 8 + 64
@@ -182,10 +190,20 @@ def t1_encode_cblk(block, orient, qmfbid, inv_step=0):
     passes = (OrcPass * 100)()
     nbps = ctypes.c_uint32()
     olen = ctypes.c_uint32()
-    n = lib().orc_t1_encode_cblk(blk.ctypes.data, w, w, h, orient, qmfbid, inv_step,
-                                 ctypes.addressof(out) + 1, cap, passes, ctypes.byref(nbps), ctypes.byref(olen))
+    nm = (ctypes.c_int32 * 100)()
+    n = lib().orc_t1_encode_cblk_nmse(blk.ctypes.data, w, w, h, orient, qmfbid, inv_step,
+                                      ctypes.addressof(out) + 1, cap, passes, ctypes.byref(nbps), ctypes.byref(olen),
+                                      nm)
     data = bytes(out)[1:1 + olen.value]
-    return data, [(passes[i].rate, passes[i].len, passes[i].term) for i in range(n)], nbps.value
+    res = (data, [(passes[i].rate, passes[i].len, passes[i].term) for i in range(n)], nbps.value)
+    return res + ([nm[i] for i in range(n)],) if nmse else res
+
+
+def t1_wmsedec(nmsedec, compno, level, orient, bpno, qmfbid, stepsize, mct_norms=None):
+    """t1_getwmsedec (t1.cpp:912-930) of one pass."""
+    norms = (ctypes.c_double * 3)(*mct_norms) if mct_norms else None
+    return lib().orc_t1_wmsedec(nmsedec, compno, level, orient, bpno, qmfbid, stepsize, norms,
+                                len(mct_norms) if mct_norms else 0)
 
 
 def t1_decode_cblk(data, numpasses, numbps, w, h, orient):

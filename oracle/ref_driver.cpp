@@ -422,7 +422,7 @@ static int plugin_dec_mode(int argc, char **argv) {
 
 // ---- concurrent codecs (thread-safety of the library) ----
 static int mt_mode(int argc, char **argv) {
-    if (argc < 12) return 2;
+    if (argc < 11) return 2;
     const uint32_t w = (uint32_t)atoi(argv[4]), h = (uint32_t)atoi(argv[5]), c = (uint32_t)atoi(argv[6]);
     const uint32_t bits = (uint32_t)atoi(argv[7]), sgnd = (uint32_t)atoi(argv[8]);
     const uint32_t threads = (uint32_t)atoi(argv[9]), reps = (uint32_t)atoi(argv[10]);

@@ -342,3 +342,49 @@ def test_mid_size_blocks_per_wave(codec, oracle, hw, irrev):
     assert b == ref
     d = codec.decompress(b)
     assert np.array_equal(d, oracle.decode(ref, nthreads=8))
+
+
+@pytest.mark.parametrize("name,dtype", [("rgb8_128x96", "uint8"), ("rgb8_128x96", "uint16"), ("rgb12_I", "uint16"),
+                                        ("rgb12_96x80", "uint16"), ("g8_off35", "uint8"), ("g16_I", "uint16"),
+                                        ("rgb8_r10_tiles", "uint8"), ("g8_off_tiles", "uint16"),
+                                        ("rgb16_64", "uint16")])
+def test_encode_sample_formats(codec, name, dtype):
+    """Image planes handed over at the image file's sample width
+    (grkgpu_compress_ex, GRKGPU_SAMPLE_U8 / U16: host, pinned host and
+    device tensors), widened to int32 on the GPU in the DC shift + MCT pass or
+    the fused DWT level 0: the reference's bytes."""
+    import torch
+    import grokimagecompression_amd as grk
+    m = MAN[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    gold = open(f"{GOLD}/{name}.j2k", "rb").read()
+    a = img.astype(dtype)
+    assert codec.compress(a, bits, p, offset=off) == gold
+    t = torch.from_numpy(a)
+    assert codec.compress(t.pin_memory(), bits, p, offset=off) == gold
+    assert codec.compress(t.cuda(), bits, p, offset=off) == gold
+    # an odd-width view of the planes (no pair loads) still matches
+    if a.shape[2] > 2:
+        sub = np.ascontiguousarray(a[:, :, 1:])
+        assert codec.compress(sub, bits, p, offset=off) == codec.compress(sub.astype(np.int32), bits, p, offset=off)
+
+
+@pytest.mark.parametrize("bits,irrev", [(12, False), (12, True), (8, False), (16, True)])
+def test_encode_signed_sample_formats(codec, bits, irrev):
+    """Signed components as int8 / int16 samples (GRKGPU_SAMPLE_I8 / I16):
+    the same codestream as their int32 planes; a format that cannot hold the
+    component (unsigned samples for a signed image, 16-bit samples for 8-bit
+    storage of a 12-bit image) is refused."""
+    import grokimagecompression_amd as grk
+    rng = np.random.default_rng(bits)
+    img = rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), size=(3, 70, 93)).astype(np.int32)
+    p = grk.CParams.make(irreversible=irrev)
+    ref = codec.compress(img, bits, p, sgnd=True)
+    small = np.int8 if bits <= 8 else np.int16
+    assert codec.compress(img.astype(small), bits, p, sgnd=True) == ref
+    with pytest.raises(grk.GrkGpuError):
+        codec.compress(img.astype(np.uint16), bits, p, sgnd=True)
+    if bits > 8:
+        with pytest.raises(grk.GrkGpuError):
+            codec.compress((img + (1 << (bits - 1))).astype(np.uint8), bits, p)

@@ -152,11 +152,15 @@ def test_row_slab_shards_match_reference(codec, name):
                              height=img.shape[1])
 
 
-def test_compress_tiles_view(codec):
+def test_compress_tiles_view():
     """compress_tiles(view=True): the same bytes as a numpy view over the
-    library's result buffer (no copy), usable as decompress_tiles input."""
+    context's pinned output buffer (no copy), usable as decompress_tiles
+    input; a slice of the view keeps the Codec -- and so the buffer -- alive
+    after every other reference to them is gone."""
+    import gc
     import torch
     import grokimagecompression_amd as grk
+    codec = grk.Codec(0)
     img = synth.synth_image(300, 500, 1, 12, 9)
     p, _ = grk.CParams.from_cli(["-t", "128,128"])
     ref = codec.compress_tiles(img, 12, p, 0, 12, grk.PART_ALL)
@@ -165,13 +169,10 @@ def test_compress_tiles_view(codec):
     out = torch.zeros((1, 300, 500), dtype=torch.int32, device="cuda:0")
     codec.decompress_tiles(v, 0, 12, out)
     assert np.array_equal(out.cpu().numpy(), img.astype(np.int32))
-    # only a slice of the view survives: it keeps the library buffer alive
-    import gc
-    head = v[:64]
-    tail = np.asarray(v[-2:])
-    del v
+    head, tail = v[:64], np.asarray(v[-2:])
+    del v, codec
     gc.collect()
-    for _ in range(3):
-        codec.compress_tiles(img, 12, p, 0, 12, grk.PART_ALL, view=True)  # churn the allocator
+    junk = [np.ones(1 << 20, np.uint8) for _ in range(8)]  # churn the host allocator
+    del junk
     gc.collect()
     assert head.tobytes() == ref[:64] and tail.tobytes() == ref[-2:]

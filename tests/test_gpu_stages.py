@@ -5,9 +5,9 @@ grkgpu_mct_inv_dcshift, on device buffers, bit-exact.
   * T1 encode: the oracle's t1_encode_cblk (restating t1.cpp t1_encode_cblk,
     :1160-1326) on the same quantised blocks -- numbps, pass count, every
     cumulative pass rate and the MQ bytes; with_distortion=1 must not change
-    them and fills the per-pass distortion terms (their values are pinned
-    end to end by the rate-controlled fixtures, whose PCRD decisions they
-    drive: tests/test_gpu_parity.py, tests/test_gpu_plugin.py).
+    them, and its per-pass distortion sums equal the oracle's restatement
+    exactly (the weighted, cumulative values are checked against the
+    reference host's own T1 in tests/test_gpu_plugin.py's debug-state run).
   * T1 decode: the oracle's t1_decode_cblk (t1.cpp:1038-1130) + the
     whole-tile post_decode scaling (T1Part1.cpp:216-330; 5/3: v/2, 9/7:
     float(v) * step), for all passes and for truncated pass counts (a layer
@@ -98,16 +98,24 @@ def test_t1_encode_blocks_vs_oracle(oracle, seed):
         assert bytes(out[o:o + len(data)]) == data, i
 
 
-def test_t1_encode_blocks_distortion(oracle):
-    cases = _blocks(3)
+@pytest.mark.parametrize("seed", [3, 5])
+def test_t1_encode_blocks_distortion(oracle, seed):
+    """with_distortion=1: the bytes and rates are unchanged, and every pass's
+    normalised distortion decrease sum (t1_encode_cblk's nmsedec, the input
+    of t1_getwmsedec, t1.cpp:912-930 / :1249-1254) equals the oracle's
+    restatement exactly (oracle/grk_oracle.c orc_t1_encode_cblk_nmse: the
+    t1_generate_luts.cpp:290-318 tables, accumulated at t1.cpp:217 / :452 /
+    :684)."""
+    cases = _blocks(seed)
     r0, o0, _ = _gpu_encode(cases, 0)
     r1, o1, _ = _gpu_encode(cases, 1)
     assert np.array_equal(o0, o1)
-    for i in range(len(cases)):
+    for i, (h, w, orient, qmfbid, inv, blk) in enumerate(cases):
         np_ = int(r1[i]["numpasses"])
         assert list(r1[i]["rate"][:np_]) == list(r0[i]["rate"][:np_])
-        if np_:
-            assert r1[i]["nmsedec"][:np_].any(), i   # the distortion terms were produced
+        _, passes, nbps, nm = oracle.t1_encode_cblk(blk, orient, qmfbid, inv, nmse=True)
+        assert np_ == len(passes), i
+        assert [int(v) for v in r1[i]["nmsedec"][:np_]] == nm, i
 
 
 def _gpu_decode(items):

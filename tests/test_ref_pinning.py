@@ -58,3 +58,22 @@ def test_plugin_abi_layout_matches_reference_headers():
     r = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "abi_check")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert " 0 mismatches" in r.stdout
+
+
+def test_oracle_nmsedec_tables_match_reference():
+    """The oracle's distortion tables (restating the generator
+    t1_generate_luts.cpp:290-318) equal the tables the reference ships and
+    compiles (t1_part1/t1_luts.h lut_nmsedec_sig / sig0 / ref / ref0)."""
+    import ctypes
+    import re
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    got = np.zeros(512, np.int16)
+    pyoracle.lib().orc_nmse_tables(got.ctypes.data_as(ctypes.c_void_p))
+    txt = open("/root/reference/src/lib/jp2/t1/t1_part1/t1_luts.h").read()
+    for k, name in enumerate(("lut_nmsedec_sig", "lut_nmsedec_sig0", "lut_nmsedec_ref", "lut_nmsedec_ref0")):
+        body = re.search(name + r"\[[^\]]*\]\s*=\s*\{([^}]*)\}", txt).group(1)
+        vals = [int(v, 0) for v in body.replace("\n", " ").split(",") if v.strip()]
+        assert vals == [int(v) for v in got[128 * k:128 * (k + 1)]], name
