@@ -132,6 +132,17 @@ CASES = [
     ("rgb8_roi_c1_I_r", (96, 128, 3, 8), "smooth", 111, ["-R", "c=1,U=7", "-I", "-r", "20,5"]),
     ("g12_roi_M1_tiles", (130, 170, 1, 12), "uniform", 112, ["-R", "c=0,U=3", "-M", "1", "-t", "64,64"]),
     ("rgb12_roi_c2_U12", (70, 90, 3, 12), "smooth", 113, ["-R", "c=2,U=12"]),
+    # fixed-quality layers (-q PSNR[,PSNR..]: cp_fixed_quality, PCRD to a
+    # distortion target per layer, TileProcessor.cpp pcrd_bisect_simple /
+    # _feasible with the distortion criterion), 5/3 and 9/7, one and several
+    # layers, both PCRD algorithms
+    ("g8_q30", (96, 128, 1, 8), "smooth", 120, ["-q", "30"]),
+    ("rgb8_q28_36_44", (96, 128, 3, 8), "smooth", 121, ["-q", "28,36,44"]),
+    ("rgb12_q40_I", (80, 96, 3, 12), "smooth", 122, ["-I", "-q", "40"]),
+    ("g12_q30_40_50_I", (70, 90, 1, 12), "smooth", 123, ["-I", "-q", "30,40,50"]),
+    ("g12_q35_45_A1", (70, 90, 1, 12), "uniform", 124, ["-q", "35,45", "-A", "1"]),
+    ("rgb8_q32_40_I_A1_prec", (150, 200, 3, 8), "smooth", 125, ["-I", "-q", "32,40", "-A", "1", "-c",
+                                                                 "[32,32],[16,16]", "-p", "RPCL"]),
 ]
 
 # Reference decodes with grk_decompress options (-l layers, -r reduce), per
@@ -162,6 +173,8 @@ DEC_VARIANTS = {
     "rgb8_M1_I_r": [["-l", "1"]],
     "rgb8_roi_c1_I_r": [["-l", "1"], ["-r", "1"]],
     "g8_roi_U5": [["-r", "2"]],
+    "rgb8_q28_36_44": [["-l", "1"], ["-l", "2"]],
+    "g12_q30_40_50_I": [["-l", "1"]],
 }
 
 
