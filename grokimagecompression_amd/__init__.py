@@ -173,7 +173,8 @@ _NP_FMT = {np.dtype(np.int32): SAMPLE_I32, np.dtype(np.uint8): SAMPLE_U8, np.dty
 class Planes(ctypes.Structure):
     """grkgpu_planes: the image planes of grkgpu_compress_ex."""
     _fields_ = [("planes", ctypes.c_void_p * MAXC), ("sample_fmt", ctypes.c_uint32), ("on_device", ctypes.c_int32),
-                ("row0", ctypes.c_uint32), ("nrows", ctypes.c_uint32)]
+                ("row0", ctypes.c_uint32), ("nrows", ctypes.c_uint32), ("col0", ctypes.c_uint32),
+                ("ncols", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):

@@ -91,6 +91,8 @@ struct grkgpu_ctx {
     // grkgpu_encode_blocks output (valid until the next call on the context)
     HostBuf h_slab;
     std::vector<grkgpu_block_info> bexp;
+    struct CoefRec { uint32_t tileno, compno, w, h; uint64_t off; };  // coefficient arena of each tile-component
+    std::vector<CoefRec> bexp_coef;
     std::vector<uint32_t> bexp_rate;
     std::vector<double> bexp_dist;
 };
@@ -689,7 +691,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                          const void *const *planes, int planes_on_device, int32_t fmt, const uint8_t **view,
                          size_t *outlen,
                          uint32_t tb = 0, uint32_t te = 0xffffffffu, uint32_t parts = GRKGPU_PART_ALL,
-                         bool export_blocks = false, int force_dist = 0, uint32_t row0 = 0, uint32_t nrows = 0) {
+                         bool export_blocks = false, int force_dist = 0, uint32_t row0 = 0, uint32_t nrows = 0,
+                         uint32_t col0 = 0, uint32_t ncols = 0) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
     CodingParams cp;
     int rc = setup_params(img, p, cp);
@@ -715,7 +718,13 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         nrows = ih;
     }
     if ((uint64_t)row0 + nrows > ih) return set_err(GRKGPU_EINVAL, "row range outside the image");
-    const uint64_t plane = (uint64_t)iw * nrows;  // samples per plane held by the caller
+    if (ncols == 0) {
+        if (col0) return set_err(GRKGPU_EINVAL, "col0 without ncols");
+        ncols = iw;
+    }
+    if ((uint64_t)col0 + ncols > iw) return set_err(GRKGPU_EINVAL, "column range outside the image");
+    const uint32_t pw = ncols;                    // row stride of the caller's planes (samples)
+    const uint64_t plane = (uint64_t)pw * nrows;  // samples per plane held by the caller
 
     // geometry for every tile of the shard, arena offsets, block table
     const uint32_t ntiles = te - tb;
@@ -737,8 +746,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         Tile &tile = tiles[t];
         tile.index = tb + t;
         tile.r = tile_rect(cp, tile.index);
-        if (tile.r.y0 - cp.image.y0 < row0 || tile.r.y1 - cp.image.y0 > row0 + nrows)
-            return set_err(GRKGPU_EINVAL, "a tile of the range lies outside the rows given");
+        if (tile.r.y0 - cp.image.y0 < row0 || tile.r.y1 - cp.image.y0 > row0 + nrows ||
+            tile.r.x0 - cp.image.x0 < col0 || tile.r.x1 - cp.image.x0 > col0 + ncols)
+            return set_err(GRKGPU_EINVAL, "a tile of the range lies outside the rows / columns given");
         tile.comps.resize(nc);
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
@@ -847,19 +857,19 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, false);
             if (!fuse || dplan.levels.empty() || dplan.levels[0].size() == before) continue;
             DwtJob &j = dplan.levels[0].back();
-            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0);
+            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * pw + (tile.r.x0 - cp.image.x0 - col0);
             const bool mct3 = cp.mct && nc >= 3 && k < 3;
             for (uint32_t i = 0; i < 3; ++i) {
                 const uint32_t pk = mct3 ? i : k;
                 j.src[i] = src_at(pk, org);
                 j.shift[i] = cp.shift[pk];
             }
-            j.src_stride = iw;
+            j.src_stride = pw;
             j.src_bytes = (uint32_t)std::min<uint64_t>((plane - org) * sb, 0xffffffffu);
             j.src_fmt = fmt;
             j.mct_mode = mct3 ? (cp.irrev ? 3 : 2) : 1;
             j.comp = (int32_t)k;
-            bool al = (iw & 1) == 0;
+            bool al = (pw & 1) == 0;
             for (uint32_t i = 0; i < 3; ++i) al = al && ((uintptr_t)j.src[i] & (2 * sb - 1)) == 0;
             j.src_vec = al ? 1 : 0;
         }
@@ -870,10 +880,10 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         SrcPlanes tsrc{};
         PlanePtrs tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
-            tsrc.p[k] = src_at(k, (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * iw + (tile.r.x0 - cp.image.x0));
+            tsrc.p[k] = src_at(k, (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * pw + (tile.r.x0 - cp.image.x0 - col0));
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
-        HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, iw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+        HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, false, s));
@@ -981,10 +991,15 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             o.numbps = cst[i].numbps;
             o.numpasses = cst[i].numpasses;
             o.len = res[i].len;
+            o.stepsize = bi.stepsize;
             o.data = c->h_slab.as<uint8_t>() + eb[i].out_off;
             o.rate = c->bexp_rate.data() + cst[i].pass0;
             o.distortion = c->bexp_dist.data() + cst[i].pass0;
         }
+        c->bexp_coef.clear();
+        for (auto &tile : tiles)
+            for (uint32_t k = 0; k < nc; ++k)
+                c->bexp_coef.push_back({tile.index, k, tile.comps[k].r.w(), tile.comps[k].r.h(), tile.comps[k].arena_off});
         grkgpu_stats &st0 = c->stats;
         memset(&st0, 0, sizeof(st0));
         hipEventElapsedTime(&st0.h2d_ms, c->ev[0], c->ev[1]);
@@ -1210,8 +1225,9 @@ extern "C" int grkgpu_compress_ex(grkgpu_ctx *c, const grkgpu_image_desc *img, c
                                   const uint8_t **out, size_t *outlen) {
     if (!in || !out || !outlen) return set_err(GRKGPU_EINVAL, "null argument");
     if (in->nrows == 0 && in->row0) return set_err(GRKGPU_EINVAL, "row0 without nrows");
+    if (in->ncols == 0 && in->col0) return set_err(GRKGPU_EINVAL, "col0 without ncols");
     return compress_impl(c, img, p, in->planes, in->on_device, (int32_t)in->sample_fmt, out, outlen, tile_begin,
-                         tile_end, parts, false, 0, in->row0, in->nrows);
+                         tile_end, parts, false, 0, in->row0, in->nrows, in->col0, in->ncols);
 }
 
 extern "C" int grkgpu_encode_blocks(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkgpu_cparams *p,
@@ -1224,6 +1240,21 @@ extern "C" int grkgpu_encode_blocks(grkgpu_ctx *c, const grkgpu_image_desc *img,
     *blocks = c->bexp.data();
     *nblocks = (uint32_t)c->bexp.size();
     return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_encode_blocks_coefficients(grkgpu_ctx *c, uint32_t tileno, uint32_t compno, int32_t *dst,
+                                                  uint32_t dst_stride) {
+    if (!c || !dst) return set_err(GRKGPU_EINVAL, "null argument");
+    for (const auto &r : c->bexp_coef) {
+        if (r.tileno != tileno || r.compno != compno) continue;
+        if (dst_stride < r.w) return set_err(GRKGPU_EINVAL, "dst_stride below the tile-component width");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipMemcpy2DAsync(dst, (size_t)dst_stride * 4, c->coef.as<int32_t>() + r.off, (size_t)r.w * 4,
+                                (size_t)r.w * 4, r.h, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return GRKGPU_OK;
+    }
+    return set_err(GRKGPU_EINVAL, "no such tile-component in the last grkgpu_encode_blocks call");
 }
 
 extern "C" int grkgpu_num_tiles(const grkgpu_image_desc *img, const grkgpu_cparams *p, uint32_t *ntiles) {

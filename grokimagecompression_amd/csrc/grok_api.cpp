@@ -190,9 +190,29 @@ struct Codec {
     grkgpu_header_info hinfo{};
     bool window = false;
     uint32_t win[4] = {0, 0, 0, 0};
+    // tile streaming, encode (grk_write_tile): next tile expected, parts written
+    uint32_t next_tile = 0;
+    bool header_written = false, eoc_written = false;
+    // tile streaming, decode (grk_read_tile_header / grk_decode_tile_data)
+    std::vector<uint32_t> tile_order;  // tiles in codestream order (first tile-part), meeting the decode area
+    bool tile_order_ready = false;
+    size_t tile_pos = 0;
+    int64_t cur_tile = -1;
+    std::vector<int32_t> reduced;  // reduced-resolution decode of the whole image (cp_reduce > 0), decoded once
+    grkgpu_image_desc reduced_desc{};
 };
 
 uint32_t cdivpow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); }
+
+struct TileRect { uint32_t x0, y0, x1, y1; };
+// tile t of the grid (j2k tile geometry: tile (p, q) spans tx0 + p tdx .. clipped to the image)
+TileRect tile_rect(uint32_t t, uint32_t tw, uint32_t tx0, uint32_t ty0, uint32_t tdx, uint32_t tdy,
+                   const grkgpu_image_desc &d) {
+    const uint32_t p = t % tw, q = t / tw;
+    return {std::max(d.x0, tx0 + p * tdx), std::max(d.y0, ty0 + q * tdy),
+            (uint32_t)std::min<uint64_t>(d.x1, (uint64_t)tx0 + (uint64_t)(p + 1) * tdx),
+            (uint32_t)std::min<uint64_t>(d.y1, (uint64_t)ty0 + (uint64_t)(q + 1) * tdy)};
+}
 
 // grk_cparameters -> grkgpu_cparams (j2k_setup_encoder's reading of them,
 // codestream/j2k.cpp:1609-2050); false for options outside grk_mi355x.h
@@ -608,14 +628,170 @@ GRK_EXPORT bool grk_get_decoded_tile(grk_codec *codec, grk_image *image, uint16_
 
 GRK_EXPORT bool grk_end_decompress(grk_codec *codec) { return codec && ((Codec *)codec)->decompressor; }
 
-GRK_EXPORT bool grk_read_tile_header(grk_codec *, uint16_t *, uint64_t *, uint32_t *, uint32_t *, uint32_t *,
-                                     uint32_t *, uint32_t *, bool *) {
-    GRK_ERROR("tile-by-tile decoding (grk_read_tile_header) is not provided; use grk_decode or grk_get_decoded_tile");
-    return false;
+// Tile order of the codestream: the tile of each first tile-part, in stream
+// order (j2k_read_tile_header reads SOT after SOT, j2k.cpp:627-960), from the
+// first SOT after the main header, following Psot (0: to the end).
+static std::vector<uint32_t> stream_tile_order(const std::vector<uint8_t> &cs, uint32_t ntiles) {
+    std::vector<uint32_t> order;
+    std::vector<uint8_t> seen(ntiles, 0);
+    auto rd16 = [&](size_t p) { return (uint32_t)cs[p] << 8 | cs[p + 1]; };
+    size_t pos = 2;  // after SOC
+    while (pos + 4 <= cs.size() && rd16(pos) != 0xFF90) pos += 2 + rd16(pos + 2);
+    while (pos + 12 <= cs.size() && rd16(pos) == 0xFF90) {
+        const uint32_t isot = rd16(pos + 4);
+        const uint32_t psot = rd16(pos + 6) << 16 | rd16(pos + 8);
+        if (isot < ntiles && !seen[isot]) {
+            seen[isot] = 1;
+            order.push_back(isot);
+        }
+        if (!psot) break;
+        pos += psot;
+    }
+    return order;
 }
-GRK_EXPORT bool grk_decode_tile_data(grk_codec *, uint16_t, uint8_t *, uint64_t) {
-    GRK_ERROR("tile-by-tile decoding (grk_decode_tile_data) is not provided");
-    return false;
+
+// the decoded rectangle of tile t: its extent at the decoded resolution
+// (TileComponent.cpp:560-582 reduced_image_dim), clipped to the decode area
+// when `clip` -- the area only selects tiles: the reference still sizes and
+// fills the whole reduced tile (get_tile_size(true) with a decode area set
+// reports the full tile, tests/golden/tiles.json)
+static TileRect tile_decoded_rect(const Codec *c, uint32_t t, bool clip) {
+    const grkgpu_header_info &h = c->hinfo;
+    const TileRect tr = tile_rect(t, h.tw, h.tx0, h.ty0, h.tdx, h.tdy, c->desc);
+    const uint32_t r = c->dparams.cp_reduce;
+    TileRect o{cdivpow2(tr.x0, r), cdivpow2(tr.y0, r), cdivpow2(tr.x1, r), cdivpow2(tr.y1, r)};
+    if (clip && c->window) {
+        o.x0 = std::max(o.x0, c->win[0]); o.y0 = std::max(o.y0, c->win[1]);
+        o.x1 = std::min(o.x1, c->win[2]); o.y1 = std::min(o.y1, c->win[3]);
+        if (o.x1 < o.x0) o.x1 = o.x0;
+        if (o.y1 < o.y0) o.y1 = o.y0;
+    }
+    return o;
+}
+
+static uint64_t tile_data_bytes(const Codec *c, const TileRect &o) {
+    uint64_t n = 0;
+    for (uint32_t k = 0; k < c->desc.numcomps; ++k)
+        n += (uint64_t)((c->desc.prec[k] + 7) >> 3) * (o.x1 - o.x0) * (o.y1 - o.y0);
+    return n;
+}
+
+// grk_read_tile_header (grok.cpp:408-423, j2k.cpp:627-960): the next tile of
+// the codestream (tiles that miss the decode area are stepped over), its
+// rectangle, component count and the bytes grk_decode_tile_data writes
+// (TileProcessor::get_tile_size(true), TileProcessor.cpp:1435-1447);
+// *go_on = false once the codestream has no tile left.
+GRK_EXPORT bool grk_read_tile_header(grk_codec *codec, uint16_t *tile_index, uint64_t *data_size, uint32_t *x0,
+                                     uint32_t *y0, uint32_t *x1, uint32_t *y1, uint32_t *nb_comps, bool *go_on) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header || !tile_index || !data_size) return false;
+    const grkgpu_header_info &h = c->hinfo;
+    if (!c->tile_order_ready) {
+        for (uint32_t t : stream_tile_order(c->cs, h.tw * h.th)) {
+            const TileRect o = tile_decoded_rect(c, t, true);
+            if (o.x1 > o.x0 && o.y1 > o.y0) c->tile_order.push_back(t);
+        }
+        c->tile_order_ready = true;
+        c->tile_pos = 0;
+    }
+    if (c->tile_pos >= c->tile_order.size()) {
+        if (go_on) *go_on = false;
+        c->cur_tile = -1;
+        return true;
+    }
+    const uint32_t t = c->tile_order[c->tile_pos++];
+    const TileRect tr = tile_rect(t, h.tw, h.tx0, h.ty0, h.tdx, h.tdy, c->desc);
+    c->cur_tile = t;
+    *tile_index = (uint16_t)t;
+    *data_size = tile_data_bytes(c, tile_decoded_rect(c, t, false));
+    if (x0) *x0 = tr.x0;
+    if (y0) *y0 = tr.y0;
+    if (x1) *x1 = tr.x1;
+    if (y1) *y1 = tr.y1;
+    if (nb_comps) *nb_comps = c->desc.numcomps;
+    if (go_on) *go_on = true;
+    return true;
+}
+
+// grk_decode_tile_data (grok.cpp:425-440, j2k.cpp:979-1060): the tile read
+// by grk_read_tile_header, decoded into data as TileProcessor::update_tile_data
+// lays it out (TileProcessor.cpp:1201-1258): planar components, 1 or 2 bytes
+// per sample by precision (signed: the value, unsigned: masked).  At full
+// resolution the tile is a window decode of its rectangle (only its
+// code-blocks); at a reduced resolution the image is decoded once and each
+// tile cropped from it.  With a decode area set, the whole tile is decoded:
+// the reference's samples there are not the tile's (most code-blocks come out
+// as zero coefficients -- a reference defect, DESIGN.md "Tile streaming"), so
+// parity is pinned on the reference's decode without an area, which equals
+// its grk_get_decoded_tile.
+GRK_EXPORT bool grk_decode_tile_data(grk_codec *codec, uint16_t tile_index, uint8_t *data, uint64_t data_size) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !data || c->cur_tile != (int64_t)tile_index) return false;
+    const TileRect o = tile_decoded_rect(c, tile_index, false);
+    const uint64_t need = tile_data_bytes(c, o);
+    if (need > data_size) return false;
+    const uint32_t w = o.x1 - o.x0, h = o.y1 - o.y0, nc = c->desc.numcomps;
+    std::vector<int32_t> buf;
+    const int32_t *src;
+    uint32_t sstride, sx0 = 0, sy0 = 0;
+    uint64_t splane;
+    {
+        Lease lease(0);
+        if (!lease.ctx) return false;
+        if (c->dparams.cp_reduce == 0) {
+            buf.resize((size_t)w * h * nc);
+            std::vector<int32_t *> planes(nc);
+            for (uint32_t k = 0; k < nc; ++k) planes[k] = buf.data() + (size_t)k * w * h;
+            grkgpu_dparams dp{0, c->dparams.cp_layer, o.x0, o.y0, o.x1, o.y1};
+            if (grkgpu_decompress_ex(lease.ctx, c->cs.data(), c->cs.size(), &dp, nullptr, planes.data(), 0)) {
+                GRK_ERROR("%s", grkgpu_last_error());
+                return false;
+            }
+            src = buf.data();
+            sstride = w;
+            splane = (uint64_t)w * h;
+        } else {
+            if (c->reduced.empty()) {
+                grkgpu_image_desc d{};
+                grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
+                const uint32_t r = c->dparams.cp_reduce;
+                const uint32_t rw = cdivpow2(c->desc.x1, r) - cdivpow2(c->desc.x0, r);
+                const uint32_t rh = cdivpow2(c->desc.y1, r) - cdivpow2(c->desc.y0, r);
+                c->reduced.resize((size_t)rw * rh * nc);
+                std::vector<int32_t *> planes(nc);
+                for (uint32_t k = 0; k < nc; ++k) planes[k] = c->reduced.data() + (size_t)k * rw * rh;
+                if (grkgpu_decompress_ex(lease.ctx, c->cs.data(), c->cs.size(), &dp, &d, planes.data(), 0)) {
+                    GRK_ERROR("%s", grkgpu_last_error());
+                    c->reduced.clear();
+                    return false;
+                }
+                c->reduced_desc = d;
+            }
+            const grkgpu_image_desc &d = c->reduced_desc;
+            src = c->reduced.data();
+            sstride = d.x1 - d.x0;
+            splane = (uint64_t)sstride * (d.y1 - d.y0);
+            sx0 = o.x0 - d.x0;
+            sy0 = o.y0 - d.y0;
+        }
+    }
+    uint8_t *dst = data;
+    for (uint32_t k = 0; k < nc; ++k) {
+        const uint32_t sz = (c->desc.prec[k] + 7) >> 3;
+        const bool sg = c->desc.sgnd[k] != 0;
+        const int32_t *p = src + splane * k + (uint64_t)sy0 * sstride + sx0;
+        for (uint32_t y = 0; y < h; ++y, p += sstride)
+            for (uint32_t x = 0; x < w; ++x) {
+                const int32_t v = p[x];
+                if (sz == 1) *dst++ = (uint8_t)(sg ? (int8_t)v : (int8_t)(v & 0xff));
+                else {
+                    const uint16_t u = (uint16_t)(sg ? (int16_t)v : (int16_t)(v & 0xffff));
+                    memcpy(dst, &u, 2);
+                    dst += 2;
+                }
+            }
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -686,11 +862,102 @@ GRK_EXPORT bool grk_encode_with_plugin(grk_codec *codec, grk_plugin_tile *tile) 
 
 GRK_EXPORT bool grk_encode(grk_codec *codec) { return grk_encode_with_plugin(codec, nullptr); }
 
-GRK_EXPORT bool grk_end_compress(grk_codec *codec) { return codec && !((Codec *)codec)->decompressor; }
+// grk_end_compress: after tile streaming, the EOC (j2k_end_encoding,
+// j2k.cpp:2234-2247; a single-tile stream was finished by its write_tile)
+GRK_EXPORT bool grk_end_compress(grk_codec *codec) {
+    Codec *c = (Codec *)codec;
+    if (!c || c->decompressor) return false;
+    if (c->header_written && !c->eoc_written) {
+        const uint8_t eoc[2] = {0xFF, 0xD9};
+        if (!c->stream->write_all(eoc, 2)) { GRK_ERROR("stream write failed"); return false; }
+        c->eoc_written = true;
+    }
+    return true;
+}
 
-GRK_EXPORT bool grk_write_tile(grk_codec *, uint16_t, uint8_t *, uint64_t) {
-    GRK_ERROR("tile-by-tile encoding (grk_write_tile) is not provided; use grk_encode");
-    return false;
+// grk_write_tile (grok.cpp:631-645, j2k.cpp:2763-2795): tile tile_index's
+// samples -- planar components, tile width x height each, 1 or 2 bytes per
+// sample by precision (TileProcessor::copy_image_data_to_tile,
+// TileProcessor.cpp:1923-1972) -- encoded on the GPU and its tile-parts
+// written to the stream; tiles in order 0 .. n-1.  The main header goes out
+// with the first tile (it is the same for every tile), the EOC at
+// grk_end_compress; a single-tile image is coded whole by its one
+// write_tile (its TLM, for the cinema profiles, needs the tile-part lengths).
+GRK_EXPORT bool grk_write_tile(grk_codec *codec, uint16_t tile_index, uint8_t *data, uint64_t data_size) {
+    Codec *c = (Codec *)codec;
+    if (!c || c->decompressor || !c->setup || !c->image || !data) return false;
+    grk_image *img = c->image;
+    grkgpu_image_desc d{};
+    if (!img->comps || !img->numcomps || img->numcomps > GRKGPU_MAX_COMPS) return false;
+    d.x0 = img->x0; d.y0 = img->y0; d.x1 = img->x1; d.y1 = img->y1;
+    d.numcomps = img->numcomps;
+    for (uint32_t k = 0; k < img->numcomps; ++k) {
+        if (img->comps[k].dx != 1 || img->comps[k].dy != 1) { GRK_ERROR("subsampling is not supported"); return false; }
+        d.prec[k] = img->comps[k].prec;
+        d.sgnd[k] = (int32_t)img->comps[k].sgnd;
+    }
+    grkgpu_cparams p;
+    if (!map_cparams(&c->cparams, d.numcomps, &p)) return false;
+    uint32_t ntiles = 0;
+    if (grkgpu_num_tiles(&d, &p, &ntiles)) { GRK_ERROR("%s", grkgpu_last_error()); return false; }
+    if (tile_index != c->next_tile || tile_index >= ntiles) {
+        GRK_ERROR("tiles must be written in order: expected tile %u, got %u", c->next_tile, tile_index);
+        return false;
+    }
+    // one sample width and signedness for all components (what grkgpu_planes carries)
+    const uint32_t sz = (d.prec[0] + 7) >> 3;
+    for (uint32_t k = 1; k < d.numcomps; ++k)
+        if (((d.prec[k] + 7) >> 3) != sz || d.sgnd[k] != d.sgnd[0]) {
+            GRK_ERROR("components of different sample sizes are not supported by grk_write_tile");
+            return false;
+        }
+    if (sz > 2) { GRK_ERROR("precision above 16 bits"); return false; }
+    const uint32_t tdx = p.tile_size_on ? p.cp_tdx : d.x1 - p.cp_tx0, tdy = p.tile_size_on ? p.cp_tdy : d.y1 - p.cp_ty0;
+    const uint32_t tw = (uint32_t)(((uint64_t)d.x1 - p.cp_tx0 + tdx - 1) / tdx);
+    const TileRect tr = tile_rect(tile_index, tw, p.cp_tx0, p.cp_ty0, tdx, tdy, d);
+    const uint64_t area = (uint64_t)(tr.x1 - tr.x0) * (tr.y1 - tr.y0);
+    if (area * sz * d.numcomps != data_size) {
+        GRK_ERROR("Size mismatch between tile data and sent data.");
+        return false;
+    }
+    grkgpu_planes pl{};
+    for (uint32_t k = 0; k < d.numcomps; ++k) pl.planes[k] = data + area * sz * k;
+    pl.sample_fmt = sz == 1 ? (d.sgnd[0] ? GRKGPU_SAMPLE_I8 : GRKGPU_SAMPLE_U8)
+                            : (d.sgnd[0] ? GRKGPU_SAMPLE_I16 : GRKGPU_SAMPLE_U16);
+    pl.on_device = 0;
+    pl.row0 = tr.y0 - d.y0;
+    pl.nrows = tr.y1 - tr.y0;
+    pl.col0 = tr.x0 - d.x0;
+    pl.ncols = tr.x1 - tr.x0;
+    Lease lease(c->cparams.deviceId);
+    if (!lease.ctx) return false;
+    const uint8_t *out = nullptr;
+    size_t len = 0;
+    if (ntiles == 1) {
+        if (grkgpu_compress_ex(lease.ctx, &d, &p, &pl, 0, 1, GRKGPU_PART_ALL, &out, &len)) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
+        c->header_written = c->eoc_written = true;
+    } else {
+        if (!c->header_written) {
+            grkgpu_planes none{};
+            none.on_device = 1;  // no samples are read for the header alone
+            if (grkgpu_compress_ex(lease.ctx, &d, &p, &none, 0, 0, GRKGPU_PART_HEADER, &out, &len)) {
+                GRK_ERROR("%s", grkgpu_last_error());
+                return false;
+            }
+            if (!c->stream->write_all(out, len)) { GRK_ERROR("stream write failed"); return false; }
+            c->header_written = true;
+        }
+        if (grkgpu_compress_ex(lease.ctx, &d, &p, &pl, tile_index, tile_index + 1u, GRKGPU_PART_TILES, &out, &len)) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
+    }
+    if (!c->stream->write_all(out, len)) { GRK_ERROR("stream write failed"); return false; }
+    ++c->next_tile;
+    return true;
 }
 
 GRK_EXPORT bool grk_set_MCT(grk_cparameters *, float *, int32_t *, uint32_t) {

@@ -1,0 +1,126 @@
+// host_pool.h -- a small worker pool for the host-side loops of the encoder
+// (rate control, Tier-2 simulation): the reference runs its PCRD bisection
+// serially on one thread per tile (TileProcessor.cpp:371-667); here each
+// bisection step's per-code-block and per-precinct work is spread over the
+// host cores, so rate control stays off the critical path of a frame whose
+// Tier-1 took a few ms on the GPU.  One process-wide pool; the calling thread
+// works on its own loop too, so concurrent callers (frames in flight on other
+// threads) never wait for an idle worker.
+#pragma once
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace grkgpu {
+
+class HostPool {
+public:
+    static HostPool &get() {
+        static HostPool p;
+        return p;
+    }
+
+    size_t workers() const { return threads_.size(); }
+
+    // f(begin, end) over [0, n) in chunks of `grain` items, on the pool and
+    // the caller; returns when every chunk has run.  The chunks are disjoint,
+    // so f may write per-item results without synchronisation.
+    void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)> &f) {
+        if (!n) return;
+        grain = std::max<size_t>(grain, 1);
+        const size_t nchunks = (n + grain - 1) / grain;
+        if (nchunks == 1 || threads_.empty()) {
+            f(0, n);
+            return;
+        }
+        Job j;
+        j.f = &f;
+        j.n = n;
+        j.grain = grain;
+        j.nchunks = nchunks;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(&j);
+        }
+        cv_.notify_all();
+        run(j);
+        // leave the queue, then wait for the workers still inside this job
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            auto it = std::find(q_.begin(), q_.end(), &j);
+            if (it != q_.end()) q_.erase(it);
+            done_cv_.wait(lk, [&] { return j.users == 0 && j.done.load() == j.nchunks; });
+        }
+    }
+
+private:
+    struct Job {
+        const std::function<void(size_t, size_t)> *f = nullptr;
+        size_t n = 0, grain = 1, nchunks = 0;
+        std::atomic<size_t> next{0}, done{0};
+        int users = 0;  // workers inside the job (guarded by mu_)
+    };
+
+    HostPool() {
+        // GRKGPU_HOST_THREADS caps the pool (default: the machine's cores, at
+        // most 16 -- a GPU box grants 16 host cores per GPU)
+        size_t n = std::thread::hardware_concurrency();
+        if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = (size_t)atoi(e);
+        n = std::min<size_t>(n ? n : 1, 16);
+        for (size_t i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : threads_) t.join();
+    }
+
+    void run(Job &j) {
+        size_t c;
+        while ((c = j.next.fetch_add(1)) < j.nchunks) {
+            const size_t b = c * j.grain;
+            (*j.f)(b, std::min(j.n, b + j.grain));
+            j.done.fetch_add(1);
+        }
+    }
+
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (stop_) return;
+            Job *j = q_.front();
+            if (j->next.load() >= j->nchunks) {  // exhausted: drop it, its caller finishes it
+                q_.pop_front();
+                continue;
+            }
+            ++j->users;
+            lk.unlock();
+            run(*j);
+            lk.lock();
+            if (--j->users == 0) done_cv_.notify_all();
+        }
+    }
+
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job *> q_;
+    std::vector<std::thread> threads_;
+    bool stop_ = false;
+};
+
+inline void host_parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)> &f) {
+    HostPool::get().parallel_for(n, grain, f);
+}
+
+}  // namespace grkgpu

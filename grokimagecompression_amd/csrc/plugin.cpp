@@ -15,14 +15,18 @@
 #include "../../include/grk_plugin_abi.h"
 #include "../../include/grk_mi355x.h"
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #define PLUGIN_API __attribute__((visibility("default")))
@@ -31,8 +35,20 @@ namespace {
 std::mutex g_mu;
 grkgpu_ctx *g_ctx = nullptr;  // one GPU context per loaded plugin (grok's plugin manager is a global too)
 bool g_verbose = false;
+int32_t g_device = 0;  // grk_plugin_init_info.deviceId: -1 = every device (grok.h:1816-1821)
+// The host-vs-accelerator parity harness of the reference (grok.h:1790-1808,
+// plugin_get_debug_state): with GRK_PLUGIN_STATE_DEBUG the host runs its own
+// Tier-1 on the coefficients the plugin hands over as image data and checks
+// every block of the plugin against it (plugin_bridge.cpp:144-258: pass
+// counts, bytes, rates, distortion within 1 %), warning on any difference.
+// A diagnostic state, chosen when the plugin is initialised:
+// GRKGPU_PLUGIN_DEBUG_STATE=<state bits> in the environment (0 / unset:
+// production, GRK_PLUGIN_STATE_NO_DEBUG).  Only the DEBUG bit is offered.
+uint32_t g_debug_state = GRK_PLUGIN_STATE_NO_DEBUG;
 
+void batch_end();
 int32_t exit_plugin(void) {
+    batch_end();  // a batch still running when the host unloads the plugin
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx) grkgpu_destroy(g_ctx);
     g_ctx = nullptr;
@@ -222,6 +238,7 @@ bool build_tree(const grkgpu_block_info *b, uint32_t n, uint32_t numcomps, uint3
                 grk_plugin_band *B = T.bands.back().get();
                 B->orient = r == 0 ? 0 : bi + 1;
                 B->numPrecincts = nprec[k][r][bi];
+                B->stepsize = 0.0f;  // the band's step size, from its blocks below
                 T.band_ptrs.back()[bi] = B;
                 T.prec_ptrs.emplace_back(B->numPrecincts);
                 for (uint32_t q = 0; q < B->numPrecincts; ++q) {
@@ -258,6 +275,7 @@ bool build_tree(const grkgpu_block_info *b, uint32_t n, uint32_t numcomps, uint3
         }
         const uint32_t bi = s.resno == 0 ? 0 : s.bandno - 1;
         precp[s.compno][s.resno][bi][s.precno]->blocks[s.cblkno] = &o;
+        T.res[s.compno][s.resno].bands[bi]->stepsize = s.stepsize;
     }
     T.tile.decode_flags = 0;
     T.tile.numComponents = numcomps;
@@ -299,40 +317,51 @@ PLUGIN_API minpf_exit_func minpf_post_load_plugin(const char *, const minpf_plat
 PLUGIN_API bool plugin_init(grk_plugin_init_info info) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_verbose = info.verbose;
+    const char *ds = getenv("GRKGPU_PLUGIN_DEBUG_STATE");
+    g_debug_state = ds && *ds ? (uint32_t)strtoul(ds, nullptr, 0) & GRK_PLUGIN_STATE_DEBUG : GRK_PLUGIN_STATE_NO_DEBUG;
+    g_device = info.deviceId;
     if (g_ctx) return true;
     return grkgpu_create(info.deviceId < 0 ? 0 : info.deviceId, &g_ctx) == GRKGPU_OK;
 }
 
-PLUGIN_API uint32_t plugin_get_debug_state(void) { return GRK_PLUGIN_STATE_NO_DEBUG; }
+PLUGIN_API uint32_t plugin_get_debug_state(void) { return g_debug_state; }
 
-// grk_plugin_encode (grok.cpp:917-935).  -1 = not handled (the host then runs
-// its CPU path, grk_compress.cpp:2206-2222).
-PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CALLBACK cb) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx || !params || !cb) return -1;
+}  // extern "C"
+
+namespace {
+
+// The coding options the plugin route cannot take (the host then encodes on
+// its CPU path), or nullptr.
+const char *encode_decline(const grkp_cparameters *params) {
+    // A single layer without rate control is formed by the host's
+    // make_single_lossless_layer BEFORE the loop that copies the plugin's
+    // passes in (TileProcessor.cpp:521 vs :537, :374 vs :404), so the host
+    // would write an empty layer: decline, the host encodes on its CPU path.
+    if (params->tcp_numlayers <= 1 && !layer_rc(params, 0))
+        return "single lossless layer: the host forms it before taking the plugin's passes; declined";
+    // Fixed quality (-q) targets tile->distotile, which only the host's own
+    // T1 accumulates (T1Encoder.cpp:51); with a plugin tile it stays 0 and
+    // the PSNR search degenerates (TileProcessor.cpp:611-635): decline.
+    if (params->cp_fixed_quality) return "fixed-quality layers need the host's own T1 distortion total; declined";
+    grkgpu_cparams p;
+    if (!map_params(params, 3, &p)) return "coding options outside the plugin's path";
+    return nullptr;
+}
+
+// One image file through the GPU (DC shift .. T1 + distortion), then the
+// host's callback with the plugin tile (grok.cpp:905-918).  outname /
+// relative: what the callback receives as the output file (batch: the input's
+// bare file name, relative to the output directory, grk_compress.cpp:1783-1797).
+int32_t encode_file(grkgpu_ctx *ctx, grkp_cparameters *params, const char *path, const char *outname, bool relative,
+                    PLUGIN_ENCODE_USER_CALLBACK cb) {
     auto create = (ImageCreate)dlsym(RTLD_DEFAULT, "grk_image_create");
     auto destroy = (ImageDestroy)dlsym(RTLD_DEFAULT, "grk_image_destroy");
     if (!create || !destroy) {
         log("host grk_image_create not found");
         return -1;
     }
-    // A single layer without rate control is formed by the host's
-    // make_single_lossless_layer BEFORE the loop that copies the plugin's
-    // passes in (TileProcessor.cpp:521 vs :537, :374 vs :404), so the host
-    // would write an empty layer: decline, the host encodes on its CPU path.
-    if (params->tcp_numlayers <= 1 && !layer_rc(params, 0)) {
-        log("single lossless layer: the host forms it before taking the plugin's passes; declined");
-        return -1;
-    }
-    // Fixed quality (-q) targets tile->distotile, which only the host's own
-    // T1 accumulates (T1Encoder.cpp:51); with a plugin tile it stays 0 and
-    // the PSNR search degenerates (TileProcessor.cpp:611-635): decline.
-    if (params->cp_fixed_quality) {
-        log("fixed-quality layers need the host's own T1 distortion total; declined");
-        return -1;
-    }
     Pnm pnm;
-    if (!read_pnm(params->infile, pnm)) {
+    if (!read_pnm(path, pnm)) {
         log("input is not a binary PGM / PPM");
         return -1;
     }
@@ -353,7 +382,7 @@ PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CA
     for (uint32_t k = 0; k < pnm.c; ++k) planes[k] = pnm.planes.data() + k * area;
     const grkgpu_block_info *blocks = nullptr;
     uint32_t nblocks = 0;
-    if (grkgpu_encode_blocks(g_ctx, &d, &p, planes.data(), 0, needs_distortion(params) ? 1 : 0, &blocks, &nblocks)) {
+    if (grkgpu_encode_blocks(ctx, &d, &p, planes.data(), 0, needs_distortion(params) ? 1 : 0, &blocks, &nblocks)) {
         log(grkgpu_last_error());
         return -1;
     }
@@ -372,12 +401,25 @@ PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CA
     grkp_image *img = create(pnm.c, cm.data(), pnm.c >= 3 ? 2 /* sRGB */ : 3 /* gray */);
     if (!img) return -1;
     img->x0 = d.x0; img->y0 = d.y0; img->x1 = d.x1; img->y1 = d.y1;
-    for (uint32_t k = 0; k < pnm.c; ++k)
-        if (img->comps[k].data) memcpy(img->comps[k].data, planes[k], area * 4);
+    for (uint32_t k = 0; k < pnm.c; ++k) {
+        if (!img->comps[k].data) continue;
+        if (g_debug_state & GRK_PLUGIN_STATE_DEBUG) {
+            // debug: the image data is the plugin's DWT output, so the host's
+            // own T1 starts from the same coefficients (TileProcessor.cpp:
+            // 988-1012 skips its DC shift, MCT and DWT in this state)
+            if (grkgpu_encode_blocks_coefficients(ctx, 0, k, img->comps[k].data, pnm.w)) {
+                log(grkgpu_last_error());
+                destroy(img);
+                return -1;
+            }
+        } else {
+            memcpy(img->comps[k].data, planes[k], area * 4);
+        }
+    }
     plugin_encode_user_callback_info info{};
-    info.input_file_name = params->infile;
-    info.outputFileNameIsRelative = false;
-    info.output_file_name = params->outfile;
+    info.input_file_name = path;
+    info.outputFileNameIsRelative = relative;
+    info.output_file_name = outname;
     info.encoder_parameters = params;
     info.image = img;
     info.tile = &T.tile;
@@ -386,35 +428,136 @@ PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CA
     return info.error_code ? -1 : 0;
 }
 
-PLUGIN_API int32_t plugin_batch_encode(const char *, const char *, grkp_cparameters *, PLUGIN_ENCODE_USER_CALLBACK) {
-    return -1;
+// ---- batch route (grk_compress / grk_decompress with -ImgDir / -OutDir,
+// grk_compress.cpp:2224-2243, grk_decompress.cpp:1237-1262) ----
+// The plugin walks the input directory itself: frames in flight on worker
+// threads, each with its own GPU context -- FRAMES_PER_DEVICE per device,
+// over every device for deviceId -1 (grok.h:1816-1821) -- so one frame's host
+// work (rate control, Tier-2, file output in the host's callback) overlaps
+// the others' GPU work.  The host polls plugin_is_batch_complete and ends the
+// batch with plugin_stop_batch_encode / _decode.
+constexpr int FRAMES_PER_DEVICE = 4;
+
+struct Batch {
+    bool decode = false;
+    std::vector<std::string> files;  // bare file names in the input directory
+    std::string in_dir, out_dir;
+    grkp_cparameters eparams{};
+    grkp_decompress_parameters dparams{};
+    PLUGIN_ENCODE_USER_CALLBACK ecb = nullptr;
+    PLUGIN_DECODE_USER_CALLBACK dcb = nullptr;
+    std::atomic<size_t> next{0};
+    std::atomic<bool> stop{false};
+    std::atomic<int> running{0};
+    std::vector<std::thread> workers;
+    std::vector<grkgpu_ctx *> ctxs;
+};
+std::mutex g_batch_mu;
+std::unique_ptr<Batch> g_batch;
+
+bool has_ext(const std::string &f, std::initializer_list<const char *> exts) {
+    const size_t dot = f.rfind('.');
+    if (dot == std::string::npos) return false;
+    std::string e = f.substr(dot + 1);
+    for (auto &ch : e) ch = (char)tolower(ch);
+    for (const char *x : exts)
+        if (e == x) return true;
+    return false;
 }
-PLUGIN_API bool plugin_is_batch_complete(void) { return true; }
-PLUGIN_API void plugin_stop_batch_encode(void) {}
-// grk_plugin_decode (grok.cpp:1031-1051), driven by grk_decompress's
-// plugin_main (grk_decompress.cpp:1186-1319) with its decode_callback
-// (:1336-1367).  The decode runs first, on the GPU, so that anything the
-// plugin cannot take (JP2 boxes, a single-tile request, a window at a reduced
-// resolution, a corrupt or unsupported stream) is declined with -1 before the
-// host has been called: the host then decodes on its CPU path.  Then:
+
+std::vector<std::string> list_dir(const char *dir, std::initializer_list<const char *> exts) {
+    std::vector<std::string> out;
+    DIR *d = opendir(dir);
+    if (!d) return out;
+    while (dirent *e = readdir(d)) {
+        const std::string n = e->d_name;
+        if (n != "." && n != ".." && has_ext(n, exts)) out.push_back(n);
+    }
+    closedir(d);
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
+std::string join_path(const std::string &dir, const std::string &name) {
+    return dir.empty() || dir.back() == '/' ? dir + name : dir + "/" + name;
+}
+
+int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const char *infile, const char *outfile,
+                    PLUGIN_DECODE_USER_CALLBACK cb);
+
+// the output file of a batch decode: <output dir>/<input stem>.<extension of
+// the requested format> (the host's post_decode writes parameters->outfile,
+// or this name when that is empty, grk_decompress.cpp:1577-1579)
+std::string decode_out_name(const Batch &b, const std::string &in) {
+    static const char *ext[] = {"", "j2k", "jp2", "ppm", "pgx", "bmp", "tif", "raw", "tga", "png", "rawl", "jpg"};
+    const uint32_t f = b.dparams.cod_format < 12 ? b.dparams.cod_format : 0;
+    const std::string stem = in.substr(0, in.find('.'));
+    return join_path(b.out_dir, stem + "." + (f ? ext[f] : "raw"));
+}
+
+void batch_worker(Batch *b, grkgpu_ctx *ctx) {
+    size_t k;
+    while (!b->stop.load() && (k = b->next.fetch_add(1)) < b->files.size()) {
+        const std::string in = join_path(b->in_dir, b->files[k]);
+        if (!b->decode) {
+            grkp_cparameters p = b->eparams;  // the host may adjust them per image (tcp_mct, ...)
+            snprintf(p.infile, sizeof(p.infile), "%s", in.c_str());
+            if (encode_file(ctx, &p, in.c_str(), b->files[k].c_str(), true, b->ecb)) log("batch: a frame failed");
+        } else {
+            grkp_decompress_parameters p = b->dparams;
+            p.infile[0] = p.outfile[0] = 0;  // per file: the callback's names
+            p.core.infile[0] = p.core.outfile[0] = 0;
+            const std::string out = decode_out_name(*b, b->files[k]);
+            if (decode_file(ctx, &p, in.c_str(), out.c_str(), b->dcb)) log("batch: a codestream failed");
+        }
+    }
+    b->running.fetch_sub(1);
+}
+
+// start the workers of a prepared batch; false if no GPU context could be made
+bool batch_start(Batch *b) {
+    std::vector<int> devs;
+    if (g_device < 0)
+        for (int d = 0; d < grkgpu_device_count(); ++d) devs.push_back(d);
+    else
+        devs.push_back(g_device);
+    for (int f = 0; f < FRAMES_PER_DEVICE; ++f)
+        for (int d : devs) {
+            grkgpu_ctx *c = nullptr;
+            if (grkgpu_create(d, &c) != GRKGPU_OK) continue;
+            b->ctxs.push_back(c);
+        }
+    if (b->ctxs.empty()) return false;
+    b->running = (int)b->ctxs.size();
+    for (auto *c : b->ctxs) b->workers.emplace_back(batch_worker, b, c);
+    return true;
+}
+
+void batch_end() {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    if (!g_batch) return;
+    g_batch->stop = true;
+    for (auto &t : g_batch->workers) t.join();
+    for (auto *c : g_batch->ctxs) grkgpu_destroy(c);
+    g_batch.reset();
+}
+
+// One codestream through the GPU decoder, then the host's callback protocol.
+// The decode runs first, on the GPU, so that anything the plugin cannot take
+// (JP2 boxes, a window at a reduced resolution, a corrupt or unsupported
+// stream) is declined with -1 before the host has been called: the host then
+// decodes on its CPU path.  Then:
 //   HEADER     the host reads the main header into its own grk_image;
 //   (plugin)   component geometry of the decoded region + the samples, in
 //              buffers of the host's allocator
 //              (grk_image_single_component_data_alloc);
 //   POST_T1    the host writes the output file (post_decode);
 //   CLEAN      the host releases stream, codec and image.
-PLUGIN_API int32_t plugin_decode(grkp_decompress_parameters *params, PLUGIN_DECODE_USER_CALLBACK cb) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx || !params || !cb) return -1;
+int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const char *infile, const char *outfile,
+                    PLUGIN_DECODE_USER_CALLBACK cb) {
     auto comp_alloc = (CompAlloc)dlsym(RTLD_DEFAULT, "grk_image_single_component_data_alloc");
     if (!comp_alloc) {
         log("host grk_image_single_component_data_alloc not found");
-        return -1;
-    }
-    const char *infile = params->infile[0] ? params->infile : params->core.infile;
-    const char *outfile = params->outfile[0] ? params->outfile : params->core.outfile;
-    if (params->nb_tile_to_decode) {
-        log("single-tile decode (grk_get_decoded_tile) not taken; declined");
         return -1;
     }
     std::vector<uint8_t> cs;
@@ -442,7 +585,7 @@ PLUGIN_API int32_t plugin_decode(grkp_decompress_parameters *params, PLUGIN_DECO
     std::vector<int32_t> samples((size_t)w * h * nc);
     std::vector<int32_t *> planes(nc);
     for (uint32_t k = 0; k < nc; ++k) planes[k] = samples.data() + (size_t)k * w * h;
-    if (grkgpu_decompress_ex(g_ctx, cs.data(), cs.size(), &dp, nullptr, planes.data(), 0)) {
+    if (grkgpu_decompress_ex(ctx, cs.data(), cs.size(), &dp, nullptr, planes.data(), 0)) {
         log(grkgpu_last_error());
         return -1;
     }
@@ -471,11 +614,111 @@ PLUGIN_API int32_t plugin_decode(grkp_decompress_parameters *params, PLUGIN_DECO
     cb(&info);
     return rc;
 }
-PLUGIN_API int32_t plugin_init_batch_decode(const char *, const char *, grkp_decompress_parameters *, void *) {
-    return -1;
+
+}  // namespace
+
+extern "C" {
+
+// grk_plugin_encode (grok.cpp:917-935).  -1 = not handled (the host then runs
+// its CPU path, grk_compress.cpp:2206-2222).
+PLUGIN_API int32_t plugin_encode(grkp_cparameters *params, PLUGIN_ENCODE_USER_CALLBACK cb) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx || !params || !cb) return -1;
+    if (const char *why = encode_decline(params)) {
+        log(why);
+        return -1;
+    }
+    return encode_file(g_ctx, params, params->infile, params->outfile, false, cb);
 }
-PLUGIN_API int32_t plugin_batch_decode(void) { return -1; }
-PLUGIN_API void plugin_stop_batch_decode(void) {}
+
+// grk_plugin_batch_encode (grok.cpp:938-955, grk_compress.cpp:2224-2243):
+// every PGM / PPM of input_dir, frames in flight over the plugin's devices;
+// the host's callback receives each input's bare file name as a relative
+// output name and writes output_dir/<name>.<format>.  0 = the batch started
+// (the host then polls plugin_is_batch_complete); -1 = not taken (options the
+// plugin declines, no input, a batch already running).
+PLUGIN_API int32_t plugin_batch_encode(const char *input_dir, const char *output_dir, grkp_cparameters *params,
+                                       PLUGIN_ENCODE_USER_CALLBACK cb) {
+    if (!input_dir || !output_dir || !params || !cb) return -1;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_ctx) return -1;
+    }
+    if (const char *why = encode_decline(params)) {
+        log(why);
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    if (g_batch) return -1;
+    auto b = std::make_unique<Batch>();
+    b->files = list_dir(input_dir, {"pgm", "ppm", "pnm"});
+    if (b->files.empty()) return -1;
+    b->in_dir = input_dir;
+    b->out_dir = output_dir;
+    b->eparams = *params;
+    b->ecb = cb;
+    if (!batch_start(b.get())) return -1;
+    g_batch = std::move(b);
+    return 0;
+}
+
+PLUGIN_API bool plugin_is_batch_complete(void) {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    return !g_batch || g_batch->running.load() == 0;
+}
+
+// the host's stop (after completion, or on a signal): pending frames are
+// dropped, frames in flight finish, the workers and their contexts go
+PLUGIN_API void plugin_stop_batch_encode(void) { batch_end(); }
+
+// grk_plugin_decode (grok.cpp:1031-1051), driven by grk_decompress's
+// plugin_main (grk_decompress.cpp:1186-1319) with its decode_callback
+// (:1336-1367); see decode_file.
+PLUGIN_API int32_t plugin_decode(grkp_decompress_parameters *params, PLUGIN_DECODE_USER_CALLBACK cb) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx || !params || !cb) return -1;
+    const char *infile = params->infile[0] ? params->infile : params->core.infile;
+    const char *outfile = params->outfile[0] ? params->outfile : params->core.outfile;
+    if (params->nb_tile_to_decode) {
+        log("single-tile decode (grk_get_decoded_tile) not taken; declined");
+        return -1;
+    }
+    return decode_file(g_ctx, params, infile, outfile, cb);
+}
+
+// grk_plugin_init_batch_decode (grok.cpp:1052-1072): remember the batch.  The
+// reference host starts it (grk_plugin_batch_decode) only when this returns
+// non-zero (grk_decompress.cpp:1242-1245), so success is 1 here.
+PLUGIN_API int32_t plugin_init_batch_decode(const char *input_dir, const char *output_dir,
+                                            grkp_decompress_parameters *params, void *cb) {
+    if (!input_dir || !output_dir || !params || !cb) return 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_ctx) return 0;
+    }
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    if (g_batch) return 0;
+    auto b = std::make_unique<Batch>();
+    b->decode = true;
+    b->files = list_dir(input_dir, {"j2k", "j2c"});
+    if (b->files.empty()) return 0;
+    b->in_dir = input_dir;
+    b->out_dir = output_dir;
+    b->dparams = *params;
+    b->dcb = (PLUGIN_DECODE_USER_CALLBACK)cb;
+    g_batch = std::move(b);
+    return 1;
+}
+
+// grk_plugin_batch_decode (grok.cpp:1074-1087): start the batch set up by
+// plugin_init_batch_decode; 0 = started.
+PLUGIN_API int32_t plugin_batch_decode(void) {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    if (!g_batch || !g_batch->decode || !g_batch->workers.empty()) return -1;
+    return batch_start(g_batch.get()) ? 0 : -1;
+}
+
+PLUGIN_API void plugin_stop_batch_decode(void) { batch_end(); }
 PLUGIN_API void plugin_debug_mqc_next_cxd(void *, uint32_t) {}
 PLUGIN_API void plugin_debug_next_cxd(void *, uint32_t) {}
 PLUGIN_API void plugin_debug_mqc_next_plane(void *) {}

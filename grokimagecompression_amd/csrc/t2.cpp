@@ -9,12 +9,15 @@
 // are the same.
 #include "t2.h"
 
+#include "host_pool.h"
+
 #include <float.h>
 #include <limits.h>
 #include <math.h>
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 
 namespace grkgpu {
 
@@ -705,6 +708,14 @@ bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ui
 // T2::encode_packets_simulate (T2.cpp:126-192): the tile's packets of layers
 // [0, max_layers) in THRESH_CALC order -- per component tile-part for the 4K
 // cinema profile with a per-component size cap -- against max_len bytes.
+//
+// A packet's header depends only on its precinct's earlier packets (tag trees,
+// inclusion and length-indicator state of the precinct's code-blocks), and a
+// precinct's packets come in increasing layer order, so the packets of
+// different precincts are simulated in parallel (one precinct's layers in
+// order), recording each packet's header and body bytes; the walk in packet
+// order then applies the reference's running budget check (simulate_packet's
+// subtractions, SOP / EPH wrap-around included) and the per-component cap.
 bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len) {
     const uint32_t pocno = cp.rsiz == RSIZ_CINEMA_4K ? 2 : 1;
     const uint32_t max_comp = cp.max_comp_size > 0 ? cp.numcomps : 1;
@@ -712,19 +723,103 @@ bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t 
     std::vector<uint8_t> include;
     TileGeom g;
     initialise_encode(cp, te, false, pis, include, g);
-    std::vector<PacketId> order;
-    for (uint32_t compno = 0; compno < max_comp; ++compno) {
-        uint64_t comp_len = 0;
+    // the simulation order: [compno][poc] groups of packets
+    std::vector<PacketId> order, part;
+    std::vector<size_t> group_end;  // end index of each (compno, poc) group
+    for (uint32_t compno = 0; compno < max_comp; ++compno)
         for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc) {
             init_encode(pis[poc], cp, te.pocs[poc], compno, kStaleTpPos, false);
-            order.clear();
-            walk(pis[poc], order);
-            for (const auto &pk : order) {
-                if (pk.layno >= max_layers) continue;
-                uint64_t b = 0;
-                if (!simulate_packet(cp, te, pk, max_len, &b)) return false;
-                comp_len += b;
-                max_len -= b;
+            part.clear();
+            walk(pis[poc], part);
+            for (const auto &pk : part)
+                if (pk.layno < max_layers) order.push_back(pk);
+            group_end.push_back(order.size());
+        }
+    // packets per precinct, in order
+    std::vector<std::vector<uint32_t>> prec_base(cp.numcomps);
+    uint32_t nprec = 0;
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        const TileComp &tc = te.tile->comps[k];
+        prec_base[k].resize(tc.res.size());
+        for (size_t r = 0; r < tc.res.size(); ++r) {
+            prec_base[k][r] = nprec;
+            nprec += tc.res[r].pw * tc.res[r].ph;
+        }
+    }
+    std::vector<uint32_t> head(nprec + 1, 0), pos(order.size());
+    for (const auto &pk : order) ++head[prec_base[pk.compno][pk.resno] + pk.precno + 1];
+    for (uint32_t i = 0; i < nprec; ++i) head[i + 1] += head[i];
+    {
+        std::vector<uint32_t> fill(head.begin(), head.end() - 1);
+        for (uint32_t i = 0; i < order.size(); ++i) {
+            const PacketId &pk = order[i];
+            pos[fill[prec_base[pk.compno][pk.resno] + pk.precno]++] = i;
+        }
+    }
+    std::vector<uint64_t> hbytes(order.size()), dbytes(order.size());
+    std::vector<uint8_t> bad(nprec, 0);
+    const uint32_t L = cp.numlayers;
+    host_parallel_for(nprec, 8, [&](size_t p0, size_t p1) {
+        for (size_t p = p0; p < p1; ++p) {
+            uint32_t prev_layer = 0;
+            for (uint32_t q = head[p]; q < head[p + 1]; ++q) {
+                const PacketId &pk = order[pos[q]];
+                if (q > head[p] && pk.layno <= prev_layer) bad[p] = 1;  // not in layer order: see below
+                prev_layer = pk.layno;
+                Resolution &res = te.tile->comps[pk.compno].res[pk.resno];
+                BitCount w;
+                packet_header(cp, te, res, pk.precno, pk.layno, w);
+                uint64_t d = 0;
+                for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+                    Band &b = res.bands[bandno];
+                    if (b.empty() || pk.precno >= b.precs.size()) continue;
+                    for (auto &c : b.precs[pk.precno].cblks) {
+                        const EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + pk.layno];
+                        if (!ly.numpasses) continue;
+                        (*te.cblk)[c.gidx].incl_cur += ly.numpasses;
+                        d += ly.len;
+                    }
+                }
+                hbytes[pos[q]] = w.bytes;
+                dbytes[pos[q]] = d;
+            }
+        }
+    });
+    // a precinct whose packets are not in increasing layer order (never seen
+    // from these iterators) would make the per-precinct split wrong: take the
+    // packet-by-packet route then
+    if (std::find(bad.begin(), bad.end(), 1) != bad.end()) {
+        for (uint32_t compno = 0, gi = 0; compno < max_comp; ++compno) {
+            uint64_t comp_len = 0;
+            for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc, ++gi) {
+                for (size_t i = gi ? group_end[gi - 1] : 0; i < group_end[gi]; ++i) {
+                    uint64_t b = 0;
+                    if (!simulate_packet(cp, te, order[i], max_len, &b)) return false;
+                    comp_len += b;
+                    max_len -= b;
+                }
+                if (cp.max_comp_size && comp_len > cp.max_comp_size) return false;
+            }
+        }
+        return true;
+    }
+    // the budget walk of simulate_packet over the recorded sizes
+    const bool sop = (cp.csty & CSTY_SOP) != 0, eph = (cp.csty & CSTY_EPH) != 0;
+    size_t i = 0, gi = 0;
+    for (uint32_t compno = 0; compno < max_comp; ++compno) {
+        uint64_t comp_len = 0;
+        for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc, ++gi) {
+            for (; i < group_end[gi]; ++i) {
+                uint64_t length = max_len, written = 0;
+                if (sop) { length -= 6; written += 6; }
+                if (hbytes[i] > length) return false;
+                written += hbytes[i];
+                length -= hbytes[i];
+                if (eph) { length -= 2; written += 2; }
+                if (dbytes[i] > length) return false;  // the body's blocks, each checked against what is left
+                written += dbytes[i];
+                comp_len += written;
+                max_len -= written;
             }
             if (cp.max_comp_size && comp_len > cp.max_comp_size) return false;
         }
@@ -744,6 +839,9 @@ void for_each_block(TileEnc &te, F f) {
                     for (auto &c : pr.cblks) f(c);
 }
 
+// The layer record of a block from its cumulative pass count (the per-block
+// body of makelayer_* / make_layer_simple); the layer's distortion is summed
+// into distolayer afterwards, in block order (sum_layer).
 void set_layer(TileEnc &te, uint32_t gidx, uint32_t layno, uint32_t L, uint32_t cumul) {
     EncCblkState &s = (*te.cblk)[gidx];
     EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
@@ -762,14 +860,31 @@ void set_layer(TileEnc &te, uint32_t gidx, uint32_t layno, uint32_t L, uint32_t 
         ly.data_off = P[s.pass0 + s.incl_prev - 1].rate;
         ly.disto = P[s.pass0 + cumul - 1].dd - P[s.pass0 + s.incl_prev - 1].dd;
     }
-    te.distolayer[layno] += ly.disto;
+}
+
+// tile->distolayer[layno] += layer->disto over the blocks that contribute
+// passes, in the reference's block order (floating-point sum order kept)
+void sum_layer(TileEnc &te, uint32_t layno, uint32_t L) {
+    double d = 0;
+    for (Cblk *c : te.blist) {
+        const EncLayer &ly = (*te.layers)[(size_t)c->gidx * L + layno];
+        if (ly.numpasses) d += ly.disto;
+    }
+    te.distolayer[layno] = d;
+}
+
+// per-block loops of the layer formation: independent blocks, on the host pool
+template <class F>
+void blocks_parallel(TileEnc &te, F f) {
+    host_parallel_for(te.blist.size(), 256, [&](size_t b0, size_t b1) {
+        for (size_t i = b0; i < b1; ++i) f(*te.blist[i]);
+    });
 }
 
 // makelayer_final (TileProcessor.cpp:783-852)
 void makelayer_final(CodingParams &cp, TileEnc &te, uint32_t layno) {
     const uint32_t L = cp.numlayers;
-    te.distolayer[layno] = 0;
-    for_each_block(te, [&](Cblk &c) {
+    blocks_parallel(te, [&](Cblk &c) {
         EncCblkState &s = (*te.cblk)[c.gidx];
         if (layno == 0) { s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0; }
         uint32_t cumul = s.incl_prev;
@@ -777,14 +892,14 @@ void makelayer_final(CodingParams &cp, TileEnc &te, uint32_t layno) {
         set_layer(te, c.gidx, layno, L, cumul);
         if ((*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
     });
+    sum_layer(te, layno, L);
 }
 
 // make_layer_simple (TileProcessor.cpp:675-780)
 void make_layer_simple(CodingParams &cp, TileEnc &te, uint32_t layno, double thresh, bool final) {
     const uint32_t L = cp.numlayers;
     const std::vector<EncPass> &P = *te.passes;
-    te.distolayer[layno] = 0;
-    for_each_block(te, [&](Cblk &c) {
+    blocks_parallel(te, [&](Cblk &c) {
         EncCblkState &s = (*te.cblk)[c.gidx];
         if (layno == 0) { s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0; }
         uint32_t cumul;
@@ -812,14 +927,14 @@ void make_layer_simple(CodingParams &cp, TileEnc &te, uint32_t layno, double thr
         set_layer(te, c.gidx, layno, L, cumul);
         if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
     });
+    sum_layer(te, layno, L);
 }
 
 // makelayer_feasible (TileProcessor.cpp:281-364)
 void makelayer_feasible(CodingParams &cp, TileEnc &te, uint32_t layno, uint16_t thresh, bool final) {
     const uint32_t L = cp.numlayers;
     const std::vector<EncPass> &P = *te.passes;
-    te.distolayer[layno] = 0;
-    for_each_block(te, [&](Cblk &c) {
+    blocks_parallel(te, [&](Cblk &c) {
         EncCblkState &s = (*te.cblk)[c.gidx];
         if (layno == 0) s.incl_prev = 0;
         uint32_t cumul = s.incl_prev;
@@ -833,6 +948,7 @@ void makelayer_feasible(CodingParams &cp, TileEnc &te, uint32_t layno, uint16_t 
         set_layer(te, c.gidx, layno, L, cumul);
         if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
     });
+    sum_layer(te, layno, L);
 }
 
 bool layer_needs_rate_control(const CodingParams &cp, uint32_t layno) {
@@ -871,20 +987,29 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
     double min_slope = DBL_MAX, max_slope = -1;
     if (single_lossless(cp, te)) return true;
     const std::vector<EncPass> &P = *te.passes;
-    for_each_block(te, [&](Cblk &c) {
-        const EncCblkState &s = (*te.cblk)[c.gidx];
-        for (uint32_t pn = 0; pn < s.numpasses; ++pn) {
-            const EncPass &ps = P[s.pass0 + pn];
-            int32_t dr;
-            double dd;
-            if (pn == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
-            else { dr = (int32_t)(ps.rate - P[s.pass0 + pn - 1].rate); dd = ps.dd - P[s.pass0 + pn - 1].dd; }
-            if (dr == 0) continue;
-            const double r = dd / dr;
-            if (r < min_slope) min_slope = r;
-            if (r > max_slope) max_slope = r;
-        }
-    });
+    {  // min / max over every pass of every block (order-free), per chunk then combined
+        std::mutex mu;
+        host_parallel_for(te.blist.size(), 512, [&](size_t b0, size_t b1) {
+            double mn = DBL_MAX, mx = -1;
+            for (size_t i = b0; i < b1; ++i) {
+                const EncCblkState &s = (*te.cblk)[te.blist[i]->gidx];
+                for (uint32_t pn = 0; pn < s.numpasses; ++pn) {
+                    const EncPass &ps = P[s.pass0 + pn];
+                    int32_t dr;
+                    double dd;
+                    if (pn == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
+                    else { dr = (int32_t)(ps.rate - P[s.pass0 + pn - 1].rate); dd = ps.dd - P[s.pass0 + pn - 1].dd; }
+                    if (dr == 0) continue;
+                    const double r = dd / dr;
+                    if (r < mn) mn = r;
+                    if (r > mx) mx = r;
+                }
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (mn < min_slope) min_slope = mn;
+            if (mx > max_slope) max_slope = mx;
+        });
+    }
     const double maxSE = tile_max_se(cp, te);
     double upper = max_slope;
     for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
@@ -967,14 +1092,17 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
     const double K = 1;
     const bool sl = single_lossless(cp, te);
     uint32_t min_slope = USHRT_MAX;
-    if (!sl) {
-        for_each_block(te, [&](Cblk &c) {
+    if (!sl) {  // per-block convex hulls (independent), then the smallest slope
+        blocks_parallel(te, [&](Cblk &c) {
             EncCblkState &s = (*te.cblk)[c.gidx];
-            EncPass *P = te.passes->data() + s.pass0;
-            convex_hull(P, s.numpasses);
+            convex_hull(te.passes->data() + s.pass0, s.numpasses);
+        });
+        for (Cblk *c : te.blist) {
+            const EncCblkState &s = (*te.cblk)[c->gidx];
+            const EncPass *P = te.passes->data() + s.pass0;
             for (uint32_t pn = 0; pn < s.numpasses; ++pn)
                 if (P[pn].slope && P[pn].slope < min_slope) min_slope = P[pn].slope;
-        });
+        }
     }
     if (sl) {
         makelayer_final(cp, te, 0);
@@ -1016,6 +1144,8 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
 
 bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
     te.distolayer.assign(cp.numlayers + 1, 0.0);
+    te.blist.clear();
+    for_each_block(te, [&](Cblk &c) { te.blist.push_back(&c); });
     if (!(cp.disto_alloc || cp.fixed_quality)) return true;
     if (cp.rate_algo == 0) return pcrd_simple(cp, te, len);
     return pcrd_feasible(cp, te, len);

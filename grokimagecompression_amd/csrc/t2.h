@@ -67,6 +67,7 @@ struct TileEnc {
     uint32_t packno = 0;                        // SOP packet counter
     double distotile = 0;
     std::vector<double> distolayer;
+    std::vector<Cblk *> blist;                  // the tile's code-blocks in for_each_block order (rate control)
 };
 
 // number of POC entries of a tile (tcp->numpocs + 1)

@@ -181,9 +181,10 @@ int grkgpu_compress_tile_rows(grkgpu_ctx *ctx, const grkgpu_image_desc *img, con
  * raw files grk_compress and the plugin read are 1 or 2 bytes per sample,
  * PNMFormat.cpp), widened to int32 on the GPU by the kernel that first reads
  * them -- so a 12-bit frame crosses PCIe as 2 B/sample.  planes[c] holds
- * rows [row0, row0 + nrows) of component c (nrows = 0: every row; a tile-row
- * shard gives only its tiles' rows, see grkgpu_compress_tile_rows), on the
- * device when on_device != 0.  Encodes tiles [tile_begin, tile_end) and
+ * rows [row0, row0 + nrows) x columns [col0, col0 + ncols) of component c
+ * (nrows / ncols = 0: every row / column; a tile-row shard gives only its
+ * tiles' rows, see grkgpu_compress_tile_rows; grk_write_tile one tile), on
+ * the device when on_device != 0.  Every tile encoded must lie inside them.  Encodes tiles [tile_begin, tile_end) and
  * emits the parts `parts` selects (GRKGPU_PART_*; 0, 0xffffffff, ALL = the
  * whole codestream, as grkgpu_compress).  *out points into the context's
  * pinned output buffer, valid until the next call on ctx (as
@@ -200,7 +201,9 @@ typedef struct {
     const void *planes[GRKGPU_MAX_COMPS];
     uint32_t sample_fmt;  /* GRKGPU_SAMPLE_* */
     int32_t on_device;
-    uint32_t row0, nrows;
+    uint32_t row0, nrows; /* rows held (relative to y0); nrows = 0: every row */
+    uint32_t col0, ncols; /* columns held (relative to x0), = the row stride; ncols = 0: every column
+                             (grk_write_tile hands one tile's samples: its rows and columns only) */
 } grkgpu_planes;
 int grkgpu_compress_ex(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                        const grkgpu_planes *planes, uint32_t tile_begin, uint32_t tile_end, uint32_t parts,
@@ -219,7 +222,8 @@ int grkgpu_compress_ex(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkg
 typedef struct {
     uint32_t tileno, compno, resno, bandno, precno, cblkno;
     uint32_t x0, y0, x1, y1;             /* code-block rectangle, band coordinates */
-    uint32_t numbps, numpasses, len, pad;
+    uint32_t numbps, numpasses, len;
+    float stepsize;                      /* the band's encoder step size (Quantizer.cpp:65-104) */
     const uint8_t *data;                 /* len MQ bytes */
     const uint32_t *rate;                /* numpasses cumulative rates */
     const double *distortion;            /* numpasses cumulative distortion decrease */
@@ -227,6 +231,16 @@ typedef struct {
 int grkgpu_encode_blocks(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                          const int32_t *const *planes, int planes_on_device, int with_distortion,
                          const grkgpu_block_info **blocks, uint32_t *nblocks);
+
+/* After grkgpu_encode_blocks on ctx (and before any other call on it): the
+ * forward DWT output of one tile-component -- the reference's tile buffer
+ * after dwt_encode (Mallat layout, dwt_utils.cpp:84-127), rows of the
+ * tile-component's width, before T1's quantisation -- copied into dst (host
+ * memory, h rows of dst_stride elements).  This is what the reference's plugin
+ * debug state hands its host as image data so that both T1s start from the
+ * same coefficients (TileProcessor.cpp:985-1012, grok.h:1790-1808). */
+int grkgpu_encode_blocks_coefficients(grkgpu_ctx *ctx, uint32_t tileno, uint32_t compno, int32_t *dst,
+                                      uint32_t dst_stride);
 
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);

@@ -235,6 +235,10 @@ typedef struct grk_plugin_init_info {
 } grk_plugin_init_info;
 
 #define GRK_PLUGIN_STATE_NO_DEBUG 0x0 /* grok.h:1791 */
+#define GRK_PLUGIN_STATE_DEBUG 0x1 /* grok.h:1806: the host recomputes T1 and compares */
+#define GRK_PLUGIN_STATE_PRE_TR1 0x2
+#define GRK_PLUGIN_STATE_DWT_QUANTIZATION 0x4
+#define GRK_PLUGIN_STATE_MCT_ONLY 0x8
 
 /* plugin_interface.h:56-67 (what the host's internal callback receives) */
 typedef struct plugin_encode_user_callback_info {

@@ -45,7 +45,7 @@ LIBSRCS := util/BufferedStream.cpp util/logger.cpp util/mem_stream.cpp util/grok
   t1/t1_part1/t1.cpp t1/t1_part1/mqc_enc.cpp t1/t1_part1/mqc_dec.cpp t1/t1_part1/T1Part1.cpp
 OBJS := $(LIBSRCS:%.cpp=$(OUT)/obj/%.o)
 
-all: $(OUT)/libgrok.so $(OUT)/ref_driver $(OUT)/abi_check $(OUT)/ref_driver_mi355x
+all: $(OUT)/libgrok.so $(OUT)/ref_driver $(OUT)/abi_check $(OUT)/ref_driver_mi355x $(OUT)/tile_driver $(OUT)/tile_driver_mi355x
 
 $(GEN)/grk_config.h: $(SRC)/grk_config.h.cmake.in
 	@mkdir -p $(GEN)
@@ -95,3 +95,11 @@ $(OUT)/abi_check: oracle/abi/abi_check.cpp oracle/abi/abi_ref.cpp oracle/abi/abi
 MILIB := grokimagecompression_amd/lib
 $(OUT)/ref_driver_mi355x: oracle/ref_driver.cpp $(MILIB)/libgrok.so $(GEN)/grk_config.h
 	$(CXX) -std=c++17 -O2 -I$(SRC) -I$(GEN) -o $@ oracle/ref_driver.cpp -L$(MILIB) -lgrok -Wl,-rpath,'$$ORIGIN/../../$(MILIB)' -lpthread
+
+# the reference's tile-streaming test programs restated (oracle/tile_driver.cpp),
+# against the reference's libgrok and against ours (tests/test_gpu_grk_api.py)
+$(OUT)/tile_driver: oracle/tile_driver.cpp $(OUT)/libgrok.so
+	$(CXX) -std=c++17 -O2 -I$(SRC) -I$(GEN) -o $@ oracle/tile_driver.cpp -L$(OUT) -lgrok -Wl,-rpath,'$$ORIGIN' -lpthread
+
+$(OUT)/tile_driver_mi355x: oracle/tile_driver.cpp $(MILIB)/libgrok.so $(GEN)/grk_config.h
+	$(CXX) -std=c++17 -O2 -I$(SRC) -I$(GEN) -o $@ oracle/tile_driver.cpp -L$(MILIB) -lgrok -Wl,-rpath,'$$ORIGIN/../../$(MILIB)' -lpthread

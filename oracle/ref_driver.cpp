@@ -39,6 +39,19 @@
 //       grk_plugin_decode(params, decode_callback) with decode_callback /
 //       pre_decode / post_decode restated (:1336-1557) -- post_decode writes
 //       the planes as dec does.  Exit 0 iff the plugin decoded; 3 if declined.
+//   ref_driver plugin-batch PLUGIN_DIR IN_DIR OUT_DIR [options]
+//       grk_compress's plugin_main in batch mode (-ImgDir / -OutDir,
+//       grk_compress.cpp:2196-2243): grk_plugin_batch_encode(in, out, params,
+//       cb), then poll grk_plugin_is_batch_complete every 100 ms and
+//       grk_plugin_stop_batch_encode; cb (plugin_compress_callback's relative
+//       output naming, :1783-1797) writes OUT_DIR/<name>.j2k.  Exit 0 iff
+//       every frame was written; 3 if the plugin declined the batch.
+//   ref_driver plugin-batch-dec PLUGIN_DIR IN_DIR OUT_DIR
+//       grk_decompress's plugin_main in batch mode (grk_decompress.cpp:
+//       1237-1262): grk_plugin_init_batch_decode, grk_plugin_batch_decode,
+//       the completion poll and grk_plugin_stop_batch_decode; the decode
+//       callback writes each image (raw int32 planes) to the output name the
+//       plugin gives.
 //   ref_driver mt IN.i32 EXPECT.j2k W H C BITS SGND THREADS REPS [options]
 //       THREADS caller threads, each with its own codecs (one codec per
 //       caller thread), encode + decode REPS times concurrently;
@@ -51,6 +64,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <string>
@@ -58,6 +73,13 @@
 #include <vector>
 
 static void err_cb(const char *msg, void *) { fprintf(stderr, "[grk error] %s", msg); }
+// warnings of the host: in the plugin debug state every difference between
+// the host's own T1 and the plugin's blocks is one (plugin_bridge.cpp:155-251)
+static int g_warnings = 0;
+static void warn_cb(const char *msg, void *) {
+    ++g_warnings;
+    fprintf(stderr, "[grk warning] %s", msg);
+}
 
 static std::vector<uint8_t> read_file(const char *p) {
     std::vector<uint8_t> v;
@@ -260,6 +282,7 @@ static bool plugin_cb(grk_plugin_encode_user_callback_info *info) {
     grk_stream *st = grk_stream_create_mem_stream(buf, cap, false, false);
     grk_codec *codec = grk_create_compress(GRK_CODEC_J2K, st);
     grk_set_error_handler(err_cb, nullptr);
+    grk_set_warning_handler(warn_cb, nullptr);
     bool ok = codec && grk_setup_encoder(codec, p, img) && grk_start_compress(codec, img) &&
               grk_encode_with_plugin(codec, info->tile) && grk_end_compress(codec);
     if (ok) g_cb_out.assign(buf, buf + grk_stream_get_write_mem_stream_length(st));
@@ -315,8 +338,70 @@ static int plugin_mode(int argc, char **argv) {
     if (rc != 0) { fprintf(stderr, "plugin declined (rc %d)\n", rc); grk_deinitialize(); return 3; }
     if (!g_cb_ok) { fprintf(stderr, "host encode with plugin tile failed\n"); grk_deinitialize(); return 1; }
     write_file(argv[4], g_cb_out.data(), g_cb_out.size());
+    printf("debug_state=%u host_warnings=%d\n", grk_plugin_get_debug_state(), g_warnings);
     grk_deinitialize();
     return 0;
+}
+
+// ---- batch encode: callbacks come from the plugin's worker threads ----
+static std::atomic<int> g_batch_written{0}, g_batch_failed{0};
+static std::string g_batch_out;
+
+static bool plugin_batch_cb(grk_plugin_encode_user_callback_info *info) {
+    // plugin_compress_callback (grk_compress.cpp:1783-1797): a relative output
+    // name is the part of the file name before its first '.' (get_file_name,
+    // common.cpp:245-248), placed in the output directory
+    std::string name = info->output_file_name ? info->output_file_name : "";
+    const std::string stem = name.substr(0, name.find('.'));
+    const std::string out = g_batch_out + "/" + stem + ".j2k";
+    grk_cparameters *p = info->encoder_parameters;
+    grk_image *img = info->image;
+    if (!img) { g_batch_failed++; return false; }
+    if (p->tcp_mct == 255) p->tcp_mct = img->numcomps >= 3 ? 1 : 0;        // grk_compress.cpp:1997-1998
+    if (p->rateControlAlgorithm == 255) p->rateControlAlgorithm = 0;        // :2015-2017
+    const size_t cap = (size_t)(img->x1 - img->x0) * (img->y1 - img->y0) * img->numcomps * 3 + (1 << 20);
+    std::vector<uint8_t> buf(cap);
+    grk_stream *st = grk_stream_create_mem_stream(buf.data(), cap, false, false);
+    grk_codec *codec = grk_create_compress(GRK_CODEC_J2K, st);
+    bool ok = codec && grk_setup_encoder(codec, p, img) && grk_start_compress(codec, img) &&
+              grk_encode_with_plugin(codec, info->tile) && grk_end_compress(codec);
+    if (ok) {
+        write_file(out.c_str(), buf.data(), grk_stream_get_write_mem_stream_length(st));
+        g_batch_written++;
+    } else {
+        g_batch_failed++;
+    }
+    if (codec) grk_destroy_codec(codec);
+    grk_stream_destroy(st);
+    return ok;
+}
+
+static int plugin_batch_mode(int argc, char **argv) {
+    if (argc < 5) return 2;
+    grk_set_error_handler(err_cb, nullptr);
+    grk_set_warning_handler(warn_cb, nullptr);
+    if (!grk_initialize(argv[2], 0)) { fprintf(stderr, "plugin not loaded from %s\n", argv[2]); return 4; }
+    grk_plugin_init_info ii;
+    ii.deviceId = -1;  // "-1 = all devices" (grk_compress -G, grok.h:1816-1821)
+    ii.verbose = getenv("GRKGPU_PLUGIN_VERBOSE") != nullptr;
+    if (!grk_plugin_init(ii)) { fprintf(stderr, "grk_plugin_init failed\n"); return 4; }
+    grk_cparameters p;
+    if (!parse_enc_opts(&p, argc - 5, argv + 5)) return 2;
+    p.decod_format = GRK_PXM_FMT;
+    p.cod_format = GRK_J2K_FMT;
+    g_batch_out = argv[4];
+    int32_t rc = grk_plugin_batch_encode(argv[3], argv[4], &p, plugin_batch_cb);
+    if (rc == 0) {  // started: wait for completion in 100 ms slices (grk_compress.cpp:2229-2241)
+        for (uint32_t i = 0; i < 6000; ++i) {
+            usleep(100 * 1000);
+            if (grk_plugin_is_batch_complete()) break;
+        }
+        grk_plugin_stop_batch_encode();
+    }
+    grk_deinitialize();
+    if (rc != 0) { fprintf(stderr, "plugin declined the batch\n"); return 3; }
+    printf("written=%d failed=%d\n", g_batch_written.load(), g_batch_failed.load());
+    return g_batch_failed ? 1 : 0;
 }
 
 // ---- plugin decode mode: grk_decompress's decode_callback (grk_decompress.cpp:1336-1557) ----
@@ -363,7 +448,11 @@ static int dec_post(grk_plugin_decode_callback_info *info) {
         if (!cm.data) return 1;
         out.insert(out.end(), cm.data, cm.data + (size_t)cm.w * cm.h);
     }
-    write_file(g_dec_out.c_str(), out.data(), out.size() * 4);
+    // post_decode's output name (grk_decompress.cpp:1577-1579): the
+    // parameters' outfile, else the one the plugin gives (batch)
+    const char *dst = info->decoder_parameters->outfile[0] ? g_dec_out.c_str() : info->output_file_name;
+    if (!dst) return 1;
+    write_file(dst, out.data(), out.size() * 4);
     printf("%u %u %u %u %u %u %u %u %u\n", img->x0, img->y0, img->x1, img->y1, img->numcomps, img->comps[0].prec,
            img->comps[0].sgnd, img->comps[0].w, img->comps[0].h);
     return 0;
@@ -389,6 +478,33 @@ static int32_t dec_callback(grk_plugin_decode_callback_info *info) {
     }
     if (info->decode_flags & GRK_DECODE_POST_T1) rc = dec_post(info);
     return rc;
+}
+
+static int plugin_batch_dec_mode(int argc, char **argv) {
+    if (argc < 5) return 2;
+    grk_decompress_parameters p;
+    memset(&p, 0, sizeof(p));
+    grk_set_default_decoder_parameters(&p.core);
+    p.decod_format = GRK_J2K_FMT;
+    p.cod_format = GRK_RAWL_FMT;
+    if (!grk_initialize(argv[2], 0)) { fprintf(stderr, "plugin not loaded from %s\n", argv[2]); return 4; }
+    grk_plugin_init_info ii;
+    ii.deviceId = -1;
+    ii.verbose = getenv("GRKGPU_PLUGIN_VERBOSE") != nullptr;
+    if (!grk_plugin_init(ii)) { fprintf(stderr, "grk_plugin_init failed\n"); return 4; }
+    // grk_decompress.cpp:1242-1262, as written there: the batch is started
+    // only if the init returns non-zero, and waited for if that start returns 0
+    int32_t success = grk_plugin_init_batch_decode(argv[3], argv[4], &p, dec_callback);
+    if (success) success = grk_plugin_batch_decode();
+    if (success == 0) {
+        for (uint32_t i = 0; i < 6000; ++i) {
+            usleep(100 * 1000);
+            if (grk_plugin_is_batch_complete()) break;
+        }
+        grk_plugin_stop_batch_decode();
+    }
+    grk_deinitialize();
+    return success == 0 ? 0 : 3;
 }
 
 static int plugin_dec_mode(int argc, char **argv) {
@@ -484,6 +600,8 @@ int main(int argc, char **argv) {
     if (mode == "plugin") return plugin_mode(argc, argv);
     if (mode == "plugin-dec") return plugin_dec_mode(argc, argv);
     if (mode == "mt") return mt_mode(argc, argv);
+    if (mode == "plugin-batch") return plugin_batch_mode(argc, argv);
+    if (mode == "plugin-batch-dec") return plugin_batch_dec_mode(argc, argv);
     if (mode == "enc" || mode == "bench") {
         const bool bench = mode == "bench";
         const int need = bench ? 10 : 9;

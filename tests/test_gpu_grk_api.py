@@ -10,7 +10,10 @@ API gets the reference's results from the MI355X path by relinking.
 
 CPU part: the library exports the reference's whole grk_* function set.
 """
+import hashlib
+import json
 import os
+import struct
 import subprocess
 
 import numpy as np
@@ -132,3 +135,79 @@ def test_grk_api_concurrent_codecs(name, tmp_path):
     r = subprocess.run([DRIVER, "mt", str(src), f"{GOLD}/{name}.j2k", str(w), str(h), str(c), str(bits), "0", "4",
                         "6"] + m["args"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
+
+
+# ---- tile streaming: grk_write_tile / grk_read_tile_header / grk_decode_tile_data /
+# grk_get_decoded_tile, through the reference's own tile programs restated in
+# oracle/tile_driver.cpp and linked against our libgrok.so.  Fixtures:
+# oracle/make_tile_golden.py (the same driver linked against the reference).
+TILE_DRIVER = os.path.join(ROOT, "oracle", "_ref", "tile_driver_mi355x")
+with open(os.path.join(GOLD, "tiles.json")) as _f:
+    TILES = json.load(_f)
+
+
+def _sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _tile_run(*args):
+    if not os.path.exists(TILE_DRIVER):
+        pytest.skip("oracle/_ref/tile_driver_mi355x not built (needs /root/reference at build time)")
+    r = subprocess.run([TILE_DRIVER] + [str(a) for a in args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+
+
+def _tiles(path):
+    out, a = {}, open(path, "rb").read()
+    o = 0
+    while o < len(a):
+        h = struct.unpack_from("<7Q", a, o)
+        out[h[0]] = (list(h), a[o + 56:o + 56 + h[6]])
+        o += 56 + h[6]
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(TILES))
+def test_tile_fixture_integrity(name):
+    assert _sha(os.path.join(GOLD, "tiles", name + ".j2k")) == TILES[name]["j2k_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(TILES))
+def test_write_tile_matches_reference(name, tmp_path):
+    """test_tile_encoder (tte*): grk_start_compress, grk_write_tile per tile,
+    grk_end_compress -- the codestream is the reference's, byte for byte."""
+    out = tmp_path / "t.j2k"
+    _tile_run("enc", *TILES[name]["args"], out)
+    assert _sha(out) == TILES[name]["j2k_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(TILES))
+def test_tile_decode_matches_reference(name, tmp_path):
+    """test_tile_decoder (ttd*): grk_read_tile_header / grk_decode_tile_data
+    over the reference's codestream, without a decode area: identical tile
+    sequence, headers and samples.  With the ttd area: identical tile sequence
+    and headers, and each tile's samples equal to its full decode (the
+    reference's own samples there are not the tile's -- see tiles.json)."""
+    m = TILES[name]
+    j2k = os.path.join(GOLD, "tiles", name + ".j2k")
+    full, area = tmp_path / "full.bin", tmp_path / "area.bin"
+    _tile_run("dec", 0, 0, 0, 0, j2k, full)
+    assert os.path.getsize(full) == m["full_bytes"] and _sha(full) == m["full_sha256"]
+    _tile_run("dec", *m["area"], j2k, area)
+    got, ref = _tiles(area), _tiles(full)
+    assert [h for h, _ in got.values()] == m["area_tiles"]
+    for t, (_, data) in got.items():
+        assert data == ref[t][1], t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(TILES))
+def test_random_tile_access_matches_reference(name, tmp_path):
+    """j2k_random_tile_access (rta*): grk_get_decoded_tile for the first, last
+    and two middle tiles, each on a fresh decompressor."""
+    out = tmp_path / "rta.bin"
+    _tile_run("rta", os.path.join(GOLD, "tiles", name + ".j2k"), out)
+    assert os.path.getsize(out) == TILES[name]["rta_bytes"] and _sha(out) == TILES[name]["rta_sha256"]

@@ -101,7 +101,9 @@ def test_registration_and_conventions():
     assert L.plugin_encode(None, None) == -1
     assert L.plugin_batch_encode(b"in", b"out", None, None) == -1
     assert L.plugin_decode(None, None) == -1
-    assert L.plugin_init_batch_decode(b"in", b"out", None, None) == -1
+    # 0 = no batch set up: the reference host starts a batch decode only on a
+    # non-zero return (grk_decompress.cpp:1242-1245)
+    assert L.plugin_init_batch_decode(b"in", b"out", None, None) == 0
     assert L.plugin_batch_decode() == -1
     assert L.plugin_is_batch_complete()
     assert EXIT(ex)() == 0
