@@ -243,36 +243,47 @@ def main():
            "note": "the H2D of each frame is inside the timed region of `value`"}
 
     # roofline: forward 9/7 DWT of the frame, measured alone after the timed
-    # region on one context (HIP events on the codec stream around the level
-    # launches): per-launch algorithmic bytes / mean launch duration.
+    # region on one context: HIP events on the codec stream around each level
+    # launch (grkgpu_set_launch_timing), MEAN over the runs; per-launch
+    # algorithmic bytes = 8 B per sample of every level the launch computes
+    # (B_DWT split per launch).
     bdwt = dwt_bytes(H, W, C)
-    fused01 = os.environ.get("GRKGPU_DWT_F01", "4") != "0"  # levels 0 + 1 in one launch (dwt.hip k_dwt_fwd01)
-    nlaunch = 4 if fused01 else 5  # fused: levels 0+1, then 2, 3, 4
     torch.cuda.synchronize()
-    iso = []
     p97 = grk.CParams.make(irreversible=True)
+    runs = []
+    codecs[0].set_launch_timing(True)
     with torch.cuda.stream(streams[0]):
-        for _ in range(3):
+        for _ in range(6):
             codecs[0].compress(frame, BITS, p97, view=True)
-            iso.append(codecs[0].stats())
-    best = min(iso, key=lambda s: s["dwt_ms"])
-    dwt_ms = best["dwt_ms"]
-    achieved = bdwt / (dwt_ms * 1e-3) / 1e9
+            runs.append((codecs[0].stats()["dwt_ms"], codecs[0].launch_times()))
+    codecs[0].set_launch_timing(False)
+    runs = runs[1:]  # the first run pays the launch-log events' creation
+    dwt_ms = sum(r[0] for r in runs) / len(runs)
+    launches = []
+    for i, l in enumerate(runs[0][1]):
+        ms = sum(r[1][i]["ms"] for r in runs) / len(runs)
+        launches.append({"kernel": l["kernel"], "levels": list(range(l["level0"], l["level0"] + l["levels"])),
+                         "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"],
+                         "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(l["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    assert sum(x["algorithmic_bytes"] for x in launches) == bdwt, "per-launch bytes must add up to B_DWT"
+    kern_ms = sum(x["us"] for x in launches) / 1e3
+    achieved = bdwt / (kern_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
         tot = sum(e["bytes"] for k, v in d["kernels"].items()
                   if ("k_dwt_fwd<true" in k or "k_dwt_fwd01<true" in k) for e in v)
-        traffic = round(tot / nlaunch)
-    kname = ("k_dwt_fwd01<9/7> (levels 0+1, LL0 kept in LDS) + k_dwt_fwd<9/7> x 3 (levels 2-4), 3 comps per launch"
-             if fused01 else "k_dwt_fwd<9/7> (5 level launches x 3 comps, dwt.hip)")
-    roofline = {"bound": "hbm", "kernel": kname,
+        traffic = round(tot)
+    roofline = {"bound": "hbm", "kernel": "forward 9/7 DWT of the frame: " + " + ".join(x["kernel"] for x in launches),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": bdwt // nlaunch, "launches": nlaunch,
-                "kernel_ms_per_launch": round(dwt_ms / nlaunch, 4),
-                "measured": "HIP events on the codec stream, 9/7 encode run alone after the timed region"}
+                "algorithmic_bytes": bdwt, "kernel_us": round(1e3 * kern_ms, 2),
+                "span_us": round(1e3 * dwt_ms, 2), "launches": launches,
+                "measured": "HIP events around each launch on the codec stream, mean of 5 lone 9/7 encodes after "
+                            "the timed region; achieved = B_DWT / sum of the launches' mean times; traffic = "
+                            "PMC bytes of the same launches (profiles/dwt_pmc_latest.json)"}
 
     # T1 figures: batch throughput + a lone frame's encode / decode T1 kernels
     with torch.cuda.stream(streams[0]):

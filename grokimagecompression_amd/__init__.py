@@ -188,6 +188,12 @@ class Stats(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class LaunchTime(ctypes.Structure):
+    """grkgpu_launch_time (include/grk_mi355x.h)."""
+    _fields_ = [("kernel", ctypes.c_char * 48), ("level0", ctypes.c_uint32), ("levels", ctypes.c_uint32),
+                ("ms", ctypes.c_float), ("pad", ctypes.c_uint32), ("bytes", ctypes.c_uint64)]
+
+
 _lib = None
 _EXPORTS = None
 
@@ -219,6 +225,8 @@ def lib():
         L.grkgpu_destroy.argtypes = [VP]
         L.grkgpu_set_stream.argtypes = [VP, VP]
         L.grkgpu_get_stats.argtypes = [VP, P(Stats)]
+        L.grkgpu_set_launch_timing.argtypes = [VP, ctypes.c_int]
+        L.grkgpu_get_launch_times.argtypes = [VP, P(LaunchTime), U32, P(U32)]
         L.grkgpu_default_cparams.argtypes = [P(CParams)]
         L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
                                       P(ctypes.c_size_t)]
@@ -361,6 +369,20 @@ class Codec:
         s = Stats()
         _check(lib().grkgpu_get_stats(self._ctx, ctypes.byref(s)))
         return s.as_dict()
+
+    def set_launch_timing(self, on=True):
+        """Time every forward-DWT launch of later compress calls (HIP events)."""
+        _check(lib().grkgpu_set_launch_timing(self._ctx, 1 if on else 0))
+
+    def launch_times(self):
+        """Forward-DWT launches of the last compress call: kernel, first level,
+        level count, device ms, algorithmic bytes (grkgpu_get_launch_times)."""
+        n = ctypes.c_uint32()
+        _check(lib().grkgpu_get_launch_times(self._ctx, None, 0, ctypes.byref(n)))
+        arr = (LaunchTime * max(1, n.value))()
+        _check(lib().grkgpu_get_launch_times(self._ctx, arr, n.value, ctypes.byref(n)))
+        return [{"kernel": t.kernel.decode(), "level0": t.level0, "levels": t.levels, "ms": t.ms, "bytes": t.bytes}
+                for t in arr[:n.value]]
 
     def _image(self, img, prec, offset, sgnd):
         """Image descriptor + grkgpu_planes of a (c,h,w) numpy array or torch

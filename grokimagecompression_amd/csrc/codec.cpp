@@ -95,6 +95,11 @@ struct grkgpu_ctx {
     std::vector<CoefRec> bexp_coef;
     std::vector<uint32_t> bexp_rate;
     std::vector<double> bexp_dist;
+    // per-launch DWT timing (grkgpu_set_launch_timing): a start / end event per
+    // launch of the last forward DWT, read after the call's final sync
+    bool launch_timing = false;
+    std::vector<hipEvent_t> lev;
+    std::vector<grkgpu_launch_time> ltimes;
 };
 
 // Device check, cached per device index (hipGetDeviceProperties is slow and
@@ -163,6 +168,7 @@ void grkgpu_destroy(grkgpu_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     for (auto &e : c->ev) if (e) hipEventDestroy(e);
+    for (auto &e : c->lev) if (e) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -172,6 +178,20 @@ int grkgpu_set_stream(grkgpu_ctx *c, void *stream) {
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     c->stream = (hipStream_t)stream;
     c->own_stream = false;
+    return GRKGPU_OK;
+}
+
+int grkgpu_set_launch_timing(grkgpu_ctx *c, int on) {
+    if (!c) return set_err(GRKGPU_EINVAL, "null ctx");
+    c->launch_timing = on != 0;
+    c->ltimes.clear();
+    return GRKGPU_OK;
+}
+
+int grkgpu_get_launch_times(grkgpu_ctx *c, grkgpu_launch_time *out, uint32_t max, uint32_t *n) {
+    if (!c || !n || (max && !out)) return set_err(GRKGPU_EINVAL, "null arg");
+    *n = (uint32_t)c->ltimes.size();
+    for (uint32_t i = 0; i < max && i < c->ltimes.size(); ++i) out[i] = c->ltimes[i];
     return GRKGPU_OK;
 }
 
@@ -590,14 +610,56 @@ static hipError_t dwt_upload(DwtPlan &P, DevBuf &djobs, HostBuf &hjobs, int irre
 // Run the levels (job table already uploaded by dwt_upload on the same stream).
 // All levels of an uploaded plan (job table at djobs, levels back to back);
 // fused 9/7 level pairs (P.f01) as one launch (8K frame: 0+1, then 2, 3, 4).
-static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, bool inverse, hipStream_t s) {
+// Launch log (grkgpu_set_launch_timing): events around every level launch
+// and each launch's kernel and algorithmic bytes (B_DWT's 8 B per sample of
+// every level it computes).
+struct LaunchLog {
+    std::vector<hipEvent_t> *ev;
+    std::vector<grkgpu_launch_time> *rec;
+};
+
+static uint64_t level_bytes(const std::vector<DwtJob> &l) {
+    uint64_t n = 0;
+    for (auto &j : l) n += 8ull * (uint64_t)j.rw * (uint64_t)j.rh;
+    return n;
+}
+
+static hipError_t log_begin(LaunchLog *log, hipStream_t s, const char *name, uint32_t lev0, uint32_t nlev, uint64_t bytes) {
+    if (!log) return hipSuccess;
+    const size_t i = log->rec->size();
+    while (log->ev->size() < 2 * (i + 1)) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        log->ev->push_back(e);
+    }
+    grkgpu_launch_time t{};
+    snprintf(t.kernel, sizeof(t.kernel), "%s", name);
+    t.level0 = lev0;
+    t.levels = nlev;
+    t.bytes = bytes;
+    log->rec->push_back(t);
+    return hipEventRecord((*log->ev)[2 * i], s);
+}
+
+static hipError_t log_end(LaunchLog *log, hipStream_t s) {
+    if (!log) return hipSuccess;
+    return hipEventRecord((*log->ev)[2 * (log->rec->size() - 1) + 1], s);
+}
+
+static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, bool inverse, hipStream_t s,
+                                 LaunchLog *log = nullptr) {
     hipError_t e = hipSuccess;
     size_t k = 0;
+    const char *wl = irrev ? "9/7" : "5/3";
+    char name[48];
     for (size_t li = 0; li < P.levels.size(); ++li) {
         const auto &l = P.levels[li];
         if (li < P.f01.size() && P.f01[li]) {
+            snprintf(name, sizeof(name), "k_dwt_fwd01<%s>", wl);
+            if ((e = log_begin(log, s, name, (uint32_t)li, 2, level_bytes(l) + level_bytes(P.levels[li + 1])))) return e;
             e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, s);
-            if (e != hipSuccess) return e;
+            if (e != hipSuccess || (e = log_end(log, s))) return e;
             k += l.size() + P.levels[li + 1].size();
             ++li;
             continue;
@@ -606,14 +668,24 @@ static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, boo
         for (auto &j : l) maxt = std::max<uint32_t>(maxt, (uint32_t)j.ntiles);
         const bool f0 = li == 0 && P.fused0 && !inverse;
         const int code = P.th[li] | (f0 ? (P.mct3 ? DWT_FUSED_MCT3 : DWT_FUSED) | (P.fmt << DWT_FMT_SHIFT) : 0);
+        snprintf(name, sizeof(name), "%s<%s,%d>", inverse ? "k_dwt_inv" : f0 && P.mct3 ? "k_dwt_fwd_mct3" : "k_dwt_fwd", wl,
+                 P.th[li] & 0xff);
+        if ((e = log_begin(log, s, name, (uint32_t)li, 1, level_bytes(l)))) return e;
         e = launch_dwt_jobs(djobs + k, (uint32_t)l.size(), maxt, code, irrev, inverse ? 1 : 0, s);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || (e = log_end(log, s))) return e;
         k += l.size();
     }
     return hipSuccess;
 }
 
-static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse, hipStream_t s) {
+// fill in the launch times once the stream has passed the logged launches
+static void log_collect(grkgpu_ctx *c) {
+    for (size_t i = 0; i < c->ltimes.size(); ++i)
+        if (hipEventElapsedTime(&c->ltimes[i].ms, c->lev[2 * i], c->lev[2 * i + 1]) != hipSuccess) c->ltimes[i].ms = -1;
+}
+
+static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse, hipStream_t s,
+                             LaunchLog *log = nullptr) {
     for (auto &cp : P.copies) {
         hipError_t e = hipMemcpyAsync(cp.first, cp.second, P.copy_elems * 4, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
@@ -623,7 +695,7 @@ static hipError_t dwt_launch(DwtPlan &P, DevBuf &djobs, int irrev, bool inverse,
                                         cp.h, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
-    return dwt_run_levels(P, djobs.as<DwtJob>(), irrev, inverse, s);
+    return dwt_run_levels(P, djobs.as<DwtJob>(), irrev, inverse, s, log);
 }
 
 static bool overlap(const Rect &a, const Rect &b) { return a.x0 < b.x1 && b.x0 < a.x1 && a.y0 < b.y1 && b.y0 < a.y1; }
@@ -886,7 +958,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
-    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, false, s));
+    c->ltimes.clear();
+    LaunchLog llog{&c->lev, &c->ltimes};
+    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, false, s, c->launch_timing ? &llog : nullptr));
     HIPCHK(hipEventRecord(c->ev[3], s));
     memcpy(c->h_blocks.p, eb.data(), (size_t)nblk * sizeof(EncBlock));
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(EncBlock), hipMemcpyHostToDevice, s));
@@ -1006,6 +1080,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         hipEventElapsedTime(&st0.dcshift_mct_ms, c->ev[1], c->ev[2]);
         hipEventElapsedTime(&st0.dwt_ms, c->ev[2], c->ev[3]);
         hipEventElapsedTime(&st0.t1_ms, c->ev[3], c->ev[4]);
+        log_collect(c);
         st0.num_cblks = nblk;
         st0.mq_symbols = nsym;
         st0.total_ms = (float)(now_ms() - t_start);
@@ -1189,6 +1264,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     hipEventElapsedTime(&st.t1_ms, c->ev[3], c->ev[4]);
     hipEventElapsedTime(&st.gather_ms, c->ev[5], c->ev[6]);
     hipEventElapsedTime(&st.d2h_ms, c->ev[6], c->ev[7]);
+    log_collect(c);
     st.host_t2_ms = (float)(t_t2_end - t_t2);
     st.total_ms = (float)(t_end - t_start);
     st.num_cblks = nblk;

@@ -177,7 +177,16 @@ struct BitWriter {
     explicit BitWriter(ByteBuf &o) : out(o) {}
     void byteout() { out.put8(buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
     void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
-    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    // the n low bits of v, MSB first: putbit() per bit, a byte's free bits at a time
+    void write(uint32_t v, uint32_t n) {
+        while (n) {
+            if (ct == 0) byteout();
+            const uint32_t k = n < ct ? n : ct;
+            n -= k;
+            ct -= k;
+            buf |= ((v >> n) & ((1u << k) - 1)) << ct;
+        }
+    }
     void flush() { byteout(); if (ct == 7) byteout(); }
     void numpasses(uint32_t n) {
         if (n == 1) write(0, 1);

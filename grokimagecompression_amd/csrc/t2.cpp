@@ -532,7 +532,16 @@ struct BitCount {
     uint32_t buf = 0, ct = 8;
     void byteout() { ++bytes; ct = (buf == 0xff) ? 7 : 8; buf = 0; }
     void putbit(uint32_t b) { if (ct == 0) byteout(); ct--; buf |= (b & 1) << ct; }
-    void write(uint32_t v, uint32_t n) { for (int i = (int)n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    // the n low bits of v, MSB first: putbit() per bit, a byte's free bits at a time
+    void write(uint32_t v, uint32_t n) {
+        while (n) {
+            if (ct == 0) byteout();
+            const uint32_t k = n < ct ? n : ct;
+            n -= k;
+            ct -= k;
+            buf |= ((v >> n) & ((1u << k) - 1)) << ct;
+        }
+    }
     void flush() { byteout(); if (ct == 7) byteout(); }
     void numpasses(uint32_t n) {
         if (n == 1) write(0, 1);
@@ -705,37 +714,82 @@ bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ui
     return true;
 }
 
-// T2::encode_packets_simulate (T2.cpp:126-192): the tile's packets of layers
-// [0, max_layers) in THRESH_CALC order -- per component tile-part for the 4K
-// cinema profile with a per-component size cap -- against max_len bytes.
-//
-// A packet's header depends only on its precinct's earlier packets (tag trees,
-// inclusion and length-indicator state of the precinct's code-blocks), and a
-// precinct's packets come in increasing layer order, so the packets of
-// different precincts are simulated in parallel (one precinct's layers in
-// order), recording each packet's header and body bytes; the walk in packet
-// order then applies the reference's running budget check (simulate_packet's
-// subtractions, SOP / EPH wrap-around included) and the per-component cap.
-bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len) {
+// Rate-control probes, evaluated incrementally with the results of a full
+// evaluation.  A bisection step forms the layer at a threshold
+// (make_layer_simple / makelayer_feasible) and simulates the tile's packets
+// (simulate_tile):
+//  * a block's pass count at threshold t follows from comparisons of t with
+//    pass slopes, each monotone in t; the comparisons a block made at its last
+//    evaluation keep their outcomes on an interval of t (two bounds per
+//    block), so a probe inside that interval leaves the block's layer record
+//    as it is and skips the block;
+//  * a packet's header depends only on its precinct's earlier packets (tag
+//    trees, inclusion and length-indicator state of the precinct's
+//    code-blocks), and a precinct's packets come in increasing layer order, so
+//    each precinct's packets are simulated on their own (in parallel), and
+//    only the precincts holding a block whose layer record changed since the
+//    last probe are simulated again; the packet order for a layer count is
+//    built once.
+struct RateProbe {
+    // per block, in te.blist order
+    std::vector<uint32_t> prec;        // precinct id
+    std::vector<double> lo_d, hi_d;    // simple: largest slope compared false, smallest compared true
+    std::vector<uint32_t> lo_u, hi_u;  // feasible: the slope it stopped at, smallest slope it passed
+    std::vector<uint8_t> valid;        // bounds hold for the current layer records
+    bool fresh = true;                 // no probe of the current layer yet: evaluate every block
+    // packets of layers [0, layers) in THRESH_CALC order, grouped per precinct
+    uint32_t layers = 0, nprec = 0, npoc = 0;  // npoc: POC groups per component
+    bool bad = false;
+    std::vector<PacketId> order;
+    std::vector<size_t> group_end;     // end index of each (compno, poc) group
+    std::vector<uint32_t> head, pos;   // packets of precinct p: order[pos[head[p] .. head[p + 1])]
+    std::vector<uint64_t> hbytes, dbytes;
+    std::vector<uint8_t> dirty;        // per precinct
+};
+
+// precinct ids of te.blist (a precinct = one resolution's precinct of a component)
+void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
+    rp.prec.clear();
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        TileComp &tc = te.tile->comps[k];
+        for (auto &res : tc.res) {
+            for (uint32_t b = 0; b < res.numbands; ++b)
+                for (size_t p = 0; p < res.bands[b].precs.size(); ++p)
+                    for (size_t n = 0; n < res.bands[b].precs[p].cblks.size(); ++n) rp.prec.push_back(base + (uint32_t)p);
+            base += res.pw * res.ph;
+        }
+    }
+    rp.nprec = base;
+    const size_t nb = rp.prec.size();
+    rp.lo_d.assign(nb, 0); rp.hi_d.assign(nb, 0);
+    rp.lo_u.assign(nb, 0); rp.hi_u.assign(nb, 0);
+    rp.valid.assign(nb, 0);
+    rp.dirty.assign(rp.nprec, 1);
+    rp.layers = 0;
+    rp.fresh = true;
+}
+
+void probe_plan(CodingParams &cp, TileEnc &te, uint32_t max_layers, RateProbe &rp) {
     const uint32_t pocno = cp.rsiz == RSIZ_CINEMA_4K ? 2 : 1;
     const uint32_t max_comp = cp.max_comp_size > 0 ? cp.numcomps : 1;
     std::vector<Pi> pis;
     std::vector<uint8_t> include;
     TileGeom g;
     initialise_encode(cp, te, false, pis, include, g);
-    // the simulation order: [compno][poc] groups of packets
-    std::vector<PacketId> order, part;
-    std::vector<size_t> group_end;  // end index of each (compno, poc) group
+    rp.npoc = std::min<uint32_t>(pocno, (uint32_t)pis.size());
+    rp.order.clear();
+    rp.group_end.clear();
+    std::vector<PacketId> part;
     for (uint32_t compno = 0; compno < max_comp; ++compno)
-        for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc) {
+        for (uint32_t poc = 0; poc < rp.npoc; ++poc) {
             init_encode(pis[poc], cp, te.pocs[poc], compno, kStaleTpPos, false);
             part.clear();
             walk(pis[poc], part);
             for (const auto &pk : part)
-                if (pk.layno < max_layers) order.push_back(pk);
-            group_end.push_back(order.size());
+                if (pk.layno < max_layers) rp.order.push_back(pk);
+            rp.group_end.push_back(rp.order.size());
         }
-    // packets per precinct, in order
     std::vector<std::vector<uint32_t>> prec_base(cp.numcomps);
     uint32_t nprec = 0;
     for (uint32_t k = 0; k < cp.numcomps; ++k) {
@@ -746,55 +800,69 @@ bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t 
             nprec += tc.res[r].pw * tc.res[r].ph;
         }
     }
-    std::vector<uint32_t> head(nprec + 1, 0), pos(order.size());
-    for (const auto &pk : order) ++head[prec_base[pk.compno][pk.resno] + pk.precno + 1];
-    for (uint32_t i = 0; i < nprec; ++i) head[i + 1] += head[i];
-    {
-        std::vector<uint32_t> fill(head.begin(), head.end() - 1);
-        for (uint32_t i = 0; i < order.size(); ++i) {
-            const PacketId &pk = order[i];
-            pos[fill[prec_base[pk.compno][pk.resno] + pk.precno]++] = i;
-        }
+    rp.head.assign(nprec + 1, 0);
+    rp.pos.assign(rp.order.size(), 0);
+    for (const auto &pk : rp.order) ++rp.head[prec_base[pk.compno][pk.resno] + pk.precno + 1];
+    for (uint32_t i = 0; i < nprec; ++i) rp.head[i + 1] += rp.head[i];
+    std::vector<uint32_t> fill(rp.head.begin(), rp.head.end() - 1);
+    for (uint32_t i = 0; i < rp.order.size(); ++i) {
+        const PacketId &pk = rp.order[i];
+        rp.pos[fill[prec_base[pk.compno][pk.resno] + pk.precno]++] = i;
     }
-    std::vector<uint64_t> hbytes(order.size()), dbytes(order.size());
-    std::vector<uint8_t> bad(nprec, 0);
+    // a precinct whose packets are not in increasing layer order (never seen
+    // from these iterators) would make the per-precinct split wrong: such a
+    // tile takes the packet-by-packet route
+    rp.bad = false;
+    for (uint32_t p = 0; p < nprec && !rp.bad; ++p)
+        for (uint32_t q = rp.head[p] + 1; q < rp.head[p + 1]; ++q)
+            if (rp.order[rp.pos[q]].layno <= rp.order[rp.pos[q - 1]].layno) rp.bad = true;
+    rp.hbytes.assign(rp.order.size(), 0);
+    rp.dbytes.assign(rp.order.size(), 0);
+    rp.dirty.assign(nprec, 1);
+    rp.layers = max_layers;
+}
+
+// the packets of one precinct, in layer order: header and body bytes
+void probe_precinct(CodingParams &cp, TileEnc &te, RateProbe &rp, uint32_t p) {
     const uint32_t L = cp.numlayers;
-    host_parallel_for(nprec, 8, [&](size_t p0, size_t p1) {
-        for (size_t p = p0; p < p1; ++p) {
-            uint32_t prev_layer = 0;
-            for (uint32_t q = head[p]; q < head[p + 1]; ++q) {
-                const PacketId &pk = order[pos[q]];
-                if (q > head[p] && pk.layno <= prev_layer) bad[p] = 1;  // not in layer order: see below
-                prev_layer = pk.layno;
-                Resolution &res = te.tile->comps[pk.compno].res[pk.resno];
-                BitCount w;
-                packet_header(cp, te, res, pk.precno, pk.layno, w);
-                uint64_t d = 0;
-                for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
-                    Band &b = res.bands[bandno];
-                    if (b.empty() || pk.precno >= b.precs.size()) continue;
-                    for (auto &c : b.precs[pk.precno].cblks) {
-                        const EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + pk.layno];
-                        if (!ly.numpasses) continue;
-                        (*te.cblk)[c.gidx].incl_cur += ly.numpasses;
-                        d += ly.len;
-                    }
-                }
-                hbytes[pos[q]] = w.bytes;
-                dbytes[pos[q]] = d;
+    for (uint32_t q = rp.head[p]; q < rp.head[p + 1]; ++q) {
+        const PacketId &pk = rp.order[rp.pos[q]];
+        Resolution &res = te.tile->comps[pk.compno].res[pk.resno];
+        BitCount w;
+        packet_header(cp, te, res, pk.precno, pk.layno, w);
+        uint64_t d = 0;
+        for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
+            Band &b = res.bands[bandno];
+            if (b.empty() || pk.precno >= b.precs.size()) continue;
+            for (auto &c : b.precs[pk.precno].cblks) {
+                const EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + pk.layno];
+                if (!ly.numpasses) continue;
+                (*te.cblk)[c.gidx].incl_cur += ly.numpasses;
+                d += ly.len;
             }
         }
-    });
-    // a precinct whose packets are not in increasing layer order (never seen
-    // from these iterators) would make the per-precinct split wrong: take the
-    // packet-by-packet route then
-    if (std::find(bad.begin(), bad.end(), 1) != bad.end()) {
+        rp.hbytes[rp.pos[q]] = w.bytes;
+        rp.dbytes[rp.pos[q]] = d;
+    }
+}
+
+// T2::encode_packets_simulate (T2.cpp:126-192): the tile's packets of layers
+// [0, max_layers) in THRESH_CALC order -- per component tile-part for the 4K
+// cinema profile with a per-component size cap -- against max_len bytes.
+// The per-packet sizes come from the precinct simulations (RateProbe); the
+// walk in packet order then applies the reference's running budget check
+// (simulate_packet's subtractions, SOP / EPH wrap-around included) and the
+// per-component cap.
+bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len, RateProbe &rp) {
+    const uint32_t max_comp = cp.max_comp_size > 0 ? cp.numcomps : 1;
+    if (rp.layers != max_layers) probe_plan(cp, te, max_layers, rp);
+    if (rp.bad) {
         for (uint32_t compno = 0, gi = 0; compno < max_comp; ++compno) {
             uint64_t comp_len = 0;
-            for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc, ++gi) {
-                for (size_t i = gi ? group_end[gi - 1] : 0; i < group_end[gi]; ++i) {
+            for (uint32_t poc = 0; poc < rp.npoc; ++poc, ++gi) {
+                for (size_t i = gi ? rp.group_end[gi - 1] : 0; i < rp.group_end[gi]; ++i) {
                     uint64_t b = 0;
-                    if (!simulate_packet(cp, te, order[i], max_len, &b)) return false;
+                    if (!simulate_packet(cp, te, rp.order[i], max_len, &b)) return false;
                     comp_len += b;
                     max_len -= b;
                 }
@@ -803,21 +871,31 @@ bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t 
         }
         return true;
     }
-    // the budget walk of simulate_packet over the recorded sizes
+    std::vector<uint32_t> todo;
+    for (uint32_t p = 0; p < rp.nprec; ++p)
+        if (rp.dirty[p] && rp.head[p + 1] > rp.head[p]) todo.push_back(p);
+    std::fill(rp.dirty.begin(), rp.dirty.end(), 0);
+    if (todo.size() > 16) {
+        host_parallel_for(todo.size(), 8, [&](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i) probe_precinct(cp, te, rp, todo[i]);
+        });
+    } else {
+        for (uint32_t p : todo) probe_precinct(cp, te, rp, p);
+    }
     const bool sop = (cp.csty & CSTY_SOP) != 0, eph = (cp.csty & CSTY_EPH) != 0;
     size_t i = 0, gi = 0;
     for (uint32_t compno = 0; compno < max_comp; ++compno) {
         uint64_t comp_len = 0;
-        for (uint32_t poc = 0; poc < pocno && poc < pis.size(); ++poc, ++gi) {
-            for (; i < group_end[gi]; ++i) {
+        for (uint32_t poc = 0; poc < rp.npoc; ++poc, ++gi) {
+            for (; i < rp.group_end[gi]; ++i) {
                 uint64_t length = max_len, written = 0;
                 if (sop) { length -= 6; written += 6; }
-                if (hbytes[i] > length) return false;
-                written += hbytes[i];
-                length -= hbytes[i];
+                if (rp.hbytes[i] > length) return false;
+                written += rp.hbytes[i];
+                length -= rp.hbytes[i];
                 if (eph) { length -= 2; written += 2; }
-                if (dbytes[i] > length) return false;  // the body's blocks, each checked against what is left
-                written += dbytes[i];
+                if (rp.dbytes[i] > length) return false;  // the body's blocks, each checked against what is left
+                written += rp.dbytes[i];
                 comp_len += written;
                 max_len -= written;
             }
@@ -895,60 +973,126 @@ void makelayer_final(CodingParams &cp, TileEnc &te, uint32_t layno) {
     sum_layer(te, layno, L);
 }
 
-// make_layer_simple (TileProcessor.cpp:675-780)
-void make_layer_simple(CodingParams &cp, TileEnc &te, uint32_t layno, double thresh, bool final) {
-    const uint32_t L = cp.numlayers;
-    const std::vector<EncPass> &P = *te.passes;
-    blocks_parallel(te, [&](Cblk &c) {
-        EncCblkState &s = (*te.cblk)[c.gidx];
-        if (layno == 0) { s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0; }
-        uint32_t cumul;
-        if (thresh == 0) {
-            cumul = s.numpasses;
-        } else {
-            cumul = s.incl_prev;
-            for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
-                const EncPass &ps = P[s.pass0 + pn];
-                uint32_t dr;
-                double dd;
-                if (cumul == 0) { dr = ps.rate; dd = ps.dd; }
-                else {
-                    dr = ps.rate - P[s.pass0 + cumul - 1].rate;
-                    dd = ps.dd - P[s.pass0 + cumul - 1].dd;
-                }
-                if (!dr) {
-                    if (dd != 0) cumul = pn + 1;
-                    continue;
-                }
-                const double slope = dd / dr;
-                if (thresh - slope < DBL_EPSILON) cumul = pn + 1;
-            }
+// make_layer_simple's per-block pass selection (TileProcessor.cpp:700-760):
+// the last pass whose slope against the passes taken so far reaches the
+// threshold; *lo / *hi = the largest slope that failed / smallest that passed
+// (the comparisons `thresh - slope < DBL_EPSILON` keep their outcomes for
+// every threshold t with !(t - *lo < DBL_EPSILON) and t - *hi < DBL_EPSILON)
+uint32_t simple_cumul(const EncCblkState &s, const EncPass *P, double thresh, double *lo, double *hi) {
+    uint32_t cumul = s.incl_prev;
+    double l = -HUGE_VAL, h = HUGE_VAL;
+    if (thresh == 0) return s.numpasses;
+    for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
+        const EncPass &ps = P[pn];
+        uint32_t dr;
+        double dd;
+        if (cumul == 0) { dr = ps.rate; dd = ps.dd; }
+        else {
+            dr = ps.rate - P[cumul - 1].rate;
+            dd = ps.dd - P[cumul - 1].dd;
         }
-        set_layer(te, c.gidx, layno, L, cumul);
-        if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
-    });
-    sum_layer(te, layno, L);
+        if (!dr) {
+            if (dd != 0) cumul = pn + 1;
+            continue;
+        }
+        const double slope = dd / dr;
+        if (thresh - slope < DBL_EPSILON) {
+            cumul = pn + 1;
+            h = std::min(h, slope);
+        } else {
+            l = std::max(l, slope);
+        }
+    }
+    *lo = l;
+    *hi = h;
+    return cumul;
 }
 
-// makelayer_feasible (TileProcessor.cpp:281-364)
-void makelayer_feasible(CodingParams &cp, TileEnc &te, uint32_t layno, uint16_t thresh, bool final) {
+// makelayer_feasible's per-block pass selection (TileProcessor.cpp:300-330):
+// passes up to the first hull slope <= thresh; the outcome holds for every
+// threshold t with *lo <= t < *hi
+uint32_t feasible_cumul(const EncCblkState &s, const EncPass *P, uint32_t thresh, uint32_t *lo, uint32_t *hi) {
+    uint32_t cumul = s.incl_prev, l = 0, h = 0x10000;
+    for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
+        const EncPass &ps = P[pn];
+        if (ps.slope) {
+            if (ps.slope <= thresh) { l = ps.slope; break; }
+            cumul = pn + 1;
+            h = std::min<uint32_t>(h, ps.slope);
+        }
+    }
+    *lo = l;
+    *hi = h;
+    return cumul;
+}
+
+// One probe or the final formation of layer `layno` at a threshold
+// (make_layer_simple, TileProcessor.cpp:675-780, or makelayer_feasible,
+// :281-364).  A probe re-evaluates only the blocks whose bounds exclude the
+// threshold (RateProbe) and marks the precincts of blocks whose record
+// changed; the final formation evaluates every block and commits
+// incl_prev.  need_sum: tile->distolayer[layno] is read afterwards.
+template <bool FEASIBLE, class T>
+void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool final, bool need_sum, RateProbe &rp) {
     const uint32_t L = cp.numlayers;
     const std::vector<EncPass> &P = *te.passes;
-    blocks_parallel(te, [&](Cblk &c) {
+    const size_t nb = te.blist.size();
+    auto eval = [&](size_t i) -> bool {  // true if the block's layer record changed
+        Cblk &c = *te.blist[i];
         EncCblkState &s = (*te.cblk)[c.gidx];
-        if (layno == 0) s.incl_prev = 0;
-        uint32_t cumul = s.incl_prev;
-        for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
-            const EncPass &ps = P[s.pass0 + pn];
-            if (ps.slope) {
-                if (ps.slope <= thresh) break;
-                cumul = pn + 1;
-            }
-        }
+        uint32_t cumul;
+        if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.lo_u[i], &rp.hi_u[i]);
+        else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.lo_d[i], &rp.hi_d[i]);
+        EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + layno];
+        const uint32_t old = ly.numpasses;
         set_layer(te, c.gidx, layno, L, cumul);
-        if (final && (*te.layers)[(size_t)c.gidx * L + layno].numpasses) s.incl_prev = cumul;
-    });
-    sum_layer(te, layno, L);
+        return ly.numpasses != old;
+    };
+    std::vector<uint32_t> redo;
+    const bool full = final || rp.fresh || (!FEASIBLE && thresh == 0);
+    if (full) {
+        if (layno == 0)
+            for (Cblk *c : te.blist) {
+                EncCblkState &s = (*te.cblk)[c->gidx];
+                s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0;
+            }
+        redo.resize(nb);
+        for (size_t i = 0; i < nb; ++i) redo[i] = (uint32_t)i;
+    } else {
+        for (size_t i = 0; i < nb; ++i) {
+            bool ok = rp.valid[i] != 0;
+            if constexpr (FEASIBLE) ok = ok && rp.lo_u[i] <= (uint32_t)thresh && (uint32_t)thresh < rp.hi_u[i];
+            else ok = ok && ((double)thresh - rp.hi_d[i] < DBL_EPSILON) && !((double)thresh - rp.lo_d[i] < DBL_EPSILON);
+            if (!ok) redo.push_back((uint32_t)i);
+        }
+    }
+    std::vector<uint8_t> changed(redo.size());
+    if (redo.size() > 2048) {
+        host_parallel_for(redo.size(), 256, [&](size_t a, size_t b) {
+            for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j]);
+        });
+    } else {
+        for (size_t j = 0; j < redo.size(); ++j) changed[j] = eval(redo[j]);
+    }
+    const bool keep = !final && (FEASIBLE || thresh != 0);
+    for (size_t j = 0; j < redo.size(); ++j) {
+        const uint32_t i = redo[j];
+        if (changed[j]) rp.dirty[rp.prec[i]] = 1;
+        rp.valid[i] = keep;
+    }
+    rp.fresh = false;
+    if (final) {
+        for (Cblk *c : te.blist) {
+            EncCblkState &s = (*te.cblk)[c->gidx];
+            const EncLayer &ly = (*te.layers)[(size_t)c->gidx * L + layno];
+            if (ly.numpasses) s.incl_prev += ly.numpasses;
+        }
+        // incl_prev moved: every bound is stale, and the next layer's probes
+        // simulate a different layer count (a new plan)
+        std::fill(rp.valid.begin(), rp.valid.end(), 0);
+        rp.fresh = true;
+    }
+    if (need_sum || final) sum_layer(te, layno, L);
 }
 
 bool layer_needs_rate_control(const CodingParams &cp, uint32_t layno) {
@@ -1011,6 +1155,8 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
         });
     }
     const double maxSE = tile_max_se(cp, te);
+    RateProbe rp;
+    probe_init(cp, te, rp);
     double upper = max_slope;
     for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
         if (layer_needs_rate_control(cp, layno)) {
@@ -1021,7 +1167,7 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
             double thresh = 0;
             for (uint32_t i = 0; i < 128; ++i) {
                 thresh = (upper == -1) ? lower : (lower + upper) / 2;
-                make_layer_simple(cp, te, layno, thresh, false);
+                form_layer<false>(cp, te, layno, thresh, false, cp.fixed_quality != 0, rp);
                 if (prevthresh != -1 && (fabs(prevthresh - thresh)) < 0.001) break;
                 prevthresh = thresh;
                 if (cp.fixed_quality) {
@@ -1029,12 +1175,12 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
                     if (achieved < distotarget) { upper = thresh; continue; }
                     lower = thresh;
                 } else {
-                    if (!simulate_tile(cp, te, layno + 1, maxlen)) { lower = thresh; continue; }
+                    if (!simulate_tile(cp, te, layno + 1, maxlen, rp)) { lower = thresh; continue; }
                     upper = thresh;
                 }
             }
             const double good = (upper == -1) ? thresh : upper;
-            make_layer_simple(cp, te, layno, good, true);
+            form_layer<false>(cp, te, layno, good, true, true, rp);
             cumdisto[layno] = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
             upper = lower - 1;
         } else {
@@ -1109,6 +1255,8 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
         return true;
     }
     const double maxSE = tile_max_se(cp, te);
+    RateProbe rp;
+    probe_init(cp, te, rp);
     uint32_t upper = USHRT_MAX;
     for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
         uint32_t lower = min_slope;
@@ -1119,18 +1267,18 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
             for (uint32_t i = 0; i < 128; ++i) {
                 const uint32_t thresh = (lower + upper) >> 1;
                 if (prevthresh != 0 && prevthresh == thresh) break;
-                makelayer_feasible(cp, te, layno, (uint16_t)thresh, false);
+                form_layer<true>(cp, te, layno, (uint16_t)thresh, false, cp.fixed_quality != 0, rp);
                 prevthresh = thresh;
                 if (cp.fixed_quality) {
                     const double achieved = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
                     if (achieved < distotarget) { upper = thresh; continue; }
                     lower = thresh;
                 } else {
-                    if (!simulate_tile(cp, te, layno + 1, maxlen)) { lower = thresh; continue; }
+                    if (!simulate_tile(cp, te, layno + 1, maxlen, rp)) { lower = thresh; continue; }
                     upper = thresh;
                 }
             }
-            makelayer_feasible(cp, te, layno, (uint16_t)upper, true);
+            form_layer<true>(cp, te, layno, (uint16_t)upper, true, true, rp);
             cumdisto[layno] = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
             upper = lower - 1;
         } else {

@@ -132,6 +132,19 @@ typedef struct {
     float pad;
 } grkgpu_stats;
 
+/* One kernel launch of the last call's forward DWT, timed with HIP events on
+ * the context's stream (grkgpu_set_launch_timing): kernel name, first level
+ * and level count it computes, device time, and its algorithmic bytes
+ * (8 B -- an int32 read and written -- per sample of every level it
+ * computes: SURVEY.md 8(d)'s B_DWT split per launch). */
+typedef struct {
+    char kernel[48];
+    uint32_t level0, levels;
+    float ms;
+    uint32_t pad;
+    uint64_t bytes;
+} grkgpu_launch_time;
+
 const char *grkgpu_version(void);
 const char *grkgpu_last_error(void);
 int grkgpu_device_count(void);
@@ -141,6 +154,11 @@ void grkgpu_destroy(grkgpu_ctx *ctx);
 /* Order all work of ctx after/with this HIP stream (hipStream_t as void*). */
 int grkgpu_set_stream(grkgpu_ctx *ctx, void *stream);
 int grkgpu_get_stats(grkgpu_ctx *ctx, grkgpu_stats *out);
+/* Time every forward-DWT launch of later compress calls (off by default: two
+ * events per launch), and read the launches of the last call: *n = their
+ * count, the first min(max, *n) are copied to out. */
+int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
+int grkgpu_get_launch_times(grkgpu_ctx *ctx, grkgpu_launch_time *out, uint32_t max, uint32_t *n);
 void grkgpu_default_cparams(grkgpu_cparams *p);
 
 /* Whole-codestream encode.  planes[c] = (y1-y0)*(x1-x0) int32 samples, on
