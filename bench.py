@@ -243,32 +243,37 @@ def main():
            "note": "the H2D of each frame is inside the timed region of `value`"}
 
     # roofline: forward 9/7 DWT of the frame, measured alone after the timed
-    # region on one context: HIP events on the codec stream around each level
-    # launch (grkgpu_set_launch_timing), MEAN over the runs; per-launch
-    # algorithmic bytes = 8 B per sample of every level the launch computes
-    # (B_DWT split per launch).
+    # region on one context.  frac: B_DWT over the MEAN device time of the
+    # frame's DWT launches (HIP events on the codec stream before the first and
+    # after the last launch, 5 encodes).  launches: each launch's own
+    # algorithmic bytes (8 B per sample of every level it computes -- B_DWT
+    # split per launch) and mean time from 5 more encodes with
+    # an event pair around every launch (grkgpu_set_launch_timing; the events
+    # add ~2 us to each short launch).
     bdwt = dwt_bytes(H, W, C)
     torch.cuda.synchronize()
     p97 = grk.CParams.make(irreversible=True)
-    runs = []
-    codecs[0].set_launch_timing(True)
+    spans, runs = [], []
     with torch.cuda.stream(streams[0]):
         for _ in range(6):
             codecs[0].compress(frame, BITS, p97, view=True)
-            runs.append((codecs[0].stats()["dwt_ms"], codecs[0].launch_times()))
-    codecs[0].set_launch_timing(False)
-    runs = runs[1:]  # the first run pays the launch-log events' creation
-    dwt_ms = sum(r[0] for r in runs) / len(runs)
+            spans.append(codecs[0].stats()["dwt_ms"])
+        codecs[0].set_launch_timing(True)
+        for _ in range(6):
+            codecs[0].compress(frame, BITS, p97, view=True)
+            runs.append(codecs[0].launch_times())
+        codecs[0].set_launch_timing(False)
+    spans, runs = spans[1:], runs[1:]  # the first of each pays one-time setup
+    dwt_ms = sum(spans) / len(spans)
     launches = []
-    for i, l in enumerate(runs[0][1]):
-        ms = sum(r[1][i]["ms"] for r in runs) / len(runs)
+    for i, l in enumerate(runs[0]):
+        ms = sum(r[i]["ms"] for r in runs) / len(runs)
         launches.append({"kernel": l["kernel"], "levels": list(range(l["level0"], l["level0"] + l["levels"])),
                          "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"],
                          "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
                          "frac": round(l["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
     assert sum(x["algorithmic_bytes"] for x in launches) == bdwt, "per-launch bytes must add up to B_DWT"
-    kern_ms = sum(x["us"] for x in launches) / 1e3
-    achieved = bdwt / (kern_ms * 1e-3) / 1e9
+    achieved = bdwt / (dwt_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     if os.path.exists(pmc):
@@ -279,11 +284,10 @@ def main():
     roofline = {"bound": "hbm", "kernel": "forward 9/7 DWT of the frame: " + " + ".join(x["kernel"] for x in launches),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes": bdwt, "kernel_us": round(1e3 * kern_ms, 2),
-                "span_us": round(1e3 * dwt_ms, 2), "launches": launches,
-                "measured": "HIP events around each launch on the codec stream, mean of 5 lone 9/7 encodes after "
-                            "the timed region; achieved = B_DWT / sum of the launches' mean times; traffic = "
-                            "PMC bytes of the same launches (profiles/dwt_pmc_latest.json)"}
+                "algorithmic_bytes": bdwt, "dwt_us": round(1e3 * dwt_ms, 2), "launches": launches,
+                "measured": "HIP events on the codec stream around the frame's DWT launches, mean of 5 lone 9/7 "
+                            "encodes after the timed region; traffic = PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE) of "
+                            "the same launches, profiles/dwt_pmc_latest.json"}
 
     # T1 figures: batch throughput + a lone frame's encode / decode T1 kernels
     with torch.cuda.stream(streams[0]):

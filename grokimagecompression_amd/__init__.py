@@ -188,6 +188,11 @@ class Stats(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class DwtOptions(ctypes.Structure):
+    """grkgpu_dwt_options (include/grk_mi355x.h)."""
+    _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64)]
+
+
 class LaunchTime(ctypes.Structure):
     """grkgpu_launch_time (include/grk_mi355x.h)."""
     _fields_ = [("kernel", ctypes.c_char * 48), ("level0", ctypes.c_uint32), ("levels", ctypes.c_uint32),
@@ -226,6 +231,9 @@ def lib():
         L.grkgpu_set_stream.argtypes = [VP, VP]
         L.grkgpu_get_stats.argtypes = [VP, P(Stats)]
         L.grkgpu_set_launch_timing.argtypes = [VP, ctypes.c_int]
+        L.grkgpu_get_dwt_options.argtypes = [P(DwtOptions)]
+        L.grkgpu_get_dwt_options.restype = None
+        L.grkgpu_set_dwt_options.argtypes = [P(DwtOptions)]
         L.grkgpu_get_launch_times.argtypes = [VP, P(LaunchTime), U32, P(U32)]
         L.grkgpu_default_cparams.argtypes = [P(CParams)]
         L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
@@ -522,6 +530,29 @@ class Codec:
         else:
             _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
         return out
+
+
+class dwt_options:
+    """Context manager over the process-wide DWT plan options
+    (grkgpu_set_dwt_options): e.g. ``with dwt_options(fuse_level0=0): ...``
+    runs the block with the separate DC shift / MCT pass; the previous options
+    come back on exit.  The defaults are the plans measured fastest."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.old = DwtOptions()
+        lib().grkgpu_get_dwt_options(ctypes.byref(self.old))
+        new = DwtOptions(self.old.fuse_level0, self.old.f01_rows, self.old.f01_min_samples)
+        for k, v in self.kw.items():
+            setattr(new, k, v)
+        _check(lib().grkgpu_set_dwt_options(ctypes.byref(new)))
+        return self
+
+    def __exit__(self, *exc):
+        _check(lib().grkgpu_set_dwt_options(ctypes.byref(self.old)))
+        return False
 
 
 # ---- stage entry points on torch device tensors (per-kernel parity tests) ----

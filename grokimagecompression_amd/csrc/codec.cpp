@@ -181,6 +181,36 @@ int grkgpu_set_stream(grkgpu_ctx *c, void *stream) {
     return GRKGPU_OK;
 }
 
+}  // extern "C"
+
+namespace grkgpu {
+static DwtOptions g_dwt_opts;
+const DwtOptions &dwt_options() { return g_dwt_opts; }
+}  // namespace grkgpu
+
+extern "C" {
+
+void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
+    if (!out) return;
+    out->fuse_level0 = g_dwt_opts.fuse_level0;
+    out->f01_rows = g_dwt_opts.f01_rows;
+    out->f01_min_samples = g_dwt_opts.f01_min_samples;
+}
+
+int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
+    if (!o) {
+        g_dwt_opts = DwtOptions();
+        return GRKGPU_OK;
+    }
+    if (o->fuse_level0 < -1 || o->fuse_level0 > 1) return set_err(GRKGPU_EINVAL, "fuse_level0 must be -1, 0 or 1");
+    if (o->f01_rows != 0 && o->f01_rows != 2 && o->f01_rows != 4 && o->f01_rows != 6)
+        return set_err(GRKGPU_EINVAL, "f01_rows must be 0, 2, 4 or 6");
+    g_dwt_opts.fuse_level0 = o->fuse_level0;
+    g_dwt_opts.f01_rows = o->f01_rows;
+    g_dwt_opts.f01_min_samples = o->f01_min_samples;
+    return GRKGPU_OK;
+}
+
 int grkgpu_set_launch_timing(grkgpu_ctx *c, int on) {
     if (!c) return set_err(GRKGPU_EINVAL, "null ctx");
     c->launch_timing = on != 0;
@@ -511,18 +541,16 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
 // the fused windows; GRKGPU_DWT_F01=0 keeps one launch per level.  Returns
 // the workgroups per job, 0 = not fused.
 static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev) {
-    const char *e = getenv("GRKGPU_DWT_F01"), *strip = getenv("GRKGPU_DWT_STRIP");
-    if (P.inverse || !irrev || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || (e && *e && !atoi(e))) return 0;
-    if (strip && *strip && atoi(strip)) return 0;  // the strip kernels' experiment keeps every level separate
+    const DwtOptions &o = dwt_options();
+    if (P.inverse || !irrev || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || !o.f01_rows) return 0;
     const auto &l0 = P.levels[li], &l1 = P.levels[li + 1];
     if (l0.empty() || l0.size() != l1.size()) return 0;
-    // only where the pair still fills the chip (GRKGPU_DWT_F01_MIN samples,
-    // default 2^23): the 8K frame's levels 2 + 3 fused took 26 us against
-    // 14 + 7 apart (378 workgroups)
-    const char *mn = getenv("GRKGPU_DWT_F01_MIN");
+    // only where the pair still fills the chip (f01_min_samples, default
+    // 2^23): the 8K frame's levels 2 + 3 fused took 26 us against 14 + 7
+    // apart (378 workgroups)
     uint64_t samples = 0;
     for (auto &j : l0) samples += (uint64_t)j.rw * j.rh;
-    if (samples < (mn && *mn ? (uint64_t)atoll(mn) : (uint64_t)1 << 23)) return 0;
+    if (samples < o.f01_min_samples) return 0;
     uint32_t maxt = 0;
     for (size_t i = 0; i < l0.size(); ++i) {
         const DwtJob &a = l0[i], &b = l1[i];
@@ -906,11 +934,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     // 132 (MCT pass) + 133 (level 0) on the 8K frame.  The 9/7 (ICT) triple
     // is left separate: fused 229 us vs 132 + 145, but the separate level-0
     // launch is the DWT whose roofline the bench reports.
-    // GRKGPU_DWT_FUSE=0/1 forces it off / on (1: also 9/7 and single
-    // components, DC shift in the loads).  Requires every tile-component to be
-    // decomposed at least once and to span its tile.
-    const char *fe = getenv("GRKGPU_DWT_FUSE");
-    bool fuse = fe && *fe ? atoi(fe) != 0 : (!cp.irrev && cp.mct && nc == 3);
+    // grkgpu_dwt_options.fuse_level0 = 0 / 1 forces it off / on (1: also 9/7
+    // and single components, DC shift in the loads).  Requires every
+    // tile-component to be decomposed at least once and to span its tile.
+    const int fo = dwt_options().fuse_level0;
+    bool fuse = fo >= 0 ? fo != 0 : (!cp.irrev && cp.mct && nc == 3);
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];

@@ -30,7 +30,6 @@
 #include <stdint.h>
 
 #include "grk_device.h"
-#include <stdlib.h>
 
 namespace grkgpu {
 
@@ -544,275 +543,6 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv(const DwtJob *__rest
 }
 
 // ---------------------------------------------------------------------------
-// Streaming kernels (big levels).  A wavefront walks NCH consecutive windows
-// down one 128-column strip and lifts vertically in a pipeline, so no input
-// row is loaded twice and no vertical lifting step is computed twice:
-//   * window 0 loads R = TH + 2*HALO raw rows and applies lifting step s
-//     (s = 1..4 for 9/7, 1..2 for 5/3) at window rows [s, R - s) of the
-//     step's parity -- exactly the positions whose inputs are complete;
-//   * the last C = 2*HALO rows are carried to the next window in that partial
-//     state; the next window appends TH new rows and applies step s at rows
-//     [C - s, R - s): precisely the positions the previous window could not
-//     finish, now that their neighbours exist;
-//   * in both cases window rows [HALO, HALO + TH) are final and are scaled,
-//     lifted horizontally and stored, as in k_dwt_fwd.
-// The next window's TH rows are loaded while the current one is lifted.
-// Used for resolutions of at least 16 x 16 (one reflection per edge).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int mirror_big(int p, int n) {
-    p = p < 0 ? -p : p;
-    p = p >= n ? 2 * (n - 1) - p : p;
-    return p < 0 ? 0 : p;  // rows far past the edge: any valid address (never kept)
-}
-
-// lifting step OP at rows k in [LO, HI) with k % 2 == PAR
-template <int OP, int PAR, int LO, int HI, int R>
-__device__ __forceinline__ void vrng(int32_t (&v)[R]) {
-#pragma unroll
-    for (int k = LO; k < HI; ++k)
-        if ((k & 1) == PAR) v[k] = lift<OP>(v[k], v[k - 1], v[k + 1]);
-}
-
-// forward vertical steps over a window; FIRST: all rows raw, else C carried
-template <bool IRREV, int R, int C, bool FIRST>
-__device__ __forceinline__ void fwd_vsteps(int32_t (&v)[R]) {
-    constexpr int B = FIRST ? 0 : C;  // step s starts at row B - s (FIRST: s)
-    if constexpr (!IRREV) {
-        vrng<0, 1, FIRST ? 1 : B - 1, R - 1>(v);
-        vrng<1, 0, FIRST ? 2 : B - 2, R - 2>(v);
-    } else {
-        vrng<2, 1, FIRST ? 1 : B - 1, R - 1>(v);
-        vrng<3, 0, FIRST ? 2 : B - 2, R - 2>(v);
-        vrng<4, 1, FIRST ? 3 : B - 3, R - 3>(v);
-        vrng<5, 0, FIRST ? 4 : B - 4, R - 4>(v);
-    }
-}
-
-template <bool IRREV, int R, int C, bool FIRST>
-__device__ __forceinline__ void inv_vsteps(int32_t (&v)[R]) {
-    constexpr int B = FIRST ? 0 : C;
-    if constexpr (!IRREV) {
-        vrng<6, 0, FIRST ? 1 : B - 1, R - 1>(v);
-        vrng<7, 1, FIRST ? 2 : B - 2, R - 2>(v);
-    } else {
-        vrng<8, 0, FIRST ? 1 : B - 1, R - 1>(v);
-        vrng<9, 1, FIRST ? 2 : B - 2, R - 2>(v);
-        vrng<10, 0, FIRST ? 3 : B - 3, R - 3>(v);
-        vrng<11, 1, FIRST ? 4 : B - 4, R - 4>(v);
-    }
-}
-
-// Load rows y0 .. y0+N-1 into lo/hi: one 8-byte load per lane per row when
-// the window's columns are inside and aligned, else two mirrored dword loads.
-template <int N>
-__device__ __forceinline__ void stream_load_fwd(int32_t (&lo)[N], int32_t (&hi)[N], rsrc_t in, int st, int y0, int rh,
-                                                bool vec, int gx0, int o0, int o1) {
-    const bool rows_in = y0 >= 0 && y0 + N <= rh;  // wave-uniform
-    if (vec) {
-#pragma unroll
-        for (int r = 0; r < N; ++r) {
-            const int so = (rows_in ? y0 + r : mirror_big(y0 + r, rh)) * st;
-            const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, so, 0);
-            lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < N; ++r) {
-            const int so = (rows_in ? y0 + r : mirror_big(y0 + r, rh)) * st;
-            lo[r] = ld32(in, o0, so); hi[r] = ld32(in, o1, so);
-        }
-    }
-}
-
-// strip of windows of this wavefront (same workgroup mapping as dwt_window)
-__device__ __forceinline__ bool dwt_strip(const DwtJob *__restrict__ jobs, int lay, int th, int nch, DwtJob &J,
-                                          int &tx, int &c0, int &c1) {
-    int ty;
-    if (!dwt_window(jobs, lay, th * nch, J, tx, ty)) return false;
-    const int nty = (J.rh + J.casy + th - 1) / th;
-    c0 = ty * nch;
-    c1 = min(c0 + nch, nty);
-    return true;
-}
-
-template <bool IRREV, int TH>
-__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_stream(const DwtJob *__restrict__ jobs, int nch, int lay) {
-    using G = DwtGeo<IRREV, TH>;
-    constexpr int R = G::R, C = 2 * G::HALO;
-    DwtJob J;
-    int tx, c0, c1;
-    if (!dwt_strip(jobs, lay, TH, nch, J, tx, c0, c1)) return;
-    const int lane = threadIdx.x & 63;
-    const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
-    const int xw = tx * G::CW - casx - G::HALO;
-    const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
-    const rsrc_t in = mkbuf(J.in, J.in_bytes);
-    const int st = (int)J.in_stride * 4;
-    const bool vec = (casx | (J.in_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
-    const int o0 = mirror_big(gx0, rw) * 4, o1 = mirror_big(gx1, rw) * 4;
-
-    const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
-    const bool lane_core = lane >= corel && lane < coreh;
-    const bool okx0 = lane_core && gx0 >= 0 && gx0 < rw, okx1 = lane_core && gx1 >= 0 && gx1 < rw;
-    const int vl = okx0 ? ((gx0 - casx) >> 1) * 4 : OOB;               // low-pass column -> L bands
-    const int vh = okx1 ? (J.snx + ((gx1 - 1 + casx) >> 1)) * 4 : OOB;  // high-pass column -> H bands
-    const rsrc_t outb = mkbuf(J.out, J.out_bytes), bandb = mkbuf(J.bands, J.bands_bytes);
-    const int ost = (int)J.out_stride * 4, bst = (int)J.bands_stride * 4;
-
-    int32_t lo[R], hi[R];
-    stream_load_fwd<R>(lo, hi, in, st, c0 * TH - casy - G::HALO, rh, vec, gx0, o0, o1);
-    for (int c = c0; c < c1; ++c) {
-        const int yw = c * TH - casy - G::HALO;
-        int32_t nlo[TH], nhi[TH];
-        if (c + 1 < c1) stream_load_fwd<TH>(nlo, nhi, in, st, yw + R, rh, vec, gx0, o0, o1);
-        if (c == c0) { fwd_vsteps<IRREV, R, C, true>(lo); fwd_vsteps<IRREV, R, C, true>(hi); }
-        else { fwd_vsteps<IRREV, R, C, false>(lo); fwd_vsteps<IRREV, R, C, false>(hi); }
-        const int lbase = c * (TH / 2) - casy - G::HALO / 2;
-        const int hbase = J.sny + c * (TH / 2) - G::HALO / 2;
-        const bool rows_all = yw + G::HALO >= 0 && yw + G::HALO + TH <= rh;  // wave-uniform
-#pragma unroll
-        for (int r = G::HALO; r < G::HALO + TH; ++r) {
-            int32_t L = lo[r], H = hi[r];
-            if (IRREV) {
-                const int32_t k = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
-                L = fixmul13(L, k); H = fixmul13(H, k);
-            }
-            if constexpr (!IRREV) {
-                H = lift<0>(H, L, from_next(L));
-                L = lift<1>(L, from_prev(H), H);
-            } else {
-                H = lift<2>(H, L, from_next(L));
-                L = lift<3>(L, from_prev(H), H);
-                H = lift<4>(H, L, from_next(L));
-                L = lift<5>(L, from_prev(H), H);
-                H = fixmul13(H, 5039);
-                L = fixmul13(L, 6659);
-            }
-            if (!rows_all) {
-                const int gy = yw + r;
-                if (gy < 0 || gy >= rh) continue;
-            }
-            if ((r & 1) == 0) {
-                const int iy = lbase + r / 2;
-                st32(L, outb, vl, iy * ost);
-                st32(H, bandb, vh, iy * bst);
-            } else {
-                const int so = (hbase + (r - 1) / 2) * bst;
-                st32(L, bandb, vl, so);
-                st32(H, bandb, vh, so);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < C; ++i) { lo[i] = lo[TH + i]; hi[i] = hi[TH + i]; }
-#pragma unroll
-        for (int i = 0; i < TH; ++i) { lo[C + i] = nlo[i]; hi[C + i] = nhi[i]; }
-    }
-}
-
-// Inverse: window row r of global row gy reads (mirrored) sub-band rows; even
-// rows from LL | HL, odd rows from LH | HH (mirroring keeps the parity).
-// Loaded rows are lifted horizontally and scaled for the vertical pass at
-// once (pointwise per row), so carried rows are never transformed twice.
-template <bool IRREV, int N>
-__device__ __forceinline__ void stream_load_inv(int32_t (&lo)[N], int32_t (&hi)[N], rsrc_t llb, rsrc_t cb, int lst,
-                                                int cst, int y0, int r0, int rh, int casy, int sny, int ix0,
-                                                int ix1) {
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-        const int my = mirror_big(y0 + r, rh);
-        if (((r0 + r) & 1) == 0) {
-            const int iy = (my - casy) >> 1;
-            lo[r] = ld32(llb, ix0, iy * lst);
-            hi[r] = ld32(cb, ix1, iy * cst);
-        } else {
-            const int so = (sny + ((my - 1 + casy) >> 1)) * cst;
-            lo[r] = ld32(cb, ix0, so);
-            hi[r] = ld32(cb, ix1, so);
-        }
-    }
-}
-
-template <bool IRREV, int N>
-__device__ __forceinline__ void inv_rows_h(int32_t (&lo)[N], int32_t (&hi)[N], int r0) {
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-        int32_t L = lo[r], H = hi[r];
-        if constexpr (!IRREV) {
-            L = lift<6>(L, from_prev(H), H);
-            H = lift<7>(H, L, from_next(L));
-        } else {
-            L = __float_as_int(__fmul_rn(__int_as_float(L), 1.230174105f));
-            H = __float_as_int(__fmul_rn(__int_as_float(H), 1.625732422f));
-            L = lift<8>(L, from_prev(H), H);
-            H = lift<9>(H, L, from_next(L));
-            L = lift<10>(L, from_prev(H), H);
-            H = lift<11>(H, L, from_next(L));
-            const float s = ((r0 + r) & 1) ? 1.625732422f : 1.230174105f;  // vertical scale of this row
-            L = __float_as_int(__fmul_rn(__int_as_float(L), s));
-            H = __float_as_int(__fmul_rn(__int_as_float(H), s));
-        }
-        lo[r] = L; hi[r] = H;
-    }
-}
-
-template <bool IRREV, int TH>
-__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv_stream(const DwtJob *__restrict__ jobs, int nch, int lay) {
-    using G = DwtGeo<IRREV, TH>;
-    constexpr int R = G::R, C = 2 * G::HALO;
-    DwtJob J;
-    int tx, c0, c1;
-    if (!dwt_strip(jobs, lay, TH, nch, J, tx, c0, c1)) return;
-    const int lane = threadIdx.x & 63;
-    const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
-    const int xw = tx * G::CW - casx - G::HALO;
-    const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
-    const int ix0 = ((mirror_big(gx0, rw) - casx) >> 1) * 4;
-    const int ix1 = (J.snx + ((mirror_big(gx1, rw) - 1 + casx) >> 1)) * 4;
-    const rsrc_t llb = mkbuf(J.in, J.in_bytes), cb = mkbuf(J.coef, J.coef_bytes);
-    const int lst = (int)J.in_stride * 4, cst = (int)J.coef_stride * 4;
-
-    const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
-    const bool lane_core = lane >= corel && lane < coreh;
-    const bool okx0 = lane_core && gx0 >= 0 && gx0 < rw, okx1 = lane_core && gx1 >= 0 && gx1 < rw;
-    const rsrc_t ob = mkbuf(J.out, J.out_bytes);
-    const int ost = (int)J.out_stride * 4;
-    const bool vec = (casx | (J.out_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= rw;  // wave-uniform
-    const int v0 = okx0 ? gx0 * 4 : OOB, v1 = okx1 ? gx1 * 4 : OOB;
-    const int vv = lane_core ? gx0 * 4 : OOB;
-
-    int32_t lo[R], hi[R];
-    stream_load_inv<IRREV, R>(lo, hi, llb, cb, lst, cst, c0 * TH - casy - G::HALO, 0, rh, casy, J.sny, ix0, ix1);
-    inv_rows_h<IRREV, R>(lo, hi, 0);
-    for (int c = c0; c < c1; ++c) {
-        const int yw = c * TH - casy - G::HALO;
-        int32_t nlo[TH], nhi[TH];
-        // next window's new rows C.. are this window's rows R.. (TH even: same parity)
-        if (c + 1 < c1)
-            stream_load_inv<IRREV, TH>(nlo, nhi, llb, cb, lst, cst, yw + R, R, rh, casy, J.sny, ix0, ix1);
-        if (c == c0) { inv_vsteps<IRREV, R, C, true>(lo); inv_vsteps<IRREV, R, C, true>(hi); }
-        else { inv_vsteps<IRREV, R, C, false>(lo); inv_vsteps<IRREV, R, C, false>(hi); }
-        const bool rows_all = yw + G::HALO >= 0 && yw + G::HALO + TH <= rh;  // wave-uniform
-#pragma unroll
-        for (int r = G::HALO; r < G::HALO + TH; ++r) {
-            const int gy = yw + r;
-            if (!rows_all && (gy < 0 || gy >= rh)) continue;
-            if (vec) {
-                const __attribute__((ext_vector_type(2))) uint32_t p = {(uint32_t)lo[r], (uint32_t)hi[r]};
-                __builtin_amdgcn_raw_buffer_store_b64(p, ob, vv, gy * ost, 0);
-            } else {
-                st32(lo[r], ob, v0, gy * ost);
-                st32(hi[r], ob, v1, gy * ost);
-            }
-        }
-        if (c + 1 < c1) inv_rows_h<IRREV, TH>(nlo, nhi, R);
-#pragma unroll
-        for (int i = 0; i < C; ++i) { lo[i] = lo[TH + i]; hi[i] = hi[TH + i]; }
-#pragma unroll
-        for (int i = 0; i < TH; ++i) { lo[C + i] = nlo[i]; hi[C + i] = nhi[i]; }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Forward levels 0 and 1 in one launch (9/7).  Level 1 reads level 0's LL
 // band, which the separate launches write to HBM and read back (2 x 4 B per
 // LL sample, a quarter of level 0's bytes); here a workgroup computes the LL
@@ -835,7 +565,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv_stream(const DwtJob 
 // level-1 windows is computed twice; in exchange 8 B per LL0 sample of HBM
 // traffic and one launch disappear.  (A variant walking 4 consecutive
 // 16-row windows per wavefront with the overlap rows carried in registers,
-// as k_dwt_fwd_stream, measured 189 us against 182 for NY = 4; non-temporal
+// measured 189 us against 182 for NY = 4; non-temporal
 // band stores 203 us.)
 // ---------------------------------------------------------------------------
 constexpr int F01_TH0 = 24;  // level-0 window rows
@@ -851,11 +581,9 @@ struct F01Geo {
     static_assert(THW * 4 == TH1 && THW % 2 == 0, "level-1 rows split into even per-wavefront windows");
 };
 
-static int env_int(const char *name, int dflt);
-// level-0 row windows per workgroup (GRKGPU_DWT_F01 = 2 / 4 / 6; 0 disables
-// the fusion on the host side)
+// level-0 row windows per workgroup (grkgpu_dwt_options.f01_rows = 2 / 4 / 6)
 int dwt01_ny() {
-    const int v = env_int("GRKGPU_DWT_F01", 4);
+    const int v = dwt_options().f01_rows;
     return v == 2 || v == 6 ? v : 4;
 }
 
@@ -984,70 +712,30 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// Rows per window: tall windows for big levels (less halo re-read), short
-// ones for small levels (more wavefronts, shorter per-wave chains).
-// GRKGPU_DWT_TH overrides the big-level choice (8/16/24/32).
-static int dwt_th_big(int irrev) {
-    static int th = [] {
-        const char *e = getenv("GRKGPU_DWT_TH");
-        int v = e ? atoi(e) : 0;
-        return (v == 8 || v == 16 || v == 24 || v == 32) ? v : 0;
-    }();
-    return th ? th : (irrev ? 24 : 32);
-}
-
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e && *e ? atoi(e) : dflt;
-}
-
-// Level geometry code: TH in the low byte; for the streaming kernels the
-// windows per strip (NCH) in bits 8..15.  GRKGPU_DWT_STRIP=1 selects the
-// streaming kernels for levels of at least GRKGPU_DWT_STRIP_MIN samples
-// (default 2^20) whose every resolution is at least 16 x 16 (GRKGPU_DWT_NCH,
-// GRKGPU_DWT_STH: windows per strip, window rows).  They are off by default:
-// on the 8K frame they read fewer bytes but ran 2-10 % slower than the
-// windowed kernels (fewer wavefronts in flight; the halo re-reads of the
-// windowed kernels hit in L2 -- FETCH_SIZE equals the algorithmic reads).
-// Read per call (the tests switch them in-process).
-int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh) {
-    if (env_int("GRKGPU_DWT_STRIP", 0) && minw >= 16 && minh >= 16 &&
-        level_samples >= (uint64_t)env_int("GRKGPU_DWT_STRIP_MIN", 1 << 20)) {
-        int th = env_int("GRKGPU_DWT_STH", irrev ? 16 : 16);
-        if (th != 8 && th != 16 && th != 24 && th != 32) th = 16;
-        int nch = env_int("GRKGPU_DWT_NCH", 8);
-        nch = nch < 1 ? 1 : (nch > 255 ? 255 : nch);
-        return th | (nch << 8);
-    }
-    // tall windows only where they still fill the chip (GRKGPU_DWT_BIGMIN samples)
-    return level_samples >= (uint64_t)env_int("GRKGPU_DWT_BIGMIN", 1 << 23) ? dwt_th_big(irrev) : 8;
+// Rows per window: tall windows for big levels (less halo re-read: 32 rows
+// for 5/3, 24 for 9/7 at >= 2^23 samples), short ones for small levels (more
+// wavefronts, shorter per-wave chains).
+int dwt_pick_th(int irrev, uint64_t level_samples, int, int) {
+    return level_samples >= ((uint64_t)1 << 23) ? (irrev ? 24 : 32) : 8;
 }
 
 void dwt_job_tiles(int irrev, int code, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles) {
-    const int th = code & 0xff, nch = code >> 8;
+    const int th = code & 0xff;
     const int cw = irrev ? DwtGeo<true, 8>::CW : DwtGeo<false, 8>::CW;
     const int tx = (rw + casx + cw - 1) / cw;
     int ty = (rh + casy + th - 1) / th;
-    if (nch) ty = (ty + nch - 1) / nch;                   // strips of nch windows
     ty = (ty + DWT_WAVES - 1) / DWT_WAVES * DWT_WAVES;  // whole workgroups (see dwt_window)
     *tiles_x = tx;
     *ntiles = tx * ty;
 }
 
+// Workgroup order: each XCD gets a contiguous run of windows (dwt_window bit 0).
+constexpr int kDwtLay = 1;
+
 template <int TH>
-static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int nch, int fused, int fmt,
+static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int inverse, int fused, int fmt,
                       hipStream_t s) {
-    const int lay = env_int("GRKGPU_DWT_LAY", 1);
-    if (nch) {
-        if (!inverse) {
-            if (irrev) hipLaunchKernelGGL((k_dwt_fwd_stream<true, TH>), grid, block, 0, s, jobs, nch, lay);
-            else hipLaunchKernelGGL((k_dwt_fwd_stream<false, TH>), grid, block, 0, s, jobs, nch, lay);
-        } else {
-            if (irrev) hipLaunchKernelGGL((k_dwt_inv_stream<true, TH>), grid, block, 0, s, jobs, nch, lay);
-            else hipLaunchKernelGGL((k_dwt_inv_stream<false, TH>), grid, block, 0, s, jobs, nch, lay);
-        }
-        return;
-    }
+    const int lay = kDwtLay;
     if (fused == 3) {  // forward level 0, MCT triples: one wavefront = the 3 components of one window
         const dim3 g3(grid.x, grid.y / 3);
 #define GRK_M3(S)                                                                         \
@@ -1079,7 +767,7 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
                             hipStream_t s) {
     if (!njobs || !max_tiles || !irrev) return hipErrorInvalidValue;
-    const int lay = env_int("GRKGPU_DWT_LAY", 1);
+    const int lay = kDwtLay;
     const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
     switch (dwt01_ny()) {
         case 2: hipLaunchKernelGGL((k_dwt_fwd01<true, 2>), g, b, 0, s, jobs0, jobs1, lay); break;
@@ -1093,16 +781,12 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
                            int inverse, hipStream_t s) {
     if (!njobs || !max_tiles) return hipSuccess;
     dim3 grid((max_tiles + DWT_WAVES - 1) / DWT_WAVES, njobs), block(64 * DWT_WAVES);
-    const int nch = (code >> 8) & 0xff;
-    const int fused = inverse || nch ? 0
-                      : (code & DWT_FUSED_MCT3) ? 3
-                      : (code & DWT_FUSED) ? 1 : 0;
+    const int fused = inverse ? 0 : (code & DWT_FUSED_MCT3) ? 3 : (code & DWT_FUSED) ? 1 : 0;
     const int fmt = (code >> DWT_FMT_SHIFT) & 7;  // image sample format of a fused level 0
     switch (code & 0xff) {
-        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
-        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
-        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
-        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, nch, fused, fmt, s); break;
+        case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
+        case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
+        case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -85,8 +85,16 @@ struct DwtJob {
     int32_t mct_mode, comp, src_vec;  // src_vec: pair loads allowed (base aligned to 2 samples, even stride)
     int32_t src_fmt, pad_;
 };
-// level geometry code (window rows | strip windows << 8) for a level of that
-// many samples whose smallest resolution is minw x minh
+// DWT plan options (grkgpu_dwt_options, set by grkgpu_set_dwt_options; the
+// defaults are the measured best -- the parity suite forces the others)
+struct DwtOptions {
+    int32_t fuse_level0 = -1;                    // -1: 3-component 5/3 tiles; 0 never; 1 always
+    int32_t f01_rows = 4;                        // 9/7 levels 0 + 1 fused: 2 / 4 / 6 row windows; 0 = apart
+    uint64_t f01_min_samples = (uint64_t)1 << 23;  // fuse a level pair from this many samples
+};
+const DwtOptions &dwt_options();
+// level geometry code (window rows) for a level of that many samples whose
+// smallest resolution is minw x minh
 int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh);
 constexpr int DWT_FUSED = 1 << 16;       // geometry-code flag: forward level with fused DC shift loads
 constexpr int DWT_FUSED_MCT3 = 1 << 17;  // ... with fused DC shift + MCT (jobs in component triples)

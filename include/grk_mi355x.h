@@ -158,6 +158,27 @@ int grkgpu_get_stats(grkgpu_ctx *ctx, grkgpu_stats *out);
  * events per launch), and read the launches of the last call: *n = their
  * count, the first min(max, *n) are copied to out. */
 int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
+
+/* DWT plan options, process-wide (later calls; not while other threads are
+ * inside a call).  The defaults are the plans measured fastest on the MI355X
+ * (DESIGN.md 3); the others stay selectable so the parity suite can check
+ * every kernel the library carries.
+ *   fuse_level0      -1 (default): the DC shift + RCT of a 3-component 5/3
+ *                    tile runs inside DWT level 0 (k_dwt_fwd_mct3); 0: never
+ *                    (separate k_dcshift_mct_fwd pass); 1: always (also 9/7
+ *                    and single components: DC shift in level 0's loads).
+ *   f01_rows         9/7 levels 0 + 1 in one launch (k_dwt_fwd01) with 2 / 4
+ *                    (default) / 6 level-0 row windows per workgroup; 0: one
+ *                    launch per level.
+ *   f01_min_samples  fuse a level pair only from this many level-l samples
+ *                    (default 2^23; 0: every qualifying pair). */
+typedef struct {
+    int32_t fuse_level0;
+    int32_t f01_rows;
+    uint64_t f01_min_samples;
+} grkgpu_dwt_options;
+void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
+int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */
 int grkgpu_get_launch_times(grkgpu_ctx *ctx, grkgpu_launch_time *out, uint32_t max, uint32_t *n);
 void grkgpu_default_cparams(grkgpu_cparams *p);
 

@@ -69,12 +69,17 @@ def test_decode_options_match_reference(codec, name, tag):
 
 @pytest.mark.parametrize("name", ["g8_off35", "rgb12_I", "rgb8_128x96", "rgb12_tiles_I", "g16_I", "rgb8_nomct",
                                   "g8_off_tiles"])
-def test_encode_fused_mct_dwt(codec, monkeypatch, name):
-    """Fused level 0 forced on (GRKGPU_DWT_FUSE=1: the DC shift in the first
-    DWT level's loads; MCT triples -- 9/7 included -- in one wavefront,
-    k_dwt_fwd_mct3): same bytes as the reference."""
+def test_encode_fused_mct_dwt(codec, name):
+    """Fused level 0 forced on (grkgpu_dwt_options.fuse_level0 = 1: the DC
+    shift in the first DWT level's loads; MCT triples -- 9/7 included -- in
+    one wavefront, k_dwt_fwd_mct3): same bytes as the reference."""
     import grokimagecompression_amd as grk
-    monkeypatch.setenv("GRKGPU_DWT_FUSE", "1")
+    with grk.dwt_options(fuse_level0=1):
+        _encode_matches(codec, name)
+
+
+def _encode_matches(codec, name):
+    import grokimagecompression_amd as grk
     m = MAN[name]
     img, bits = _img(m)
     p, off = grk.CParams.from_cli(m["args"])
@@ -82,16 +87,13 @@ def test_encode_fused_mct_dwt(codec, monkeypatch, name):
 
 
 @pytest.mark.parametrize("name", ["rgb8_128x96", "rgb12_96x80", "rgb16_64", "rgb8_r10_tiles", "rgb8_uniform_64"])
-def test_encode_unfused_rct(codec, monkeypatch, name):
+def test_encode_unfused_rct(codec, name):
     """A 3-component 5/3 tile fuses the DC shift + RCT into DWT level 0 by
-    default (k_dwt_fwd_mct3); GRKGPU_DWT_FUSE=0 keeps the separate
+    default (k_dwt_fwd_mct3); fuse_level0 = 0 keeps the separate
     k_dcshift_mct_fwd pass, which must give the same bytes."""
     import grokimagecompression_amd as grk
-    monkeypatch.setenv("GRKGPU_DWT_FUSE", "0")
-    m = MAN[name]
-    img, bits = _img(m)
-    p, off = grk.CParams.from_cli(m["args"])
-    assert codec.compress(img, bits, p, offset=off) == open(f"{GOLD}/{name}.j2k", "rb").read()
+    with grk.dwt_options(fuse_level0=0):
+        _encode_matches(codec, name)
 
 
 def test_device_resident_roundtrip(codec):
@@ -145,61 +147,25 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
 @pytest.mark.parametrize("numres", [3, 6])
-def test_dwt_fused01_stage_vs_oracle(oracle, monkeypatch, ny, shape_off, numres):
+def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
     """9/7 level pairs in one launch (k_dwt_fwd01, LL in LDS; default for
     pairs of >= 2^23 samples whose resolutions are >= 16 x 16, here forced
     onto every qualifying pair: 0+1, 2+3, ...), at each workgroup height
-    (GRKGPU_DWT_F01 = 2 / 4 / 6 level-0 row windows; 0 = two launches), on
-    odd sizes and offsets (every cas parity, image edges inside the windows)."""
+    (grkgpu_dwt_options.f01_rows = 2 / 4 / 6 level-0 row windows; 0 = two
+    launches), on odd sizes and offsets (every cas parity, image edges inside
+    the windows)."""
     import torch
     import grokimagecompression_amd as grk
-    monkeypatch.setenv("GRKGPU_DWT_F01", ny)
-    monkeypatch.setenv("GRKGPU_DWT_F01_MIN", "0")  # fuse every qualifying pair, not only chip-filling ones
     (h, w), (x0, y0) = shape_off
     rng = np.random.default_rng(h * 31 + w + numres)
     a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
     ref = oracle.dwt_fwd(a, x0, y0, numres, True)
     t = torch.from_numpy(a).cuda()
-    grk.dwt_fwd(t, x0, y0, numres, True)
-    torch.cuda.synchronize()
-    assert np.array_equal(t.cpu().numpy(), ref)
-
-
-@pytest.mark.parametrize("irrev", [False, True])
-@pytest.mark.parametrize("shape_off", [((64, 64), (0, 0)), ((77, 100), (3, 5)), ((129, 200), (1, 1)),
-                                       ((513, 257), (0, 3)), ((300, 497), (2, 2)), ((37, 260), (1, 1)),
-                                       ((16, 16), (1, 1)), ((700, 1030), (1, 0))])
-@pytest.mark.parametrize("sth_nch", [(8, 1), (16, 3), (24, 2), (32, 8)])
-def test_dwt_strip_stage_vs_oracle(oracle, monkeypatch, irrev, shape_off, sth_nch):
-    """The strip kernels (windows walking down 128-column strips with the
-    overlap rows carried in registers) forced onto every level they accept
-    (resolutions >= 16 x 16), at several window heights and strip lengths."""
-    import torch
-    import grokimagecompression_amd as grk
-    monkeypatch.setenv("GRKGPU_DWT_STRIP", "1")
-    monkeypatch.setenv("GRKGPU_DWT_STRIP_MIN", "0")
-    monkeypatch.setenv("GRKGPU_DWT_STH", str(sth_nch[0]))
-    monkeypatch.setenv("GRKGPU_DWT_NCH", str(sth_nch[1]))
-    (h, w), (x0, y0) = shape_off
-    numres = 5
-    rng = np.random.default_rng(h * 7 + w + sth_nch[0])
-    a = rng.integers(-(1 << 20) if irrev else -4096, 1 << 20 if irrev else 4096, size=(h, w)).astype(np.int32)
-    ref = oracle.dwt_fwd(a, x0, y0, numres, irrev)
-    t = torch.from_numpy(a).cuda()
-    grk.dwt_fwd(t, x0, y0, numres, irrev)
-    torch.cuda.synchronize()
-    assert np.array_equal(t.cpu().numpy(), ref)
-    if not irrev:
-        grk.dwt_inv(t, x0, y0, numres, False)
+    # fuse every qualifying pair, not only chip-filling ones
+    with grk.dwt_options(f01_rows=int(ny), f01_min_samples=0):
+        grk.dwt_fwd(t, x0, y0, numres, True)
         torch.cuda.synchronize()
-        assert np.array_equal(t.cpu().numpy(), a)
-    else:
-        f = (rng.standard_normal((h, w)) * 100).astype(np.float32).view(np.int32)
-        ref = oracle.dwt_inv(f, x0, y0, numres, True)
-        t = torch.from_numpy(f.copy()).cuda()
-        grk.dwt_inv(t, x0, y0, numres, True)
-        torch.cuda.synchronize()
-        assert np.array_equal(t.cpu().numpy(), ref)
+    assert np.array_equal(t.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("irrev", [False, True])
