@@ -26,6 +26,7 @@
 #include "../../include/grk_mi355x.h"
 #include "codestream.h"
 #include "grk_device.h"
+#include "host_pool.h"
 #include "t2.h"
 
 using namespace grkgpu;
@@ -1206,47 +1207,75 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         tile_bound = ts - 12 - pocsz - 4;
     }
     std::vector<uint8_t> tlm;  // TLM records (j2k_update_tlm, j2k.cpp:6649-6660)
-    double t_rate = 0;
-    std::vector<PacketId> order;
-    for (auto &tile : tiles) {
-        TileEnc tenc;
-        tenc.tile = &tile;
-        tenc.cblk = &cst;
-        tenc.passes = &passes;
-        tenc.layers = &layers;
-        init_enc_pocs(cp, tenc);
-        CodingParams cpt = cp;
-        uint32_t ntp = 0;
-        for (uint32_t v : tp_counts[tile.index]) ntp += v;
-        tile_rates(tile.r, ntp, cpt.rates);
-        tenc.distotile = 0;
-        for (auto &tc : tile.comps) for_each_cblk(tc, [&](Band &, Cblk &cb) { tenc.distotile += blk_disto[cb.gidx]; });
-        const double tr0 = now_ms();
-        if (!rate_allocate(cpt, tenc, tile_bound)) return set_err(GRKGPU_EINVAL, "rate allocation failed");
-        t_rate += now_ms() - tr0;
-        tenc.packno = 0;
-        uint32_t tpno = 0;
-        for (uint32_t pino = 0; pino < tenc.pocs.size(); ++pino) {
-            for (uint32_t tpn = 0; tpn < tp_counts[tile.index][pino]; ++tpn) {
-                const size_t sot = hdr.size();
-                hdr.put16(0xFF90); hdr.put16(10); hdr.put16(tile.index); hdr.put32(0); hdr.put8(tpno); hdr.put8(ntp);
-                if (tpno == 0 && !cinema && cp.numpocs) write_poc(hdr, cpt);
-                hdr.put16(0xFF93);
-                plan.push_back({sot, (uint32_t)(hdr.size() - sot), 0});
-                const size_t first = plan.size() - 1;
-                encode_packet_order(cpt, tenc, pino, tpn, order);
-                for (auto &pk : order)
-                    if (pk.layno < L) write_packet(cpt, tenc, pk, hdr, plan);
-                uint64_t psot = 0;
-                for (size_t i = first; i < plan.size(); ++i) psot += plan[i].len;
-                hdr.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
-                if (cinema) {
-                    tlm.push_back((uint8_t)tile.index);
-                    for (int b = 3; b >= 0; --b) tlm.push_back((uint8_t)(psot >> (8 * b)));
+    // Tiles are independent in rate control and Tier-2 (their blocks, layer
+    // records and packet state are disjoint): each tile's tile-parts are
+    // formed on the host pool into its own header blob and plan, then
+    // appended in tile order (header runs rebased onto the shared blob).
+    struct TileOut {
+        ByteBuf hdr;
+        std::vector<PlanItem> plan;
+        std::vector<uint8_t> tlm;
+        double rate_ms = 0;
+        bool ok = true;
+    };
+    std::vector<TileOut> touts(tiles.size());
+    double t_rate = 0;  // summed over tiles (host CPU time of the rate allocation)
+    host_parallel_for(tiles.size(), 1, [&](size_t t0, size_t t1) {
+        std::vector<PacketId> order;
+        for (size_t ti = t0; ti < t1; ++ti) {
+            Tile &tile = tiles[ti];
+            TileOut &to = touts[ti];
+            TileEnc tenc;
+            tenc.tile = &tile;
+            tenc.cblk = &cst;
+            tenc.passes = &passes;
+            tenc.layers = &layers;
+            init_enc_pocs(cp, tenc);
+            CodingParams cpt = cp;
+            uint32_t ntp = 0;
+            for (uint32_t v : tp_counts[tile.index]) ntp += v;
+            tile_rates(tile.r, ntp, cpt.rates);
+            tenc.distotile = 0;
+            for (auto &tc : tile.comps) for_each_cblk(tc, [&](Band &, Cblk &cb) { tenc.distotile += blk_disto[cb.gidx]; });
+            const double tr0 = now_ms();
+            if (!rate_allocate(cpt, tenc, tile_bound)) { to.ok = false; continue; }
+            to.rate_ms = now_ms() - tr0;
+            tenc.packno = 0;
+            uint32_t tpno = 0;
+            ByteBuf &th = to.hdr;
+            for (uint32_t pino = 0; pino < tenc.pocs.size(); ++pino) {
+                for (uint32_t tpn = 0; tpn < tp_counts[tile.index][pino]; ++tpn) {
+                    const size_t sot = th.size();
+                    th.put16(0xFF90); th.put16(10); th.put16(tile.index); th.put32(0); th.put8(tpno); th.put8(ntp);
+                    if (tpno == 0 && !cinema && cp.numpocs) write_poc(th, cpt);
+                    th.put16(0xFF93);
+                    to.plan.push_back({sot, (uint32_t)(th.size() - sot), 0});
+                    const size_t first = to.plan.size() - 1;
+                    encode_packet_order(cpt, tenc, pino, tpn, order);
+                    for (auto &pk : order)
+                        if (pk.layno < L) write_packet(cpt, tenc, pk, th, to.plan);
+                    uint64_t psot = 0;
+                    for (size_t i = first; i < to.plan.size(); ++i) psot += to.plan[i].len;
+                    th.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
+                    if (cinema) {
+                        to.tlm.push_back((uint8_t)tile.index);
+                        for (int b = 3; b >= 0; --b) to.tlm.push_back((uint8_t)(psot >> (8 * b)));
+                    }
+                    ++tpno;
                 }
-                ++tpno;
             }
         }
+    });
+    for (auto &to : touts) {
+        if (!to.ok) return set_err(GRKGPU_EINVAL, "rate allocation failed");
+        t_rate += to.rate_ms;
+        const uint64_t base = hdr.size();
+        hdr.putn(to.hdr.v.data(), to.hdr.size());
+        for (PlanItem it : to.plan) {
+            if (it.kind == 0) it.src += base;
+            plan.push_back(it);
+        }
+        tlm.insert(tlm.end(), to.tlm.begin(), to.tlm.end());
     }
     if ((parts & GRKGPU_PART_HEADER) && tlm_at && tlm.size() == 5ull * total_tile_parts)
         memcpy(hdr.v.data() + tlm_at, tlm.data(), tlm.size());  // j2k_write_updated_tlm (:2555-2577)
@@ -1550,56 +1579,74 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     for (uint32_t k = 0; k < cp.numcomps; ++k) any_roi = any_roi || cp.roishift[k];
     std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
-    std::vector<uint8_t> tilebuf;
     bool too_deep = false;
+    // Packet headers of the tiles, parsed in parallel on the host pool (each
+    // tile's geometry, tag trees and code-block segments are its own); then
+    // the arenas and the DecBlock table in tile order.
+    std::vector<std::vector<uint8_t>> tbufs(nsh);  // tiles of several tile-parts: their data concatenated
+    std::vector<uint8_t> contig(nsh, 1);
+    std::vector<int> terr(nsh, 0);                 // 1: bad POC marker, 2: corrupt packet header
+    host_parallel_for(nsh, 1, [&](size_t l0, size_t l1) {
+        for (size_t lt = l0; lt < l1; ++lt) {
+            const uint32_t t = tb + (uint32_t)lt;
+            Tile &tile = tiles[lt];
+            tile.index = t;
+            tile.r = tile_rect(cp, t);
+            if (win && !overlap(tile.r, wr)) continue;  // left without components: skipped below
+            tile.comps.resize(nc);
+            for (uint32_t k = 0; k < nc; ++k) build_tilecomp(tile.comps[k], tile.r, cp, k, false);
+            // tile data: single tile-part -> decode in place; else concatenate
+            const uint8_t *td;
+            size_t tlen;
+            uint64_t base;
+            contig[lt] = tparts[t].size() <= 1;
+            if (contig[lt]) {
+                td = tparts[t].empty() ? csb : csb + tparts[t][0].first;
+                tlen = tparts[t].empty() ? 0 : tparts[t][0].second;
+                base = tparts[t].empty() ? 0 : tparts[t][0].first;
+            } else {
+                std::vector<uint8_t> &tbuf = tbufs[lt];
+                for (auto &pp : tparts[t]) tbuf.insert(tbuf.end(), csb + pp.first, csb + pp.first + pp.second);
+                td = tbuf.data();
+                tlen = tbuf.size();
+                base = 0;
+            }
+            // packets in the tile's progression (T2::decode_packets, T2.cpp:194-258),
+            // POC entries of the main header followed by the tile's own
+            CodingParams tcp = cp;
+            bool ok = true;
+            for (auto &pc : tpocs[t]) ok = ok && parse_poc(csb + pc.first, pc.second, tcp);
+            if (!ok) { terr[lt] = 1; continue; }
+            std::vector<PacketId> order;
+            decode_packet_order(tcp, tile, order);
+            size_t off = 0;
+            uint32_t packno = 0;
+            for (const auto &pk : order) {
+                if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
+                const bool skip = max_layers && pk.layno >= max_layers;
+                int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
+                                             base + off, tcp.csty, &packno, skip, tcp.cblksty);
+                if (used < 0) { terr[lt] = 2; break; }
+                off += (size_t)used;
+            }
+        }
+    });
     for (uint32_t lt = 0; lt < nsh; ++lt) {
-        const uint32_t t = tb + lt;
+        if (terr[lt] == 1) return set_err(GRKGPU_ECORRUPT, "Error reading POC marker");
+        if (terr[lt] == 2) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
+    }
+    for (uint32_t lt = 0; lt < nsh; ++lt) {
         Tile &tile = tiles[lt];
-        tile.index = t;
-        tile.r = tile_rect(cp, t);
-        if (win && !overlap(tile.r, wr)) continue;  // left without components: skipped below
-        tile.comps.resize(nc);
+        if (tile.comps.empty()) continue;
         for (uint32_t k = 0; k < nc; ++k) {
-            build_tilecomp(tile.comps[k], tile.r, cp, k, false);
             tile.comps[k].arena_off = arena;
             uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
             arena += (area + 63) & ~63ull;
             lloff[lt * nc + k] = llarena;
             llarena += ll_geom(tile.comps[k]).elems;
         }
-        // tile data: single tile-part -> decode in place; else concatenate
-        const uint8_t *td;
-        size_t tlen;
-        uint64_t base;
-        bool contiguous = tparts[t].size() <= 1;
-        if (contiguous) {
-            td = tparts[t].empty() ? csb : csb + tparts[t][0].first;
-            tlen = tparts[t].empty() ? 0 : tparts[t][0].second;
-            base = tparts[t].empty() ? 0 : tparts[t][0].first;
-        } else {
-            tilebuf.clear();
-            for (auto &pp : tparts[t]) tilebuf.insert(tilebuf.end(), csb + pp.first, csb + pp.first + pp.second);
-            td = tilebuf.data();
-            tlen = tilebuf.size();
-            base = 0;
-        }
-        // packets in the tile's progression (T2::decode_packets, T2.cpp:194-258),
-        // POC entries of the main header followed by the tile's own
-        CodingParams tcp = cp;
-        for (auto &pc : tpocs[t])
-            if (!parse_poc(csb + pc.first, pc.second, tcp)) return set_err(GRKGPU_ECORRUPT, "Error reading POC marker");
-        std::vector<PacketId> order;
-        decode_packet_order(tcp, tile, order);
-        size_t off = 0;
-        uint32_t packno = 0;
-        for (const auto &pk : order) {
-            if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
-            const bool skip = max_layers && pk.layno >= max_layers;
-            int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
-                                         base + off, tcp.csty, &packno, skip, tcp.cblksty);
-            if (used < 0) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
-            off += (size_t)used;
-        }
+        const bool contiguous = contig[lt] != 0;
+        const std::vector<uint8_t> &tilebuf = tbufs[lt];
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
             const BandNeed need = win ? window_need(tc, wr) : BandNeed();
