@@ -414,6 +414,8 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
     __shared__ uint32_t s_cx[LANES * 21];
+    __shared__ uint32_t s_ring[LANES * FB_RING];  // bit readers' word rings (t1_flat.h FlatBits), slot stride 64
+    static_assert(LANES == 64, "the word rings interleave 64 lanes");
     for (uint32_t k = threadIdx.x; k < 2048; k += LANES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
     for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
     for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
@@ -442,6 +444,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
         for (uint32_t y = 0; y < b.h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
         mq_reset_words(cxw, T.mq);
         BitDecT<LAZY> d;
+        d.set_ring(s_ring + threadIdx.x, 6);
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
         SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
         t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, st, T, cxw, pa, pb, sty, cur, roi ? roi[i] : 0u);
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     }
     const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
     t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, st, T,
-                 cxw, pa, pb);
+                 cxw, pa, pb, s_ring + threadIdx.x, 6);
 }
 
 // Rebuild of the decoded values from the lane-interleaved bit-plane rows:

@@ -21,6 +21,13 @@
 #pragma once
 #include "t1_lane.h"
 
+// T1_WALK(event, value): a host analysis hook on the walk (pass start: 0,
+// pass type; stripe start: 1, row; column start: 2, column); empty in the
+// library (tests/cpp/t1_walk_sim.cpp defines it).
+#ifndef T1_WALK
+#define T1_WALK(ev, v)
+#endif
+
 namespace grkgpu {
 
 // sign LUT in window order: bit0 sigN, 1 negN, 2 sigW, 3 negW, 4 sigE, 5 negE,
@@ -70,6 +77,7 @@ struct DecTables {
 template <int CUP_, class D>
 GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr, bool cup_rt = false) {
     const bool CUP = CUP_ < 0 ? cup_rt : CUP_ != 0;
+    T1_WALK(2, x);
     uint32_t P = win18(s.sig, x);
     const uint32_t vis4 = col4(s.vis, x);
     const uint32_t rows = (1u << nr) - 1;
@@ -135,6 +143,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
 // magnitude refinement of one column
 template <class D>
 GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+    T1_WALK(2, x);
     const uint32_t P = win18(s.sig, x);
     const uint32_t rows = (1u << nr) - 1;
     uint32_t m4 = win_self4(P) & ~col4(s.vis, x) & rows;
@@ -181,6 +190,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
     int passtype = 2;
     for (uint32_t passno = 0; passno < numpasses && bpno >= 0; ++passno) {
         segs.at_pass(d, passno, t1_pass_raw(sty, bpno, passtype, rawbps));
+        T1_WALK(0, passtype);
         const RP sa = sigafter + (uint32_t)bpno * 64;
         const RP rb = refbit + (uint32_t)bpno * 64;
         // Each pass type loads and stores only the state rows it reads or
@@ -189,6 +199,8 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
         // fewer VGPRs for the lane decoder and fewer state round trips.
         for (uint32_t k = 0; k < h; k += 4) {
             const uint32_t nr = h - k < 4 ? h - k : 4;
+            d.fill();  // the bit source tops up its word ring with the stripe's row loads
+            T1_WALK(1, k);
             Stripe s;
 #pragma unroll
             for (int i = 0; i < 6; ++i) s.sig[i] = st.sig[k + i];

@@ -83,16 +83,26 @@ GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, u
 
 // ---------------------------------------------------------------------------
 // Bit reader over the unstuffed words: 64-bit MSB-aligned window W holding
-// NB >= 32 valid bits after every refill; 4-word chunks (uint4) are fetched
-// when the current one is used up (no prefetch register: the decoder's VGPR
-// budget sets its occupancy).  Past the end it returns 1-bits.
+// NB >= 32 valid bits after every refill, fed one word at a time from a
+// per-lane ring of FB_RING words (LDS on the device: word j of a lane at
+// ring[(j % FB_RING) << rsh], so the 64 lanes' words of one slot sit in 64
+// different banks).  The ring is topped up from the stream in HBM at the
+// start of every stripe (fill: one or two 16-byte chunks, loaded together
+// with the stripe's state rows, whose wait the decoder pays anyway); inside
+// the stripe a refill is an LDS read, and only a ring that runs dry (a
+// stripe coding more than ~300 bits) waits on HBM.  Fetching the stream
+// straight from HBM at each 16-byte boundary stalled the whole wavefront on
+// a memory round trip about every second decision step (64 lanes, ~130
+// decisions per chunk each).  Past the end of the stream it returns 1-bits.
 // ---------------------------------------------------------------------------
+constexpr uint32_t FB_RING = 16;  // words per lane
 struct FlatBits {
     uint64_t W;
     uint32_t NB;
-    uint4 cur;
-    uint32_t wi;            // next word of `cur` (0..3)
-    uint32_t chunk;         // index of the chunk held in `cur`
+    uint32_t *ring;         // this lane's ring (see above)
+    uint32_t rsh;           // slot stride = 1 << rsh words
+    uint32_t rp, wp;        // words taken from / put into the ring (wp - rp held)
+    uint32_t chunk;         // next chunk of the stream to fetch
     uint32_t nchunks;
     const uint4 *base;
 };
@@ -101,12 +111,44 @@ struct FlatBits {
 // the last chunk (no branch around the load, no select on its result)
 GRK_HD uint4 fb_load(const FlatBits &b, uint32_t ci) { return b.base[ci < b.nchunks ? ci : b.nchunks - 1]; }
 
-GRK_HD uint32_t fb_word(FlatBits &b) {
-    const uint32_t v = b.wi == 0 ? b.cur.x : b.wi == 1 ? b.cur.y : b.wi == 2 ? b.cur.z : b.cur.w;
-    if (++b.wi == 4) {
-        b.wi = 0;
-        b.cur = fb_load(b, ++b.chunk);  // no chunk prefetch: 4 VGPRs fewer (decoder occupancy)
+GRK_HD void fb_put(FlatBits &b, const uint4 &c) {
+    b.ring[((b.wp + 0) % FB_RING) << b.rsh] = c.x;
+    b.ring[((b.wp + 1) % FB_RING) << b.rsh] = c.y;
+    b.ring[((b.wp + 2) % FB_RING) << b.rsh] = c.z;
+    b.ring[((b.wp + 3) % FB_RING) << b.rsh] = c.w;
+    b.wp += 4;
+}
+
+// top the ring up to at least FB_RING - 4 words (both chunk loads issued
+// before either is stored)
+GRK_HD void fb_fill(FlatBits &b) {
+    const uint32_t held = b.wp - b.rp;
+    if (held <= FB_RING - 8) {
+        const uint4 c0 = fb_load(b, b.chunk), c1 = fb_load(b, b.chunk + 1);
+        b.chunk += 2;
+        fb_put(b, c0);
+        fb_put(b, c1);
+    } else if (held <= FB_RING - 4) {
+        const uint4 c0 = fb_load(b, b.chunk++);
+        fb_put(b, c0);
     }
+}
+
+GRK_HD void fb_start(FlatBits &b, const uint32_t *words, uint32_t nwords) {
+    b.base = (const uint4 *)words;
+    b.nchunks = (nwords + 3) >> 2;
+    b.chunk = 0;
+    b.rp = b.wp = 0;
+    fb_fill(b);
+}
+
+GRK_HD uint32_t fb_word(FlatBits &b) {
+    if (b.wp == b.rp) {  // dry: straight from HBM
+        const uint4 c0 = fb_load(b, b.chunk++);
+        fb_put(b, c0);
+    }
+    const uint32_t v = b.ring[(b.rp % FB_RING) << b.rsh];
+    ++b.rp;
     return v;
 }
 
@@ -120,18 +162,21 @@ template <bool LAZY>
 struct BitDecT {
     static constexpr bool kLazy = LAZY;
     FlatBits bits;
-    uint32_t A, C, consumed, cq;
+    uint32_t A, C, consumed, cq, cqn;  // cq: next carry event, cqn: the one after
     const uint32_t *cp;
     bool raw;  // the current segment is raw (BYPASS): bits straight from the stream
+    // the lane's word ring (FlatBits), set once before the first init
+    GRK_HD void set_ring(uint32_t *ring, uint32_t rsh) {
+        bits.ring = ring;
+        bits.rsh = rsh;
+    }
+    // stripe start (t1_decode_passes): top the word ring up from HBM
+    GRK_HD void fill() { fb_fill(bits); }
     // raw segment (mqc_raw_init_dec / mqc_raw_decode, mqc_dec.cpp:195-200,
     // mqc_dec_inl.h:90-112): the unstuffed stream IS the raw bit sequence --
     // 7 bits from the byte after a 0xFF, 1-bits from a marker on
     GRK_HD void init_raw(const uint32_t *words, uint32_t nwords) {
-        bits.base = (const uint4 *)words;
-        bits.nchunks = (nwords + 3) >> 2;
-        bits.cur = fb_load(bits, 0);
-        bits.chunk = 0;
-        bits.wi = 0;
+        fb_start(bits, words, nwords);
         const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
         bits.W = (w0 << 32) | w1;
         bits.NB = 64;
@@ -148,11 +193,7 @@ struct BitDecT {
     }
     GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
         raw = false;
-        bits.base = (const uint4 *)words;
-        bits.nchunks = (nwords + 3) >> 2;
-        bits.cur = fb_load(bits, 0);
-        bits.chunk = 0;
-        bits.wi = 0;
+        fb_start(bits, words, nwords);
         const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
         const uint64_t v = (w0 << 32) | w1;
         C = (uint32_t)(v >> 33);  // first 31 stream bits (INITDEC: consumed 24, then 7 shifts)
@@ -163,6 +204,13 @@ struct BitDecT {
         cq = carries[0];
         cp = carries + 1;
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
+        cqn = cq == 0xffffffffu ? cq : *cp++;  // the sentinel ends the list: never read past it
+    }
+    // the carry event after the one just applied: cqn was loaded one event
+    // earlier, so the per-decision compare never waits on a load
+    GRK_HD void next_carry() {
+        cq = cqn;
+        cqn = cq == 0xffffffffu ? cq : *cp++;
     }
     GRK_HD uint32_t decode(uint32_t *cxw, const uint32_t *tab, uint32_t cx) {
         if constexpr (LAZY) {
@@ -185,7 +233,7 @@ struct BitDecT {
         bits.NB -= n;
         A = a << n;
         const uint32_t c1 = consumed + n;
-        if (cq < c1) { C += 1u << (16 + c1 - cq); cq = *cp++; }  // carry event (see Unstuff)
+        if (cq < c1) { C += 1u << (16 + c1 - cq); next_carry(); }  // carry event (see Unstuff)
         consumed = c1;
         if (bits.NB < 32) {
             bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
@@ -227,13 +275,15 @@ struct SegCursor {
 
 // v5: the nested pass / stripe / column walk (lanes of a wavefront stay
 // converged on the pass structure) fed by the unstuffed bit stream.
+// ring / rsh: the lane's word ring (FlatBits).
 template <class ST = BlockState, class RP = uint64_t *>
 GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
                          uint32_t numbps, uint32_t w, uint32_t h, ST &st, const DecTables &T, uint32_t *cxw,
-                         RP sa, RP rb) {
+                         RP sa, RP rb, uint32_t *ring, uint32_t rsh) {
     for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
     mq_reset_words(cxw, T.mq);
     BitDec d;
+    d.set_ring(ring, rsh);
     d.init(words, nwords, carries);
     t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sa, rb);
 }

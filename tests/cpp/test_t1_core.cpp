@@ -96,7 +96,8 @@ int main(int argc, char **argv) {
             std::fill(scr.pa, scr.pa + 32 * 64, ~0ull);
             std::fill(scr.pb, scr.pb + 32 * 64, ~0ull);
             for (int i = 0; i < 66; ++i) { scr.st.sig[i] = scr.st.neg[i] = scr.st.vis[i] = scr.st.ref[i] = ~0ull; }
-            t1_decode_v5(wp, nw, carr.data(), np, onb, w, h, scr.st, DT, cx4, scr.pa, scr.pb);
+            uint32_t ring[FB_RING];
+            t1_decode_v5(wp, nw, carr.data(), np, onb, w, h, scr.st, DT, cx4, scr.pa, scr.pb, ring, 0);
             std::vector<int32_t> v5(w * h);
             for (uint32_t y = 0; y < h; ++y)
                 for (uint32_t x = 0; x < w; ++x) v5[y * w + x] = t1_rebuild(x, y, dp, scr.pa, scr.pb, scr.st.neg[y + 1]);
