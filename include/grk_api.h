@@ -18,12 +18,15 @@
  *   - coding options of grk_mi355x.h: any tiling, 5/3 or 9/7, RCT / ICT,
  *     code-block sizes, precincts, the five progressions, POC, SOP / EPH,
  *     tile-parts, quality layers with -r / -q rate control (both PCRD
- *     algorithms), the cinema 2K / 4K profiles; not code-block mode switches
- *     (cblk_sty), HTJ2K (isHT), ROI, custom MCT (grk_set_MCT);
- *   - decode: whole image, cp_reduce, cp_layer, grk_set_decode_area windows
- *     and single tiles (grk_get_decoded_tile); tile-by-tile streaming
- *     (grk_read_tile_header / grk_decode_tile_data / grk_write_tile) is not
- *     provided, nor codestream index / info objects;
+ *     algorithms), the cinema 2K / 4K profiles, the code-block mode switches
+ *     (cblk_sty BYPASS / RESET / TERMALL / VSC / PTERM / SEGSYM) and ROI
+ *     (roi_compno / roi_shift); not HTJ2K (isHT) or custom MCT (grk_set_MCT);
+ *   - encode tile by tile: grk_write_tile (tiles in order, as the reference's
+ *     test_tile_encoder);
+ *   - decode: whole image, cp_reduce, cp_layer, grk_set_decode_area windows,
+ *     single tiles (grk_get_decoded_tile) and tile-by-tile streaming
+ *     (grk_read_tile_header / grk_decode_tile_data); codestream index / info
+ *     objects (grk_get_cstr_info / grk_get_cstr_index) are not provided;
  *   - the plugin entry points report "no plugin" (this library IS the
  *     accelerated path).
  */
