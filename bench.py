@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[2], the metric's 8K RGB case): synthetic
 the image whose reference codestream hashes are pinned in
 tests/golden/manifest_large.json).  One step = per pair of codec contexts,
 encode + decode of the frame with the 9/7 irreversible path (grk_compress -I)
-and encode + decode with the 5/3 lossless path; 6 such pairs (12 frames) are in
+and encode + decode with the 5/3 lossless path; 8 such pairs (16 frames) are in
 flight per GPU, each on its own codec context, HIP stream and host thread.
 
   value            SURVEY 8(d)'s metric: every frame starts in pinned host
@@ -69,7 +69,7 @@ if int(_arg("--gpus", "1")) > 1 and "WORLD_SIZE" not in os.environ:
 # reads the value when the process starts, so with fewer than needed the bench
 # reruns itself as a child process (nothing has touched the GPU yet) and exits
 # with the child's status.
-HW_QUEUES = min(32, max(16, int(_arg("--concurrency", "12")) + 4))
+HW_QUEUES = min(32, max(16, int(_arg("--concurrency", "16")) + 4))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < HW_QUEUES:
     sys.exit(subprocess.call([sys.executable] + sys.argv, env=dict(os.environ, GPU_MAX_HW_QUEUES=str(HW_QUEUES))))
 
@@ -124,7 +124,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident (no input H2D) leg")
-    ap.add_argument("--concurrency", type=int, default=12, help="frames in flight per GPU: 1, or an even number (half 9/7, half 5/3)")
+    ap.add_argument("--concurrency", type=int, default=16, help="frames in flight per GPU: 1, or an even number (half 9/7, half 5/3)")
     ap.add_argument("--workload", default="8k", choices=["8k", "c5", "c4"])
     args = ap.parse_args()
 

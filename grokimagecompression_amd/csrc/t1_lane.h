@@ -658,15 +658,19 @@ GRK_HD uint32_t mqel_step(MqEncLane &e, const uint32_t *tab, uint32_t w, uint32_
     const uint32_t nmps = mps ^ (is_mps ? 0u : (w >> 28) & 1u);
     const uint32_t tw = tab[nidx];
     uint32_t n = clz32(na) - 16;
-    if (n < e.ct) {
-        na <<= n; e.c <<= n; e.ct -= n;
-    } else {
-        do {
-            const uint32_t sh = n < e.ct ? n : e.ct;
-            na <<= sh; e.c <<= sh; e.ct -= sh; n -= sh;
-            if (e.ct == 0) mqel_byteout_bf(e);
-        } while (n);
+    // renormalisation: shift to each byte boundary the n bits cross, BYTEOUT
+    // there (the first one straight-line: the lanes that cross one are a few
+    // of the 64 in any step, so the divergent block is kept short), then the
+    // rest of the shift, shared by every lane
+    if (n >= e.ct) {
+        na <<= e.ct; e.c <<= e.ct; n -= e.ct;
+        mqel_byteout_bf(e);
+        while (n >= e.ct) {  // a second / third boundary (n <= 15): rare
+            na <<= e.ct; e.c <<= e.ct; n -= e.ct;
+            mqel_byteout_bf(e);
+        }
     }
+    na <<= n; e.c <<= n; e.ct -= n;
     e.a = na;
     return keep ? w : (tw | (nmps << 31));
 }
