@@ -63,6 +63,16 @@ GRK_HD void setcol4(uint64_t *r4, uint32_t x, uint32_t bits) {
 // self bits of the window (rows k..k+3 of column x)
 GRK_HD uint32_t win_self4(uint32_t P) { return ((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 8) & 4) | ((P >> 10) & 8); }
 
+// Keep v computed at this point for every lane: stops the compiler from
+// sinking its producer (an LDS read) into a branch around its one use.
+GRK_HD void keep_here(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(v));
+#else
+    (void)v;
+#endif
+}
+
 struct DecTables {
     const uint8_t *zc;   // 512 entries for this block's orientation
     const uint8_t *sc;   // 256, window order
@@ -97,14 +107,17 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         if (!todo) return false;
         r = (uint32_t)__builtin_ctz(todo);
     }
-    uint32_t Q = 0, newsig = 0, newneg = 0, newvis = 0, si = 0;
-    bool haveQ = false;
+    // the sign window, read at the column start by every lane: a lane's first
+    // sign symbol comes at almost every decision step of a wavefront, so a
+    // lazy read would be a branch entered at every step
+    uint32_t Q = win18(s.neg, x), newsig = 0, newneg = 0, newvis = 0, si = 0;
     // The symbol-kind transitions are selects, not branches: the 64 lanes of
     // a wavefront sit in different kinds, and every branch taken by any lane
     // costs the whole wavefront its exec-mask bookkeeping.
     for (;;) {
         const uint32_t sh = 3 * r;
         const uint32_t zcx = T.zc[(P >> sh) & 0x1FF];  // read for every kind (LDS, in bounds)
+        keep_here(zcx);
         const uint32_t cx = kind == 0 ? zcx : kind == 1 ? (si & 0x7f) : kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
         const uint32_t bit = d.decode(cxw, T.mq, cx);
         if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
@@ -123,10 +136,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         todo = k4 ? rows & ~((2u << r) - 1) : todo;
         const bool advance = k1 || (k0 && !bit);
         kind = k0 ? bit : k1 ? 0u : kind == 2 ? 3u : k3 ? 4u : 1u;
-        if (kind == 1 && !advance) {
-            if (!haveQ) { Q = win18(s.neg, x); haveQ = true; }
-            si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
-        }
+        if (kind == 1 && !advance) si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
         todo = advance ? todo & ~((2u << r) - 1) : todo;
         if (advance && !todo) break;
         r = advance ? (uint32_t)__builtin_ctz(todo | 0x10u) : r;

@@ -1,12 +1,19 @@
-# A/B bench: bash scripts/gpu_ab.sh TAG "ENV=.." "ENV=.." ...  (parity suite first)
+#!/bin/bash
+# GPU box: A/B of two library builds on one box -- A = lib_ab/ (the
+# reference build), B = lib/ (the change) -- alternating runs of
+# scripts/t1_ab.py (lone-frame T1 medians, 16-context batch throughput).
+# Usage: bash scripts/gpu_ab.sh TAG [rounds]
 set -o pipefail
-O=gpurun_out/$1; shift
-mkdir -p $O
-[ -n "$NOTEST" ] || timeout -k 10 400 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-[ -n "$NOTEST" ] || tail -1 $O/pytest.txt
-i=0
-for spec in "$@"; do
-  i=$((i+1))
-  (export $(echo $spec | tr ',' ' '); timeout -k 10 300 python -u bench.py --steps ${STEPS:-6} --warmup 1 --no-cpu-baseline --concurrency ${CONC:-12} > $O/b$i.json 2> $O/b$i.err) || { tail -5 $O/b$i.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/b$i.json')); print('$spec', d['value'], d['ms_per_step'], {k: round(v['t1_ms'],1) for k,v in d['stage_ms'].items()})"
+TAG=${1:-ab}
+N=${2:-3}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export GPU_MAX_HW_QUEUES=20
+AB=$PWD/grokimagecompression_amd/lib_ab/libgrk_mi355x.so
+for round in $(seq 1 $N); do
+  for v in A B; do
+    if [ $v = A ]; then export GRKGPU_LIB=$AB; else unset GRKGPU_LIB; fi
+    timeout -k 10 300 python -u scripts/t1_ab.py > $OUT/${v}_$round.json 2> $OUT/${v}_$round.err || { echo "run $v failed"; tail $OUT/${v}_$round.err; exit 1; }
+    echo "$v$round $(cat $OUT/${v}_$round.json)"
+  done
 done
