@@ -190,7 +190,8 @@ class Stats(ctypes.Structure):
 
 class DwtOptions(ctypes.Structure):
     """grkgpu_dwt_options (include/grk_mi355x.h)."""
-    _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64)]
+    _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64),
+                ("f01_small_min_samples", ctypes.c_uint64)]
 
 
 class LaunchTime(ctypes.Structure):
@@ -544,7 +545,8 @@ class dwt_options:
     def __enter__(self):
         self.old = DwtOptions()
         lib().grkgpu_get_dwt_options(ctypes.byref(self.old))
-        new = DwtOptions(self.old.fuse_level0, self.old.f01_rows, self.old.f01_min_samples)
+        new = DwtOptions(self.old.fuse_level0, self.old.f01_rows, self.old.f01_min_samples,
+                         self.old.f01_small_min_samples)
         for k, v in self.kw.items():
             setattr(new, k, v)
         _check(lib().grkgpu_set_dwt_options(ctypes.byref(new)))

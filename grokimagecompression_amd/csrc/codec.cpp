@@ -196,6 +196,7 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->fuse_level0 = g_dwt_opts.fuse_level0;
     out->f01_rows = g_dwt_opts.f01_rows;
     out->f01_min_samples = g_dwt_opts.f01_min_samples;
+    out->f01_small_min_samples = g_dwt_opts.f01_small_min_samples;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -209,6 +210,7 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     g_dwt_opts.fuse_level0 = o->fuse_level0;
     g_dwt_opts.f01_rows = o->f01_rows;
     g_dwt_opts.f01_min_samples = o->f01_min_samples;
+    g_dwt_opts.f01_small_min_samples = o->f01_small_min_samples;
     return GRKGPU_OK;
 }
 
@@ -464,6 +466,7 @@ struct DwtPlan {
     int32_t fmt = SMP_I32;  // ... reading image samples of this format
     bool inverse = false;
     std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
+    std::vector<uint8_t> f01ny; // ... and its level-0 row windows per workgroup
 };
 
 // inverse with numres_dec < tc.numres (reduced-resolution decode): only the
@@ -541,24 +544,29 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
 // MCT one, and the resolutions are big enough (>= 16 samples each way) for
 // the fused windows; GRKGPU_DWT_F01=0 keeps one launch per level.  Returns
 // the workgroups per job, 0 = not fused.
-static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev) {
+static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny) {
     const DwtOptions &o = dwt_options();
     if (P.inverse || !irrev || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || !o.f01_rows) return 0;
     const auto &l0 = P.levels[li], &l1 = P.levels[li + 1];
     if (l0.empty() || l0.size() != l1.size()) return 0;
     // only where the pair still fills the chip (f01_min_samples, default
-    // 2^23): the 8K frame's levels 2 + 3 fused took 26 us against 14 + 7
-    // apart (378 workgroups)
+    // 2^23): the 8K frame's levels 2 + 3 fused with 4 row windows took
+    // 26 us against 14 + 7 apart (378 workgroups); smaller pairs (from
+    // f01_small_min_samples, 2^20) with 2 row windows per workgroup, twice the
+    // workgroups: levels 2 + 3 then cost what the two launches did, minus a
+    // launch boundary (frame DWT span 249 -> 245 us with per-launch events)
     uint64_t samples = 0;
     for (auto &j : l0) samples += (uint64_t)j.rw * j.rh;
-    if (samples < o.f01_min_samples) return 0;
+    if (samples >= o.f01_min_samples) *ny = o.f01_rows;
+    else if (samples >= o.f01_small_min_samples) *ny = 2;
+    else return 0;
     uint32_t maxt = 0;
     for (size_t i = 0; i < l0.size(); ++i) {
         const DwtJob &a = l0[i], &b = l1[i];
         if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
         if (a.out != b.in) return 0;  // level l + 1 must read level l's LL
         int tx;
-        const int n = dwt01_tiles(irrev, b.rw, b.rh, b.casx, b.casy, &tx);
+        const int n = dwt01_tiles(irrev, *ny, b.rw, b.rh, b.casx, b.casy, &tx);
         if (n <= 0) return 0;
         maxt = std::max<uint32_t>(maxt, (uint32_t)n);
     }
@@ -589,9 +597,12 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
     // reads that slot (for a fused pair: the pair's input), in which case it
     // takes the other one -- no launch reads and writes one buffer.
     P.f01.assign(P.levels.size(), 0);
+    P.f01ny.assign(P.levels.size(), 0);
     bool any = false;
-    for (size_t l = 0; l + 1 < P.levels.size(); ++l)
-        if ((P.f01[l] = dwt_f01_tiles(P, l, irrev))) { any = true; ++l; }
+    for (size_t l = 0; l + 1 < P.levels.size(); ++l) {
+        int ny = 4;
+        if ((P.f01[l] = dwt_f01_tiles(P, l, irrev, &ny))) { P.f01ny[l] = (uint8_t)ny; any = true; ++l; }
+    }
     // the re-deal below pairs job i of every level (one tile-component)
     for (auto &l : P.levels) any = any && l.size() == P.levels[0].size();
     if (!any) {
@@ -687,7 +698,7 @@ static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, boo
         if (li < P.f01.size() && P.f01[li]) {
             snprintf(name, sizeof(name), "k_dwt_fwd01<%s>", wl);
             if ((e = log_begin(log, s, name, (uint32_t)li, 2, level_bytes(l) + level_bytes(P.levels[li + 1])))) return e;
-            e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, s);
+            e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, P.f01ny[li], s);
             if (e != hipSuccess || (e = log_end(log, s))) return e;
             k += l.size() + P.levels[li + 1].size();
             ++li;

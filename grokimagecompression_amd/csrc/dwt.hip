@@ -581,15 +581,9 @@ struct F01Geo {
     static_assert(THW * 4 == TH1 && THW % 2 == 0, "level-1 rows split into even per-wavefront windows");
 };
 
-// level-0 row windows per workgroup (grkgpu_dwt_options.f01_rows = 2 / 4 / 6)
-int dwt01_ny() {
-    const int v = dwt_options().f01_rows;
-    return v == 2 || v == 6 ? v : 4;
-}
-
-int dwt01_tiles(int irrev, int rw1, int rh1, int casx1, int casy1, int *tiles_x) {
+// ny: level-0 row windows per workgroup (2 / 4 / 6)
+int dwt01_tiles(int irrev, int ny, int rw1, int rh1, int casx1, int casy1, int *tiles_x) {
     if (!irrev) return 0;  // 9/7 only
-    const int ny = dwt01_ny();
     const int cw = F01Geo<true, 4>::CW1;
     const int th = ny == 2 ? F01Geo<true, 2>::TH1 : ny == 6 ? F01Geo<true, 6>::TH1 : F01Geo<true, 4>::TH1;
     *tiles_x = (rw1 + casx1 + cw - 1) / cw;
@@ -765,11 +759,11 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
 // Forward levels 0 + 1 of a 9/7 plan in one launch (k_dwt_fwd01); jobs1[i]
 // is level 1 of the tile-component of jobs0[i].
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
-                            hipStream_t s) {
+                            int ny, hipStream_t s) {
     if (!njobs || !max_tiles || !irrev) return hipErrorInvalidValue;
     const int lay = kDwtLay;
     const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
-    switch (dwt01_ny()) {
+    switch (ny) {
         case 2: hipLaunchKernelGGL((k_dwt_fwd01<true, 2>), g, b, 0, s, jobs0, jobs1, lay); break;
         case 6: hipLaunchKernelGGL((k_dwt_fwd01<true, 6>), g, b, 0, s, jobs0, jobs1, lay); break;
         default: hipLaunchKernelGGL((k_dwt_fwd01<true, 4>), g, b, 0, s, jobs0, jobs1, lay); break;

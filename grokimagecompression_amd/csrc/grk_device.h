@@ -91,6 +91,7 @@ struct DwtOptions {
     int32_t fuse_level0 = -1;                    // -1: 3-component 5/3 tiles; 0 never; 1 always
     int32_t f01_rows = 4;                        // 9/7 levels 0 + 1 fused: 2 / 4 / 6 row windows; 0 = apart
     uint64_t f01_min_samples = (uint64_t)1 << 23;  // fuse a level pair from this many samples
+    uint64_t f01_small_min_samples = (uint64_t)1 << 20;  // ... and, with 2 row windows, smaller pairs from this many
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -104,9 +105,10 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
                            int inverse, hipStream_t s);
 // forward 9/7 levels 0 and 1 in one launch (dwt.hip k_dwt_fwd01): workgroups
 // per job from dwt01_tiles (level-1 geometry), 0 if unsupported
-int dwt01_tiles(int irrev, int rw1, int rh1, int casx1, int casy1, int *tiles_x);
+// (ny: level-0 row windows per workgroup, 2 / 4 / 6)
+int dwt01_tiles(int irrev, int ny, int rw1, int rh1, int casx1, int casy1, int *tiles_x);
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
-                            hipStream_t s);
+                            int ny, hipStream_t s);
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.

@@ -171,11 +171,15 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    (default) / 6 level-0 row windows per workgroup; 0: one
  *                    launch per level.
  *   f01_min_samples  fuse a level pair only from this many level-l samples
- *                    (default 2^23; 0: every qualifying pair). */
+ *                    (default 2^23; 0: every qualifying pair).
+ *   f01_small_min_samples  fuse smaller pairs too, from this many samples,
+ *                    with 2 row windows per workgroup (default 2^20: the 8K
+ *                    frame's levels 2 + 3; all ones: never). */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
     uint64_t f01_min_samples;
+    uint64_t f01_small_min_samples;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */

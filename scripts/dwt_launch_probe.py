@@ -1,7 +1,8 @@
 """Per-launch forward DWT times on the GPU box (HIP events, grkgpu_set_launch_timing):
 the 8K 12-bit RGB frame, 9/7 and 5/3 encodes, mean over N runs.  Each argument is
-a comma-separated ENV=VALUE list; every spec runs in its own child process.
-  python scripts/dwt_launch_probe.py "" "GRKGPU_DWT_F01W=8" ..."""
+a comma-separated list of grkgpu_dwt_options fields (NAME=VALUE); every spec
+runs in its own child process.
+  python scripts/dwt_launch_probe.py "" "f01_small_min_samples=1048576" ..."""
 import json
 import os
 import subprocess
@@ -19,6 +20,11 @@ def one(n=8):
     t = torch.from_numpy(img).cuda()
     codec = grk.Codec(0)
     codec.set_launch_timing(True)
+    opts = {}
+    for kv in filter(None, os.environ.get("DWT_OPTS", "").split(",")):
+        k, v = kv.split("=", 1)
+        opts[k] = int(v)
+    grk.dwt_options(**opts).__enter__()
     out = {}
     for irrev in (True, False):
         p = grk.CParams.make(irreversible=irrev)
@@ -44,9 +50,6 @@ if __name__ == "__main__":
         one()
         sys.exit(0)
     for spec in sys.argv[1:] or [""]:
-        env = dict(os.environ)
-        for kv in filter(None, spec.split(",")):
-            k, v = kv.split("=", 1)
-            env[k] = v
+        env = dict(os.environ, DWT_OPTS=spec)
         print("==", spec or "(default)", flush=True)
         subprocess.run([sys.executable, __file__, "--one"], env=env, check=True, timeout=300)

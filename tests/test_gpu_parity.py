@@ -142,7 +142,7 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
         assert np.array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("ny", ["2", "4", "6", "0"])
+@pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix"])
 @pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
@@ -161,8 +161,11 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
     a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
     ref = oracle.dwt_fwd(a, x0, y0, numres, True)
     t = torch.from_numpy(a).cuda()
-    # fuse every qualifying pair, not only chip-filling ones
-    with grk.dwt_options(f01_rows=int(ny), f01_min_samples=0):
+    # fuse every qualifying pair, not only chip-filling ones ("mix": pairs of
+    # >= 2^16 samples with 4 row windows, smaller ones with 2)
+    opts = dict(f01_rows=4, f01_min_samples=1 << 16, f01_small_min_samples=0) if ny == "mix" else \
+        dict(f01_rows=int(ny), f01_min_samples=0)
+    with grk.dwt_options(**opts):
         grk.dwt_fwd(t, x0, y0, numres, True)
         torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), ref)
