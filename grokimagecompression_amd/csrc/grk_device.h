@@ -91,7 +91,7 @@ struct DwtOptions {
     int32_t fuse_level0 = -1;                    // -1: 3-component 5/3 tiles; 0 never; 1 always
     int32_t f01_rows = 4;                        // 9/7 levels 0 + 1 fused: 2 / 4 / 6 row windows; 0 = apart
     uint64_t f01_min_samples = (uint64_t)1 << 23;  // fuse a level pair from this many samples
-    uint64_t f01_small_min_samples = (uint64_t)1 << 20;  // ... and, with 2 row windows, smaller pairs from this many
+    uint64_t f01_small_min_samples = ~(uint64_t)0;  // ... and, with 2 row windows, smaller pairs from this many
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose

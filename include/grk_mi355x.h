@@ -173,8 +173,9 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *   f01_min_samples  fuse a level pair only from this many level-l samples
  *                    (default 2^23; 0: every qualifying pair).
  *   f01_small_min_samples  fuse smaller pairs too, from this many samples,
- *                    with 2 row windows per workgroup (default 2^20: the 8K
- *                    frame's levels 2 + 3; all ones: never). */
+ *                    with 2 row windows per workgroup (default all ones:
+ *                    never -- the 8K frame's levels 2 + 3 fused this way
+ *                    took 26 us of kernel time against 14 + 7 apart). */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
