@@ -853,17 +853,27 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
     uint64_t sym_total = 0;
     uint32_t maxdepth = 1;
+    // tile geometry (independent per tile) on the host pool, then the block
+    // table in tile order
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        const Rect r = tile_rect(cp, tb + t);
+        if (r.y0 - cp.image.y0 < row0 || r.y1 - cp.image.y0 > row0 + nrows || r.x0 - cp.image.x0 < col0 ||
+            r.x1 - cp.image.x0 > col0 + ncols)
+            return set_err(GRKGPU_EINVAL, "a tile of the range lies outside the rows / columns given");
+    }
+    host_parallel_for(ntiles, 1, [&](size_t t0, size_t t1) {
+        for (size_t t = t0; t < t1; ++t) {
+            Tile &tile = tiles[t];
+            tile.index = tb + (uint32_t)t;
+            tile.r = tile_rect(cp, tile.index);
+            tile.comps.resize(nc);
+            for (uint32_t k = 0; k < nc; ++k) build_tilecomp(tile.comps[k], tile.r, cp, k, true);
+        }
+    });
     for (uint32_t t = 0; t < ntiles; ++t) {
         Tile &tile = tiles[t];
-        tile.index = tb + t;
-        tile.r = tile_rect(cp, tile.index);
-        if (tile.r.y0 - cp.image.y0 < row0 || tile.r.y1 - cp.image.y0 > row0 + nrows ||
-            tile.r.x0 - cp.image.x0 < col0 || tile.r.x1 - cp.image.x0 > col0 + ncols)
-            return set_err(GRKGPU_EINVAL, "a tile of the range lies outside the rows / columns given");
-        tile.comps.resize(nc);
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
-            build_tilecomp(tc, tile.r, cp, k, true);
             tc.arena_off = arena;
             uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
             arena += (area + 63) & ~63ull;
@@ -1042,47 +1052,56 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     } else {
         mct_numcomps = nc;
     }
+    // per-block pass records: validate and lay the blocks' passes out (prefix
+    // sum), then fill them on the host pool (blocks are independent)
     uint64_t nsym = 0;
     {
-        size_t npass = 0;
-        for (uint32_t i = 0; i < nblk; ++i) npass += std::min<uint32_t>(res[i].numpasses, GRK_MAX_PASSES);
-        passes.reserve(npass);
-    }
-    for (uint32_t i = 0; i < nblk; ++i) {
-        const EncResult &r = res[i];
-        if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
-        if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
-        const uint32_t np = r.numpasses;
-        if (np && r.rate[np - 1] > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
-        nsym += r.nsym;
-        EncCblkState &st = cst[i];
-        st.numbps = r.numbps;
-        st.numpasses = np;
-        st.pass0 = (uint32_t)passes.size();
-        st.dev_off = eb[i].out_off;
-        double cum = 0.0;
-        for (uint32_t k = 0; k < np; ++k) {
-            EncPass ps;
-            ps.rate = r.rate[k];
-            ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
-            // t1_enc_is_term_pass (t1.cpp:1131-1151)
-            {
-                const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
-                const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
-                ps.term = t1_pass_term(cp.cblksty, bp, pt, r.numbps);
-            }
-            ps.slope = 0;
-            if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
-                const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
-                const BlkInfo &bi = binfo[i];
-                cum += t1_wmsedec(r.nmsedec[k], bi.compno, bi.level, bi.orient, bpno, cp.irrev ? 0 : 1,
-                                  (double)bi.stepsize, mct_norms, mct_numcomps);
-            }
-            ps.dd = cum;
-            passes.push_back(ps);
+        uint32_t npass = 0;
+        for (uint32_t i = 0; i < nblk; ++i) {
+            const EncResult &r = res[i];
+            if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
+            if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
+            const uint32_t np = r.numpasses;
+            if (np && r.rate[np - 1] > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+            nsym += r.nsym;
+            EncCblkState &st = cst[i];
+            st.numbps = r.numbps;
+            st.numpasses = np;
+            st.pass0 = npass;
+            st.dev_off = eb[i].out_off;
+            npass += np;
         }
-        blk_disto[i] = cum;
+        passes.resize(npass);
     }
+    host_parallel_for(nblk, 1024, [&](size_t b0, size_t b1) {
+        for (size_t i = b0; i < b1; ++i) {
+            const EncResult &r = res[i];
+            const uint32_t np = r.numpasses;
+            EncPass *out = passes.data() + cst[i].pass0;
+            double cum = 0.0;
+            for (uint32_t k = 0; k < np; ++k) {
+                EncPass ps;
+                ps.rate = r.rate[k];
+                ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
+                // t1_enc_is_term_pass (t1.cpp:1131-1151)
+                {
+                    const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                    const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
+                    ps.term = t1_pass_term(cp.cblksty, bp, pt, r.numbps);
+                }
+                ps.slope = 0;
+                if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
+                    const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                    const BlkInfo &bi = binfo[i];
+                    cum += t1_wmsedec(r.nmsedec[k], bi.compno, bi.level, bi.orient, bpno, cp.irrev ? 0 : 1,
+                                      (double)bi.stepsize, mct_norms, mct_numcomps);
+                }
+                ps.dd = cum;
+                out[k] = ps;
+            }
+            blk_disto[i] = cum;
+        }
+    });
     if (export_blocks) {
         // the MQ slab to pinned host memory, then one record per block
         HIPCHK(c->h_slab.ensure(out_total + 256));
