@@ -545,8 +545,8 @@ class dwt_options:
     def __enter__(self):
         self.old = DwtOptions()
         lib().grkgpu_get_dwt_options(ctypes.byref(self.old))
-        new = DwtOptions(self.old.fuse_level0, self.old.f01_rows, self.old.f01_min_samples,
-                         self.old.f01_small_min_samples)
+        new = DwtOptions()
+        ctypes.pointer(new)[0] = self.old
         for k, v in self.kw.items():
             setattr(new, k, v)
         _check(lib().grkgpu_set_dwt_options(ctypes.byref(new)))

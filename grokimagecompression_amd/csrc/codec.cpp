@@ -542,7 +542,7 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
 // k_dwt_fwd01: level l + 1 lifted from level l's LL band kept in LDS) when
 // every tile-component has both levels, level l is not the fused DC shift +
 // MCT one, and the resolutions are big enough (>= 16 samples each way) for
-// the fused windows; GRKGPU_DWT_F01=0 keeps one launch per level.  Returns
+// the fused windows; f01_rows = 0 keeps one launch per level.  Returns
 // the workgroups per job, 0 = not fused.
 static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny) {
     const DwtOptions &o = dwt_options();

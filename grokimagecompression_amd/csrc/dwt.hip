@@ -44,6 +44,11 @@ struct DwtGeo {
     static constexpr int R = TH + 2 * HALO;        // window rows
 };
 
+// One v_mad_i64_i32 + v_alignbit.  The 64-bit multiply issues at about a
+// quarter of the 32-bit rate, and the forward 9/7 levels are VALU-issue-bound
+// (DESIGN.md §3), but the exact split into two 24-bit multiplies
+// (ah b + ((al b + 4096) >> 13), scripts/mulrate.hip) costs more: the 24-bit
+// multiplies issue at half rate (8K frame: 252 vs 216 us).
 __device__ __forceinline__ int32_t fixmul13(int32_t a, int32_t b) {
     return (int32_t)(((int64_t)a * (int64_t)b + 4096) >> 13);
 }

@@ -620,7 +620,8 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
 }
 
 // MQ-code one block from its per-plane symbol streams (slot p at
-// sym + p * slot_words).  Same outputs as t1_encode_lane.  The serial loop is
+// sym + p * slot_words); the bytes are those of mqc_enc.cpp's coder over the
+// symbol order of t1.cpp:1182-1326 (tests/test_gpu_parity.py).  The loop is
 // built for a lone lane: symbols are consumed in 16-byte chunks while the
 // chunk two ahead is in flight (the only wait on it sits at the chunk end),
 // the next symbol's context word is read from LDS before the current one is

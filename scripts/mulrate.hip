@@ -1,0 +1,65 @@
+// Issue-rate probe for the 9/7 lifting multiply: fixmul13 as one 64-bit
+// v_mad_i64_i32 (+ alignbit) against the 24-bit decomposition (5 full-rate
+// ops), and a plain 32-bit add chain for scale.  8 independent chains per
+// lane, 4096 workgroups of 256 lanes; prints ns per wave instruction slot.
+//   hipcc --offload-arch=gfx950 -O3 -o mulrate scripts/mulrate.hip && ./mulrate
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+__device__ __forceinline__ int32_t fm64(int32_t a, int32_t b) {
+    return (int32_t)(((int64_t)a * (int64_t)b + 4096) >> 13);
+}
+__device__ __forceinline__ int32_t fm24(int32_t a, int32_t b) {
+    const uint32_t lo = (((uint32_t)a & 0x1fffu) * (uint32_t)b + 4096u) >> 13;
+    return (int32_t)((uint32_t)(a >> 13) * (uint32_t)b + lo);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k(int32_t *out, int32_t seed, int iters) {
+    constexpr int32_t c = 12994;  // a lifting constant (compile-time, as in dwt.hip)
+    int32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = seed + threadIdx.x * 8 + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if constexpr (MODE == 0) x[i] = x[i] - fm64(x[i] + 77, c);
+            else if constexpr (MODE == 1) x[i] = x[i] - fm24(x[i] + 77, c);
+            else x[i] = (x[i] + 77) ^ (x[i] >> 3);
+        }
+    }
+    int32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += x[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+int main() {
+    const int nb = 4096, iters = 2048;
+    int32_t *out;
+    if (hipMalloc(&out, nb * 256 * 4) != hipSuccess) return 1;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const char *names[3] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain"};
+    for (int mode = 0; mode < 3; ++mode) {
+        for (int rep = 0; rep < 2; ++rep) {
+            hipEventRecord(e0, 0);
+            if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else hipLaunchKernelGGL(k<2>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            hipEventRecord(e1, 0);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            // lane-steps: nb * 256 lanes * iters * 8 chains; per SIMD (1024 SIMDs, 64 lanes / wave)
+            const double wave_steps = (double)nb * 4 * iters * 8;
+            if (rep) printf("%-26s %.3f ms  %.3f ns per wave-step per SIMD\n", names[mode], ms, ms * 1e6 / (wave_steps / 1024));
+        }
+    }
+    int32_t h[4];
+    hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
+    printf("check %d\n", h[0]);
+    return 0;
+}

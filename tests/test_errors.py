@@ -205,6 +205,27 @@ def test_encoder_parameter_checks():
     assert grk.lib().grkgpu_num_tiles(ctypes.byref(d), ctypes.byref(grk.CParams.make()), ctypes.byref(n)) != 0
 
 
+def test_dwt_options_checks():
+    """grkgpu_set_dwt_options validates every field and the context manager
+    restores the previous plan options (host code only)."""
+    import ctypes
+    grk = _grk()
+    cur = grk.DwtOptions()
+    grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
+    assert (cur.fuse_level0, cur.f01_rows, cur.f01_min_samples) == (-1, 4, 1 << 23)
+    with grk.dwt_options(f01_rows=6, fuse_level0=0):
+        grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
+        assert (cur.f01_rows, cur.fuse_level0, cur.f01_min_samples) == (6, 0, 1 << 23)
+    grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
+    assert (cur.f01_rows, cur.fuse_level0) == (4, -1)
+    for kw in (dict(f01_rows=3), dict(f01_rows=8), dict(fuse_level0=2)):
+        with pytest.raises(grk.GrkGpuError):
+            with grk.dwt_options(**kw):
+                pass
+    grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
+    assert (cur.f01_rows, cur.fuse_level0) == (4, -1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["rgb12_I", "g8_256", "g16_128", "rgb8_128x96"])
 def test_cut_stream_matches_oracle(codec, oracle, name):
