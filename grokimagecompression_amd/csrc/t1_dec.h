@@ -150,24 +150,24 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     return false;
 }
 
-// magnitude refinement of one column
+// magnitude refinement of one column.  The pass never changes significance,
+// so the stripe's rows to refine (e) and their "a neighbour is significant"
+// rows (nb: the 8-neighbourhood of t1.cpp's T1_SIGMA_NEIGHBOURS) are formed
+// once per stripe with row-mask operations; a column only extracts its bits.
 template <class D>
-GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr) {
+GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, const uint64_t *e, const uint64_t *nb,
+                          const uint64_t *ref, uint64_t *bit, uint32_t x) {
     T1_WALK(2, x);
-    const uint32_t P = win18(s.sig, x);
-    const uint32_t rows = (1u << nr) - 1;
-    uint32_t m4 = win_self4(P) & ~col4(s.vis, x) & rows;
-    const uint32_t ref4 = col4(s.ref, x);
-    const uint32_t mem = m4;
+    uint32_t m4 = col4(e, x);
+    const uint32_t ref4 = col4(ref, x), nb4 = col4(nb, x);
     uint32_t bits = 0;
     while (m4) {
         const uint32_t r = (uint32_t)__builtin_ctz(m4);
         m4 &= m4 - 1;
-        const uint32_t cx = ((ref4 >> r) & 1) ? CX_MAG + 2 : CX_MAG + (((P >> (3 * r)) & 0x1EF) ? 1u : 0u);
+        const uint32_t cx = CX_MAG + (((ref4 >> r) & 1) ? 2u : (nb4 >> r) & 1);  // t1.cpp dec_refpass contexts
         bits |= d.decode(cxw, T.mq, cx) << r;
     }
-    setcol4(s.ref, x, mem);
-    setcol4(s.bit, x, bits);
+    setcol4(bit, x, bits);
 }
 
 // Codeword segments of a block: a single one (NoSegs) or a cursor that
@@ -220,20 +220,24 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
 #pragma unroll
             for (int i = 0; i < 4; ++i) s.vis[i] = passtype == 0 ? 0 : (uint64_t)st.vis[k + 1 + i];
             if (passtype == 1) {
+                uint64_t e[4], nb[4], mem = 0;  // rows to refine, rows with a significant neighbour
 #pragma unroll
-                for (int i = 0; i < 4; ++i) { s.ref[i] = st.ref[k + 1 + i]; s.bit[i] = 0; }
-                uint64_t mem = 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if ((uint32_t)r < nr) mem |= s.sig[r + 1] & ~s.vis[r];
+                for (int i = 0; i < 4; ++i) {
+                    s.ref[i] = st.ref[k + 1 + i];
+                    s.bit[i] = 0;
+                    const uint64_t sg = s.sig[i + 1];
+                    e[i] = (uint32_t)i < nr ? sg & ~s.vis[i] : 0;
+                    nb[i] = dil(s.sig[i]) | dil(s.sig[i + 2]) | (sg << 1) | (sg >> 1);
+                    mem |= e[i];
+                }
                 while (mem) {
                     const uint32_t x = ctz64(mem);
                     mem &= mem - 1;
-                    d3_mrp_column(d, cxw, T, s, x, nr);
+                    d3_mrp_column(d, cxw, T, e, nb, s.ref, s.bit, x);
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    st.ref[k + 1 + i] = s.ref[i];
+                    st.ref[k + 1 + i] = s.ref[i] | e[i];  // every refined sample is now "refined once"
                     if ((uint32_t)i < nr) rb[k + i] = s.bit[i];
                 }
                 continue;
