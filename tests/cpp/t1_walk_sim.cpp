@@ -98,6 +98,9 @@ int main() {
     uint64_t st_nested = 0, st_colsteps = 0, st_stripe = 0, st_pass = 0, st_block = 0, st_stripes = 0;
     // per pass type (0 SPP, 1 MRP, 2 CUP): nested symbol steps, column steps, stripe-flat and pass-flat steps
     uint64_t pt_nested[3] = {}, pt_cols[3] = {}, pt_stripe[3] = {}, pt_pass[3] = {}, pt_dec[3] = {};
+    // column steps in which every lane's column took one decision (cleanup:
+    // mostly aggregation-0 columns, whose set-up could be skipped)
+    uint64_t pt_cols1[3] = {};
     for (auto &bk : blks)
         for (auto &ps : bk.passes)
             for (auto &sp : ps.stripes) { pt_dec[ps.type] += sp.lead; for (uint32_t c : sp.cols) pt_dec[ps.type] += c; }
@@ -148,6 +151,7 @@ int main() {
                         const Stripe_ &s = blks[i].passes[p].stripes[k];
                         if (j < s.cols.size()) m = std::max(m, s.cols[j]);
                     }
+                    if (m == 1) pt_cols1[ptype]++;
                     st_nested += m;
                     pt_nested[ptype] += m;
                 }
@@ -167,6 +171,8 @@ int main() {
                         "stripe-flat %llu | pass-flat %llu\n", t, (unsigned long long)pt_dec[t],
                 (unsigned long long)(pt_dec[t] / 64), (unsigned long long)pt_nested[t], (unsigned long long)pt_cols[t],
                 (unsigned long long)pt_stripe[t], (unsigned long long)pt_pass[t]);
+    fprintf(stderr, "column steps with one decision on every lane: spp %llu mrp %llu cup %llu\n",
+            (unsigned long long)pt_cols1[0], (unsigned long long)pt_cols1[1], (unsigned long long)pt_cols1[2]);
     fprintf(stderr, "decisions by context (bit 0 / bit 1):\n");
     for (int c = 0; c < 19; ++c)
         fprintf(stderr, "  cx %2d: %10llu %10llu\n", c, (unsigned long long)g_cx[c][0], (unsigned long long)g_cx[c][1]);
