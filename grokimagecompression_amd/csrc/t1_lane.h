@@ -382,6 +382,15 @@ struct SymOut {
         ++n;
         if ((n & 3) == 0) { out[(n >> 2) - 1] = acc; acc = 0; }
     }
+    // cnt (<= 4) symbols at once, packed in `word` from its low byte up: at
+    // most one store
+    GRK_HD void put_n(uint32_t word, uint32_t cnt) {
+        const uint32_t f = (n & 3) * 8;
+        const uint64_t v = (uint64_t)acc | ((uint64_t)word << f);
+        n += cnt;
+        if (f + cnt * 8 >= 32) { out[(n >> 2) - 1] = (uint32_t)v; acc = (uint32_t)(v >> 32); }
+        else acc = (uint32_t)v;
+    }
     GRK_HD void flush() { if (n & 3) out[n >> 2] = acc; }
 };
 
@@ -523,28 +532,36 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
     }
     cnt[0] = so.n;
     // ---- magnitude refinement: members = significant before this plane ----
+    // The context offset of every member is fixed for the stripe (refined
+    // before: 2, else a significant neighbour: 1), so it is formed as two
+    // row masks up front and a column's symbols are packed into one word.
     for (uint32_t k = 0; k < h; k += 4) {
-        uint64_t m[4], rf[4], bit[4], sS[6];
+        uint64_t m[4], o0[4], o1[4], bit[4], sS[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) sS[i] = ldrow(postS, (int32_t)(k + i) - 1, h);
         if (vsc) sS[5] = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             m[r] = ldrow(above, (int32_t)(k + r), h);
-            rf[r] = ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
+            o1[r] = ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
             bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+            const uint64_t nb = dil(sS[r]) | dil(sS[r + 2]) | (sS[r + 1] << 1) | (sS[r + 1] >> 1);
+            o0[r] = nb & ~o1[r];
         }
         uint64_t cols = m[0] | m[1] | m[2] | m[3];
         while (cols) {
             const uint32_t x = ctz64(cols);
             cols &= cols - 1;
+            uint32_t word = 0, sh = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (!((m[r] >> x) & 1)) continue;
-                const uint64_t nb = dil(sS[r]) | dil(sS[r + 2]) | (sS[r + 1] << 1) | (sS[r + 1] >> 1);
-                uint32_t cx = ((rf[r] >> x) & 1) ? CX_MAG + 2 : CX_MAG + (uint32_t)((nb >> x) & 1);
-                so.put(cx | (uint32_t)((bit[r] >> x) & 1) << 5);
+                const uint32_t pr = (uint32_t)(m[r] >> x) & 1;
+                const uint32_t sym = CX_MAG + ((uint32_t)(o0[r] >> x) & 1) + (((uint32_t)(o1[r] >> x) & 1) << 1) +
+                                     (((uint32_t)(bit[r] >> x) & 1) << 5);
+                word |= pr ? sym << sh : 0;
+                sh += pr << 3;
             }
+            so.put_n(word, sh >> 3);
         }
     }
     cnt[1] = so.n - cnt[0];
