@@ -391,6 +391,16 @@ struct SymOut {
         if (f + cnt * 8 >= 32) { out[(n >> 2) - 1] = (uint32_t)v; acc = (uint32_t)(v >> 32); }
         else acc = (uint32_t)v;
     }
+    // cnt (<= 8) symbols at once: at most two stores
+    GRK_HD void put_n64(uint64_t word, uint32_t cnt) {
+        const uint32_t f = (n & 3) * 8, tot = (n & 3) + cnt, i = n >> 2;
+        const uint64_t lo = (uint64_t)acc | (word << f);
+        const uint32_t hi = f ? (uint32_t)(word >> (64 - f)) : 0u;
+        n += cnt;
+        if (tot >= 4) out[i] = (uint32_t)lo;
+        if (tot >= 8) out[i + 1] = (uint32_t)(lo >> 32);
+        acc = tot >= 8 ? hi : tot >= 4 ? (uint32_t)(lo >> 32) : (uint32_t)lo;
+    }
     GRK_HD void flush() { if (n & 3) out[n >> 2] = acc; }
 };
 
@@ -513,20 +523,26 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             if ((uint32_t)r < nr) { postS[k + r] = post[r]; visS[k + r] = coded[r]; }
         }
         uint64_t cols = coded[0] | coded[1] | coded[2] | coded[3];
+        // a column's symbols (<= 4 ZC + 4 SC) go out as one packed word
         while (cols) {
             const uint32_t x = ctz64(cols);
             cols &= cols - 1;
+            uint64_t word = 0;
+            uint32_t sh = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if (!((coded[r] >> x) & 1)) continue;
                 const uint32_t s = (uint32_t)((post[r] >> x) & 1);
-                so.put(ctx_at(cz[r], x) | s << 5);
+                word |= (uint64_t)(ctx_at(cz[r], x) | s << 5) << sh;
+                sh += 8;
                 if (s) {
                     const uint64_t up = r == 0 ? U : post[r - 1], dn = r == 3 ? D : pre[r + 1];
-                    so.put(sc_symbol(sc, post[r] << 1, ng[r + 1] << 1, pre[r] >> 1, ng[r + 1] >> 1, up, ng[r], dn,
-                                     ng[r + 2], ng[r + 1], x, raw_spp));
+                    word |= (uint64_t)sc_symbol(sc, post[r] << 1, ng[r + 1] << 1, pre[r] >> 1, ng[r + 1] >> 1, up,
+                                                ng[r], dn, ng[r + 2], ng[r + 1], x, raw_spp) << sh;
+                    sh += 8;
                 }
             }
+            so.put_n64(word, sh >> 3);
         }
         U = post[3];
     }
@@ -596,6 +612,8 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             cz[r] = zc_slices(up << 1, up, ne >> 1, pc[r] << 1, sS[r] >> 1, dnc << 1, dn, dn >> 1, orient);
         }
         uint64_t cols = cand[0] | cand[1] | cand[2] | cand[3];
+        // a column's symbols go out as packed words: the aggregation / run
+        // symbols (<= 3), then the rows' ZC / SC symbols (<= 8)
         while (cols) {
             const uint32_t x = ctz64(cols);
             cols &= cols - 1;
@@ -604,25 +622,33 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             if ((agg >> x) & 1) {
                 uint32_t colbits = (uint32_t)((bit[0] >> x) & 1) | (uint32_t)((bit[1] >> x) & 1) << 1 |
                                    (uint32_t)((bit[2] >> x) & 1) << 2 | (uint32_t)((bit[3] >> x) & 1) << 3;
-                so.put(CX_AGG | (colbits ? 1u : 0u) << 5);
-                if (!colbits) continue;
-                uint32_t run = (uint32_t)__builtin_ctz(colbits);
-                so.put(CX_UNI | (run >> 1) << 5);
-                so.put(CX_UNI | (run & 1) << 5);
+                if (!colbits) {
+                    so.put(CX_AGG);
+                    continue;
+                }
+                const uint32_t run = (uint32_t)__builtin_ctz(colbits);
+                so.put_n((CX_AGG | 1u << 5) | (CX_UNI | (run >> 1) << 5) << 8 | (CX_UNI | (run & 1) << 5) << 16, 3);
                 r0 = (int)run;
                 rl = true;
             }
+            uint64_t word = 0;
+            uint32_t sh = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if (r < r0 || !((cand[r] >> x) & 1)) continue;
                 const uint32_t s = (uint32_t)((bit[r] >> x) & 1);
-                if (!(rl && r == r0)) so.put(ctx_at(cz[r], x) | s << 5);
+                if (!(rl && r == r0)) {
+                    word |= (uint64_t)(ctx_at(cz[r], x) | s << 5) << sh;
+                    sh += 8;
+                }
                 if (s) {
                     const uint64_t up = r == 0 ? U : pc[r - 1], dn = r == 3 ? D : sS[r + 1];
-                    so.put(sc_symbol(sc, pc[r] << 1, ng[r + 1] << 1, sS[r] >> 1, ng[r + 1] >> 1, up, ng[r], dn,
-                                     ng[r + 2], ng[r + 1], x));
+                    word |= (uint64_t)sc_symbol(sc, pc[r] << 1, ng[r + 1] << 1, sS[r] >> 1, ng[r + 1] >> 1, up, ng[r],
+                                                dn, ng[r + 2], ng[r + 1], x) << sh;
+                    sh += 8;
                 }
             }
+            so.put_n64(word, sh >> 3);
         }
         U = pc[3];
     }
