@@ -315,7 +315,7 @@ def main():
            "frac": round(value / world / roof_mpix, 5)}
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
         ncpu = min(16, os.cpu_count() or 1)
         if args.workload == "c5":
             refargs = [["-cinema4K", "24"]]
