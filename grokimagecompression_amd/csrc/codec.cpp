@@ -1502,6 +1502,12 @@ extern "C" int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_hea
     hi->tx0 = cp.tx0; hi->ty0 = cp.ty0; hi->tdx = cp.tdx; hi->tdy = cp.tdy; hi->tw = cp.tw; hi->th = cp.th;
     hi->numlayers = cp.numlayers;
     hi->prog = cp.prog;
+    hi->numcomps = cp.numcomps;
+    hi->numgbits = cp.numgbits;
+    hi->qntsty = cp.qntsty;
+    hi->nsteps = std::min<uint32_t>(cp.nsteps, 97);
+    for (uint32_t b = 0; b < hi->nsteps; ++b) { hi->step_expn[b] = cp.ss[b].expn; hi->step_mant[b] = cp.ss[b].mant; }
+    for (uint32_t k = 0; k < cp.numcomps && k < 16; ++k) hi->roishift[k] = cp.roishift[k];
     return GRKGPU_OK;
 }
 

@@ -159,7 +159,7 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
             const StepSize &st = cp.ss[off + bandno];
             b.stepsize = (float)((1.0 + st.mant / 2048.0) * std::pow(2.0, (int32_t)(numbps - st.expn))) *
                          (encoder ? 1.0f : 0.5f);
-            b.numbps = cp.roishift[compno] + st.expn + 2 - 1;  // guard bits 2 (j2k.cpp:1834), + ROI (Quantizer.cpp:90-93)
+            b.numbps = cp.roishift[compno] + st.expn + cp.numgbits - 1;  // + ROI (Quantizer.cpp:90-93)
             b.inv_step = (uint32_t)((8192.0 / b.stepsize) + 0.5f);
             uint32_t np = res.pw * res.ph;
             b.precs.assign(np, Precinct());
@@ -225,7 +225,7 @@ void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at, uint
     if (prt)
         for (uint32_t r = 0; r < cp.numres; ++r) cs.put8(cp.prcw[r] + (cp.prch[r] << 4));
     cs.put16(0xFF5C); cs.put16(3 + nb * (cp.irrev ? 2 : 1));  // QCD
-    cs.put8((2u << 5) | (cp.irrev ? 2u : 0u));
+    cs.put8((cp.numgbits << 5) | (cp.irrev ? 2u : 0u));
     for (uint32_t i = 0; i < nb; ++i) {
         if (cp.irrev) cs.put16((cp.ss[i].expn << 11) | cp.ss[i].mant);
         else cs.put8(cp.ss[i].expn << 3);
@@ -510,7 +510,10 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             if (L < 4) { err = "Error reading QCD marker"; return false; }  // j2k.cpp:4075
             uint32_t sq = p[0] & 0x1f;
             if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
+            cp.numgbits = p[0] >> 5;  // j2k_read_SQcd_SQcc: tccp->numgbits
             uint32_t nb = sq == 0 ? (L - 3) : (L - 3) / 2;
+            cp.qntsty = sq;
+            cp.nsteps = nb;
             for (uint32_t i = 0; i < nb && i < 3 * 33 + 1; ++i) {
                 if (sq == 0) cp.ss[i] = {(uint32_t)(p[1 + i] >> 3), 0};
                 else { uint32_t v = rd16(p + 1 + 2 * i); cp.ss[i] = {v >> 11, v & 0x7ff}; }

@@ -46,6 +46,9 @@ struct CodingParams {
     uint32_t tdx = 0, tdy = 0, tx0 = 0, ty0 = 0, tw = 1, th = 1;
     uint32_t numlayers = 1, prog = 0, cblksty = 0;
     StepSize ss[3 * 33 + 1];
+    uint32_t numgbits = 2;  // guard bits (QCD Sqcd >> 5; the encoder writes 2, j2k.cpp:1834)
+    uint32_t qntsty = 0;    // QCD Sqcd & 0x1f (0 none, 2 scalar expounded), as read; nsteps step sizes
+    uint32_t nsteps = 0;
     int32_t shift[16] = {};
     // coding style (Scod): precinct partition, SOP, EPH; log2 precinct size per resolution
     uint32_t csty = 0;

@@ -981,8 +981,63 @@ GRK_EXPORT void grk_dump_codec(grk_codec *codec, int32_t, FILE *out) {
             h.numlayers, h.prog, h.numresolutions, h.cblockw_init, h.cblockh_init, h.csty, h.cblk_sty,
             h.irreversible ? 0 : 1, h.mct);
 }
-GRK_EXPORT grk_codestream_info_v2 *grk_get_cstr_info(grk_codec *) { return nullptr; }
-GRK_EXPORT void grk_destroy_cstr_info(grk_codestream_info_v2 **p) { if (p) *p = nullptr; }
+// grk_get_cstr_info (grok.cpp:673-679 -> j2k_get_cstr_info,
+// j2k_dump.cpp:326-400): the main header's tile grid and the default coding /
+// quantisation parameters of every component (one COD / QCD for all: COC /
+// QCC are rejected by the parser).  tile_info stays null ("not filled from the
+// main header").  Kept as the reference does it: compno is not set (0), and
+// prcw / prch are copied with numresolutions BYTES (memcpy, :366-369), so
+// only the first numresolutions / 4 entries arrive.
+GRK_EXPORT grk_codestream_info_v2 *grk_get_cstr_info(grk_codec *codec) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header) return nullptr;
+    const grkgpu_header_info &h = c->hinfo;
+    auto *ci = (grk_codestream_info_v2 *)calloc(1, sizeof(grk_codestream_info_v2));
+    if (!ci) return nullptr;
+    ci->nbcomps = h.numcomps;
+    ci->tx0 = h.tx0; ci->ty0 = h.ty0; ci->tdx = h.tdx; ci->tdy = h.tdy; ci->tw = h.tw; ci->th = h.th;
+    grk_tile_info_v2 &t = ci->m_default_tile_info;
+    t.csty = h.csty;
+    t.prg = (int32_t)h.prog;
+    t.numlayers = h.numlayers;
+    t.mct = h.mct;
+    t.tccp_info = (grk_tccp_info *)calloc(h.numcomps ? h.numcomps : 1, sizeof(grk_tccp_info));
+    if (!t.tccp_info) { free(ci); return nullptr; }
+    uint32_t prcw[GRKP_MAXRLVLS], prch[GRKP_MAXRLVLS];  // tccp->prcw / prch: log2 sizes
+    for (uint32_t r = 0; r < GRKP_MAXRLVLS; ++r) {
+        prcw[r] = (uint32_t)__builtin_ctz(h.prcw_init[r]);
+        prch[r] = (uint32_t)__builtin_ctz(h.prch_init[r]);
+    }
+    for (uint32_t k = 0; k < h.numcomps; ++k) {
+        grk_tccp_info &q = t.tccp_info[k];
+        q.csty = (uint8_t)(h.csty & 1u);  // tccp->csty = Scod & J2K_CCP_CSTY_PRT (j2k.cpp:3875)
+        q.numresolutions = h.numresolutions;
+        q.cblkw = (uint32_t)__builtin_ctz(h.cblockw_init);
+        q.cblkh = (uint32_t)__builtin_ctz(h.cblockh_init);
+        q.cblk_sty = (uint8_t)h.cblk_sty;
+        q.qmfbid = h.irreversible ? 0 : 1;
+        if (q.numresolutions < GRKP_MAXRLVLS) {
+            memcpy(q.prch, prch, q.numresolutions);
+            memcpy(q.prcw, prcw, q.numresolutions);
+        }
+        q.qntsty = (uint8_t)h.qntsty;
+        q.numgbits = (uint8_t)h.numgbits;
+        const uint32_t nb = h.qntsty == 1 ? 1 : h.numresolutions * 3 - 2;
+        if (nb < GRK_J2K_MAXBANDS)
+            for (uint32_t b = 0; b < nb; ++b) {
+                q.stepsizes_mant[b] = b < h.nsteps ? h.step_mant[b] : 0;
+                q.stepsizes_expn[b] = b < h.nsteps ? h.step_expn[b] : 0;
+            }
+        q.roishift = k < 16 ? h.roishift[k] : 0;
+    }
+    return ci;
+}
+GRK_EXPORT void grk_destroy_cstr_info(grk_codestream_info_v2 **p) {
+    if (!p || !*p) return;
+    free((*p)->m_default_tile_info.tccp_info);
+    free(*p);
+    *p = nullptr;
+}
 GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *) { return nullptr; }
 GRK_EXPORT void grk_destroy_cstr_index(grk_codestream_index **p) { if (p) *p = nullptr; }
 

@@ -25,8 +25,10 @@
  *     test_tile_encoder);
  *   - decode: whole image, cp_reduce, cp_layer, grk_set_decode_area windows,
  *     single tiles (grk_get_decoded_tile) and tile-by-tile streaming
- *     (grk_read_tile_header / grk_decode_tile_data); codestream index / info
- *     objects (grk_get_cstr_info / grk_get_cstr_index) are not provided;
+ *     (grk_read_tile_header / grk_decode_tile_data); the main header's
+ *     codestream info (grk_get_cstr_info, after grk_read_header); the
+ *     codestream index (grk_get_cstr_index: marker / tile-part positions) is
+ *     not provided (nullptr);
  *   - the plugin entry points report "no plugin" (this library IS the
  *     accelerated path).
  */
@@ -52,8 +54,35 @@ typedef grkp_dparameters grk_dparameters;
 typedef grkp_decompress_parameters grk_decompress_parameters;
 typedef void *grk_codec;   /* grok.h:797 */
 typedef void *grk_stream;  /* grok.h:836 */
-typedef struct grk_codestream_info_v2 grk_codestream_info_v2;
 typedef struct grk_codestream_index grk_codestream_index;
+
+/* Codestream info of the main header (grok.h:1080-1156, filled by
+ * j2k_get_cstr_info, j2k_dump.cpp:326-400); layouts checked by oracle/abi/. */
+#define GRK_J2K_MAXBANDS (3 * GRKP_MAXRLVLS - 2)
+typedef struct grk_tccp_info {      /* grok.h:1083-1113 */
+    uint32_t compno;
+    uint8_t csty;
+    uint32_t numresolutions, cblkw, cblkh;
+    uint8_t cblk_sty, qmfbid, qntsty;
+    uint32_t stepsizes_mant[GRK_J2K_MAXBANDS];
+    uint32_t stepsizes_expn[GRK_J2K_MAXBANDS];
+    uint8_t numgbits;
+    uint32_t roishift;
+    uint32_t prcw[GRKP_MAXRLVLS];
+    uint32_t prch[GRKP_MAXRLVLS];
+} grk_tccp_info;
+typedef struct grk_tile_info_v2 {   /* grok.h:1118-1132 */
+    uint16_t tileno;
+    uint32_t csty;
+    int32_t prg;                    /* GRK_PROG_ORDER */
+    uint32_t numlayers, mct;
+    grk_tccp_info *tccp_info;
+} grk_tile_info_v2;
+typedef struct grk_codestream_info_v2 { /* grok.h:1137-1156 */
+    uint32_t tx0, ty0, tdx, tdy, tw, th, nbcomps;
+    grk_tile_info_v2 m_default_tile_info;
+    grk_tile_info_v2 *tile_info;
+} grk_codestream_info_v2;
 
 typedef enum { GRK_CODEC_UNKNOWN = -1, GRK_CODEC_J2K = 0, GRK_CODEC_JP2 = 2 } GRK_CODEC_FORMAT; /* grok.h:365-368 */
 typedef enum {                                                                           /* grok.h:348-359 */

@@ -288,12 +288,17 @@ int grkgpu_encode_blocks_coefficients(grkgpu_ctx *ctx, uint32_t tileno, uint32_t
 
 /* Parse the main header only. */
 int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_desc *img);
-/* The coding parameters of the main header (grk_header_info, grok.h:620-689). */
+/* The coding parameters of the main header (grk_header_info, grok.h:620-689),
+ * plus its quantisation (QCD: Sqcd guard bits and style, the step sizes as
+ * read) and ROI shifts (RGN) -- what grk_get_cstr_info reports. */
 typedef struct {
     uint32_t cblockw_init, cblockh_init, irreversible, mct, rsiz, numresolutions, csty, cblk_sty;
     uint32_t prcw_init[33], prch_init[33];  /* precinct size per resolution (samples) */
     uint32_t tx0, ty0, tdx, tdy, tw, th;   /* tile grid */
     uint32_t numlayers, prog;
+    uint32_t numcomps, numgbits, qntsty, nsteps;  /* QCD: guard bits, style, step sizes read */
+    uint32_t step_expn[97], step_mant[97];
+    uint32_t roishift[16];                 /* RGN per component */
 } grkgpu_header_info;
 int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_header_info *info);
 

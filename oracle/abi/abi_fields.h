@@ -59,7 +59,15 @@
     S(DCBINFO) F(DCBINFO, deviceId) F(DCBINFO, init_decoders_func) F(DCBINFO, inputFile) F(DCBINFO, outputFile) \
     F(DCBINFO, decod_format) F(DCBINFO, cod_format) F(DCBINFO, l_stream) F(DCBINFO, l_codec)                  \
     F(DCBINFO, decoder_parameters) F(DCBINFO, header_info) F(DCBINFO, image) F(DCBINFO, plugin_owns_image)    \
-    F(DCBINFO, tile) F(DCBINFO, error_code) F(DCBINFO, decode_flags)
+    F(DCBINFO, tile) F(DCBINFO, error_code) F(DCBINFO, decode_flags)                                        \
+    S(TCCPINFO) F(TCCPINFO, compno) F(TCCPINFO, csty) F(TCCPINFO, numresolutions) F(TCCPINFO, cblkw)          \
+    F(TCCPINFO, cblkh) F(TCCPINFO, cblk_sty) F(TCCPINFO, qmfbid) F(TCCPINFO, qntsty)                         \
+    F(TCCPINFO, stepsizes_mant) F(TCCPINFO, stepsizes_expn) F(TCCPINFO, numgbits) F(TCCPINFO, roishift)      \
+    F(TCCPINFO, prcw) F(TCCPINFO, prch)                                                                      \
+    S(TILEINFO2) F(TILEINFO2, tileno) F(TILEINFO2, csty) F(TILEINFO2, prg) F(TILEINFO2, numlayers)           \
+    F(TILEINFO2, mct) F(TILEINFO2, tccp_info)                                                                \
+    S(CSINFO) F(CSINFO, tx0) F(CSINFO, ty0) F(CSINFO, tdx) F(CSINFO, tdy) F(CSINFO, tw) F(CSINFO, th)         \
+    F(CSINFO, nbcomps) F(CSINFO, m_default_tile_info) F(CSINFO, tile_info)
 
 #define ABI_EMIT_S(tag) {#tag, "sizeof", sizeof(T_##tag)},
 #define ABI_EMIT_F(tag, field) {#tag, #field, offsetof(T_##tag, field)},

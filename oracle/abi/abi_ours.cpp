@@ -1,6 +1,6 @@
 // Layout table of include/grk_plugin_abi.h's re-declarations.  Test infrastructure.
 #include <stddef.h>
-#include "../../include/grk_plugin_abi.h"
+#include "../../include/grk_api.h"
 #include "abi_fields.h"
 using T_CPARAMS = grkp_cparameters;
 using T_POC = grkp_poc;
@@ -22,4 +22,7 @@ using T_HINFO = grkp_header_info;
 using T_DPARAMS = grkp_dparameters;
 using T_DECOMP = grkp_decompress_parameters;
 using T_DCBINFO = PluginDecodeCallbackInfo;
+using T_TCCPINFO = grk_tccp_info;
+using T_TILEINFO2 = grk_tile_info_v2;
+using T_CSINFO = grk_codestream_info_v2;
 extern const AbiEntry abi_ours[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

@@ -23,4 +23,7 @@ using T_HINFO = grk_header_info;
 using T_DPARAMS = grk_dparameters;
 using T_DECOMP = grk_decompress_parameters;
 using T_DCBINFO = grk::PluginDecodeCallbackInfo;
+using T_TCCPINFO = grk_tccp_info;
+using T_TILEINFO2 = grk_tile_info_v2;
+using T_CSINFO = grk_codestream_info_v2;
 extern const AbiEntry abi_ref[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

@@ -86,7 +86,7 @@ clean:
 .PHONY: all clean
 
 # layout check of include/grk_plugin_abi.h against the reference headers
-$(OUT)/abi_check: oracle/abi/abi_check.cpp oracle/abi/abi_ref.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_fields.h include/grk_plugin_abi.h $(GEN)/grk_config.h
+$(OUT)/abi_check: oracle/abi/abi_check.cpp oracle/abi/abi_ref.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_fields.h include/grk_plugin_abi.h include/grk_api.h $(GEN)/grk_config.h
 	$(CXX) -std=c++17 -O0 -w $(INC) -o $@ oracle/abi/abi_check.cpp oracle/abi/abi_ours.cpp oracle/abi/abi_ref.cpp
 
 # the same driver linked against OUR grk_* library (grokimagecompression_amd/

@@ -57,6 +57,9 @@
 //       caller thread), encode + decode REPS times concurrently;
 //       exit 0 iff every encode equals EXPECT.j2k and every decode equals the
 //       first decode (lossless: the input).
+//   ref_driver info IN.j2k
+//       grk_read_header, then grk_get_cstr_info printed field by field (the
+//       grk_dump path, grk_dump.cpp:494-500) and grk_destroy_cstr_info.
 // IN.i32 / OUT.i32: planar int32 little-endian (c, h, w).  dec prints
 // "x0 y0 x1 y1 numcomps prec sgnd" of the decoded image on stdout.
 #include <grok.h>
@@ -592,7 +595,7 @@ static int mt_mode(int argc, char **argv) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 4) {
+    if (argc < 4 && !(argc == 3 && std::string(argv[1]) == "info")) {
         fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
         return 2;
     }
@@ -643,6 +646,42 @@ int main(int argc, char **argv) {
         } else {
             write_file(argv[3], cs.data(), cs.size());
         }
+        grk_deinitialize();
+        return 0;
+    }
+    if (mode == "info") {  // grk_dump-style: grk_read_header, then grk_get_cstr_info (grk_dump.cpp:494-500)
+        std::vector<uint8_t> cs = read_file(argv[2]);
+        grk_initialize(nullptr, 0);
+        grk_stream *st = grk_stream_create_mem_stream(cs.data(), cs.size(), false, true);
+        grk_codec *codec = grk_create_decompress(GRK_CODEC_J2K, st);
+        grk_set_error_handler(err_cb, nullptr);
+        grk_dparameters dp;
+        grk_set_default_decoder_parameters(&dp);
+        grk_header_info hi;
+        memset(&hi, 0, sizeof(hi));
+        grk_image *img = nullptr;
+        if (!(codec && grk_setup_decoder(codec, &dp) && grk_read_header(codec, &hi, &img))) return 1;
+        grk_codestream_info_v2 *ci = grk_get_cstr_info(codec);
+        if (!ci) { fprintf(stderr, "no cstr info\n"); return 1; }
+        printf("grid %u %u %u %u %u %u comps %u tile_info %d\n", ci->tx0, ci->ty0, ci->tdx, ci->tdy, ci->tw, ci->th,
+               ci->nbcomps, ci->tile_info != nullptr);
+        const grk_tile_info_v2 &t = ci->m_default_tile_info;
+        printf("default tileno %u csty %u prg %d layers %u mct %u\n", t.tileno, t.csty, (int)t.prg, t.numlayers, t.mct);
+        for (uint32_t k = 0; k < ci->nbcomps; ++k) {
+            const grk_tccp_info &q = t.tccp_info[k];
+            printf("comp %u compno %u csty %u res %u cblk %u %u sty %u qmfbid %u qntsty %u gbits %u roi %u\n", k,
+                   q.compno, q.csty, q.numresolutions, q.cblkw, q.cblkh, q.cblk_sty, q.qmfbid, q.qntsty, q.numgbits,
+                   q.roishift);
+            printf(" steps");
+            for (uint32_t b = 0; b < GRK_J2K_MAXBANDS; ++b) printf(" %u/%u", q.stepsizes_expn[b], q.stepsizes_mant[b]);
+            printf("\n prc");
+            for (uint32_t r = 0; r < GRK_J2K_MAXRLVLS; ++r) printf(" %ux%u", q.prcw[r], q.prch[r]);
+            printf("\n");
+        }
+        grk_destroy_cstr_info(&ci);
+        printf("destroyed %d\n", ci == nullptr);
+        grk_destroy_codec(codec);
+        grk_stream_destroy(st);
         grk_deinitialize();
         return 0;
     }

@@ -7,6 +7,7 @@ kernels reproduce the reference's operation order with no FMA contraction;
 tolerance 0, i.e. max-abs 0 vs the reference decoder's output).
 """
 import hashlib
+import json
 
 import numpy as np
 import pytest
@@ -43,6 +44,21 @@ def test_decode_matches_reference(codec, name):
     gold = open(f"{GOLD}/{name}.j2k", "rb").read()
     ref = np.load(f"{GOLD}/{name}.dec.npy")
     d = codec.decompress(gold)
+    assert d.shape == ref.shape
+    assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
+
+
+GBITS = sorted(json.load(open(f"{GOLD}/manifest_gbits.json")))
+
+
+@pytest.mark.parametrize("tag", GBITS)
+def test_decode_guard_bits_match_reference(codec, tag):
+    """Goldens whose QCD guard-bit count is patched from Grok's 2 to 1 / 3
+    (oracle/make_golden_gbits.py): band bit-planes = expn + guard bits - 1
+    (j2k_read_SQcd_SQcc), so every code-block's bit-plane count moves; the
+    decode equals the reference's own decode of the patched stream."""
+    ref = np.load(f"{GOLD}/{tag}.dec.npy")
+    d = codec.decompress(open(f"{GOLD}/{tag}.j2k", "rb").read())
     assert d.shape == ref.shape
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 

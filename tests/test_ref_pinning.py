@@ -44,6 +44,32 @@ def test_small_fixtures_regenerate_bit_exact():
     assert "mismatches 0" in out
 
 
+def test_guard_bit_fixtures_regenerate():
+    """tests/golden/*.gb<N>.*: goldens with patched QCD guard bits, decoded by
+    the reference (oracle/make_golden_gbits.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "make_golden_gbits.py"), "--check"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
+def test_cstr_info_matches_reference():
+    """grk_get_cstr_info of our libgrok.so (ref_driver_mi355x: the same driver
+    relinked against it; header parsing needs no GPU) prints exactly what the
+    reference's does for every golden and guard-bit fixture: tile grid,
+    default coding style, per-component code-block / quantisation / precinct
+    fields, with the reference's quirks (compno 0, byte-count precinct copy)."""
+    import glob
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    ours = os.path.join(ROOT, "oracle", "_ref", "ref_driver_mi355x")
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "*.j2k")))
+    assert len(files) > 50
+    for f in files:
+        a = subprocess.run([ref, "info", f], capture_output=True, text=True, timeout=60)
+        b = subprocess.run([ours, "info", f], capture_output=True, text=True, timeout=60)
+        assert a.returncode == 0, f + a.stderr
+        assert b.returncode == 0 and b.stdout == a.stdout, (f, a.stdout[:400], b.stdout[:400], b.stderr)
+
+
 def test_c1_config_hash_regenerates():
     out = _check("--large", "--only", "C1_512_gray8")
     assert "C1_512_gray8 ok" in out
