@@ -9,8 +9,12 @@ and encode + decode with the 5/3 lossless path; 8 such pairs (16 frames) are in
 flight per GPU, each on its own codec context, HIP stream and host thread.
 
   value            whole-job throughput with each frame's int32 planes
-                   already resident in HBM when the timed region starts (the
-                   bench contract); the codestream crosses PCIe once each way
+                   already resident in HBM when the timed region starts.  The
+                   task's bench contract fixes this: "`value` is whole-job
+                   throughput with inputs already resident in HBM when the
+                   timed region starts (if the boundary hands over host
+                   buffers, note the PCIe-inclusive rate in DESIGN.md -- it is
+                   never `value`)".  The codestream crosses PCIe once each way
                    per frame (host Tier-2 / headers), the decoded frame stays
                    in HBM.
   pcie_inclusive   SURVEY 8(d)'s end-to-end variant, reported beside it:
@@ -20,13 +24,18 @@ flight per GPU, each on its own codec context, HIP stream and host thread.
                    on the GPU).
   t1               MQ symbols/s and code-blocks/s (batch and lone frame).
   e2e_frac         value / (8e12 / B_e2e), B_e2e = C (ceil(prec/8) + 4 * 4/3 + 4).
-  roofline         the forward 9/7 DWT (dominant HBM kernel), HIP events.
+  roofline         the forward 9/7 DWT (dominant HBM kernel): B_DWT over the
+                   sum of its launches' device times; roofline.inverse the
+                   same for the decode's inverse 9/7 DWT.
   cpu_baseline     the REFERENCE (Grok 5.1.0 libgrok compiled from source,
-                   oracle/_ref) on the host cores, one frame pair.
+                   oracle/_ref) on every host core of the process's affinity
+                   mask, one frame pair.
 
 Multi-GPU: one process per GPU (torch.distributed.run), each codes its own
 frames -- a frame batch, no data-path collective; "scaling":
-"weak".  value = frames*pixels of all ranks / max-over-ranks time.
+"weak".  value = frames*pixels of all ranks / max-over-ranks time.  Rank r
+uses device LOCAL_RANK % device_count (so --gpus 2 also runs on one GPU); the
+timing barrier and max reduction go over gloo -- no RCCL communicator.
 `python bench.py --gpus N` run directly (no WORLD_SIZE) launches the N ranks
 itself before anything touches a GPU.
 
@@ -96,6 +105,23 @@ def b_e2e(c, prec):
     return c * (-(-prec // 8) + 4.0 * 4.0 / 3.0 + 4.0)
 
 
+def max_over_ranks(dist, el):
+    """The job's time: the slowest rank's (gloo, host tensor)."""
+    if dist is None:
+        return el
+    t = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def host_threads():
+    """The host cores this process may run on (its affinity mask)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_reference(img, bits, args_list, threads, label):
     """Time the reference (oracle/_ref/ref_driver over Grok's libgrok) on the
     host: encode + decode of img for each argument list; returns seconds."""
@@ -132,14 +158,18 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rank -> device as grk_compress -G maps its devices (grk_compress.cpp:423-426):
+    # LOCAL_RANK modulo the devices present, so N ranks also run on fewer GPUs
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     if args.gpus != world:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     dist = None
     if world > 1:
+        # the ranks never exchange frame data (no collectives on
+        # the data path); the timing barrier and the max-over-ranks reduction
+        # of one float go over gloo, so no RCCL communicator is created
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
 
     import grokimagecompression_amd as grk
@@ -215,11 +245,7 @@ def main():
         run_steps(n, src)
         barrier()
         el = time.perf_counter() - t0
-        if dist is not None:
-            t = torch.tensor([el], dtype=torch.float64, device="cuda:%d" % local)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
+        return max_over_ranks(dist, el)
 
     pix_per_step = 2 * npairs * H * W
     # value: the frames already resident in HBM when the timed region starts
@@ -248,38 +274,53 @@ def main():
                 "note": "same steps, each frame copied H2D from pinned host memory (uint16, 12-bit samples) "
                         "inside the timed region"}
 
-    # roofline: forward 9/7 DWT of the frame, measured alone after the timed
-    # region on one context.  frac: B_DWT over the MEAN device time of the
-    # frame's DWT launches (HIP events on the codec stream before the first and
-    # after the last launch, 5 encodes).  launches: each launch's own
-    # algorithmic bytes (8 B per sample of every level it computes -- B_DWT
-    # split per launch) and mean time from 5 more encodes with
-    # an event pair around every launch (grkgpu_set_launch_timing; the events
-    # add ~2 us to each short launch).
+    # roofline: the 9/7 DWT of the frame, measured alone after the timed
+    # region on one context, forward (encode) and inverse (decode).  Each
+    # launch's device time comes from an event pair around it on the codec
+    # stream (grkgpu_set_launch_timing), mean of 5 encodes / decodes after one
+    # warm-up; its algorithmic bytes are 8 B per sample of every level it
+    # computes (B_DWT split per launch).  frac = B_DWT over the
+    # SUM of the frame's per-launch means (the figure a rocprofv3 kernel
+    # summary of the same launches reproduces: profiles/r04*_kernel_stats*),
+    # peak 8 TB/s; span_us = events around the whole level sequence.
     bdwt = dwt_bytes(H, W, C)
     torch.cuda.synchronize()
     p97 = grk.CParams.make(irreversible=True)
-    spans, runs = [], []
+
+    def launch_table(runs):
+        out = []
+        for i, l in enumerate(runs[0]):
+            ms = sum(r[i]["ms"] for r in runs) / len(runs)
+            out.append({"kernel": l["kernel"], "levels": list(range(l["level0"], l["level0"] + l["levels"])),
+                        "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"],
+                        "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
+                        "frac": round(l["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        assert sum(x["algorithmic_bytes"] for x in out) == bdwt, "per-launch bytes must add up to B_DWT"
+        return out
+
+    spans, fruns, iruns, ispans = [], [], [], []
     with torch.cuda.stream(streams[0]):
         for _ in range(6):
             codecs[0].compress(frame, BITS, p97, view=True)
             spans.append(codecs[0].stats()["dwt_ms"])
+        cs97 = bytes(codecs[0].compress(frame, BITS, p97, view=True))
+        for _ in range(6):
+            codecs[0].decompress(cs97, out=outs[0][0])
+            ispans.append(codecs[0].stats()["dwt_ms"])
         codecs[0].set_launch_timing(True)
         for _ in range(6):
             codecs[0].compress(frame, BITS, p97, view=True)
-            runs.append(codecs[0].launch_times())
+            fruns.append(codecs[0].launch_times())
+        for _ in range(6):
+            codecs[0].decompress(cs97, out=outs[0][0])
+            iruns.append(codecs[0].launch_times())
         codecs[0].set_launch_timing(False)
-    spans, runs = spans[1:], runs[1:]  # the first of each pays one-time setup
-    dwt_ms = sum(spans) / len(spans)
-    launches = []
-    for i, l in enumerate(runs[0]):
-        ms = sum(r[i]["ms"] for r in runs) / len(runs)
-        launches.append({"kernel": l["kernel"], "levels": list(range(l["level0"], l["level0"] + l["levels"])),
-                         "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"],
-                         "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
-                         "frac": round(l["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
-    assert sum(x["algorithmic_bytes"] for x in launches) == bdwt, "per-launch bytes must add up to B_DWT"
-    achieved = bdwt / (dwt_ms * 1e-3) / 1e9
+    # the first of each pays one-time setup
+    spans, ispans, fruns, iruns = spans[1:], ispans[1:], fruns[1:], iruns[1:]
+    launches, ilaunches = launch_table(fruns), launch_table(iruns)
+    dwt_us = sum(x["us"] for x in launches)
+    idwt_us = sum(x["us"] for x in ilaunches)
+    achieved = bdwt / (dwt_us * 1e-6) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     # the PMC passes (scripts/pmc_bench.sh) profile the default 8K workload only
@@ -291,10 +332,17 @@ def main():
     roofline = {"bound": "hbm", "kernel": "forward 9/7 DWT of the frame: " + " + ".join(x["kernel"] for x in launches),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes": bdwt, "dwt_us": round(1e3 * dwt_ms, 2), "launches": launches,
-                "measured": "HIP events on the codec stream around the frame's DWT launches, mean of 5 lone 9/7 "
-                            "encodes after the timed region; traffic = PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE) of "
-                            "the same launches, profiles/dwt_pmc_latest.json"}
+                "algorithmic_bytes": bdwt, "dwt_us": round(dwt_us, 2),
+                "span_us": round(1e3 * sum(spans) / len(spans), 2), "launches": launches,
+                "measured": "sum of the frame's per-launch device times (HIP event pair around each DWT launch on "
+                            "the codec stream, mean of 5 lone 9/7 encodes after the timed region); traffic = PMC "
+                            "bytes (FETCH_SIZE x 2 + WRITE_SIZE) of the same launches, profiles/dwt_pmc_latest.json",
+                "inverse": {"kernel": "inverse 9/7 DWT of the frame (decode): " +
+                                      " + ".join(x["kernel"] for x in ilaunches),
+                            "achieved": round(bdwt / (idwt_us * 1e-6) / 1e9, 1), "unit": "GB/s",
+                            "frac": round(bdwt / (idwt_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                            "algorithmic_bytes": bdwt, "dwt_us": round(idwt_us, 2),
+                            "span_us": round(1e3 * sum(ispans) / len(ispans), 2), "launches": ilaunches}}
 
     # T1 figures: batch throughput + a lone frame's encode / decode T1 kernels
     with torch.cuda.stream(streams[0]):
@@ -316,7 +364,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
-        ncpu = min(16, os.cpu_count() or 1)
+        ncpu = host_threads()
         if args.workload == "c5":
             refargs = [["-cinema4K", "24"]]
             npx = H * W
@@ -406,11 +454,7 @@ def bench_c4(args, grk, synth, dist, world, rank, local):
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda:%d" % local)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(dist, time.perf_counter() - t0)
     if rank == 0:
         print(json.dumps({"metric": "Mpixels/sec encode+decode, 16K tiled, tile shards",
                           "value": round(H * W * args.steps / el / 1e6, 2), "unit": "Mpixels/s", "n_gpus": world,

@@ -191,7 +191,8 @@ class Stats(ctypes.Structure):
 class DwtOptions(ctypes.Structure):
     """grkgpu_dwt_options (include/grk_mi355x.h)."""
     _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64),
-                ("f01_small_min_samples", ctypes.c_uint64)]
+                ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+                ("inv01_min_samples", ctypes.c_uint64)]
 
 
 class LaunchTime(ctypes.Structure):
@@ -246,6 +247,10 @@ def lib():
         L.grkgpu_read_header.argtypes = [VP, ctypes.c_size_t, P(ImageDesc)]
         L.grkgpu_decompress.argtypes = [VP, VP, ctypes.c_size_t, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_free.argtypes = [VP]
+        L.grkgpu_take_output.argtypes = [VP, P(VP), P(ctypes.c_size_t)]
+        L.grkgpu_give_output.argtypes = [VP, VP, ctypes.c_size_t]
+        L.grkgpu_free_output.argtypes = [VP]
+        L.grkgpu_free_output.restype = None
         L.grkgpu_num_tiles.argtypes = [P(ImageDesc), P(CParams), P(U32)]
         L.grkgpu_compress_tiles.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32,
                                             P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
@@ -292,17 +297,41 @@ def _buf_ptr(buf):
 PART_TILES, PART_HEADER, PART_EOC, PART_ALL = 0, 1, 2, 3
 
 
+def _fmt_fits(fmt, prec, sgnd):
+    """Can samples of format fmt carry a (prec, sgnd) component at their own
+    width (grkgpu_compress_ex's rule)?  Otherwise the caller widens to int32."""
+    if fmt == SAMPLE_I32:
+        return True
+    bits = 8 if fmt in (SAMPLE_U8, SAMPLE_I8) else 16
+    signed = fmt in (SAMPLE_I8, SAMPLE_I16)
+    return bool(sgnd) == signed and prec <= bits
+
+
 class _CtxView:
-    """Owner of a numpy view of a context's pinned output buffer: it keeps the
-    Codec (and so the buffer) alive for as long as any view or slice of it
-    exists -- numpy arrays made from __array_interface__ keep this object as
-    their base, and every view of them keeps that base.  The bytes stay those
-    of the call that made the view until the next compress call on the Codec."""
+    """Owner of a numpy view of a context's pinned output buffer.  It takes
+    the buffer out of the context (grkgpu_take_output: the Codec's next
+    compress allocates its own, so later calls never overwrite or free these
+    bytes) and gives it back when the last view or slice of it is gone
+    (grkgpu_give_output; freed instead if the Codec was closed) -- numpy
+    arrays made from __array_interface__ keep this object as their base, and
+    every view of them keeps that base.  A caller that drops its view before
+    the next compress (the bench) gets the same buffer back every time."""
 
     def __init__(self, codec, ptr, n):
         self.codec = codec
+        self.buf, self.cap = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().grkgpu_take_output(codec._ctx, ctypes.byref(self.buf), ctypes.byref(self.cap)))
         addr = ctypes.cast(ptr, ctypes.c_void_p).value
         self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (addr, False), "version": 3}
+
+    def __del__(self):
+        try:
+            if self.codec._ctx:
+                lib().grkgpu_give_output(self.codec._ctx, self.buf, self.cap)
+            else:
+                lib().grkgpu_free_output(self.buf)
+        except Exception:
+            pass
 
 
 def num_tiles(shape, prec, params, offset=(0, 0)):
@@ -407,7 +436,7 @@ class Codec:
             d.sgnd[k] = 1 if sgnd else 0
         pl = Planes()
         if isinstance(img, np.ndarray):
-            if img.dtype not in _NP_FMT:
+            if img.dtype not in _NP_FMT or not _fmt_fits(_NP_FMT[img.dtype], prec, sgnd):
                 img = img.astype(np.int32)
             img = np.ascontiguousarray(img)
             fmt = _NP_FMT[img.dtype]
@@ -421,6 +450,8 @@ class Codec:
                 tf[torch.uint16] = SAMPLE_U16
             if img.dtype not in tf or not img.is_contiguous():
                 raise GrkGpuError("image tensor must be contiguous int32 / uint16 / int16 / uint8 / int8")
+            if not _fmt_fits(tf[img.dtype], prec, sgnd):
+                img = img.to(torch.int32)  # e.g. 12-bit unsigned samples held in int16
             fmt = tf[img.dtype]
             on_dev = img.is_cuda
             if on_dev:
@@ -443,7 +474,7 @@ class Codec:
         image file (uint8 / int8 / uint16 / int16: widened on the GPU, so a host
         frame crosses PCIe at its own width).  Returns the .j2k codestream as
         bytes, or (view=True) as a zero-copy numpy uint8 view of the context's
-        pinned output buffer, valid until the next call on this Codec."""
+        pinned output buffer, valid for as long as the view lives (_CtxView)."""
         return self.compress_tiles(img, prec, params or CParams.make(), 0, 0xFFFFFFFF, PART_ALL, offset, sgnd,
                                    view=view)
 
@@ -452,7 +483,7 @@ class Codec:
         """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
         (plus the main header / EOC when `parts` asks for them) as bytes, or
         (view=True) as a numpy uint8 view of the context's pinned output
-        buffer (no copy), valid until the next compress call on this Codec.
+        buffer (no copy), valid for as long as the view lives (_CtxView).
         row0 / height: img holds only image rows [row0, row0 + img rows) of an
         image `height` rows tall (a tile-row shard)."""
         d, pl, keep = self._image(img, prec, offset, sgnd)

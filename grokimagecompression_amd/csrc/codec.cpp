@@ -101,6 +101,8 @@ struct grkgpu_ctx {
     bool launch_timing = false;
     std::vector<hipEvent_t> lev;
     std::vector<grkgpu_launch_time> ltimes;
+    // guards h_out against grkgpu_give_output from another thread
+    std::mutex out_mu;
 };
 
 // Device check, cached per device index (hipGetDeviceProperties is slow and
@@ -197,6 +199,9 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->f01_rows = g_dwt_opts.f01_rows;
     out->f01_min_samples = g_dwt_opts.f01_min_samples;
     out->f01_small_min_samples = g_dwt_opts.f01_small_min_samples;
+    out->inv01 = g_dwt_opts.inv01;
+    out->reserved_ = 0;
+    out->inv01_min_samples = g_dwt_opts.inv01_min_samples;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -207,11 +212,40 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->fuse_level0 < -1 || o->fuse_level0 > 1) return set_err(GRKGPU_EINVAL, "fuse_level0 must be -1, 0 or 1");
     if (o->f01_rows != 0 && o->f01_rows != 2 && o->f01_rows != 4 && o->f01_rows != 6)
         return set_err(GRKGPU_EINVAL, "f01_rows must be 0, 2, 4 or 6");
+    if (o->inv01 != 0 && o->inv01 != 2 && o->inv01 != 4) return set_err(GRKGPU_EINVAL, "inv01 must be 0, 2 or 4");
+    g_dwt_opts.inv01 = o->inv01;
+    g_dwt_opts.inv01_min_samples = o->inv01_min_samples;
     g_dwt_opts.fuse_level0 = o->fuse_level0;
     g_dwt_opts.f01_rows = o->f01_rows;
     g_dwt_opts.f01_min_samples = o->f01_min_samples;
     g_dwt_opts.f01_small_min_samples = o->f01_small_min_samples;
     return GRKGPU_OK;
+}
+
+int grkgpu_take_output(grkgpu_ctx *c, void **buf, size_t *cap) {
+    if (!c || !buf || !cap) return set_err(GRKGPU_EINVAL, "null arg");
+    std::lock_guard<std::mutex> lk(c->out_mu);
+    *buf = c->h_out.p;
+    *cap = c->h_out.cap;
+    c->h_out.p = nullptr;
+    c->h_out.cap = 0;
+    return GRKGPU_OK;
+}
+
+int grkgpu_give_output(grkgpu_ctx *c, void *buf, size_t cap) {
+    if (!buf) return GRKGPU_OK;
+    if (!c) {
+        hipHostFree(buf);
+        return GRKGPU_OK;
+    }
+    std::lock_guard<std::mutex> lk(c->out_mu);
+    if (cap > c->h_out.cap) std::swap(buf, c->h_out.p), std::swap(cap, c->h_out.cap);
+    if (buf) hipHostFree(buf);
+    return GRKGPU_OK;
+}
+
+void grkgpu_free_output(void *buf) {
+    if (buf) hipHostFree(buf);
 }
 
 int grkgpu_set_launch_timing(grkgpu_ctx *c, int on) {
@@ -467,6 +501,7 @@ struct DwtPlan {
     bool inverse = false;
     std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
     std::vector<uint8_t> f01ny; // ... and its level-0 row windows per workgroup
+    uint32_t i01 = 0;           // inverse: workgroups per job if the last two levels run fused (k_dwt_inv01)
 };
 
 // inverse with numres_dec < tc.numres (reduced-resolution decode): only the
@@ -572,8 +607,33 @@ static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny) {
     return maxt;
 }
 
+// The two largest inverse levels (the last two of an inverse plan) in one
+// launch (dwt.hip k_dwt_inv01: the smaller one's output kept in LDS) when
+// every tile-component has both, the second reads the first's output, both
+// resolutions are >= 16 samples each way and the larger level has at least
+// inv01_min_samples samples.  Returns the workgroups per job, 0 = apart.
+static uint32_t dwt_inv01_plan(const DwtPlan &P, int irrev) {
+    const DwtOptions &o = dwt_options();
+    const size_t n = P.levels.size();
+    if (!P.inverse || !o.inv01 || n < 2) return 0;
+    const auto &la = P.levels[n - 2], &lb = P.levels[n - 1];
+    if (la.empty() || la.size() != lb.size()) return 0;
+    uint64_t samples = 0;
+    for (auto &j : lb) samples += (uint64_t)j.rw * j.rh;
+    if (samples < o.inv01_min_samples) return 0;
+    uint32_t maxt = 0;
+    for (size_t i = 0; i < la.size(); ++i) {
+        const DwtJob &a = la[i], &b = lb[i];
+        if (b.in != a.out || b.snx != a.rw || b.sny != a.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16)
+            return 0;
+        maxt = std::max<uint32_t>(maxt, (uint32_t)dwt_inv01_tiles(irrev, b.rw, b.rh, b.casx, b.casy));
+    }
+    return maxt;
+}
+
 // Pick each level's window height from the level's total size; tile counts.
 static void dwt_finalize(DwtPlan &P, int irrev) {
+    P.i01 = dwt_inv01_plan(P, irrev);
     P.th.assign(P.levels.size(), 8);
     for (size_t l = 0; l < P.levels.size(); ++l) {
         uint64_t samples = 0;
@@ -698,6 +758,16 @@ static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, boo
             snprintf(name, sizeof(name), "k_dwt_fwd01<%s>", wl);
             if ((e = log_begin(log, s, name, (uint32_t)li, 2, level_bytes(l) + level_bytes(P.levels[li + 1])))) return e;
             e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, P.f01ny[li], s);
+            if (e != hipSuccess || (e = log_end(log, s))) return e;
+            k += l.size() + P.levels[li + 1].size();
+            ++li;
+            continue;
+        }
+        if (inverse && P.i01 && li + 2 == P.levels.size()) {
+            snprintf(name, sizeof(name), "k_dwt_inv01<%s>", wl);
+            if ((e = log_begin(log, s, name, (uint32_t)li, 2, level_bytes(l) + level_bytes(P.levels[li + 1])))) return e;
+            e = launch_dwt_inv01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.i01, irrev,
+                                 dwt_options().inv01, s);
             if (e != hipSuccess || (e = log_end(log, s))) return e;
             k += l.size() + P.levels[li + 1].size();
             ++li;
@@ -1325,6 +1395,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->gather.ensure(gi.size() * sizeof(GatherItem) + hdr.size() + 512));
     HIPCHK(c->h_gather.ensure(gi.size() * sizeof(GatherItem) + hdr.size() + 512));
     HIPCHK(c->packed.ensure(total + 256));
+    std::unique_lock<std::mutex> out_lk(c->out_mu);
     HIPCHK(c->h_out.ensure(total + 256));
     const size_t gbytes = gi.size() * sizeof(GatherItem);
     const size_t hoff = (gbytes + 255) & ~(size_t)255;
@@ -1790,7 +1861,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                             (const uint32_t *)(c->segs.as<uint8_t>() + segbytes), cp.cblksty,
                             roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes : nullptr));
     HIPCHK(hipEventRecord(c->ev[2], s));
-    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s));
+    c->ltimes.clear();
+    LaunchLog llog{&c->lev, &c->ltimes};
+    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s, c->launch_timing ? &llog : nullptr));
     HIPCHK(hipEventRecord(c->ev[3], s));
     PlanePtrs dst{};
     if (planes_on_device) {
@@ -1843,6 +1916,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     hipEventElapsedTime(&st.dwt_ms, c->ev[2], c->ev[3]);
     hipEventElapsedTime(&st.dcshift_mct_ms, c->ev[3], c->ev[4]);
     hipEventElapsedTime(&st.d2h_ms, c->ev[4], c->ev[5]);
+    log_collect(c);
     st.host_t2_ms = (float)(t_t2 - t_start);
     st.total_ms = (float)(t_end - t_start);
     st.num_cblks = nblk;

@@ -430,6 +430,54 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd_mct3(const DwtJob *_
 // ---------------------------------------------------------------------------
 // inverse level
 // ---------------------------------------------------------------------------
+// Inverse lifting of a window (dwt.cpp:724-858 5/3, :1544-1738 9/7):
+// horizontal on every window row (the vertical pass needs the halo rows),
+// then vertical.
+template <bool IRREV, int R>
+__device__ __forceinline__ void inv_lift(int32_t (&lo)[R], int32_t (&hi)[R], int rw, int rh, int casx, int casy) {
+    if (rw > 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int32_t L = lo[r], H = hi[r];
+            if constexpr (!IRREV) {
+                L = lift<6>(L, from_prev(H), H);
+                H = lift<7>(H, L, from_next(L));
+            } else {
+                L = __float_as_int(__fmul_rn(__int_as_float(L), 1.230174105f));
+                H = __float_as_int(__fmul_rn(__int_as_float(H), 1.625732422f));
+                L = lift<8>(L, from_prev(H), H);
+                H = lift<9>(H, L, from_next(L));
+                L = lift<10>(L, from_prev(H), H);
+                H = lift<11>(H, L, from_next(L));
+            }
+            lo[r] = L; hi[r] = H;
+        }
+    } else if (!IRREV && casx) {  // single column, odd origin: S0 /= 2 (dwt.cpp:341)
+#pragma unroll
+        for (int r = 0; r < R; ++r) { lo[r] /= 2; hi[r] /= 2; }
+    }
+    if (rh > 1) {
+        if constexpr (!IRREV) {
+            vstep<6, 0>(lo); vstep<6, 0>(hi);
+            vstep<7, 1>(lo); vstep<7, 1>(hi);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float s = (r & 1) ? 1.625732422f : 1.230174105f;
+                lo[r] = __float_as_int(__fmul_rn(__int_as_float(lo[r]), s));
+                hi[r] = __float_as_int(__fmul_rn(__int_as_float(hi[r]), s));
+            }
+            vstep<8, 0>(lo); vstep<8, 0>(hi);
+            vstep<9, 1>(lo); vstep<9, 1>(hi);
+            vstep<10, 0>(lo); vstep<10, 0>(hi);
+            vstep<11, 1>(lo); vstep<11, 1>(hi);
+        }
+    } else if (!IRREV && casy) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) { lo[r] /= 2; hi[r] /= 2; }
+    }
+}
+
 template <bool IRREV, int TH>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv(const DwtJob *__restrict__ jobs, int lay) {
     using G = DwtGeo<IRREV, TH>;
@@ -482,49 +530,7 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv(const DwtJob *__rest
         }
         }
     }
-    // horizontal on every window row (the vertical pass needs the halo rows)
-    if (rw > 1) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            int32_t L = lo[r], H = hi[r];
-            if constexpr (!IRREV) {
-                L = lift<6>(L, from_prev(H), H);
-                H = lift<7>(H, L, from_next(L));
-            } else {
-                L = __float_as_int(__fmul_rn(__int_as_float(L), 1.230174105f));
-                H = __float_as_int(__fmul_rn(__int_as_float(H), 1.625732422f));
-                L = lift<8>(L, from_prev(H), H);
-                H = lift<9>(H, L, from_next(L));
-                L = lift<10>(L, from_prev(H), H);
-                H = lift<11>(H, L, from_next(L));
-            }
-            lo[r] = L; hi[r] = H;
-        }
-    } else if (!IRREV && casx) {  // single column, odd origin: S0 /= 2 (dwt.cpp:341)
-#pragma unroll
-        for (int r = 0; r < R; ++r) { lo[r] /= 2; hi[r] /= 2; }
-    }
-    // vertical
-    if (rh > 1) {
-        if constexpr (!IRREV) {
-            vstep<6, 0>(lo); vstep<6, 0>(hi);
-            vstep<7, 1>(lo); vstep<7, 1>(hi);
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float s = (r & 1) ? 1.625732422f : 1.230174105f;
-                lo[r] = __float_as_int(__fmul_rn(__int_as_float(lo[r]), s));
-                hi[r] = __float_as_int(__fmul_rn(__int_as_float(hi[r]), s));
-            }
-            vstep<8, 0>(lo); vstep<8, 0>(hi);
-            vstep<9, 1>(lo); vstep<9, 1>(hi);
-            vstep<10, 0>(lo); vstep<10, 0>(hi);
-            vstep<11, 1>(lo); vstep<11, 1>(hi);
-        }
-    } else if (!IRREV && casy) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) { lo[r] /= 2; hi[r] /= 2; }
-    }
+    inv_lift<IRREV, R>(lo, hi, rw, rh, casx, casy);
     const int corel = G::HALO / 2, coreh = corel + G::CW / 2;
     if (lane < corel || lane >= coreh) return;
     const bool okx0 = gx0 >= 0 && gx0 < rw, okx1 = gx1 >= 0 && gx1 < rw;
@@ -706,6 +712,171 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
         fwd_vertical<IRREV, RW>(lo, hi, rh1, casy1);
         fwd_horizontal_store<IRREV, F::THW, F::W1>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
     }
+}
+
+// ---------------------------------------------------------------------------
+// The two largest inverse levels in one launch (the mirror of k_dwt_fwd01).
+// Separately, the first writes the LL band of the second (the resolution
+// below the full one) to HBM and the second reads it back: 8 B per LL sample,
+// 20 % of the pair's bytes.  Here a workgroup owns an output core of
+// 2 NPX x 2 NPY samples of the larger resolution R_b:
+//   * stage A reconstructs the R_a samples (R_a = the LL band of R_b) that
+//     core's synthesis windows read -- NPX + H pairs wide plus one column of
+//     parity slack, i.e. one window of CW columns, NA windows of THA rows --
+//     from R_a's LL band and bands in HBM (k_dwt_inv's windows), into LDS;
+//   * stage B runs k_dwt_inv's windows over the core (2 x NB windows of CW x
+//     THB), their low-pass samples read from LDS (whole-sample symmetric
+//     extension applied to the LDS indices; stage A covered every real sample
+//     a mirrored index reaches), their high-pass bands from HBM, and stores
+//     the owned samples of R_b.
+// R_a's halo rows / columns are reconstructed by two workgroups (~1.1x of
+// stage A's lifting); the launch boundary and the LL round trip go away.
+// ---------------------------------------------------------------------------
+constexpr int kDwtLayInv01 = 1;  // XCD-contiguous workgroup runs
+
+template <bool IRREV, int NA_ = 2>
+struct I01Geo {
+    static constexpr int H = IRREV ? 4 : 2;
+    static constexpr int CW = DWT_WIN - 2 * H;            // window core columns (120 / 124)
+    static constexpr int NA = NA_, THA = 48 / NA_;        // stage A: NA windows of THA rows
+    static constexpr int TR = NA * THA;                   // LDS tile rows (R_a)
+    static constexpr int NPX = CW - H - 2;                // owned R_b pairs per row (114 / 120)
+    static constexpr int NPY = TR - H - 2;                // owned R_b pair rows (42 / 44)
+    static constexpr int THB = 22;                        // stage B window rows
+    static constexpr int NB = (2 * NPY + THB - 1) / THB;  // stage B row windows (4)
+    static constexpr int NBX = (2 * NPX + CW - 1) / CW;   // stage B column windows (2)
+};
+
+int dwt_inv01_tiles(int irrev, int rw_b, int rh_b, int casx_b, int casy_b) {
+    const int cx = irrev ? 2 * I01Geo<true>::NPX : 2 * I01Geo<false>::NPX;
+    const int cy = irrev ? 2 * I01Geo<true>::NPY : 2 * I01Geo<false>::NPY;
+    return ((rw_b + casx_b + cx - 1) / cx) * ((rh_b + casy_b + cy - 1) / cy);
+}
+
+template <bool IRREV, int NA>
+__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv01(const DwtJob *__restrict__ jobsA,
+                                                             const DwtJob *__restrict__ jobsB, int lay) {
+    using G = I01Geo<IRREV, NA>;
+    constexpr int H = G::H, CW = G::CW;
+    __shared__ int32_t tile[G::TR][CW];
+    const int gx = gridDim.x;
+    int L = blockIdx.y * gx + blockIdx.x;
+    if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+    const int job = L / gx, wg = L % gx;
+    const DwtJob &JA = jobsA[job];
+    const DwtJob &JB = jobsB[job];
+    const int rwb = JB.rw, rhb = JB.rh, casxb = JB.casx, casyb = JB.casy;
+    const int ntx = (rwb + casxb + 2 * G::NPX - 1) / (2 * G::NPX), nty = (rhb + casyb + 2 * G::NPY - 1) / (2 * G::NPY);
+    if (wg >= ntx * nty) return;  // uniform over the workgroup
+    const int tx = wg % ntx, ty = wg / ntx;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // owned core of R_b: [bx0, bx0 + 2 NPX) x [by0, by0 + 2 NPY), bx0 = casx_b (mod 2)
+    const int bx0 = tx * 2 * G::NPX - casxb, by0 = ty * 2 * G::NPY - casyb;
+    // R_a samples stage B reads: pairs [m - H/2, m + NPX + H/2); the tile's
+    // origin takes R_a's parity (k_dwt_inv's window alignment), one sample of slack
+    const int mx = (bx0 - casxb) >> 1, my = (by0 - casyb) >> 1;
+    const int ax0 = mx - H / 2, ay0 = my - H / 2;
+    const int axA = ax0 - ((ax0 - JA.casx) & 1), ayA = ay0 - ((ay0 - JA.casy) & 1);
+
+    // ---- stage A: R_a tile [axA, axA + CW) x [ayA, ayA + TR) into LDS ----
+    for (int k = w; k < G::NA; k += DWT_WAVES) {
+        constexpr int R = G::THA + 2 * H;
+        const int rw = JA.rw, rh = JA.rh, casx = JA.casx, casy = JA.casy;
+        const int xw = axA - H, yw = ayA + k * G::THA - H;
+        const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
+        const int ix0 = ((mirror_idx(gx0, rw) - casx) >> 1) * 4;
+        const int ix1 = (JA.snx + ((mirror_idx(gx1, rw) - 1 + casx) >> 1)) * 4;
+        const rsrc_t llb = mkbuf(JA.in, JA.in_bytes), cb = mkbuf(JA.coef, JA.coef_bytes);
+        const int lst = (int)JA.in_stride * 4, cst = (int)JA.coef_stride * 4;
+        int32_t lo[R], hi[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int my2 = mirror_idx(yw + r, rh);
+            if ((r & 1) == 0) {
+                const int iy = (my2 - casy) >> 1;
+                lo[r] = ld32(llb, ix0, iy * lst);
+                hi[r] = ld32(cb, ix1, iy * cst);
+            } else {
+                const int so = (JA.sny + ((my2 - 1 + casy) >> 1)) * cst;
+                lo[r] = ld32(cb, ix0, so);
+                hi[r] = ld32(cb, ix1, so);
+            }
+        }
+        inv_lift<IRREV, R>(lo, hi, rw, rh, casx, casy);
+        if (lane >= H / 2 && lane < H / 2 + CW / 2) {
+            const int c = gx0 - axA;  // in [0, CW - 1)
+#pragma unroll
+            for (int r = H; r < H + G::THA; ++r) {
+                tile[k * G::THA + r - H][c] = lo[r];
+                tile[k * G::THA + r - H][c + 1] = hi[r];
+            }
+        }
+    }
+    __syncthreads();
+    // ---- stage B: R_b windows over the owned core, low-pass from LDS ----
+    for (int k = w; k < G::NBX * G::NB; k += DWT_WAVES) {
+        constexpr int R = G::THB + 2 * H;
+        const int kx = k % G::NBX, ky = k / G::NBX;
+        const int xw = bx0 + kx * CW - H, yw = by0 + ky * G::THB - H;
+        const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
+        const int ta = min(max(((mirror_idx(gx0, rwb) - casxb) >> 1) - axA, 0), CW - 1);  // LDS column
+        const int ix1 = (JB.snx + ((mirror_idx(gx1, rwb) - 1 + casxb) >> 1)) * 4;
+        const int ixl = ((mirror_idx(gx0, rwb) - casxb) >> 1) * 4;  // LH column
+        const rsrc_t cb = mkbuf(JB.coef, JB.coef_bytes);
+        const int cst = (int)JB.coef_stride * 4;
+        int32_t lo[R], hi[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int my2 = mirror_idx(yw + r, rhb);
+            if ((r & 1) == 0) {
+                const int iy = (my2 - casyb) >> 1;
+                lo[r] = tile[min(max(iy - ayA, 0), G::TR - 1)][ta];
+                hi[r] = ld32(cb, ix1, iy * cst);
+            } else {
+                const int so = (JB.sny + ((my2 - 1 + casyb) >> 1)) * cst;
+                lo[r] = ld32(cb, ixl, so);
+                hi[r] = ld32(cb, ix1, so);
+            }
+        }
+        inv_lift<IRREV, R>(lo, hi, rwb, rhb, casxb, casyb);
+        const int cx1 = bx0 + 2 * G::NPX, cy1 = by0 + 2 * G::NPY;  // owned core end
+        const bool lane_core = lane >= H / 2 && lane < H / 2 + CW / 2;
+        const bool okx0 = lane_core && gx0 >= 0 && gx0 < rwb && gx0 < cx1;
+        const bool okx1 = lane_core && gx1 >= 0 && gx1 < rwb && gx1 < cx1;
+        const rsrc_t ob = mkbuf(JB.out, JB.out_bytes);
+        const int ost = (int)JB.out_stride * 4;
+        const int v0 = okx0 ? gx0 * 4 : OOB, v1 = okx1 ? gx1 * 4 : OOB;
+        // pair stores: even origin, width and stride put both samples of a
+        // pair on the same side of every bound (wave-uniform)
+        const bool vec = (casxb | (rwb & 1) | (JB.out_stride & 1)) == 0;
+#pragma unroll
+        for (int r = H; r < H + G::THB; ++r) {
+            const int gy = yw + r;
+            if (gy < 0 || gy >= rhb || gy >= cy1) continue;  // wave-uniform
+            if (vec) {
+                const __attribute__((ext_vector_type(2))) uint32_t pv = {(uint32_t)lo[r], (uint32_t)hi[r]};
+                __builtin_amdgcn_raw_buffer_store_b64(pv, ob, v0, gy * ost, 0);
+            } else {
+                st32(lo[r], ob, v0, gy * ost);
+                st32(hi[r], ob, v1, gy * ost);
+            }
+        }
+    }
+}
+
+// na: stage-A row windows per workgroup (2 of 24 rows, 4 of 12)
+hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t njobs, uint32_t max_tiles, int irrev,
+                            int na, hipStream_t s) {
+    if (!njobs || !max_tiles) return hipErrorInvalidValue;
+    const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
+    if (na == 4) {
+        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 4>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+        else hipLaunchKernelGGL((k_dwt_inv01<false, 4>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+    } else {
+        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 2>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+        else hipLaunchKernelGGL((k_dwt_inv01<false, 2>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+    }
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

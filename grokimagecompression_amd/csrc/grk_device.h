@@ -92,6 +92,9 @@ struct DwtOptions {
     int32_t f01_rows = 4;                        // 9/7 levels 0 + 1 fused: 2 / 4 / 6 row windows; 0 = apart
     uint64_t f01_min_samples = (uint64_t)1 << 23;  // fuse a level pair from this many samples
     uint64_t f01_small_min_samples = ~(uint64_t)0;  // ... and, with 2 row windows, smaller pairs from this many
+    int32_t inv01 = 2;                               // the two largest inverse levels in one launch (k_dwt_inv01):
+                                                     // 2 / 4 stage-A row windows per workgroup; 0 = apart
+    uint64_t inv01_min_samples = (uint64_t)1 << 23;  // ... when the larger has this many samples
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -107,6 +110,11 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
 // per job from dwt01_tiles (level-1 geometry), 0 if unsupported
 // (ny: level-0 row windows per workgroup, 2 / 4 / 6)
 int dwt01_tiles(int irrev, int ny, int rw1, int rh1, int casx1, int casy1, int *tiles_x);
+// the last two inverse levels in one launch (k_dwt_inv01): workgroups per job
+// for a larger level of rw_b x rh_b; jobsA / jobsB = the two levels
+int dwt_inv01_tiles(int irrev, int rw_b, int rh_b, int casx_b, int casy_b);
+hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t njobs, uint32_t max_tiles, int irrev,
+                            int na, hipStream_t s);
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
                             int ny, hipStream_t s);
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,

@@ -56,7 +56,8 @@ void emit(const Handler &h, const char *fmt, ...) {
 // different contexts, and a context is created only when all are leased.
 std::mutex g_mu;
 std::vector<std::vector<grkgpu_ctx *>> g_free;  // [device] idle contexts
-std::vector<grkgpu_ctx *> g_all;                // every context created (grk_deinitialize)
+std::vector<grkgpu_ctx *> g_all;                // every live context (grk_deinitialize)
+std::vector<grkgpu_ctx *> g_retired;            // leased when grk_deinitialize ran: destroyed on return
 
 struct Lease {
     grkgpu_ctx *ctx = nullptr;
@@ -83,6 +84,13 @@ struct Lease {
     ~Lease() {
         if (!ctx) return;
         std::lock_guard<std::mutex> lk(g_mu);
+        auto r = std::find(g_retired.begin(), g_retired.end(), ctx);
+        if (r != g_retired.end()) {  // grk_deinitialize ran during this call
+            g_retired.erase(r);
+            grkgpu_destroy(ctx);
+            return;
+        }
+        if ((size_t)device >= g_free.size()) g_free.resize(device + 1);
         g_free[device].push_back(ctx);
     }
     Lease(const Lease &) = delete;
@@ -298,8 +306,15 @@ GRK_EXPORT const char *grk_version(void) { return "5.1.0"; }
 GRK_EXPORT bool grk_initialize(const char *, uint32_t) { return false; }  // "plugin loaded" (grok.cpp:152-160): none
 
 GRK_EXPORT void grk_deinitialize(void) {
+    // idle contexts go now; a context leased by a grk_encode / grk_decode
+    // still running on another thread is destroyed when that call returns it
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto *c : g_all) grkgpu_destroy(c);  // callers must have finished their codec calls
+    for (auto *c : g_all) {
+        bool idle = false;
+        for (auto &f : g_free) idle = idle || std::find(f.begin(), f.end(), c) != f.end();
+        if (idle) grkgpu_destroy(c);
+        else g_retired.push_back(c);
+    }
     g_all.clear();
     g_free.clear();
 }
@@ -494,11 +509,22 @@ GRK_EXPORT void grk_set_default_decoder_parameters(grk_dparameters *p) {
     if (p) memset(p, 0, sizeof(*p));
 }
 
+// The tile-streaming caches (grk_read_tile_header's tile sequence, clipped to
+// the decode area; grk_decode_tile_data's reduced-resolution image) follow
+// the decode area and parameters: dropped whenever either is set again.
+static void reset_tile_caches(Codec *c) {
+    c->tile_order.clear();
+    c->tile_order_ready = false;
+    c->tile_pos = 0;
+    c->reduced.clear();
+}
+
 GRK_EXPORT bool grk_setup_decoder(grk_codec *codec, grk_dparameters *p) {
     Codec *c = (Codec *)codec;
     if (!c || !p) return false;
     if (!c->decompressor) { GRK_ERROR("Codec provided to grk_setup_decoder is not a decompressor handler."); return false; }
     c->dparams = *p;
+    reset_tile_caches(c);  // reduce / layers may have changed
     return true;
 }
 
@@ -564,6 +590,7 @@ GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t
                                     uint32_t y1) {
     Codec *c = (Codec *)codec;
     if (!c || !c->decompressor || !c->have_header || !image) return false;
+    reset_tile_caches(c);  // the tile sequence is clipped to the area
     if (!x0 && !y0 && !x1 && !y1) {
         c->window = false;
         return true;

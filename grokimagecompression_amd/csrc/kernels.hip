@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
                                                  const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res,
                                                  uint32_t cblksty) {
     __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_ring[32 * 64];  // SymOut: 32 words per lane, word j at (j % 32) * 64 + lane
     for (uint32_t k = threadIdx.x; k < 256; k += 64) s_sc[k] = sc_lut_entry(k);
     __syncthreads();
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
     uint8_t *base = sym + off + (uint64_t)p * slot;
     t1_model_plane(b.w, b.h, b.orient, S.pa + p * 64, S.pb + p * 64, p + 1 < numbps ? S.pb + (p + 1) * 64 : nullptr,
                    S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4,
-                   cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps));
+                   cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps), s_ring + threadIdx.x);
 }
 
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words

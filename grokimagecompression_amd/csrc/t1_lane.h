@@ -374,13 +374,57 @@ GRK_HD uint32_t sym_stream_bytes(uint32_t w, uint32_t h) {
 }
 GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h) + 2 * 64 * 8; }
 
+// A lane's symbol stream, 4 symbols per word.  On the GPU the 64 lanes of a
+// wavefront write 64 different streams, and a word stored straight to HBM is
+// a 4-byte piece of its own cache line, evicted before the line fills: the
+// model kernel wrote 3.55 GB per 8K 9/7 frame for 0.76 GB of symbols
+// (DESIGN.md 3).  So words go to a per-lane ring of 32 words in LDS (word j
+// of lane l at ring[(j % 32) * 64], ring = lds + l: the 64 lanes hit 64
+// banks; 8 KB per wavefront) and leave in whole 64-byte runs -- four 16-byte stores of one lane
+// back to back -- at the stripe ends (stripe_flush, where the lanes of a
+// wavefront meet), or early when a dense stripe fills the ring.  The host
+// build stores words directly.
 struct SymOut {
     uint32_t *out;
     uint32_t acc, n;
+    uint32_t *ring = nullptr;  // device: this lane's ring (stride 64 words)
+    uint32_t done = 0;         // device: words already written to out
+    GRK_HD void store(uint32_t i, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        ring[(i & 31) * 64] = v;
+#else
+        out[i] = v;
+#endif
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // words [done, done + 16) -> out, as four 16-byte stores
+    __device__ void run16() {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u4 v;
+            v.x = ring[((done + 4 * q) & 31) * 64];
+            v.y = ring[((done + 4 * q + 1) & 31) * 64];
+            v.z = ring[((done + 4 * q + 2) & 31) * 64];
+            v.w = ring[((done + 4 * q + 3) & 31) * 64];
+            *(u4 *)(out + done + 4 * q) = v;
+        }
+        done += 16;
+    }
+    __device__ void room() {  // a dense stripe: keep <= 26 words unwritten (a put adds <= 2)
+        if ((n >> 2) - done >= 24) run16();
+    }
+#endif
     GRK_HD void put(uint32_t b) {
         acc |= b << ((n & 3) * 8);
         ++n;
-        if ((n & 3) == 0) { out[(n >> 2) - 1] = acc; acc = 0; }
+        if ((n & 3) == 0) {
+            store((n >> 2) - 1, acc);
+            acc = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+            room();
+#endif
+        }
     }
     // cnt (<= 4) symbols at once, packed in `word` from its low byte up: at
     // most one store
@@ -388,8 +432,15 @@ struct SymOut {
         const uint32_t f = (n & 3) * 8;
         const uint64_t v = (uint64_t)acc | ((uint64_t)word << f);
         n += cnt;
-        if (f + cnt * 8 >= 32) { out[(n >> 2) - 1] = (uint32_t)v; acc = (uint32_t)(v >> 32); }
-        else acc = (uint32_t)v;
+        if (f + cnt * 8 >= 32) {
+            store((n >> 2) - 1, (uint32_t)v);
+            acc = (uint32_t)(v >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+            room();
+#endif
+        } else {
+            acc = (uint32_t)v;
+        }
     }
     // cnt (<= 8) symbols at once: at most two stores
     GRK_HD void put_n64(uint64_t word, uint32_t cnt) {
@@ -397,11 +448,28 @@ struct SymOut {
         const uint64_t lo = (uint64_t)acc | (word << f);
         const uint32_t hi = f ? (uint32_t)(word >> (64 - f)) : 0u;
         n += cnt;
-        if (tot >= 4) out[i] = (uint32_t)lo;
-        if (tot >= 8) out[i + 1] = (uint32_t)(lo >> 32);
+        if (tot >= 4) store(i, (uint32_t)lo);
+        if (tot >= 8) store(i + 1, (uint32_t)(lo >> 32));
         acc = tot >= 8 ? hi : tot >= 4 ? (uint32_t)(lo >> 32) : (uint32_t)lo;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (tot >= 4) room();
+#endif
     }
-    GRK_HD void flush() { if (n & 3) out[n >> 2] = acc; }
+    // the lanes of the wavefront write their complete 64-byte runs together
+    GRK_HD void stripe_flush() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        while ((n >> 2) - done >= 16) run16();
+#endif
+    }
+    GRK_HD void flush() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        stripe_flush();
+        if (n & 3) ring[((n >> 2) & 31) * 64] = acc;
+        for (uint32_t j = done; j < (n + 3) >> 2; ++j) out[j] = ring[(j & 31) * 64];
+#else
+        if (n & 3) out[n >> 2] = acc;
+#endif
+    }
 };
 
 // Bit-sliced zero-coding context (t1_generate_luts.cpp:63-140) for 64
@@ -471,11 +539,12 @@ GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0
 // 1 0 1 0 in the uniform context (mqc_segmark_enc, t1.cpp:1244-1245).
 GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64_t *bitp, const uint64_t *above,
                            const uint64_t *ref, const uint64_t *negr, uint64_t *tmp, const uint8_t *sc,
-                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0, bool raw_spp = false) {
+                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0, bool raw_spp = false,
+                           uint32_t *ring = nullptr) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     const bool vsc = (cblksty & CBLKSTY_VSC) != 0;
     uint64_t *postS = tmp, *visS = tmp + 64;
-    SymOut so{out, 0, 0};
+    SymOut so{out, 0, 0, ring, 0};
     // ---- significance propagation ----
     uint64_t U = 0;  // post-SPP significance of row k-1
     for (uint32_t k = 0; k < h; k += 4) {
@@ -545,6 +614,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             so.put_n64(word, sh >> 3);
         }
         U = post[3];
+        so.stripe_flush();
     }
     cnt[0] = so.n;
     // ---- magnitude refinement: members = significant before this plane ----
@@ -579,6 +649,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             }
             so.put_n(word, sh >> 3);
         }
+        so.stripe_flush();
     }
     cnt[1] = so.n - cnt[0];
     // ---- cleanup (+ run-length) ----
@@ -651,6 +722,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
             so.put_n64(word, sh >> 3);
         }
         U = pc[3];
+        so.stripe_flush();
     }
     if (cblksty & CBLKSTY_SEGSYM) {
         so.put(CX_UNI | 1u << 5);

@@ -154,9 +154,9 @@ void grkgpu_destroy(grkgpu_ctx *ctx);
 /* Order all work of ctx after/with this HIP stream (hipStream_t as void*). */
 int grkgpu_set_stream(grkgpu_ctx *ctx, void *stream);
 int grkgpu_get_stats(grkgpu_ctx *ctx, grkgpu_stats *out);
-/* Time every forward-DWT launch of later compress calls (off by default: two
- * events per launch), and read the launches of the last call: *n = their
- * count, the first min(max, *n) are copied to out. */
+/* Time every DWT launch of later compress (forward) and decompress (inverse)
+ * calls (off by default: two events per launch), and read the launches of the
+ * last call: *n = their count, the first min(max, *n) are copied to out. */
 int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
 
 /* DWT plan options, process-wide (later calls; not while other threads are
@@ -175,12 +175,20 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *   f01_small_min_samples  fuse smaller pairs too, from this many samples,
  *                    with 2 row windows per workgroup (default all ones:
  *                    never -- the 8K frame's levels 2 + 3 fused this way
- *                    took 26 us of kernel time against 14 + 7 apart). */
+ *                    took 26 us of kernel time against 14 + 7 apart).
+ *   inv01            2 (default) / 4: the two largest inverse levels in one
+ *                    launch (k_dwt_inv01, with 2 / 4 row windows for the
+ *                    smaller level per workgroup) when the larger has at
+ *                    least inv01_min_samples samples (default 2^23; 0: any
+ *                    size); 0: one launch per level. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
     uint64_t f01_min_samples;
     uint64_t f01_small_min_samples;
+    int32_t inv01;
+    int32_t reserved_;
+    uint64_t inv01_min_samples;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */
@@ -197,6 +205,17 @@ int grkgpu_compress(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_
  * stays valid until the next call on ctx (like the reference's memory stream). */
 int grkgpu_compress_view(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                          const int32_t *const *planes, int planes_on_device, const uint8_t **out, size_t *outlen);
+
+/* Output-buffer hand-off for views that must outlive later calls: take the
+ * context's pinned output buffer (holding the last compress's codestream) out
+ * of the context -- its next compress allocates a buffer of its own -- and
+ * give a taken buffer back when done with it (the context keeps the larger of
+ * it and its current buffer and frees the other; with ctx = NULL, or after
+ * grkgpu_destroy, use grkgpu_free_output).  *buf = NULL if the context holds
+ * no buffer. */
+int grkgpu_take_output(grkgpu_ctx *ctx, void **buf, size_t *cap);
+int grkgpu_give_output(grkgpu_ctx *ctx, void *buf, size_t cap);
+void grkgpu_free_output(void *buf);
 
 /* Tile shards (multi-GPU): tiles are independent through the
  * whole path, and a codestream is [main header][tile-parts in tile order]

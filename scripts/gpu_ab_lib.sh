@@ -7,7 +7,7 @@ TAG=${1:-ab}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 AB=$PWD/grokimagecompression_amd/lib_ab/libgrk_mi355x.so
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for v in A B; do
     if [ $v = B ]; then export GRKGPU_LIB=$AB; else unset GRKGPU_LIB; fi
     timeout -k 10 200 python -u scripts/probe_perf.py 8k > $OUT/probe_${v}_$round.txt 2>&1 || { echo "probe $v failed"; tail $OUT/probe_${v}_$round.txt; exit 1; }

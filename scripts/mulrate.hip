@@ -15,6 +15,16 @@ __device__ __forceinline__ int32_t fm24(int32_t a, int32_t b) {
     return (int32_t)((uint32_t)(a >> 13) * (uint32_t)b + lo);
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+// the 16-bit split through the packed dot products: (s*c + 4096) >> 13 =
+// 8 (s_hi c) + ((s_lo c + 4096) >> 13), exact mod 2^32 for 0 <= c < 2^15
+__device__ __forceinline__ int32_t fmdot(int32_t a, int32_t b) {
+    const uint32_t X = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), u16x2{(unsigned short)b, 0}, 4096u, false);
+    const int32_t Y = __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), i16x2{0, (short)b}, 0, false);
+    return (int32_t)(((uint32_t)Y << 3) + (X >> 13));
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k(int32_t *out, int32_t seed, int iters) {
     constexpr int32_t c = 12994;  // a lifting constant (compile-time, as in dwt.hip)
@@ -26,6 +36,7 @@ __global__ __launch_bounds__(256) void k(int32_t *out, int32_t seed, int iters) 
         for (int i = 0; i < 8; ++i) {
             if constexpr (MODE == 0) x[i] = x[i] - fm64(x[i] + 77, c);
             else if constexpr (MODE == 1) x[i] = x[i] - fm24(x[i] + 77, c);
+            else if constexpr (MODE == 3) x[i] = x[i] - fmdot(x[i] + 77, c);
             else x[i] = (x[i] + 77) ^ (x[i] >> 3);
         }
     }
@@ -42,24 +53,25 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *names[3] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain"};
-    for (int mode = 0; mode < 3; ++mode) {
+    const char *names[4] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain", "dot2 fixmul13"};
+    for (int mode = 0; mode < 4; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             hipEventRecord(e0, 0);
             if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
-            else hipLaunchKernelGGL(k<2>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else hipLaunchKernelGGL(k<3>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             hipEventRecord(e1, 0);
             hipEventSynchronize(e1);
             float ms = 0;
             hipEventElapsedTime(&ms, e0, e1);
             // lane-steps: nb * 256 lanes * iters * 8 chains; per SIMD (1024 SIMDs, 64 lanes / wave)
             const double wave_steps = (double)nb * 4 * iters * 8;
-            if (rep) printf("%-26s %.3f ms  %.3f ns per wave-step per SIMD\n", names[mode], ms, ms * 1e6 / (wave_steps / 1024));
+            int32_t h[4];
+            hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
+            if (rep) printf("%-26s %.3f ms  %.3f ns per wave-step per SIMD  (check %d %d)\n", names[mode], ms,
+                            ms * 1e6 / (wave_steps / 1024), h[0], h[3]);
         }
     }
-    int32_t h[4];
-    hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
-    printf("check %d\n", h[0]);
     return 0;
 }

@@ -213,12 +213,13 @@ def test_dwt_options_checks():
     cur = grk.DwtOptions()
     grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
     assert (cur.fuse_level0, cur.f01_rows, cur.f01_min_samples) == (-1, 4, 1 << 23)
+    assert (cur.inv01, cur.inv01_min_samples) == (2, 1 << 23)
     with grk.dwt_options(f01_rows=6, fuse_level0=0):
         grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
         assert (cur.f01_rows, cur.fuse_level0, cur.f01_min_samples) == (6, 0, 1 << 23)
     grk.lib().grkgpu_get_dwt_options(ctypes.byref(cur))
     assert (cur.f01_rows, cur.fuse_level0) == (4, -1)
-    for kw in (dict(f01_rows=3), dict(f01_rows=8), dict(fuse_level0=2)):
+    for kw in (dict(f01_rows=3), dict(f01_rows=8), dict(fuse_level0=2), dict(inv01=1), dict(inv01=3), dict(inv01=-1)):
         with pytest.raises(grk.GrkGpuError):
             with grk.dwt_options(**kw):
                 pass

@@ -33,5 +33,30 @@ def test_bench_line_keeps_the_contract():
         assert k in rf, k
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # frac = B_DWT over the sum of the frame's per-launch device times
+    assert abs(rf["algorithmic_bytes"] / (rf["dwt_us"] * 1e-6) / 1e9 - rf["achieved"]) < 0.5
+    assert abs(sum(x["us"] for x in rf["launches"]) - rf["dwt_us"]) < 0.05
+    inv = rf["inverse"]
+    assert 0 < inv["frac"] < 1 and inv["launches"] and sum(x["algorithmic_bytes"] for x in inv["launches"]) == \
+        rf["algorithmic_bytes"]
     assert d["cpu_baseline"] is None  # --no-cpu-baseline
     assert d["pcie_inclusive"]["value"] > 0 and d["pcie_inclusive"]["steps"] == 1
+
+
+def test_bench_two_ranks_on_one_gpu():
+    """--gpus 2 launches two ranks itself (torch.distributed.run); rank r takes
+    device LOCAL_RANK % device_count, so on a one-GPU lease both share it;
+    the timing barrier / max reduction go over gloo.  One JSON line (rank 0)
+    with n_gpus 2 and the frames of both ranks in value."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup",
+                        "1", "--concurrency", "2", "--no-cpu-baseline", "--no-pcie"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["frames_per_step_per_gpu"] == 2
+    assert d["cpu_baseline"] is None and d["pcie_inclusive"] is None
+    # value counts both ranks' frames over the slower rank's time
+    px = 7680 * 4320
+    assert abs(d["value"] - 2 * 2 * px * d["steps"] / (d["ms_per_step"] * 1e-3 * d["steps"]) / 1e6) < 0.01 * d["value"]

@@ -188,6 +188,41 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
 
 
 @pytest.mark.parametrize("irrev", [False, True])
+@pytest.mark.parametrize("fused", [0, 2, 4])
+@pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
+                                       ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
+                                       ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1)),
+                                       ((260, 37), (0, 0)), ((2160, 4096), (1, 0))])
+@pytest.mark.parametrize("numres", [2, 3, 6])
+def test_dwt_inv01_stage_vs_oracle(oracle, irrev, fused, shape_off, numres):
+    """The two largest inverse levels in one launch (k_dwt_inv01: the smaller
+    level's output in LDS; default when the larger has >= 2^23 samples), here
+    forced onto every size (inv01_min_samples = 0) with 2 / 4 row windows of
+    the smaller level per workgroup (0 = two launches), on odd
+    sizes and offsets (every cas parity, image edges inside the windows):
+    5/3 inverts the forward transform exactly, 9/7 (float, no FMA) equals the
+    oracle's inverse bit for bit."""
+    import torch
+    import grokimagecompression_amd as grk
+    (h, w), (x0, y0) = shape_off
+    rng = np.random.default_rng(h * 7 + w + numres)
+    with grk.dwt_options(inv01=fused, inv01_min_samples=0):
+        if not irrev:
+            a = rng.integers(-4096, 4096, size=(h, w)).astype(np.int32)
+            t = torch.from_numpy(oracle.dwt_fwd(a, x0, y0, numres, False)).cuda()
+            grk.dwt_inv(t, x0, y0, numres, False)
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), a)
+        else:
+            f = (rng.standard_normal((h, w)) * 100).astype(np.float32).view(np.int32)
+            ref = oracle.dwt_inv(f, x0, y0, numres, True)
+            t = torch.from_numpy(f.copy()).cuda()
+            grk.dwt_inv(t, x0, y0, numres, True)
+            torch.cuda.synchronize()
+            assert np.array_equal(t.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("irrev", [False, True])
 def test_mct_stage_vs_oracle(oracle, irrev):
     import torch
     import grokimagecompression_amd as grk
@@ -358,9 +393,12 @@ def test_encode_sample_formats(codec, name, dtype):
 @pytest.mark.parametrize("bits,irrev", [(12, False), (12, True), (8, False), (16, True)])
 def test_encode_signed_sample_formats(codec, bits, irrev):
     """Signed components as int8 / int16 samples (GRKGPU_SAMPLE_I8 / I16):
-    the same codestream as their int32 planes; a format that cannot hold the
-    component (unsigned samples for a signed image, 16-bit samples for 8-bit
-    storage of a 12-bit image) is refused."""
+    the same codestream as their int32 planes.  A format that cannot hold the
+    component (unsigned samples for a signed image, 8-bit samples of a 12-bit
+    image) is refused by the C ABI; the Python layer widens such numpy / torch
+    samples to int32 first, so they encode exactly as their int32 planes."""
+    import ctypes
+    import torch
     import grokimagecompression_amd as grk
     rng = np.random.default_rng(bits)
     img = rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), size=(3, 70, 93)).astype(np.int32)
@@ -368,8 +406,18 @@ def test_encode_signed_sample_formats(codec, bits, irrev):
     ref = codec.compress(img, bits, p, sgnd=True)
     small = np.int8 if bits <= 8 else np.int16
     assert codec.compress(img.astype(small), bits, p, sgnd=True) == ref
-    with pytest.raises(grk.GrkGpuError):
-        codec.compress(img.astype(np.uint16), bits, p, sgnd=True)
+    mism = [((np.abs(img) % (1 << (bits - 1))).astype(np.uint16), True)]  # in range, unsigned storage
     if bits > 8:
-        with pytest.raises(grk.GrkGpuError):
-            codec.compress((img + (1 << (bits - 1))).astype(np.uint8), bits, p)
+        mism.append(((img + (1 << (bits - 1))).astype(np.uint8), False))
+    for a, sg in mism:
+        wide = codec.compress(a.astype(np.int32), bits, p, sgnd=sg)
+        assert codec.compress(a, bits, p, sgnd=sg) == wide
+        if a.dtype == np.uint8:  # torch has no uint16 before 2.3: checked on uint8
+            assert codec.compress(torch.from_numpy(a).cuda(), bits, p, sgnd=sg) == wide
+        # the ABI refuses the format itself
+        d, pl, keep = codec._image(a.astype(np.int32), bits, (0, 0), sg)
+        pl.sample_fmt = grk.SAMPLE_U16 if a.dtype == np.uint16 else grk.SAMPLE_U8
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        assert grk.lib().grkgpu_compress_ex(codec._ctx, ctypes.byref(d), ctypes.byref(p), ctypes.byref(pl), 0,
+                                            0xFFFFFFFF, grk.PART_ALL, ctypes.byref(out), ctypes.byref(n)) != 0

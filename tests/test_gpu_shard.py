@@ -176,3 +176,35 @@ def test_compress_tiles_view():
     del junk
     gc.collect()
     assert head.tobytes() == ref[:64] and tail.tobytes() == ref[-2:]
+
+
+def test_view_outlives_later_compress():
+    """A view stays valid across later compress calls on its Codec, including
+    a larger one that needs a bigger output buffer (the view took the buffer
+    out of the context: grkgpu_take_output); views dropped before the next
+    call hand their buffer back (grkgpu_give_output)."""
+    import gc
+    import grokimagecompression_amd as grk
+    codec = grk.Codec(0)
+    small = synth.synth_image(64, 80, 1, 8, 1)
+    big = synth.synth_image(600, 700, 3, 12, 2)
+    ref_small = codec.compress(small, 8)
+    v1 = codec.compress(small, 8, view=True)
+    v2 = codec.compress(small, 8, view=True)  # v1 still alive: a new buffer
+    ref_big = codec.compress(big, 12)
+    v3 = codec.compress(big, 12, view=True)
+    junk = [np.ones(1 << 20, np.uint8) for _ in range(8)]
+    del junk
+    assert v1.tobytes() == ref_small and v2.tobytes() == ref_small and v3.tobytes() == ref_big
+    sl = v1[10:20]
+    del v1, v2
+    gc.collect()
+    for _ in range(3):  # views dropped between calls: the buffer goes round
+        w = codec.compress(big, 12, view=True)
+        assert w.tobytes() == ref_big
+        del w
+    assert sl.tobytes() == ref_small[10:20] and v3.tobytes() == ref_big
+    codec.close()  # a view outliving its Codec frees its buffer itself
+    assert v3.tobytes() == ref_big
+    del v3, sl
+    gc.collect()
