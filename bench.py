@@ -115,11 +115,26 @@ def max_over_ranks(dist, el):
 
 
 def host_threads():
-    """The host cores this process may run on (its affinity mask)."""
+    """The host cores this process may run on: its affinity mask, capped by
+    the cgroup's CPU quota where one is set (cgroup v2 cpu.max) -- on a
+    shared node the mask lists every core while the quota is the share."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    for qf, pf in (("/sys/fs/cgroup/cpu.max", None),
+                   ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            if pf is None:
+                quota, period = open(qf).read().split()[:2]
+            else:
+                quota, period = open(qf).read().strip(), open(pf).read().strip()
+            if quota not in ("max", "-1"):
+                n = min(n, max(1, -(-int(quota) // int(period))))
+            break
+        except (OSError, ValueError):
+            continue
+    return n
 
 
 def cpu_reference(img, bits, args_list, threads, label):

@@ -182,7 +182,7 @@ class Stats(ctypes.Structure):
                 ("t1_ms", ctypes.c_float), ("gather_ms", ctypes.c_float), ("d2h_ms", ctypes.c_float),
                 ("host_t2_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("num_cblks", ctypes.c_uint64),
                 ("cs_bytes", ctypes.c_uint64), ("mq_symbols", ctypes.c_uint64), ("rate_ms", ctypes.c_float),
-                ("pad", ctypes.c_float)]
+                ("packet_ms", ctypes.c_float)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -191,7 +191,7 @@ class Stats(ctypes.Structure):
 class DwtOptions(ctypes.Structure):
     """grkgpu_dwt_options (include/grk_mi355x.h)."""
     _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64),
-                ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+                ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("pair_group", ctypes.c_int32),
                 ("inv01_min_samples", ctypes.c_uint64)]
 
 

@@ -200,7 +200,7 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->f01_min_samples = g_dwt_opts.f01_min_samples;
     out->f01_small_min_samples = g_dwt_opts.f01_small_min_samples;
     out->inv01 = g_dwt_opts.inv01;
-    out->reserved_ = 0;
+    out->pair_group = g_dwt_opts.pair_group;
     out->inv01_min_samples = g_dwt_opts.inv01_min_samples;
 }
 
@@ -213,7 +213,9 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->f01_rows != 0 && o->f01_rows != 2 && o->f01_rows != 4 && o->f01_rows != 6)
         return set_err(GRKGPU_EINVAL, "f01_rows must be 0, 2, 4 or 6");
     if (o->inv01 != 0 && o->inv01 != 2 && o->inv01 != 4) return set_err(GRKGPU_EINVAL, "inv01 must be 0, 2 or 4");
+    if (o->pair_group < 0 || o->pair_group > 4096) return set_err(GRKGPU_EINVAL, "pair_group must be 0 .. 4096");
     g_dwt_opts.inv01 = o->inv01;
+    g_dwt_opts.pair_group = o->pair_group;
     g_dwt_opts.inv01_min_samples = o->inv01_min_samples;
     g_dwt_opts.fuse_level0 = o->fuse_level0;
     g_dwt_opts.f01_rows = o->f01_rows;
@@ -502,13 +504,17 @@ struct DwtPlan {
     std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
     std::vector<uint8_t> f01ny; // ... and its level-0 row windows per workgroup
     uint32_t i01 = 0;           // inverse: workgroups per job if the last two levels run fused (k_dwt_inv01)
+    bool restricted = false;    // inverse jobs limited to output regions (window decode)
 };
 
 // inverse with numres_dec < tc.numres (reduced-resolution decode): only the
 // levels up to resolution numres_dec - 1; the last writes that resolution
 // compactly (stride = its width) into `work`.
+// resneed (window decode, inverse): per resolution the region (absolute
+// resolution coordinates) whose samples the window needs (window_need); each
+// inverse level then runs only the windows over its region.
 static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *coef, int32_t *llbase, int irrev,
-                        bool inverse, uint32_t numres_dec = 0) {
+                        bool inverse, uint32_t numres_dec = 0, const std::vector<Rect> *resneed = nullptr) {
     const uint32_t stride = tc.r.w(), rows = tc.r.h();
     P.inverse = inverse;
     if (!inverse || numres_dec == 0 || numres_dec > tc.numres) numres_dec = tc.numres;
@@ -569,6 +575,13 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
         j.rw = (int32_t)cur.w(); j.rh = (int32_t)cur.h();
         j.casx = (int32_t)(cur.x0 & 1); j.casy = (int32_t)(cur.y0 & 1);
         j.snx = (int32_t)lo.w(); j.sny = (int32_t)lo.h();
+        if (inverse && resneed && lvl + 1 < resneed->size()) {
+            const Rect &n = (*resneed)[lvl + 1];  // region of the resolution this level reconstructs
+            j.reg_x0 = (int32_t)n.x0 - (int32_t)cur.x0; j.reg_x1 = (int32_t)n.x1 - (int32_t)cur.x0;
+            j.reg_y0 = (int32_t)n.y0 - (int32_t)cur.y0; j.reg_y1 = (int32_t)n.y1 - (int32_t)cur.y0;
+            if (j.reg_x1 <= j.reg_x0 || j.reg_y1 <= j.reg_y0) j.reg_x0 = j.reg_y0 = 0, j.reg_x1 = j.reg_y1 = 1;
+            P.restricted = true;
+        }
         P.levels[lvl].push_back(j);
     }
 }
@@ -615,7 +628,7 @@ static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny) {
 static uint32_t dwt_inv01_plan(const DwtPlan &P, int irrev) {
     const DwtOptions &o = dwt_options();
     const size_t n = P.levels.size();
-    if (!P.inverse || !o.inv01 || n < 2) return 0;
+    if (!P.inverse || !o.inv01 || n < 2 || P.restricted) return 0;
     const auto &la = P.levels[n - 2], &lb = P.levels[n - 1];
     if (la.empty() || la.size() != lb.size()) return 0;
     uint64_t samples = 0;
@@ -648,7 +661,7 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
         // components: 8-row windows (measured on the 8K frame: 5/3 162 us at
         // TH 8, 168 at 16, 194 at 32; 9/7 229 / 319 / 330)
         if (l == 0 && P.mct3) P.th[l] = 8;
-        for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j.rw, j.rh, j.casx, j.casy, &j.tiles_x, &j.ntiles);
+        for (auto &j : P.levels[l]) dwt_job_tiles(irrev, P.th[l], j);
     }
     // Fused level pairs (k_dwt_fwd01).  A fused pair never writes its first
     // level's LL band, so the LL ping-pong is re-dealt: every level reads the
@@ -840,12 +853,16 @@ static void for_each_cblk(TileComp &tc, F f, uint32_t maxres = 0xffffffffu, cons
 // influences the window is decoded and the window's samples come out exactly
 // as in a full decode (dwt.cpp decode_tile_53 / _97 compute each output from
 // its support only).
-static BandNeed window_need(const TileComp &tc, const Rect &win) {
+// resneed (optional): per resolution the region of its samples the window
+// needs (the inverse DWT levels run only over these).
+static BandNeed window_need(const TileComp &tc, const Rect &win, std::vector<Rect> *resneed = nullptr) {
     constexpr uint32_t M = 4;
     BandNeed need(tc.numres);
     Rect n = intersect(win, tc.res[tc.numres - 1].r);
+    if (resneed) resneed->assign(tc.numres, Rect{});
     for (int32_t r = (int32_t)tc.numres - 1; r >= 0; --r) {
         const Resolution &res = tc.res[r];
+        if (resneed) (*resneed)[r] = n;
         if (r == 0) {
             need[0][0] = intersect(n, res.bands[0].r);
             break;
@@ -1314,13 +1331,12 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         ByteBuf hdr;
         std::vector<PlanItem> plan;
         std::vector<uint8_t> tlm;
-        double rate_ms = 0;
+        double rate_ms = 0, packet_ms = 0;
         bool ok = true;
     };
     std::vector<TileOut> touts(tiles.size());
     double t_rate = 0;  // summed over tiles (host CPU time of the rate allocation)
     host_parallel_for(tiles.size(), 1, [&](size_t t0, size_t t1) {
-        std::vector<PacketId> order;
         for (size_t ti = t0; ti < t1; ++ti) {
             Tile &tile = tiles[ti];
             TileOut &to = touts[ti];
@@ -1338,36 +1354,99 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             for (auto &tc : tile.comps) for_each_cblk(tc, [&](Band &, Cblk &cb) { tenc.distotile += blk_disto[cb.gidx]; });
             const double tr0 = now_ms();
             if (!rate_allocate(cpt, tenc, tile_bound)) { to.ok = false; continue; }
-            to.rate_ms = now_ms() - tr0;
-            tenc.packno = 0;
-            uint32_t tpno = 0;
-            ByteBuf &th = to.hdr;
-            for (uint32_t pino = 0; pino < tenc.pocs.size(); ++pino) {
+            const double tp0 = now_ms();
+            to.rate_ms = tp0 - tr0;
+            // The tile-parts' packets (T2::encode_packets per tile-part,
+            // T2.cpp:64-125).  Tile-parts whose packets touch disjoint
+            // precincts (tile-parts split by component or resolution, no POC
+            // revisiting a precinct: the cinema profiles) are independent --
+            // a packet header's state is its precinct's tag trees and its
+            // code-blocks' inclusion records -- and are written in parallel,
+            // each from its own SOP packet number; the bytes are the same.
+            struct TpOut {
+                uint32_t pino, tpn, packno0 = 0;
+                std::vector<PacketId> order;
+                ByteBuf hdr;
+                std::vector<PlanItem> plan;
+            };
+            std::vector<TpOut> tps;
+            for (uint32_t pino = 0; pino < tenc.pocs.size(); ++pino)
                 for (uint32_t tpn = 0; tpn < tp_counts[tile.index][pino]; ++tpn) {
-                    const size_t sot = th.size();
-                    th.put16(0xFF90); th.put16(10); th.put16(tile.index); th.put32(0); th.put8(tpno); th.put8(ntp);
-                    if (tpno == 0 && !cinema && cp.numpocs) write_poc(th, cpt);
-                    th.put16(0xFF93);
-                    to.plan.push_back({sot, (uint32_t)(th.size() - sot), 0});
-                    const size_t first = to.plan.size() - 1;
-                    encode_packet_order(cpt, tenc, pino, tpn, order);
-                    for (auto &pk : order)
-                        if (pk.layno < L) write_packet(cpt, tenc, pk, th, to.plan);
-                    uint64_t psot = 0;
-                    for (size_t i = first; i < to.plan.size(); ++i) psot += to.plan[i].len;
-                    th.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
-                    if (cinema) {
-                        to.tlm.push_back((uint8_t)tile.index);
-                        for (int b = 3; b >= 0; --b) to.tlm.push_back((uint8_t)(psot >> (8 * b)));
+                    tps.push_back(TpOut{pino, tpn});
+                    encode_packet_order(cpt, tenc, pino, tpn, tps.back().order);
+                }
+            bool disjoint = tps.size() > 1;
+            {
+                std::vector<int32_t> owner;  // precinct -> tile-part
+                std::vector<std::vector<uint32_t>> pb(nc);  // first precinct index of (component, resolution)
+                uint32_t np = 0;
+                for (uint32_t k = 0; k < nc; ++k) {
+                    pb[k].resize(tile.comps[k].numres);
+                    for (uint32_t r = 0; r < tile.comps[k].numres; ++r) {
+                        pb[k][r] = np;
+                        np += tile.comps[k].res[r].pw * tile.comps[k].res[r].ph;
                     }
-                    ++tpno;
+                }
+                owner.assign(np, -1);
+                uint32_t packno = 0;
+                for (size_t j = 0; j < tps.size() && disjoint; ++j) {
+                    tps[j].packno0 = packno;
+                    for (auto &pk : tps[j].order) {
+                        if (pk.layno >= L) continue;
+                        ++packno;
+                        int32_t &o = owner[pb[pk.compno][pk.resno] + pk.precno];
+                        if (o >= 0 && o != (int32_t)j) { disjoint = false; break; }
+                        o = (int32_t)j;
+                    }
                 }
             }
+            auto write_tp = [&](TpOut &t, TileEnc &te) {
+                for (auto &pk : t.order)
+                    if (pk.layno < L) write_packet(cpt, te, pk, t.hdr, t.plan);
+            };
+            if (disjoint) {
+                host_parallel_for(tps.size(), 1, [&](size_t j0, size_t j1) {
+                    for (size_t j = j0; j < j1; ++j) {
+                        TileEnc te = tenc;  // shares the tile's state; its own packet counter
+                        te.packno = tps[j].packno0;
+                        write_tp(tps[j], te);
+                    }
+                });
+            } else {
+                for (auto &t : tps) write_tp(t, tenc);
+            }
+            uint32_t tpno = 0;
+            ByteBuf &th = to.hdr;
+            for (auto &t : tps) {
+                const size_t sot = th.size();
+                th.put16(0xFF90); th.put16(10); th.put16(tile.index); th.put32(0); th.put8(tpno); th.put8(ntp);
+                if (tpno == 0 && !cinema && cp.numpocs) write_poc(th, cpt);
+                th.put16(0xFF93);
+                to.plan.push_back({sot, (uint32_t)(th.size() - sot), 0});
+                const size_t first = to.plan.size() - 1;
+                const uint64_t base = th.size();
+                th.putn(t.hdr.v.data(), t.hdr.size());
+                for (PlanItem it : t.plan) {
+                    if (it.kind == 0) it.src += base;
+                    to.plan.push_back(it);
+                }
+                uint64_t psot = 0;
+                for (size_t i = first; i < to.plan.size(); ++i) psot += to.plan[i].len;
+                th.set32(sot + 6, (uint32_t)psot);  // Psot (j2k.cpp:2418-2426)
+                if (cinema) {
+                    to.tlm.push_back((uint8_t)tile.index);
+                    for (int b = 3; b >= 0; --b) to.tlm.push_back((uint8_t)(psot >> (8 * b)));
+                }
+                ++tpno;
+            }
+            to.packet_ms = now_ms() - tp0;
         }
     });
+    double t_packets = 0;
     for (auto &to : touts) {
         if (!to.ok) return set_err(GRKGPU_EINVAL, "rate allocation failed");
         t_rate += to.rate_ms;
+        t_packets += to.packet_ms;
         const uint64_t base = hdr.size();
         hdr.putn(to.hdr.v.data(), to.hdr.size());
         for (PlanItem it : to.plan) {
@@ -1428,6 +1507,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     st.cs_bytes = total;
     st.mq_symbols = nsym;
     st.rate_ms = (float)t_rate;
+    st.packet_ms = (float)t_packets;
     return GRKGPU_OK;
 }
 
@@ -1847,8 +1927,13 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < tile.comps.size(); ++k) {
             const TileComp &tc = tile.comps[k];
+            // a window decode reconstructs, per level, only the windows over
+            // the region the window's samples depend on
+            std::vector<Rect> rn;
+            if (win) window_need(tc, wr, &rn);
             dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
-                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true, numres_dec);
+                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true, numres_dec,
+                        win ? &rn : nullptr);
         }
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     // window decode: the coefficients of the code-blocks left undecoded are

@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "grk_device.h"
 
 namespace grkgpu {
@@ -106,11 +108,15 @@ template <int OP> __device__ __forceinline__ int32_t lift(int32_t t, int32_t l, 
     }
 }
 
-// vertical step over rows [lo, hi) of parity PAR (0 low, 1 high)
-template <int OP, int PAR, int R>
+// vertical lifting step S (0-based) over the window rows of parity PAR (0
+// low, 1 high).  The rows a window keeps are [H, R - H), H = the number of
+// steps (the halo), so step S only needs rows [S + 1, R - 1 - S): the rows
+// further out feed nothing that is kept.
+template <int OP, int PAR, int S, int R>
 __device__ __forceinline__ void vstep(int32_t (&v)[R]) {
+    constexpr int K0 = ((S + 1) & 1) == PAR ? S + 1 : S + 2;
 #pragma unroll
-    for (int k = PAR == 0 ? 2 : 1; k + 1 < R; k += 2) v[k] = lift<OP>(v[k], v[k - 1], v[k + 1]);
+    for (int k = K0; k + 1 + S < R; k += 2) v[k] = lift<OP>(v[k], v[k - 1], v[k + 1]);
 }
 
 // Linear workgroup id -> position in an order where each XCD (workgroups are
@@ -118,6 +124,22 @@ __device__ __forceinline__ void vstep(int32_t (&v)[R]) {
 __device__ __forceinline__ int xcd_remap(int L, int total) {
     const int q = total >> 3, r = total & 7, x = L & 7, k = L >> 3;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// Workgroup wg of a pair kernel (row-major over ntx x nty) -> (tx, ty) in
+// groups of G columns walked top to bottom (G = 0: row-major): a workgroup's
+// vertical neighbour then runs G workgroups later on the same XCD, while the
+// rows both read are still in its L2.
+__device__ __forceinline__ void group_order(int wg, int ntx, int nty, int G, int &tx, int &ty) {
+    if (G <= 0 || G >= ntx) { tx = wg % ntx; ty = wg / ntx; return; }
+    const int full = ntx / G, per = G * nty, g = wg / per;
+    if (g < full) {
+        const int rem = wg - g * per;
+        ty = rem / G; tx = g * G + rem % G;
+    } else {
+        const int rem = wg - full * per, gw = ntx - full * G;
+        ty = rem / gw; tx = full * G + rem % gw;
+    }
 }
 
 // Window of this wavefront.  The launch is a 2-D grid (x: workgroups of one
@@ -140,7 +162,6 @@ __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int 
     else { wg = L % gx; job = L / gx; }
     J = jobs[job];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nty = (J.rh + J.casy + th - 1) / th;
     if (lay & 2) {
         tx = wg % J.tiles_x;
         ty = (wg / J.tiles_x) * DWT_WAVES + w;
@@ -149,7 +170,10 @@ __device__ __forceinline__ bool dwt_window(const DwtJob *__restrict__ jobs, int 
         tx = tile % J.tiles_x;
         ty = tile / J.tiles_x;
     }
-    return ty < nty;
+    const bool ok = ty < J.win_ny;
+    tx += J.win_x0;
+    ty += J.win_y0;
+    return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -221,13 +245,13 @@ template <bool IRREV, int R>
 __device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R], int rh, int casy) {
     if (rh > 1) {
         if constexpr (!IRREV) {
-            vstep<0, 1>(lo); vstep<0, 1>(hi);
-            vstep<1, 0>(lo); vstep<1, 0>(hi);
+            vstep<0, 1, 0>(lo); vstep<0, 1, 0>(hi);
+            vstep<1, 0, 1>(lo); vstep<1, 0, 1>(hi);
         } else {
-            vstep<2, 1>(lo); vstep<2, 1>(hi);
-            vstep<3, 0>(lo); vstep<3, 0>(hi);
-            vstep<4, 1>(lo); vstep<4, 1>(hi);
-            vstep<5, 0>(lo); vstep<5, 0>(hi);
+            vstep<2, 1, 0>(lo); vstep<2, 1, 0>(hi);
+            vstep<3, 0, 1>(lo); vstep<3, 0, 1>(hi);
+            vstep<4, 1, 2>(lo); vstep<4, 1, 2>(hi);
+            vstep<5, 0, 3>(lo); vstep<5, 0, 3>(hi);
         }
     } else if (!IRREV && casy) {  // single row, odd origin: S0 <<= 1 (dwt53.cpp:161)
 #pragma unroll
@@ -458,8 +482,8 @@ __device__ __forceinline__ void inv_lift(int32_t (&lo)[R], int32_t (&hi)[R], int
     }
     if (rh > 1) {
         if constexpr (!IRREV) {
-            vstep<6, 0>(lo); vstep<6, 0>(hi);
-            vstep<7, 1>(lo); vstep<7, 1>(hi);
+            vstep<6, 0, 0>(lo); vstep<6, 0, 0>(hi);
+            vstep<7, 1, 1>(lo); vstep<7, 1, 1>(hi);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -467,10 +491,10 @@ __device__ __forceinline__ void inv_lift(int32_t (&lo)[R], int32_t (&hi)[R], int
                 lo[r] = __float_as_int(__fmul_rn(__int_as_float(lo[r]), s));
                 hi[r] = __float_as_int(__fmul_rn(__int_as_float(hi[r]), s));
             }
-            vstep<8, 0>(lo); vstep<8, 0>(hi);
-            vstep<9, 1>(lo); vstep<9, 1>(hi);
-            vstep<10, 0>(lo); vstep<10, 0>(hi);
-            vstep<11, 1>(lo); vstep<11, 1>(hi);
+            vstep<8, 0, 0>(lo); vstep<8, 0, 0>(hi);
+            vstep<9, 1, 1>(lo); vstep<9, 1, 1>(hi);
+            vstep<10, 0, 2>(lo); vstep<10, 0, 2>(hi);
+            vstep<11, 1, 3>(lo); vstep<11, 1, 3>(hi);
         }
     } else if (!IRREV && casy) {
 #pragma unroll
@@ -617,7 +641,8 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
     const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
     const int ntx = (rw1 + casx1 + F::CW1 - 1) / F::CW1, nty = (rh1 + casy1 + F::TH1 - 1) / F::TH1;
     if (wg >= ntx * nty) return;  // uniform over the workgroup
-    const int tx1 = wg % ntx, ty1 = wg / ntx;
+    int tx1, ty1;
+    group_order(wg, ntx, nty, lay >> 8, tx1, ty1);
     const int xw1 = tx1 * F::CW1 - casx1 - H, yw1 = ty1 * F::TH1 - casy1 - H;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // level-0 pairs (LL0 coordinates) whose bands this workgroup stores
@@ -732,7 +757,6 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
 // R_a's halo rows / columns are reconstructed by two workgroups (~1.1x of
 // stage A's lifting); the launch boundary and the LL round trip go away.
 // ---------------------------------------------------------------------------
-constexpr int kDwtLayInv01 = 1;  // XCD-contiguous workgroup runs
 
 template <bool IRREV, int NA_ = 2>
 struct I01Geo {
@@ -768,7 +792,8 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv01(const DwtJob *__re
     const int rwb = JB.rw, rhb = JB.rh, casxb = JB.casx, casyb = JB.casy;
     const int ntx = (rwb + casxb + 2 * G::NPX - 1) / (2 * G::NPX), nty = (rhb + casyb + 2 * G::NPY - 1) / (2 * G::NPY);
     if (wg >= ntx * nty) return;  // uniform over the workgroup
-    const int tx = wg % ntx, ty = wg / ntx;
+    int tx, ty;
+    group_order(wg, ntx, nty, lay >> 8, tx, ty);
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // owned core of R_b: [bx0, bx0 + 2 NPX) x [by0, by0 + 2 NPY), bx0 = casx_b (mod 2)
     const int bx0 = tx * 2 * G::NPX - casxb, by0 = ty * 2 * G::NPY - casyb;
@@ -869,12 +894,13 @@ hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t n
                             int na, hipStream_t s) {
     if (!njobs || !max_tiles) return hipErrorInvalidValue;
     const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
+    const int lay = 1 | (dwt_options().pair_group << 8);  // XCD-contiguous runs, column groups
     if (na == 4) {
-        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 4>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
-        else hipLaunchKernelGGL((k_dwt_inv01<false, 4>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 4>), g, b, 0, s, jobsA, jobsB, lay);
+        else hipLaunchKernelGGL((k_dwt_inv01<false, 4>), g, b, 0, s, jobsA, jobsB, lay);
     } else {
-        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 2>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
-        else hipLaunchKernelGGL((k_dwt_inv01<false, 2>), g, b, 0, s, jobsA, jobsB, kDwtLayInv01);
+        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 2>), g, b, 0, s, jobsA, jobsB, lay);
+        else hipLaunchKernelGGL((k_dwt_inv01<false, 2>), g, b, 0, s, jobsA, jobsB, lay);
     }
     return hipGetLastError();
 }
@@ -889,14 +915,23 @@ int dwt_pick_th(int irrev, uint64_t level_samples, int, int) {
     return level_samples >= ((uint64_t)1 << 23) ? (irrev ? 24 : 32) : 8;
 }
 
-void dwt_job_tiles(int irrev, int code, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles) {
+void dwt_job_tiles(int irrev, int code, DwtJob &j) {
     const int th = code & 0xff;
     const int cw = irrev ? DwtGeo<true, 8>::CW : DwtGeo<false, 8>::CW;
-    const int tx = (rw + casx + cw - 1) / cw;
-    int ty = (rh + casy + th - 1) / th;
-    ty = (ty + DWT_WAVES - 1) / DWT_WAVES * DWT_WAVES;  // whole workgroups (see dwt_window)
-    *tiles_x = tx;
-    *ntiles = tx * ty;
+    // window (tx, ty) holds the core [tx cw - casx, +cw) x [ty th - casy, +th)
+    int x0 = 0, y0 = 0, x1 = j.rw, y1 = j.rh;
+    if (j.reg_x1 > 0) {
+        x0 = std::max(0, j.reg_x0); y0 = std::max(0, j.reg_y0);
+        x1 = std::min(j.rw, j.reg_x1); y1 = std::min(j.rh, j.reg_y1);
+        if (x1 <= x0 || y1 <= y0) x0 = y0 = 0, x1 = y1 = 1;  // empty: one window, harmless
+    }
+    j.win_x0 = (x0 + j.casx) / cw;
+    j.win_y0 = (y0 + j.casy) / th;
+    const int tx = (x1 - 1 + j.casx) / cw - j.win_x0 + 1;
+    const int ny = (y1 - 1 + j.casy) / th - j.win_y0 + 1;
+    j.win_ny = ny;
+    j.tiles_x = tx;
+    j.ntiles = tx * ((ny + DWT_WAVES - 1) / DWT_WAVES * DWT_WAVES);  // whole workgroups (see dwt_window)
 }
 
 // Workgroup order: each XCD gets a contiguous run of windows (dwt_window bit 0).
@@ -937,7 +972,7 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
                             int ny, hipStream_t s) {
     if (!njobs || !max_tiles || !irrev) return hipErrorInvalidValue;
-    const int lay = kDwtLay;
+    const int lay = kDwtLay | (dwt_options().pair_group << 8);
     const dim3 g(max_tiles, njobs), b(64 * DWT_WAVES);
     switch (ny) {
         case 2: hipLaunchKernelGGL((k_dwt_fwd01<true, 2>), g, b, 0, s, jobs0, jobs1, lay); break;

@@ -84,6 +84,13 @@ struct DwtJob {
     int32_t shift[3];
     int32_t mct_mode, comp, src_vec;  // src_vec: pair loads allowed (base aligned to 2 samples, even stride)
     int32_t src_fmt, pad_;
+    // the windows a launch runs for this job: columns [win_x0, win_x0 +
+    // tiles_x), rows [win_y0, win_y0 + win_ny) of the level's window grid
+    // (dwt_job_tiles; all of them unless reg_* restricts the output region:
+    // window decode, grk_set_decode_area)
+    int32_t win_x0, win_y0, win_ny;
+    int32_t reg_x0, reg_y0, reg_x1, reg_y1;  // output region (resolution-relative); reg_x1 = 0: all
+    int32_t pad2_;
 };
 // DWT plan options (grkgpu_dwt_options, set by grkgpu_set_dwt_options; the
 // defaults are the measured best -- the parity suite forces the others)
@@ -95,6 +102,7 @@ struct DwtOptions {
     int32_t inv01 = 2;                               // the two largest inverse levels in one launch (k_dwt_inv01):
                                                      // 2 / 4 stage-A row windows per workgroup; 0 = apart
     uint64_t inv01_min_samples = (uint64_t)1 << 23;  // ... when the larger has this many samples
+    int32_t pair_group = 0;  // fused level pairs: workgroups walk groups of this many columns top-down (0: row-major)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -103,7 +111,9 @@ int dwt_pick_th(int irrev, uint64_t level_samples, int minw, int minh);
 constexpr int DWT_FUSED = 1 << 16;       // geometry-code flag: forward level with fused DC shift loads
 constexpr int DWT_FUSED_MCT3 = 1 << 17;  // ... with fused DC shift + MCT (jobs in component triples)
 constexpr int DWT_FMT_SHIFT = 18;        // bits 18-20: SampleFmt of the fused level's image planes (I32 / U8 / U16)
-void dwt_job_tiles(int irrev, int th, int rw, int rh, int casx, int casy, int32_t *tiles_x, int32_t *ntiles);
+// the window grid of a job at `th` window rows: tiles_x, ntiles (whole
+// workgroups) and win_* (restricted to reg_* when set)
+void dwt_job_tiles(int irrev, int th, DwtJob &j);
 hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_tiles, int th, int irrev,
                            int inverse, hipStream_t s);
 // forward 9/7 levels 0 and 1 in one launch (dwt.hip k_dwt_fwd01): workgroups

@@ -150,24 +150,53 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     return false;
 }
 
-// magnitude refinement of one column.  The pass never changes significance,
-// so the stripe's rows to refine (e) and their "a neighbour is significant"
-// rows (nb: the 8-neighbourhood of t1.cpp's T1_SIGMA_NEIGHBOURS) are formed
-// once per stripe with row-mask operations; a column only extracts its bits.
+// Magnitude refinement, 8 columns at a time.  The pass never changes
+// significance, so the stripe's rows to refine (e) and their "a neighbour is
+// significant" rows (nb: the 8-neighbourhood of t1.cpp's T1_SIGMA_NEIGHBOURS)
+// are formed once per stripe with row-mask operations.  Its decisions come in
+// column-major order within the stripe (column x, rows k..k+3), so a group of
+// 8 columns is turned into one 32-bit word with bit 4c + i = row i of column
+// c (nib4): the group's decisions are the word's set bits in order, their
+// contexts bits of two more such words, and the refinement bits are gathered
+// in a fourth and spread back into the rows once per group -- no per-column
+// extraction of row bits.
+GRK_HD uint32_t spread8(uint32_t b) {  // bit c of b -> bit 4c
+    b = (b | (b << 12)) & 0x000F000Fu;
+    b = (b | (b << 6)) & 0x03030303u;
+    return (b | (b << 3)) & 0x11111111u;
+}
+GRK_HD uint32_t unspread8(uint32_t x) {  // bit 4c of x -> bit c
+    x &= 0x11111111u;
+    x = (x | (x >> 3)) & 0x03030303u;
+    x = (x | (x >> 6)) & 0x000F000Fu;
+    return (x | (x >> 12)) & 0xFFu;
+}
+GRK_HD uint32_t nib4(const uint64_t *r4, uint32_t sh) {
+    return spread8((uint32_t)(r4[0] >> sh) & 0xFFu) | spread8((uint32_t)(r4[1] >> sh) & 0xFFu) << 1 |
+           spread8((uint32_t)(r4[2] >> sh) & 0xFFu) << 2 | spread8((uint32_t)(r4[3] >> sh) & 0xFFu) << 3;
+}
+
 template <class D>
-GRK_HD void d3_mrp_column(D &d, uint32_t *cxw, const DecTables &T, const uint64_t *e, const uint64_t *nb,
-                          const uint64_t *ref, uint64_t *bit, uint32_t x) {
-    T1_WALK(2, x);
-    uint32_t m4 = col4(e, x);
-    const uint32_t ref4 = col4(ref, x), nb4 = col4(nb, x);
-    uint32_t bits = 0;
-    while (m4) {
-        const uint32_t r = (uint32_t)__builtin_ctz(m4);
-        m4 &= m4 - 1;
-        const uint32_t cx = CX_MAG + (((ref4 >> r) & 1) ? 2u : (nb4 >> r) & 1);  // t1.cpp dec_refpass contexts
-        bits |= d.decode(cxw, T.mq, cx) << r;
+GRK_HD void d3_mrp_stripe(D &d, uint32_t *cxw, const DecTables &T, const uint64_t *e, const uint64_t *nb,
+                          const uint64_t *ref, uint64_t *bit, uint64_t mem) {
+    for (uint32_t g = 0; g < 8; ++g) {
+        const uint32_t sh = 8 * g;
+        if (!((mem >> sh) & 0xFFu)) continue;
+        T1_WALK(2, sh);
+        uint32_t E = nib4(e, sh);
+        const uint32_t R = nib4(ref, sh), N = nib4(nb, sh);
+        uint32_t res = 0;
+        while (E) {
+            const uint32_t pos = (uint32_t)__builtin_ctz(E);
+            E &= E - 1;
+            const uint32_t cx = CX_MAG + (((R >> pos) & 1) ? 2u : (N >> pos) & 1);  // t1.cpp dec_refpass contexts
+            res |= d.decode(cxw, T.mq, cx) << pos;
+        }
+        if (res) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bit[i] |= (uint64_t)unspread8(res >> i) << sh;
+        }
     }
-    setcol4(bit, x, bits);
 }
 
 // Codeword segments of a block: a single one (NoSegs) or a cursor that
@@ -230,11 +259,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                     nb[i] = dil(s.sig[i]) | dil(s.sig[i + 2]) | (sg << 1) | (sg >> 1);
                     mem |= e[i];
                 }
-                while (mem) {
-                    const uint32_t x = ctz64(mem);
-                    mem &= mem - 1;
-                    d3_mrp_column(d, cxw, T, e, nb, s.ref, s.bit, x);
-                }
+                if (mem) d3_mrp_stripe(d, cxw, T, e, nb, s.ref, s.bit, mem);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     st.ref[k + 1 + i] = s.ref[i] | e[i];  // every refined sample is now "refined once"

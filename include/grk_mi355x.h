@@ -128,8 +128,8 @@ typedef struct {
     float h2d_ms, dcshift_mct_ms, dwt_ms, t1_ms, gather_ms, d2h_ms, host_t2_ms, total_ms;
     uint64_t num_cblks, cs_bytes;
     uint64_t mq_symbols;  /* MQ symbols coded (encode) */
-    float rate_ms;        /* host rate allocation (PCRD) time */
-    float pad;
+    float rate_ms;        /* host rate allocation (PCRD) time (summed over tiles) */
+    float packet_ms;      /* host packet / tile-part writing time (summed over tiles) */
 } grkgpu_stats;
 
 /* One kernel launch of the last call's forward DWT, timed with HIP events on
@@ -180,14 +180,17 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    launch (k_dwt_inv01, with 2 / 4 row windows for the
  *                    smaller level per workgroup) when the larger has at
  *                    least inv01_min_samples samples (default 2^23; 0: any
- *                    size); 0: one launch per level. */
+ *                    size); 0: one launch per level.
+ *   pair_group       workgroup order of the fused level pairs (k_dwt_fwd01,
+ *                    k_dwt_inv01): 0 (default) row-major; G > 0: groups of G
+ *                    workgroup columns, each walked top to bottom. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
     uint64_t f01_min_samples;
     uint64_t f01_small_min_samples;
     int32_t inv01;
-    int32_t reserved_;
+    int32_t pair_group;
     uint64_t inv01_min_samples;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */

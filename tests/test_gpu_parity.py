@@ -158,7 +158,7 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
         assert np.array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix"])
+@pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix", "g3"])
 @pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
@@ -179,8 +179,9 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
     t = torch.from_numpy(a).cuda()
     # fuse every qualifying pair, not only chip-filling ones ("mix": pairs of
     # >= 2^16 samples with 4 row windows, smaller ones with 2)
+    # "g3": workgroups walk groups of 3 columns top-down (pair_group)
     opts = dict(f01_rows=4, f01_min_samples=1 << 16, f01_small_min_samples=0) if ny == "mix" else \
-        dict(f01_rows=int(ny), f01_min_samples=0)
+        dict(f01_rows=4, f01_min_samples=0, pair_group=3) if ny == "g3" else dict(f01_rows=int(ny), f01_min_samples=0)
     with grk.dwt_options(**opts):
         grk.dwt_fwd(t, x0, y0, numres, True)
         torch.cuda.synchronize()
@@ -188,7 +189,7 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
 
 
 @pytest.mark.parametrize("irrev", [False, True])
-@pytest.mark.parametrize("fused", [0, 2, 4])
+@pytest.mark.parametrize("fused", [0, 2, 4, "2g3"])
 @pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1)),
@@ -206,7 +207,8 @@ def test_dwt_inv01_stage_vs_oracle(oracle, irrev, fused, shape_off, numres):
     import grokimagecompression_amd as grk
     (h, w), (x0, y0) = shape_off
     rng = np.random.default_rng(h * 7 + w + numres)
-    with grk.dwt_options(inv01=fused, inv01_min_samples=0):
+    opts = dict(inv01=2, pair_group=3) if fused == "2g3" else dict(inv01=fused)
+    with grk.dwt_options(inv01_min_samples=0, **opts):
         if not irrev:
             a = rng.integers(-4096, 4096, size=(h, w)).astype(np.int32)
             t = torch.from_numpy(oracle.dwt_fwd(a, x0, y0, numres, False)).cuda()
