@@ -87,6 +87,8 @@ struct grkgpu_ctx {
     bool own_stream = false;
     DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf, segs;
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs, h_segs;
+    DevBuf dwtjobs53;  // decode: the 5/3 tile-components' job table when 9/7 ones share the call
+    HostBuf h_dwtjobs53;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
     // grkgpu_encode_blocks output (valid until the next call on the context)
@@ -1638,17 +1640,20 @@ extern "C" int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_hea
     std::string err;
     if (!parse_main_header(cs, len, cp, sot, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
     memset(hi, 0, sizeof(*hi));
-    hi->cblockw_init = 1u << cp.cblkw;
-    hi->cblockh_init = 1u << cp.cblkh;
-    hi->irreversible = (uint32_t)cp.irrev;
+    // the code-block / wavelet / precinct fields are component 0's (j2k.cpp:
+    // 445-467 reads tcp->tccps[0]: a main COC for component 0 shows here)
+    const CompParams &c0 = cp.comp[0];
+    hi->cblockw_init = 1u << c0.cblkw;
+    hi->cblockh_init = 1u << c0.cblkh;
+    hi->irreversible = (uint32_t)c0.irrev;
     hi->mct = (uint32_t)cp.mct;
     hi->rsiz = cp.rsiz;
-    hi->numresolutions = cp.numres;
+    hi->numresolutions = c0.numres;
     hi->csty = cp.csty;
-    hi->cblk_sty = cp.cblksty;
+    hi->cblk_sty = c0.cblksty;
     for (uint32_t r = 0; r < 33; ++r) {
-        hi->prcw_init[r] = 1u << cp.prcw[r];
-        hi->prch_init[r] = 1u << cp.prch[r];
+        hi->prcw_init[r] = 1u << c0.prcw[r];
+        hi->prch_init[r] = 1u << c0.prch[r];
     }
     hi->tx0 = cp.tx0; hi->ty0 = cp.ty0; hi->tdx = cp.tdx; hi->tdy = cp.tdy; hi->tw = cp.tw; hi->th = cp.th;
     hi->numlayers = cp.numlayers;
@@ -1659,6 +1664,30 @@ extern "C" int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_hea
     hi->nsteps = std::min<uint32_t>(cp.nsteps, 97);
     for (uint32_t b = 0; b < hi->nsteps; ++b) { hi->step_expn[b] = cp.ss[b].expn; hi->step_mant[b] = cp.ss[b].mant; }
     for (uint32_t k = 0; k < cp.numcomps && k < 16; ++k) hi->roishift[k] = cp.roishift[k];
+    return GRKGPU_OK;
+}
+
+extern "C" int grkgpu_read_comp_info(const uint8_t *cs, size_t len, uint32_t compno, grkgpu_comp_info *ci) {
+    if (!cs || !ci) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    size_t sot = 0;
+    std::string err;
+    if (!parse_main_header(cs, len, cp, sot, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
+    if (compno >= cp.numcomps) return set_err(GRKGPU_EINVAL, "component index out of range");
+    const CompParams &c = cp.comp[compno];
+    memset(ci, 0, sizeof(*ci));
+    ci->csty = c.csty;
+    ci->numresolutions = c.numres;
+    ci->cblkw = c.cblkw;
+    ci->cblkh = c.cblkh;
+    ci->cblk_sty = c.cblksty;
+    ci->qmfbid = c.irrev ? 0 : 1;
+    for (uint32_t r = 0; r < 33; ++r) { ci->prcw[r] = c.prcw[r]; ci->prch[r] = c.prch[r]; }
+    ci->qntsty = c.qntsty;
+    ci->numgbits = c.numgbits;
+    ci->nsteps = std::min<uint32_t>(c.nsteps, 100);
+    for (uint32_t b = 0; b < ci->nsteps; ++b) { ci->step_expn[b] = c.ss[b].expn; ci->step_mant[b] = c.ss[b].mant; }
+    ci->roishift = cp.roishift[compno];
     return GRKGPU_OK;
 }
 
@@ -1701,7 +1730,6 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     }
     if (reduce >= cp.numres)  // j2k.cpp:6994
         return set_err(GRKGPU_EINVAL, "reduce must be smaller than the number of resolutions");
-    const uint32_t numres_dec = cp.numres - reduce;
     Rect wr{};  // window, clipped to the image
     if (win) {
         if (reduce) return set_err(GRKGPU_EINVAL, "window decode at a reduced resolution is not supported");
@@ -1726,8 +1754,14 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (reduce && !whole) return set_err(GRKGPU_EINVAL, "reduced decode of a tile range is not supported");
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
+    // and the coding-parameter markers of their headers (COD / COC / QCD /
+    // QCC / RGN / POC / PPT, j2k.cpp:3829-4990), applied to the tile's own
+    // copy of the parameters below
+    struct TpMarker { uint32_t m; size_t off; uint32_t len; };
     std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
-    std::vector<std::vector<std::pair<size_t, uint32_t>>> tpocs(ntiles);  // tile-part header POC segments
+    std::vector<std::vector<TpMarker>> tmarks(ntiles);
+    std::vector<std::vector<uint32_t>> tpseq(ntiles);  // codestream-order index of each of the tile's tile-parts
+    uint32_t ntp_total = 0;
     while (pos + 2 <= len) {
         uint32_t m = rd16(csb + pos);
         if (m == 0xFFD9) break;
@@ -1740,17 +1774,37 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         pos += 12;
         while (pos + 4 <= end && rd16(csb + pos) != 0xFF93) {
             uint32_t mm = rd16(csb + pos);
-            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5E || mm == 0xFF61)
-                return set_err(GRKGPU_EUNSUPPORTED, "tile-part header COD/QCD/COC/QCC/RGN/PPT markers not supported");
             const uint32_t ml = rd16(csb + pos + 2);
             if (ml < 2 || pos + 2 + ml > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part header marker");
-            if (mm == 0xFF5F) tpocs[isot].push_back({pos + 4, ml - 2});  // j2k_read_poc on the tile's tcp
+            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5E || mm == 0xFF5F ||
+                mm == 0xFF61)
+                tmarks[isot].push_back({mm, pos + 4, ml - 2});
             pos += 2 + ml;
         }
         pos += 2;
         if (pos > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part");
         tparts[isot].push_back({pos, end - pos});
+        tpseq[isot].push_back(ntp_total++);
         pos = end;
+    }
+    // PPM (j2k_merge_ppm, j2k.cpp:4766-4900): the main header's packed packet
+    // headers, Zppm order, as Nppm / Ippm pairs -- the i-th pair holds the
+    // headers of the codestream's i-th tile-part
+    std::vector<uint8_t> ppm_buf;
+    std::vector<std::pair<size_t, size_t>> ppm_chunk;  // (offset in ppm_buf, Nppm)
+    if (!cp.ppm.empty()) {
+        std::vector<uint8_t> raw;
+        for (auto &q : cp.ppm) raw.insert(raw.end(), csb + q.off, csb + q.off + q.len);
+        size_t o = 0;
+        while (o < raw.size()) {
+            if (o + 4 > raw.size()) return set_err(GRKGPU_ECORRUPT, "Not enough bytes to read Nppm");
+            const uint32_t nppm = rd32(raw.data() + o);
+            o += 4;
+            if (o + nppm > raw.size()) return set_err(GRKGPU_ECORRUPT, "Corrupted PPM markers");
+            ppm_chunk.push_back({ppm_buf.size(), nppm});
+            ppm_buf.insert(ppm_buf.end(), raw.begin() + o, raw.begin() + o + nppm);
+            o += nppm;
+        }
     }
 
     // host Tier-2 over every tile of the shard; code-block segments -> DecBlock table
@@ -1761,8 +1815,6 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     std::vector<DecBlock> db;
     std::vector<DecSeg> dsegs;        // codeword segments of all blocks
     std::vector<uint8_t> droi;        // per-block ROI shift (empty: no ROI)
-    bool any_roi = false;
-    for (uint32_t k = 0; k < cp.numcomps; ++k) any_roi = any_roi || cp.roishift[k];
     std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     bool too_deep = false;
@@ -1770,17 +1822,91 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     // tile's geometry, tag trees and code-block segments are its own); then
     // the arenas and the DecBlock table in tile order.
     std::vector<std::vector<uint8_t>> tbufs(nsh);  // tiles of several tile-parts: their data concatenated
+    std::vector<std::vector<uint8_t>> tpacked(nsh);  // packed packet headers (PPM / PPT) of each tile
+    std::vector<uint8_t> tpacked_on(nsh, 0);
     std::vector<uint8_t> contig(nsh, 1);
-    std::vector<int> terr(nsh, 0);                 // 1: bad POC marker, 2: corrupt packet header
+    // 1: bad POC marker, 2: corrupt packet header, 3: bad tile-part COD / COC
+    // / QCD / QCC / RGN / PPT, 4: tile-component parameters this decoder does
+    // not take (code-block style, wavelet or MCT other than the main header's,
+    // reduce >= its resolutions)
+    std::vector<int> terr(nsh, 0);
+    std::vector<std::array<uint8_t, 16>> troi(nsh);  // per tile: ROI shift of each component
+    std::vector<int32_t> tmct(nsh, cp.mct);            // per tile: MCT (a tile COD may change it)
     host_parallel_for(nsh, 1, [&](size_t l0, size_t l1) {
         for (size_t lt = l0; lt < l1; ++lt) {
             const uint32_t t = tb + (uint32_t)lt;
             Tile &tile = tiles[lt];
             tile.index = t;
             tile.r = tile_rect(cp, t);
+            for (uint32_t k = 0; k < 16; ++k) troi[lt][k] = cp.roishift[k];
             if (win && !overlap(tile.r, wr)) continue;  // left without components: skipped below
+            // the tile's coding parameters: the main header's, then its
+            // tile-part headers' markers (precedence tile COC > tile COD >
+            // main COC > main COD; QCC / QCD alike); POC entries appended
+            CodingParams tcp = cp;
+            {
+                bool tcod = false, tqcd = false, tcoc[16] = {}, tqcc[16] = {}, ok = true;
+                std::string e;
+                std::vector<PpxSeg> ppt;
+                for (const TpMarker &mk : tmarks[t]) {
+                    const uint8_t *mp = csb + mk.off;
+                    if (mk.m == 0xFF52) { ok = parse_cod(mp, mk.len, tcp, e); tcod = true; }
+                    else if (mk.m == 0xFF5C) { ok = parse_qcd(mp, mk.len, tcp, e); tqcd = true; }
+                    else if (mk.m == 0xFF53) { const int32_t k = parse_coc(mp, mk.len, tcp, e); ok = k >= 0; if (ok) tcoc[k] = true; }
+                    else if (mk.m == 0xFF5D) { const int32_t k = parse_qcc(mp, mk.len, tcp, e); ok = k >= 0; if (ok) tqcc[k] = true; }
+                    else if (mk.m == 0xFF5E) {  // RGN (j2k_read_rgn, j2k.cpp:5555-5604)
+                        const uint32_t room = nc <= 256 ? 1 : 2;
+                        const uint32_t k = room == 2 ? rd16(mp) : mp[0];
+                        ok = mk.len == 2 + room && k < nc;
+                        if (ok) tcp.roishift[k] = mp[room + 1];
+                    } else if (mk.m == 0xFF5F) {
+                        if (!parse_poc(mp, mk.len, tcp)) { terr[lt] = 1; break; }
+                    } else if (mk.m == 0xFF61) {  // PPT (j2k_read_ppt, j2k.cpp:4901-4978): Zppt, Ippt
+                        ok = mk.len >= 1;
+                        if (ok) ppt.push_back({mp[0], mk.off + 1, (size_t)mk.len - 1});
+                    }
+                    if (!ok) break;
+                }
+                if (terr[lt]) continue;
+                if (!ok) { terr[lt] = 3; continue; }
+                for (uint32_t k = 0; k < 16; ++k) {
+                    if (tcod && !tcoc[k]) comp_style_from_cod(tcp, k);
+                    if (tqcd && !tqcc[k]) comp_quant_from_qcd(tcp, k);
+                }
+                for (uint32_t k = 0; k < nc; ++k) {
+                    const CompParams &cc = tcp.comp[k];
+                    if (cc.cblksty != cp.cblksty || reduce >= cc.numres || cc.cblkw > 6 || cc.cblkh > 6) ok = false;
+                    troi[lt][k] = tcp.roishift[k];
+                }
+                // MCT over components of different wavelets: the reference
+                // picks the transform by component 0's alone
+                if (tcp.mct && nc >= 3 && (tcp.comp[1].irrev != tcp.comp[0].irrev ||
+                                           tcp.comp[2].irrev != tcp.comp[0].irrev))
+                    ok = false;
+                tmct[lt] = tcp.mct;
+                if (!ok) { terr[lt] = 4; continue; }
+                // the tile's packed packet headers: its PPT segments in Zppt
+                // order (j2k_merge_ppt), or its tile-parts' PPM chunks
+                std::sort(ppt.begin(), ppt.end(), [](const PpxSeg &a, const PpxSeg &b) { return a.z < b.z; });
+                for (size_t q = 1; q < ppt.size(); ++q)
+                    if (ppt[q].z == ppt[q - 1].z) ok = false;  // "Zppt already read" (j2k.cpp:4958)
+                std::vector<uint8_t> &ph = tpacked[lt];
+                ph.clear();
+                if (!ppm_chunk.empty()) {
+                    for (uint32_t q : tpseq[t]) {
+                        if (q >= ppm_chunk.size()) { ok = false; break; }
+                        ph.insert(ph.end(), ppm_buf.begin() + ppm_chunk[q].first,
+                                  ppm_buf.begin() + ppm_chunk[q].first + ppm_chunk[q].second);
+                    }
+                    tpacked_on[lt] = 1;
+                } else if (!ppt.empty()) {
+                    for (auto &q : ppt) ph.insert(ph.end(), csb + q.off, csb + q.off + q.len);
+                    tpacked_on[lt] = 1;
+                }
+                if (!ok) { terr[lt] = 3; continue; }
+            }
             tile.comps.resize(nc);
-            for (uint32_t k = 0; k < nc; ++k) build_tilecomp(tile.comps[k], tile.r, cp, k, false);
+            for (uint32_t k = 0; k < nc; ++k) build_tilecomp(tile.comps[k], tile.r, tcp, k, false);
             // tile data: single tile-part -> decode in place; else concatenate
             const uint8_t *td;
             size_t tlen;
@@ -1799,19 +1925,17 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             }
             // packets in the tile's progression (T2::decode_packets, T2.cpp:194-258),
             // POC entries of the main header followed by the tile's own
-            CodingParams tcp = cp;
-            bool ok = true;
-            for (auto &pc : tpocs[t]) ok = ok && parse_poc(csb + pc.first, pc.second, tcp);
-            if (!ok) { terr[lt] = 1; continue; }
             std::vector<PacketId> order;
             decode_packet_order(tcp, tile, order);
             size_t off = 0;
             uint32_t packno = 0;
+            PackedHdr packed{tpacked[lt].data(), tpacked[lt].size(), 0};
             for (const auto &pk : order) {
                 if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
                 const bool skip = max_layers && pk.layno >= max_layers;
                 int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
-                                             base + off, tcp.csty, &packno, skip, tcp.cblksty);
+                                             base + off, tcp.csty, &packno, skip, tcp.cblksty,
+                                             tpacked_on[lt] ? &packed : nullptr);
                 if (used < 0) { terr[lt] = 2; break; }
                 off += (size_t)used;
             }
@@ -1820,7 +1944,15 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     for (uint32_t lt = 0; lt < nsh; ++lt) {
         if (terr[lt] == 1) return set_err(GRKGPU_ECORRUPT, "Error reading POC marker");
         if (terr[lt] == 2) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
+        if (terr[lt] == 3) return set_err(GRKGPU_ECORRUPT, "corrupt tile-part header marker (COD/COC/QCD/QCC/RGN/PPT/PPM)");
+        if (terr[lt] == 4)
+            return set_err(GRKGPU_EUNSUPPORTED, "tile-component coding style not supported (code-block style "
+                                                "differing from the main header's, MCT over components of different "
+                                                "wavelets, or reduce too large)");
     }
+    bool any_roi = false;
+    for (uint32_t lt = 0; lt < nsh; ++lt)
+        for (uint32_t k = 0; k < nc; ++k) any_roi = any_roi || troi[lt][k];
     for (uint32_t lt = 0; lt < nsh; ++lt) {
         Tile &tile = tiles[lt];
         if (tile.comps.empty()) continue;
@@ -1843,7 +1975,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 d.w = cb.r.w();
                 d.h = cb.r.h();
                 d.orient = band.bandno;
-                d.irrev = cp.irrev;
+                d.irrev = tc.irrev;
                 d.step = band.stepsize;
                 // passes beyond the last bit-plane are not decoded (t1_decode_cblk
                 // stops at bpno < 0, t1.cpp:1086-1090)
@@ -1873,7 +2005,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     dsegs.push_back(ds);
                 }
                 d.data_off = cb.segs.empty() ? 0 : dsegs[seg_first.back()].data_off;
-                if (any_roi) droi.push_back(cp.roishift[k]);
+                if (any_roi) droi.push_back(troi[lt][k]);
                 // no bytes: the block stays zero (T1Part1::decode returns before
                 // t1_decode_cblk when the block has no data, T1Part1.cpp:139-140)
                 if (!d.len) d.numpasses = 0;
@@ -1883,7 +2015,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 // scratch holds 32 planes
                 if (d.numpasses && d.numbps >= 31) too_deep = true;
                 db.push_back(d);
-            }, numres_dec, win ? &need : nullptr);
+            }, tc.numres - reduce, win ? &need : nullptr);
         }
     }
     if (too_deep) return set_err(GRKGPU_ECORRUPT, "unsupported bpno_plus_one >= 31 (code-block bit-planes + ROI shift)");
@@ -1923,7 +2055,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     }
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(DecBlock), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.p, segbytes + sfbytes + roibytes, hipMemcpyHostToDevice, s));
-    DwtPlan dplan;
+    // one plan per wavelet (COC / tile COD may mix 5/3 and 9/7 components)
+    DwtPlan dplan[2];
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < tile.comps.size(); ++k) {
             const TileComp &tc = tile.comps[k];
@@ -1931,11 +2064,12 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             // the region the window's samples depend on
             std::vector<Rect> rn;
             if (win) window_need(tc, wr, &rn);
-            dwt_plan_tc(dplan, tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
-                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, true, numres_dec,
+            dwt_plan_tc(dplan[tc.irrev], tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
+                        c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], tc.irrev, true, tc.numres - reduce,
                         win ? &rn : nullptr);
         }
-    HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
+    HIPCHK(dwt_upload(dplan[1], c->dwtjobs, c->h_dwtjobs, 1, s));
+    HIPCHK(dwt_upload(dplan[0], c->dwtjobs53, c->h_dwtjobs53, 0, s));
     // window decode: the coefficients of the code-blocks left undecoded are
     // zero (they lie outside every window sample's support; zero keeps the
     // 9/7 float lifting free of stale NaNs)
@@ -1948,7 +2082,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(hipEventRecord(c->ev[2], s));
     c->ltimes.clear();
     LaunchLog llog{&c->lev, &c->ltimes};
-    HIPCHK(dwt_launch(dplan, c->dwtjobs, cp.irrev, true, s, c->launch_timing ? &llog : nullptr));
+    HIPCHK(dwt_launch(dplan[1], c->dwtjobs, 1, true, s, c->launch_timing ? &llog : nullptr));
+    HIPCHK(dwt_launch(dplan[0], c->dwtjobs53, 0, true, s, c->launch_timing ? &llog : nullptr));
     HIPCHK(hipEventRecord(c->ev[3], s));
     PlanePtrs dst{};
     if (planes_on_device) {
@@ -1966,7 +2101,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     for (auto &tile : tiles) {
         if (tile.comps.empty()) continue;  // outside the window
         PlanePtrs tsrc{}, tdst{};
-        const Rect tr = tile.comps[0].res[numres_dec - 1].r;  // the tile at the decoded resolution
+        const Rect tr = tile.comps[0].res[tile.comps[0].numres - 1 - reduce].r;  // the tile at the decoded resolution
         const Rect out = win ? intersect(tr, wr) : tr;        // its part of the output
         if (out.empty()) continue;
         for (uint32_t k = 0; k < nc; ++k) {
@@ -1974,8 +2109,10 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                         (out.x0 - tr.x0);
             tdst.p[k] = dst.p[k] + (uint64_t)(out.y0 - iy0) * iw + (out.x0 - ix0);
         }
-        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, iw, nc, sh, mn, mx, cp.mct, cp.irrev,
-                                      s));
+        int32_t wmask = 0;  // components holding 9/7 (float) samples
+        for (uint32_t k = 0; k < nc; ++k) wmask |= tile.comps[k].irrev << k;
+        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, iw, nc, sh, mn, mx,
+                                      tmct[tile.index - tb], wmask, s));
     }
     HIPCHK(hipEventRecord(c->ev[4], s));
     if (!planes_on_device) {
@@ -2073,7 +2210,8 @@ extern "C" int grkgpu_mct_inv_dcshift(int32_t *const *planes, uint32_t numcomps,
         if (sgnd[k]) { mn.v[k] = -(1 << (prec[k] - 1)); mx.v[k] = (1 << (prec[k] - 1)) - 1; }
         else { mn.v[k] = 0; mx.v[k] = (1 << prec[k]) - 1; }
     }
-    HIPCHK(launch_mct_inv_dcshift(p, stride, w, h, p, stride, numcomps, sh, mn, mx, mct, irreversible, (hipStream_t)stream));
+    HIPCHK(launch_mct_inv_dcshift(p, stride, w, h, p, stride, numcomps, sh, mn, mx, mct, irreversible ? 0xFFFF : 0,
+                                  (hipStream_t)stream));
     return GRKGPU_OK;
 }
 

@@ -75,6 +75,29 @@ void generate_qcd(CodingParams &cp) {
             cp.ss[s++] = irrev_step(base / (h * h));
         }
     }
+    cp.nsteps = s;
+    sync_comps(cp);
+}
+
+void comp_style_from_cod(CodingParams &cp, uint32_t k) {
+    CompParams &c = cp.comp[k];
+    c.numres = cp.numres; c.cblkw = cp.cblkw; c.cblkh = cp.cblkh; c.cblksty = cp.cblksty; c.irrev = cp.irrev;
+    c.csty = cp.csty & CSTY_PRT;
+    memcpy(c.prcw, cp.prcw, sizeof(c.prcw));
+    memcpy(c.prch, cp.prch, sizeof(c.prch));
+}
+
+void comp_quant_from_qcd(CodingParams &cp, uint32_t k) {
+    CompParams &c = cp.comp[k];
+    c.qntsty = cp.qntsty; c.numgbits = cp.numgbits; c.nsteps = cp.nsteps;
+    memcpy(c.ss, cp.ss, sizeof(c.ss));
+}
+
+void sync_comps(CodingParams &cp) {
+    for (uint32_t k = 0; k < 16; ++k) {
+        comp_style_from_cod(cp, k);
+        comp_quant_from_qcd(cp, k);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -123,14 +146,16 @@ void TagTree::setvalue(uint32_t leaf, int64_t v) {
 }
 
 void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32_t compno, bool encoder) {
+    const CompParams &cc = cp.comp[compno];  // the component's COD / COC and QCD / QCC
     tc.r = tr;
-    tc.numres = cp.numres;
-    tc.res.assign(cp.numres, Resolution());
-    for (uint32_t resno = 0; resno < cp.numres; ++resno) {
+    tc.numres = cc.numres;
+    tc.irrev = cc.irrev;
+    tc.res.assign(cc.numres, Resolution());
+    for (uint32_t resno = 0; resno < cc.numres; ++resno) {
         Resolution &res = tc.res[resno];
-        const uint32_t lev = cp.numres - 1 - resno;
+        const uint32_t lev = cc.numres - 1 - resno;
         res.r = {ceildivpow2(tr.x0, lev), ceildivpow2(tr.y0, lev), ceildivpow2(tr.x1, lev), ceildivpow2(tr.y1, lev)};
-        const uint32_t pdx = cp.prcw[resno], pdy = cp.prch[resno];  // log2 precinct size (COD SPcod I_i)
+        const uint32_t pdx = cc.prcw[resno], pdy = cc.prch[resno];  // log2 precinct size (COD SPcod I_i)
         uint32_t tpx0 = (res.r.x0 >> pdx) << pdx, tpy0 = (res.r.y0 >> pdy) << pdy;
         uint32_t bpx1 = ceildivpow2(res.r.x1, pdx) << pdx, bpy1 = ceildivpow2(res.r.y1, pdy) << pdy;
         res.pw = (res.r.x0 == res.r.x1) ? 0 : ((bpx1 - tpx0) >> pdx);
@@ -138,7 +163,7 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
         uint32_t tlcbgx, tlcbgy, cbgw, cbgh;
         if (resno == 0) { tlcbgx = tpx0; tlcbgy = tpy0; cbgw = pdx; cbgh = pdy; res.numbands = 1; }
         else { tlcbgx = ceildivpow2(tpx0, 1); tlcbgy = ceildivpow2(tpy0, 1); cbgw = pdx - 1; cbgh = pdy - 1; res.numbands = 3; }
-        const uint32_t cbw = std::min(cp.cblkw, cbgw), cbh = std::min(cp.cblkh, cbgh);
+        const uint32_t cbw = std::min(cc.cblkw, cbgw), cbh = std::min(cc.cblkh, cbgh);
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
             Band &b = res.bands[bandno];
             if (resno == 0) {
@@ -153,13 +178,13 @@ void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32
                 b.r.y1 = (uint32_t)(((uint64_t)tr.y1 - (y0b << lev) + d - 1) >> (lev + 1));
             }
             // Quantizer::setBandStepSizeAndBps (Quantizer.cpp:65-104)
-            uint32_t gain = cp.irrev ? 0 : (b.bandno == 0 ? 0 : (b.bandno < 3 ? 1 : 2));
+            uint32_t gain = cc.irrev ? 0 : (b.bandno == 0 ? 0 : (b.bandno < 3 ? 1 : 2));
             uint32_t numbps = cp.prec[compno] + gain;
             uint32_t off = resno == 0 ? 0 : 3 * resno - 2;
-            const StepSize &st = cp.ss[off + bandno];
+            const StepSize &st = cc.ss[off + bandno];
             b.stepsize = (float)((1.0 + st.mant / 2048.0) * std::pow(2.0, (int32_t)(numbps - st.expn))) *
                          (encoder ? 1.0f : 0.5f);
-            b.numbps = cp.roishift[compno] + st.expn + cp.numgbits - 1;  // + ROI (Quantizer.cpp:90-93)
+            b.numbps = cp.roishift[compno] + st.expn + cc.numgbits - 1;  // + ROI (Quantizer.cpp:90-93)
             b.inv_step = (uint32_t)((8192.0 / b.stepsize) + 0.5f);
             uint32_t np = res.pw * res.ph;
             b.precs.assign(np, Precinct());
@@ -304,7 +329,8 @@ struct BitReader {
 }  // namespace
 
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
-                      uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data, uint32_t cblksty) {
+                      uint64_t base_off, uint32_t csty, uint32_t *packno, bool skip_data, uint32_t cblksty,
+                      PackedHdr *hdr) {
     // passes per codeword segment (T2::init_seg, T2.cpp:821-850): 1 when every
     // pass is terminated; BYPASS: 10 for the first, then 2 (raw) and 1 (MQ)
     // alternately; else 109 (a longer block is cut there, T2.cpp:566-577)
@@ -342,10 +368,15 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
             hstart = 6;
         }
     }
-    BitReader r(p + hstart, n - hstart);
+    // the header bits: in the packet (after the SOP), or the packed headers
+    // of the tile (PPT) / tile-part (PPM) when the stream carries them there
+    // (T2::read_packet_header, T2.cpp:366-392)
+    const uint8_t *hp = hdr ? hdr->p + hdr->off : p + hstart;
+    const size_t hn = hdr ? (hdr->off <= hdr->n ? hdr->n - hdr->off : 0) : n - hstart;
+    BitReader r(hp, hn);
     struct Part { Cblk *c; uint32_t seg, passes, len; };  // one segment's share of this packet
     std::vector<Part> parts;
-    if (n > hstart && r.read(1)) {
+    if (hn && r.read(1)) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
             Band &b = res.bands[bandno];
             if (b.empty() || precno >= b.precs.size()) continue;
@@ -396,9 +427,13 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
     }
     r.align();
     if (r.err) return -1;
-    size_t off = hstart + r.off;
-    // EPH (T2.cpp:405-418 / 640-652): skipped when present
-    if ((csty & CSTY_EPH) && off + 2 <= n && p[off] == 0xFF && p[off + 1] == 0x92) off += 2;
+    // EPH (T2.cpp:405-418 / 640-652): skipped when present -- it ends the
+    // header, wherever the header is
+    size_t hoff = r.off;
+    if ((csty & CSTY_EPH) && hoff + 2 <= hn && hp[hoff] == 0xFF && hp[hoff + 1] == 0x92) hoff += 2;
+    size_t off = hstart;
+    if (hdr) hdr->off += hoff;
+    else off += hoff;
     for (auto &pt : parts) {
         // T2::read_packet_data (T2.cpp:686-698): a segment running past the
         // tile data is truncated to what is there (the decoder reads the
@@ -448,6 +483,99 @@ bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp) {
     return true;
 }
 
+// SPcod / SPcoc (j2k_read_SPCod_SPCoc, j2k.cpp:6978-7025): decomposition
+// levels, code-block size and style, transform, precinct sizes; prt: the
+// Scod / Scoc precinct flag
+static bool parse_spcod(const uint8_t *p, uint32_t size, bool prt, CompParams &c, std::string &err) {
+    if (size < 5) { err = "Error reading SPCod SPCoc element"; return false; }
+    c.numres = p[0] + 1u; c.cblkw = p[1] + 2u; c.cblkh = p[2] + 2u; c.cblksty = p[3];
+    c.irrev = p[4] == 0;
+    c.csty = prt ? 1u : 0u;
+    if (c.numres > 33) { err = "Number of resolutions is greater than GRK_J2K_MAXRLVLS"; return false; }
+    if (p[1] > 8 || p[2] > 8 || p[1] + p[2] > 8) { err = "Error reading SPCod SPCoc element, invalid code-block size"; return false; }
+    if (p[4] > 1) { err = "Invalid qmfbid"; return false; }
+    if (prt) {
+        if (size != 5 + c.numres) { err = "Error reading SPCod SPCoc element"; return false; }
+        for (uint32_t r = 0; r < c.numres; ++r) {
+            c.prcw[r] = p[5 + r] & 0xf;
+            c.prch[r] = p[5 + r] >> 4;
+            if (r && (!c.prcw[r] || !c.prch[r])) { err = "invalid precinct size"; return false; }
+        }
+    } else {
+        if (size != 5) { err = "Error reading SPCod SPCoc element"; return false; }
+        for (uint32_t r = 0; r < c.numres; ++r) c.prcw[r] = c.prch[r] = 15;
+    }
+    return true;
+}
+
+bool parse_cod(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err) {
+    // j2k_read_cod (j2k.cpp:3829-3884): Scod, SGcod (progression, layers, MCT), SPcod
+    if (size < 10) { err = "Error reading COD marker"; return false; }
+    if (p[0] & ~7u) { err = "unknown Scod bits"; return false; }
+    cp.csty = p[0];
+    cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
+    if (cp.numlayers == 0) { err = "Invalid number of layers in COD marker"; return false; }
+    if (cp.prog > 4) { err = "Unknown progression order in COD marker"; return false; }
+    CompParams c;
+    if (!parse_spcod(p + 5, size - 5, (cp.csty & CSTY_PRT) != 0, c, err)) return false;
+    cp.numres = c.numres; cp.cblkw = c.cblkw; cp.cblkh = c.cblkh; cp.cblksty = c.cblksty; cp.irrev = c.irrev;
+    memcpy(cp.prcw, c.prcw, sizeof(cp.prcw));
+    memcpy(cp.prch, c.prch, sizeof(cp.prch));
+    return true;
+}
+
+int32_t parse_coc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err) {
+    const uint32_t room = cp.numcomps <= 256 ? 1 : 2;
+    if (size < room + 1) { err = "Error reading COC marker"; return -1; }
+    const uint32_t k = room == 2 ? rd16(p) : p[0];
+    if (k >= cp.numcomps) { err = "Error reading COC marker (bad number of components)"; return -1; }
+    if (p[room] & ~1u) { err = "unknown Scoc bits"; return -1; }
+    CompParams c = cp.comp[k];
+    if (!parse_spcod(p + room + 1, size - room - 1, (p[room] & 1) != 0, c, err)) return -1;
+    CompParams &d = cp.comp[k];
+    d.numres = c.numres; d.cblkw = c.cblkw; d.cblkh = c.cblkh; d.cblksty = c.cblksty; d.irrev = c.irrev;
+    d.csty = c.csty;
+    memcpy(d.prcw, c.prcw, sizeof(d.prcw));
+    memcpy(d.prch, c.prch, sizeof(d.prch));
+    return (int32_t)k;
+}
+
+// SQcd / SQcc + SPqcd / SPqcc (j2k_read_SQcd_SQcc, j2k.cpp:7047-7135): the
+// style (0 none: 8-bit exponents; 2 scalar expounded: 16-bit expn / mantissa),
+// guard bits, one step size per band
+static bool parse_sqcd(const uint8_t *p, uint32_t size, CompParams &c, std::string &err) {
+    if (size < 1) { err = "Error reading QCD marker"; return false; }
+    const uint32_t sq = p[0] & 0x1f;
+    if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
+    c.numgbits = p[0] >> 5;
+    const uint32_t nb = std::min<uint32_t>(sq == 0 ? (size - 1) : (size - 1) / 2, 3 * 33 + 1);
+    c.qntsty = sq;
+    c.nsteps = nb;
+    for (uint32_t i = 0; i < nb; ++i) {
+        if (sq == 0) c.ss[i] = {(uint32_t)(p[1 + i] >> 3), 0};
+        else { const uint32_t v = rd16(p + 1 + 2 * i); c.ss[i] = {v >> 11, v & 0x7ff}; }
+    }
+    return true;
+}
+
+bool parse_qcd(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err) {
+    if (size < 2) { err = "Error reading QCD marker"; return false; }  // j2k.cpp:4075
+    CompParams c;
+    if (!parse_sqcd(p, size, c, err)) return false;
+    cp.qntsty = c.qntsty; cp.numgbits = c.numgbits; cp.nsteps = c.nsteps;
+    memcpy(cp.ss, c.ss, sizeof(cp.ss));
+    return true;
+}
+
+int32_t parse_qcc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err) {
+    const uint32_t room = cp.numcomps <= 256 ? 1 : 2;
+    if (size < room + 1) { err = "Error reading QCC marker"; return -1; }
+    const uint32_t k = room == 2 ? rd16(p) : p[0];
+    if (k >= cp.numcomps) { err = "Invalid component number in QCC marker"; return -1; }
+    if (!parse_sqcd(p + room, size - room, cp.comp[k], err)) return -1;
+    return (int32_t)k;
+}
+
 bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &first_sot, std::string &err) {
     if (len < 4 || rd16(cs) != 0xFF4F) { err = "missing SOC"; return false; }
     size_t pos = 2;
@@ -482,43 +610,26 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             cp.th = ceildiv(cp.image.y1 - cp.ty0, cp.tdy);
             have_siz = true;
         } else if (m == 0xFF52) {
-            if (L < 12) { err = "Error reading COD marker"; return false; }
-            if (p[0] & ~7u) { err = "unknown Scod bits"; return false; }
-            cp.csty = p[0];
-            cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
-            cp.numres = p[5] + 1u; cp.cblkw = p[6] + 2u; cp.cblkh = p[7] + 2u; cp.cblksty = p[8];
-            cp.irrev = p[9] == 0;
-            // read_SPCod_SPCoc, j2k.cpp:6978-7025 / COD layers j2k.cpp:3855
-            if (cp.numlayers == 0) { err = "Invalid number of layers in COD marker"; return false; }
-            if (cp.numres > 33) { err = "Number of resolutions is greater than GRK_J2K_MAXRLVLS"; return false; }
-            if (p[6] > 8 || p[7] > 8 || p[6] + p[7] > 8) { err = "Error reading SPCod SPCoc element, invalid code-block size"; return false; }
-            if (p[9] > 1) { err = "Invalid qmfbid"; return false; }
-            if (cp.prog > 4) { err = "Unknown progression order in COD marker"; return false; }
-            // precinct partition (SPcod I_i, one byte per resolution; j2k.cpp read_SPCod_SPCoc)
-            if (cp.csty & CSTY_PRT) {
-                if (L != 12 + cp.numres) { err = "Error reading SPCod SPCoc element"; return false; }
-                for (uint32_t r = 0; r < cp.numres; ++r) {
-                    cp.prcw[r] = p[10 + r] & 0xf;
-                    cp.prch[r] = p[10 + r] >> 4;
-                    if ((r && (!cp.prcw[r] || !cp.prch[r]))) { err = "invalid precinct size"; return false; }
-                }
-            } else {
-                for (uint32_t r = 0; r < cp.numres; ++r) cp.prcw[r] = cp.prch[r] = 15;
-            }
+            if (!parse_cod(p, L - 2, cp, err)) return false;
             have_cod = true;
         } else if (m == 0xFF5C) {
-            if (L < 4) { err = "Error reading QCD marker"; return false; }  // j2k.cpp:4075
-            uint32_t sq = p[0] & 0x1f;
-            if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
-            cp.numgbits = p[0] >> 5;  // j2k_read_SQcd_SQcc: tccp->numgbits
-            uint32_t nb = sq == 0 ? (L - 3) : (L - 3) / 2;
-            cp.qntsty = sq;
-            cp.nsteps = nb;
-            for (uint32_t i = 0; i < nb && i < 3 * 33 + 1; ++i) {
-                if (sq == 0) cp.ss[i] = {(uint32_t)(p[1 + i] >> 3), 0};
-                else { uint32_t v = rd16(p + 1 + 2 * i); cp.ss[i] = {v >> 11, v & 0x7ff}; }
-            }
+            if (!parse_qcd(p, L - 2, cp, err)) return false;
             have_qcd = true;
+        } else if (m == 0xFF53) {  // COC (j2k_read_coc, j2k.cpp:3991-4060)
+            if (!have_siz) { err = "COC before SIZ"; return false; }
+            const int32_t k = parse_coc(p, L - 2, cp, err);
+            if (k < 0) return false;
+            cp.coc_set[k] = true;
+        } else if (m == 0xFF5D) {  // QCC (j2k_read_qcc, j2k.cpp:4160-4200)
+            if (!have_siz) { err = "QCC before SIZ"; return false; }
+            const int32_t k = parse_qcc(p, L - 2, cp, err);
+            if (k < 0) return false;
+            cp.qcc_set[k] = true;
+        } else if (m == 0xFF60) {  // PPM (j2k_read_ppm, j2k.cpp:4693-4765): Zppm, then Nppm / Ippm pairs
+            if (L < 3) { err = "Error reading PPM marker"; return false; }
+            for (auto &q : cp.ppm)
+                if (q.z == p[0]) { err = "Zppm already read"; return false; }
+            cp.ppm.push_back({p[0], pos + 5, (size_t)L - 3});
         } else if (m == 0xFF5F) {
             if (!parse_poc(p, L - 2, cp)) { err = "Error reading POC marker"; return false; }
         } else if (m == 0xFF5E) {  // RGN (j2k_read_rgn, j2k.cpp:5555-5604)
@@ -528,18 +639,25 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             const uint32_t comp = room == 2 ? rd16(p) : p[0];
             if (comp >= cp.numcomps) { err = "bad component number in RGN"; return false; }
             cp.roishift[comp] = p[room + 1];  // Srgn != 0 is only a warning there
-        } else if (m == 0xFF53 || m == 0xFF5D || m == 0xFF60) {
-            err = "COC/QCC/PPM markers not supported";
-            return false;
         }
         pos += 2 + L;
     }
     if (!have_siz || !have_cod || !have_qcd) { err = "incomplete main header"; return false; }
+    // COD / QCD for every component without its own COC / QCC
+    for (uint32_t k = 0; k < 16; ++k) {
+        if (!cp.coc_set[k]) comp_style_from_cod(cp, k);
+        if (!cp.qcc_set[k]) comp_quant_from_qcd(cp, k);
+    }
+    std::sort(cp.ppm.begin(), cp.ppm.end(), [](const PpxSeg &a, const PpxSeg &b) { return a.z < b.z; });
     // j2k_read_header stops at the first SOT; a stream that ends before it is truncated
     if (first_sot == 0) { err = "truncated main header (no SOT)"; return false; }
     // mode switches: BYPASS, RESET, TERMALL, VSC, PTERM, SEGSYM; not HT (0x40)
     if (cp.cblksty & ~0x3Fu) { err = "HT code-block style not supported"; return false; }
     if (cp.cblkw > 6 || cp.cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        if (cp.comp[k].cblksty & ~0x3Fu) { err = "HT code-block style not supported"; return false; }
+        if (cp.comp[k].cblkw > 6 || cp.comp[k].cblkh > 6) { err = "code-blocks larger than 64 not supported"; return false; }
+    }
     for (uint32_t k = 0; k < cp.numcomps; ++k) cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
     return true;
 }

@@ -35,6 +35,28 @@ struct PocSpec {
 constexpr uint32_t CSTY_PRT = 1, CSTY_SOP = 2, CSTY_EPH = 4;  // Scod bits (j2k.h J2K_CP_CSTY_*)
 constexpr uint16_t RSIZ_CINEMA_2K = 3, RSIZ_CINEMA_4K = 4;     // grok.h:160-161
 
+// Coding style and quantisation of one component (the reference's grk_tccp):
+// COD / COC and QCD / QCC of the main header or of a tile's first tile-part
+// header, resolved in the order of precedence tile COC > tile COD > main COC
+// > main COD (QCC / QCD alike; j2k_read_cod / _coc / _qcd / _qcc,
+// j2k.cpp:3829-4160).  The encoder writes one COD / QCD: every component
+// gets the global values (sync_comps).
+struct CompParams {
+    uint32_t numres = 6, cblkw = 6, cblkh = 6, cblksty = 0;
+    uint32_t csty = 0;  // Scoc (tccp->csty): the precinct flag
+    int32_t irrev = 0;
+    uint8_t prcw[33], prch[33];
+    uint32_t qntsty = 0, numgbits = 2, nsteps = 0;
+    StepSize ss[3 * 33 + 1];
+};
+
+// A PPM / PPT marker segment (packed packet headers): its index Zppm / Zppt
+// and where its data lies in the codestream.
+struct PpxSeg {
+    uint32_t z;
+    size_t off, len;
+};
+
 // Coding parameters as j2k_setup_encoder derives them (codestream/j2k.cpp:1609-2050)
 struct CodingParams {
     uint32_t numcomps = 0;
@@ -72,10 +94,27 @@ struct CodingParams {
     // marker, j2k.cpp:1997-2001 / 5482-5604): adds to every band's bit-plane
     // count, and the decoder shifts decoded magnitudes >= 2^roishift down
     uint8_t roishift[16] = {};
+    // per component (decoder: COC / QCC resolved; encoder: sync_comps)
+    CompParams comp[16];
+    bool coc_set[16] = {}, qcc_set[16] = {};  // main-header COC / QCC seen
+    std::vector<PpxSeg> ppm;                  // main-header PPM segments
     CodingParams() {
         for (int i = 0; i < 33; ++i) prcw[i] = prch[i] = 15;
     }
 };
+
+// COD's coding style / QCD's quantisation -> component k (the global fields)
+void comp_style_from_cod(CodingParams &cp, uint32_t k);
+void comp_quant_from_qcd(CodingParams &cp, uint32_t k);
+// every component from the global COD / QCD values (the encoder's one COD / QCD)
+void sync_comps(CodingParams &cp);
+// COC / QCC marker segment bodies (size bytes) -> cp.comp[...]; returns the
+// component or -1 when malformed
+int32_t parse_coc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err);
+int32_t parse_qcc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err);
+// COD / QCD marker segment bodies -> the global fields
+bool parse_cod(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err);
+bool parse_qcd(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err);
 
 // TagTree (codestream/TagTree.cpp)
 struct TagTree {
@@ -131,6 +170,7 @@ struct Resolution {
 struct TileComp {
     Rect r;
     uint32_t numres = 0;
+    int32_t irrev = 0;  // 9/7 (COD / COC transform 0)
     std::vector<Resolution> res;
     uint64_t arena_off = 0;  // element offset of this tile-component's buffers
 };
@@ -233,8 +273,15 @@ bool parse_poc(const uint8_t *p, uint32_t size, CodingParams &cp);
 // T2.cpp:314-725); csty: SOP / EPH markers; packno: SOP packet counter;
 // skip_data: a layer beyond the decoded ones (T2::skip_packet); cblksty: the
 // code-block style (segment boundaries)
+// hdr: packed packet headers (PPM / PPT, j2k.cpp:4693-4990): the packet's
+// header bits are read from hdr->p + hdr->off (advanced past them and the
+// EPH), its SOP marker and body from p; nullptr: everything from p
+struct PackedHdr {
+    const uint8_t *p = nullptr;
+    size_t n = 0, off = 0;
+};
 int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t layno, const uint8_t *p, size_t n,
                       uint64_t base_off, uint32_t csty = 0, uint32_t *packno = nullptr, bool skip_data = false,
-                      uint32_t cblksty = 0);
+                      uint32_t cblksty = 0, PackedHdr *hdr = nullptr);
 
 }  // namespace grkgpu

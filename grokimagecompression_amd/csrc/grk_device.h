@@ -59,7 +59,9 @@ struct GatherItem { uint64_t src, dst; uint32_t len, pad; };  // pad: 0 = header
 hipError_t launch_dcshift_mct_fwd(const SrcPlanes &src, int32_t fmt, uint32_t sstride, const PlanePtrs &dst,
                                   uint32_t tw, uint32_t th, uint32_t ncomp, const ShiftArr &shift, int32_t mct,
                                   int32_t irrev, hipStream_t s);
-// src rows at sstride elements (a window of a tile buffer), dst rows at dstride
+// src rows at sstride elements (a window of a tile buffer), dst rows at dstride;
+// irrev: bit k set = component k holds 9/7 (float) samples; MCT follows
+// component 0's wavelet
 hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32_t tw, uint32_t th,
                                   const PlanePtrs &dst, uint32_t dstride, uint32_t ncomp, const ShiftArr &shift,
                                   const ShiftArr &mn, const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s);

@@ -196,6 +196,7 @@ struct Codec {
     bool have_header = false;
     grkgpu_image_desc desc{};
     grkgpu_header_info hinfo{};
+    std::vector<grkgpu_comp_info> cinfo;  // per component (main COD / COC, QCD / QCC)
     bool window = false;
     uint32_t win[4] = {0, 0, 0, 0};
     // tile streaming, encode (grk_write_tile): next tile expected, parts written
@@ -540,6 +541,12 @@ GRK_EXPORT bool grk_read_header(grk_codec *codec, grk_header_info *hi, grk_image
             GRK_ERROR("%s", grkgpu_last_error());
             return false;
         }
+        c->cinfo.assign(c->desc.numcomps, grkgpu_comp_info{});
+        for (uint32_t k = 0; k < c->desc.numcomps; ++k)
+            if (grkgpu_read_comp_info(c->cs.data(), c->cs.size(), k, &c->cinfo[k])) {
+                GRK_ERROR("%s", grkgpu_last_error());
+                return false;
+            }
         c->have_header = true;
     }
     if (c->dparams.cp_reduce >= c->hinfo.numresolutions) {  // j2k.cpp:6994
@@ -574,7 +581,7 @@ GRK_EXPORT bool grk_read_header(grk_codec *codec, grk_header_info *hi, grk_image
         hi->mct = h.mct;
         hi->rsiz = (uint16_t)h.rsiz;
         hi->numresolutions = h.numresolutions;
-        hi->csty = (uint8_t)h.csty;
+        hi->csty = (uint8_t)c->cinfo[0].csty;  // tccps[0]->csty: the precinct flag (j2k.cpp:461)
         hi->cblk_sty = (uint8_t)h.cblk_sty;
         for (int i = 0; i < 33; ++i) { hi->prcw_init[i] = h.prcw_init[i]; hi->prch_init[i] = h.prch_init[i]; }
         hi->cp_tx0 = h.tx0; hi->cp_ty0 = h.ty0; hi->cp_tdx = h.tdx; hi->cp_tdy = h.tdy;
@@ -1010,8 +1017,8 @@ GRK_EXPORT void grk_dump_codec(grk_codec *codec, int32_t, FILE *out) {
 }
 // grk_get_cstr_info (grok.cpp:673-679 -> j2k_get_cstr_info,
 // j2k_dump.cpp:326-400): the main header's tile grid and the default coding /
-// quantisation parameters of every component (one COD / QCD for all: COC /
-// QCC are rejected by the parser).  tile_info stays null ("not filled from the
+// quantisation parameters of every component (COD / QCD, or the component's
+// main-header COC / QCC).  tile_info stays null ("not filled from the
 // main header").  Kept as the reference does it: compno is not set (0), and
 // prcw / prch are copied with numresolutions BYTES (memcpy, :366-369), so
 // only the first numresolutions / 4 entries arrive.
@@ -1030,32 +1037,30 @@ GRK_EXPORT grk_codestream_info_v2 *grk_get_cstr_info(grk_codec *codec) {
     t.mct = h.mct;
     t.tccp_info = (grk_tccp_info *)calloc(h.numcomps ? h.numcomps : 1, sizeof(grk_tccp_info));
     if (!t.tccp_info) { free(ci); return nullptr; }
-    uint32_t prcw[GRKP_MAXRLVLS], prch[GRKP_MAXRLVLS];  // tccp->prcw / prch: log2 sizes
-    for (uint32_t r = 0; r < GRKP_MAXRLVLS; ++r) {
-        prcw[r] = (uint32_t)__builtin_ctz(h.prcw_init[r]);
-        prch[r] = (uint32_t)__builtin_ctz(h.prch_init[r]);
-    }
     for (uint32_t k = 0; k < h.numcomps; ++k) {
+        const grkgpu_comp_info &cc = c->cinfo[k];
         grk_tccp_info &q = t.tccp_info[k];
-        q.csty = (uint8_t)(h.csty & 1u);  // tccp->csty = Scod & J2K_CCP_CSTY_PRT (j2k.cpp:3875)
-        q.numresolutions = h.numresolutions;
-        q.cblkw = (uint32_t)__builtin_ctz(h.cblockw_init);
-        q.cblkh = (uint32_t)__builtin_ctz(h.cblockh_init);
-        q.cblk_sty = (uint8_t)h.cblk_sty;
-        q.qmfbid = h.irreversible ? 0 : 1;
-        if (q.numresolutions < GRKP_MAXRLVLS) {
+        q.csty = (uint8_t)cc.csty;  // tccp->csty = Scod / Scoc & J2K_CCP_CSTY_PRT (j2k.cpp:3875)
+        q.numresolutions = cc.numresolutions;
+        q.cblkw = cc.cblkw;
+        q.cblkh = cc.cblkh;
+        q.cblk_sty = (uint8_t)cc.cblk_sty;
+        q.qmfbid = cc.qmfbid;
+        if (q.numresolutions < GRKP_MAXRLVLS) {  // tccp->prcw / prch: log2 sizes, numresolutions BYTES
+            uint32_t prcw[GRKP_MAXRLVLS], prch[GRKP_MAXRLVLS];
+            for (uint32_t r = 0; r < GRKP_MAXRLVLS; ++r) { prcw[r] = cc.prcw[r]; prch[r] = cc.prch[r]; }
             memcpy(q.prch, prch, q.numresolutions);
             memcpy(q.prcw, prcw, q.numresolutions);
         }
-        q.qntsty = (uint8_t)h.qntsty;
-        q.numgbits = (uint8_t)h.numgbits;
-        const uint32_t nb = h.qntsty == 1 ? 1 : h.numresolutions * 3 - 2;
+        q.qntsty = (uint8_t)cc.qntsty;
+        q.numgbits = (uint8_t)cc.numgbits;
+        const uint32_t nb = cc.qntsty == 1 ? 1 : cc.numresolutions * 3 - 2;
         if (nb < GRK_J2K_MAXBANDS)
             for (uint32_t b = 0; b < nb; ++b) {
-                q.stepsizes_mant[b] = b < h.nsteps ? h.step_mant[b] : 0;
-                q.stepsizes_expn[b] = b < h.nsteps ? h.step_expn[b] : 0;
+                q.stepsizes_mant[b] = b < cc.nsteps ? cc.step_mant[b] : 0;
+                q.stepsizes_expn[b] = b < cc.nsteps ? cc.step_expn[b] : 0;
             }
-        q.roishift = k < 16 ? h.roishift[k] : 0;
+        q.roishift = cc.roishift;
     }
     return ci;
 }

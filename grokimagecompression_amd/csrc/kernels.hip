@@ -79,7 +79,7 @@ __global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t sstride, uint32_t tw, 
     uint32_t c0 = 0;
     if (mct && ncomp >= 3) {
         int32_t o[3];
-        if (!irrev) {
+        if (!(irrev & 1)) {
             int32_t yv = src.p[0][si], u = src.p[1][si], v = src.p[2][si];
             int32_t g = yv - ((u + v) >> 2);
             o[0] = v + g; o[1] = g; o[2] = u + g;
@@ -99,7 +99,7 @@ __global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t sstride, uint32_t tw, 
     }
     for (uint32_t c = c0; c < ncomp; ++c) {
         int32_t v = src.p[c][si];
-        if (irrev) v = (int32_t)rintf(__int_as_float(v));
+        if ((irrev >> c) & 1) v = (int32_t)rintf(__int_as_float(v));
         v += shift.v[c];
         dst.p[c][di] = v < minv.v[c] ? minv.v[c] : (v > maxv.v[c] ? maxv.v[c] : v);
     }

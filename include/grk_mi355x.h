@@ -323,6 +323,19 @@ typedef struct {
     uint32_t roishift[16];                 /* RGN per component */
 } grkgpu_header_info;
 int grkgpu_read_header_info(const uint8_t *cs, size_t len, grkgpu_header_info *info);
+/* One component's coding style and quantisation as the main header sets them
+ * (COD / QCD, or that component's COC / QCC; the reference's default tcp
+ * tccps[compno], j2k_dump.cpp:357-390 reads the same): precinct flag, levels,
+ * log2 code-block size, mode switches, wavelet (qmfbid 1 = 5/3), log2
+ * precinct sizes, QCD / QCC style, guard bits and step sizes, ROI shift. */
+typedef struct {
+    uint32_t csty, numresolutions, cblkw, cblkh, cblk_sty, qmfbid;
+    uint32_t prcw[33], prch[33];
+    uint32_t qntsty, numgbits, nsteps;
+    uint32_t step_expn[100], step_mant[100];
+    uint32_t roishift;
+} grkgpu_comp_info;
+int grkgpu_read_comp_info(const uint8_t *cs, size_t len, uint32_t compno, grkgpu_comp_info *info);
 
 /* Whole-codestream decode into caller-provided planes (device or host). */
 int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_image_desc *img,

@@ -63,6 +63,62 @@ def test_decode_guard_bits_match_reference(codec, tag):
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
 
+MARKERS = json.load(open(f"{GOLD}/manifest_markers.json"))
+
+
+@pytest.mark.parametrize("tag", sorted(MARKERS))
+def test_decode_marker_fixtures_match_reference(codec, tag):
+    """Streams with main-header COC / QCC, tile-part COD / COC / QCD / QCC /
+    RGN, PPM and PPT (oracle/make_golden_markers.py: spliced / rewritten from
+    reference-encoded streams, decoded by the reference): per-tile and
+    per-component numres, code-block and precinct sizes, progression, layer
+    count, wavelet, quantisation and ROI shift, packet headers read from the
+    packed-header segments -- bit-exact with the reference's decode."""
+    m = MARKERS[tag]
+    cs = open(f"{GOLD}/{tag}.j2k", "rb").read()
+    assert hashlib.sha256(cs).hexdigest() == m["j2k_sha256"]
+    if m.get("dec") == "error":
+        with pytest.raises(Exception):
+            codec.decompress(cs)
+        return
+    ref = np.load(f"{GOLD}/{tag}.dec.npy")
+    d = codec.decompress(cs)
+    assert d.shape == ref.shape
+    assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
+
+
+MARKER_VARIANTS = sorted((t, v) for t in MARKERS for v in MARKERS[t].get("variants", {}))
+
+
+@pytest.mark.parametrize("tag,vt", MARKER_VARIANTS)
+def test_decode_marker_fixture_options_match_reference(codec, tag, vt):
+    """-r / -l over per-tile-component numres and packed headers, against the
+    reference's decode with the same option."""
+    a = MARKERS[tag]["variants"][vt]["args"]
+    reduce = int(a[a.index("-r") + 1]) if "-r" in a else 0
+    layers = int(a[a.index("-l") + 1]) if "-l" in a else 0
+    ref = np.load(f"{GOLD}/{tag}.{vt}.dec.npy")
+    d = codec.decompress(open(f"{GOLD}/{tag}.j2k", "rb").read(), reduce=reduce, layers=layers)
+    assert d.shape == ref.shape
+    assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
+
+
+@pytest.mark.parametrize("tag", ["mk_tile_coc", "mk_ppt_tparts", "mk_main_coc"])
+def test_marker_fixtures_reduce_and_window(codec, tag):
+    """The per-component / packed-header streams through -r 1 and a window:
+    the window equals the crop of the full decode, and -r 1 equals a reduced
+    decode of the same stream by the per-tile-component numres (every
+    component of these keeps >= 2 resolutions)."""
+    cs = open(f"{GOLD}/{tag}.j2k", "rb").read()
+    full = codec.decompress(cs)
+    h, w = full.shape[1:]
+    x0, y0, x1, y1 = w // 5, h // 7, w - w // 4, h - h // 6
+    win = codec.decompress(cs, window=(x0, y0, x1, y1))
+    assert np.array_equal(win, full[:, y0:y1, x0:x1])
+    red = codec.decompress(cs, reduce=1)
+    assert red.shape == (full.shape[0], (h + 1) // 2, (w + 1) // 2)
+
+
 VARIANTS = sorted((n, tag) for n in MAN for tag in MAN[n].get("variants", {}))
 
 

@@ -52,6 +52,15 @@ def test_guard_bit_fixtures_regenerate():
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
 
 
+def test_marker_fixtures_regenerate():
+    """tests/golden/mk_*: COC / QCC / tile-part COD / QCD / RGN / PPM / PPT
+    streams assembled from reference-encoded streams and decoded by the
+    reference (oracle/make_golden_markers.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "make_golden_markers.py"), "--check"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
 def test_cstr_info_matches_reference():
     """grk_get_cstr_info of our libgrok.so (ref_driver_mi355x: the same driver
     relinked against it; header parsing needs no GPU) prints exactly what the
