@@ -1850,7 +1850,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 std::vector<PpxSeg> ppt;
                 for (const TpMarker &mk : tmarks[t]) {
                     const uint8_t *mp = csb + mk.off;
-                    if (mk.m == 0xFF52) { ok = parse_cod(mp, mk.len, tcp, e); tcod = true; }
+                    if (mk.m == 0xFF52) {  // sets every component, a COC before it included
+                        ok = parse_cod(mp, mk.len, tcp, e);
+                        tcod = true;
+                        for (uint32_t k = 0; k < 16; ++k) tcoc[k] = false;
+                    }
                     else if (mk.m == 0xFF5C) { ok = parse_qcd(mp, mk.len, tcp, e); tqcd = true; }
                     else if (mk.m == 0xFF53) { const int32_t k = parse_coc(mp, mk.len, tcp, e); ok = k >= 0; if (ok) tcoc[k] = true; }
                     else if (mk.m == 0xFF5D) { const int32_t k = parse_qcc(mp, mk.len, tcp, e); ok = k >= 0; if (ok) tqcc[k] = true; }
@@ -1873,6 +1877,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     if (tcod && !tcoc[k]) comp_style_from_cod(tcp, k);
                     if (tqcd && !tqcc[k]) comp_quant_from_qcd(tcp, k);
                 }
+                if (!check_qcd_steps(tcp, cp.qcc_set, tqcd, tqcc, e)) { terr[lt] = 5; continue; }
                 for (uint32_t k = 0; k < nc; ++k) {
                     const CompParams &cc = tcp.comp[k];
                     if (cc.cblksty != cp.cblksty || reduce >= cc.numres || cc.cblkw > 6 || cc.cblkh > 6) ok = false;
@@ -1945,6 +1950,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         if (terr[lt] == 1) return set_err(GRKGPU_ECORRUPT, "Error reading POC marker");
         if (terr[lt] == 2) return set_err(GRKGPU_ECORRUPT, "corrupt packet header");
         if (terr[lt] == 3) return set_err(GRKGPU_ECORRUPT, "corrupt tile-part header marker (COD/COC/QCD/QCC/RGN/PPT/PPM)");
+        if (terr[lt] == 5)
+            return set_err(GRKGPU_ECORRUPT, "QCD marker: number of step sizes is less than 3 * (tile decompositions) + 1");
         if (terr[lt] == 4)
             return set_err(GRKGPU_EUNSUPPORTED, "tile-component coding style not supported (code-block style "
                                                 "differing from the main header's, MCT over components of different "

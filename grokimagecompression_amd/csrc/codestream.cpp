@@ -543,17 +543,51 @@ int32_t parse_coc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string
 // SQcd / SQcc + SPqcd / SPqcc (j2k_read_SQcd_SQcc, j2k.cpp:7047-7135): the
 // style (0 none: 8-bit exponents; 2 scalar expounded: 16-bit expn / mantissa),
 // guard bits, one step size per band
+// Style 1 (scalar derived) carries one step size; band b >= 1 then gets
+// expn0 - (b - 1) / 3 (not below 0) and mant0 (Quantizer.cpp:326-336).  The
+// marker must hold exactly its step sizes (j2k_read_qcd / _qcc: bytes left
+// over are an error).
 static bool parse_sqcd(const uint8_t *p, uint32_t size, CompParams &c, std::string &err) {
-    if (size < 1) { err = "Error reading QCD marker"; return false; }
+    if (size < 1) { err = "Error reading SQcd or SQcc element"; return false; }
     const uint32_t sq = p[0] & 0x1f;
-    if (sq != 0 && sq != 2) { err = "scalar-derived quantisation not supported"; return false; }
+    if (sq > 2) { err = "unknown quantisation style"; return false; }
     c.numgbits = p[0] >> 5;
-    const uint32_t nb = std::min<uint32_t>(sq == 0 ? (size - 1) : (size - 1) / 2, 3 * 33 + 1);
+    const uint32_t body = size - 1;
+    const uint32_t nb = sq == 0 ? body : (sq == 1 ? 1 : body / 2);
+    if ((sq == 0 && body != nb) || (sq != 0 && body != 2 * nb)) { err = "Error reading QCD marker"; return false; }
     c.qntsty = sq;
-    c.nsteps = nb;
-    for (uint32_t i = 0; i < nb; ++i) {
+    c.nsteps = std::min<uint32_t>(nb, 3 * 33 + 1);
+    for (uint32_t i = 0; i < c.nsteps; ++i) {
         if (sq == 0) c.ss[i] = {(uint32_t)(p[1 + i] >> 3), 0};
         else { const uint32_t v = rd16(p + 1 + 2 * i); c.ss[i] = {v >> 11, v & 0x7ff}; }
+    }
+    if (sq == 1)
+        for (uint32_t b = 1; b < 3 * 33 + 1; ++b) {
+            const uint32_t d = (b - 1) / 3;
+            c.ss[b] = {c.ss[0].expn > d ? c.ss[0].expn - d : 0, c.ss[0].mant};
+        }
+    return true;
+}
+
+bool check_qcd_steps(const CodingParams &cp, const bool *qcc, bool tile_qcd, const bool *tile_qcc, std::string &err) {
+    // j2k.cpp:868-930: the main QCD's step sizes must cover the deepest
+    // component it governs (3 L + 1), and so must a tile QCD's
+    if (cp.main_qntsty == 1) return true;
+    uint32_t dmax = 0;
+    for (uint32_t k = 0; k < cp.numcomps; ++k)
+        if (!qcc[k] && !tile_qcd && !tile_qcc[k]) dmax = std::max(dmax, cp.comp[k].numres - 1);
+    if (cp.main_nsteps < 3 * dmax + 1) {
+        err = "From Main QCD marker, number of step sizes is less than 3 * (tile decompositions) + 1";
+        return false;
+    }
+    if (tile_qcd && cp.qntsty != 1) {
+        dmax = 0;
+        for (uint32_t k = 0; k < cp.numcomps; ++k)
+            if (!tile_qcc[k]) dmax = std::max(dmax, cp.comp[k].numres - 1);
+        if (cp.nsteps < 3 * dmax + 1) {
+            err = "From Tile QCD marker, number of step sizes is less than 3 * (tile decompositions) + 1";
+            return false;
+        }
     }
     return true;
 }
@@ -611,9 +645,14 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
             have_siz = true;
         } else if (m == 0xFF52) {
             if (!parse_cod(p, L - 2, cp, err)) return false;
+            // COD sets every component (j2k_copy_tile_component_parameters,
+            // j2k.cpp:3889): a COC read before it is overwritten
+            for (uint32_t k = 0; k < 16; ++k) cp.coc_set[k] = false;
             have_cod = true;
         } else if (m == 0xFF5C) {
             if (!parse_qcd(p, L - 2, cp, err)) return false;
+            cp.main_qntsty = cp.qntsty;
+            cp.main_nsteps = cp.nsteps;
             have_qcd = true;
         } else if (m == 0xFF53) {  // COC (j2k_read_coc, j2k.cpp:3991-4060)
             if (!have_siz) { err = "COC before SIZ"; return false; }

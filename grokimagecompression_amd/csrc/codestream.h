@@ -97,6 +97,7 @@ struct CodingParams {
     // per component (decoder: COC / QCC resolved; encoder: sync_comps)
     CompParams comp[16];
     bool coc_set[16] = {}, qcc_set[16] = {};  // main-header COC / QCC seen
+    uint32_t main_qntsty = 0, main_nsteps = 0;  // the main QCD's (tcp->main_qcd_qntsty / _numStepSizes)
     std::vector<PpxSeg> ppm;                  // main-header PPM segments
     CodingParams() {
         for (int i = 0; i < 33; ++i) prcw[i] = prch[i] = 15;
@@ -108,6 +109,9 @@ void comp_style_from_cod(CodingParams &cp, uint32_t k);
 void comp_quant_from_qcd(CodingParams &cp, uint32_t k);
 // every component from the global COD / QCD values (the encoder's one COD / QCD)
 void sync_comps(CodingParams &cp);
+// the QCD step-size count check of j2k.cpp:868-930 over a tile's resolved
+// components: qcc = main QCC seen, tile_qcd / tile_qcc = the tile's own
+bool check_qcd_steps(const CodingParams &cp, const bool *qcc, bool tile_qcd, const bool *tile_qcc, std::string &err);
 // COC / QCC marker segment bodies (size bytes) -> cp.comp[...]; returns the
 // component or -1 when malformed
 int32_t parse_coc(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &err);

@@ -301,9 +301,49 @@ def case_mixed_wavelet(tmp):
     return write(main, [dict(isot=0, tpsot=0, tnsot=1, hdr=[], body=body)]), None
 
 
+def case_siqnt(tmp):
+    """9/7 stream whose QCD is rewritten to scalar-derived (style 1): only
+    the LL step size travels, every other band derives its exponent from it
+    (Quantizer.cpp:326-336)."""
+    img = synth(80, 96, 3, 12, 311)
+    main, tps = parse(enc(img, 12, ["-I", "-n", "5"], tmp))
+    out = []
+    for m, pl in main:
+        if m == QCD:
+            pl = bytes([(pl[0] & 0xE0) | 1]) + pl[1:3]
+        out.append((m, pl))
+    return write(out, tps), None
+
+
+def case_qcd_short(tmp):
+    """Reversible QCD with fewer exponents than the 3 L + 1 bands: the
+    reference refuses it (j2k.cpp:889-895)."""
+    img = synth(64, 64, 1, 8, 312)
+    main, tps = parse(enc(img, 8, ["-n", "4"], tmp))
+    out = [(m, pl[:-3] if m == QCD else pl) for m, pl in main]
+    return write(out, tps), None
+
+
+def case_coc_then_cod(tmp):
+    """A main-header COC written BEFORE the COD: the COD then sets every
+    component (j2k_copy_tile_component_parameters, j2k.cpp:3889), so the
+    COC's values are dropped.  The stream is a plain single-component one
+    with a COC of other parameters placed ahead of its COD."""
+    img = synth(64, 64, 1, 8, 313)
+    main, tps = parse(enc(img, 8, ["-n", "4", "-b", "32,32"], tmp))
+    other = parse(enc(img, 8, ["-n", "2", "-b", "16,16"], tmp))[0]
+    out = []
+    for m, pl in main:
+        if m == COD:
+            out.append((COC, coc_of(find(other, COD)[0], 0)))
+        out.append((m, pl))
+    return write(out, tps), img
+
+
 CASES = [("tile_cod", case_tile_cod), ("main_coc", case_main_coc), ("tile_coc", case_tile_coc),
          ("tp_cod_copy", case_tp_cod_copy), ("tile_rgn", case_tile_rgn), ("ppt", case_ppt), ("ppm", case_ppm), ("ppt_tparts", case_ppt_tparts),
-         ("ppm_1tile", case_ppm_1tile), ("mixed_wavelet", case_mixed_wavelet)]
+         ("ppm_1tile", case_ppm_1tile), ("mixed_wavelet", case_mixed_wavelet), ("siqnt", case_siqnt),
+         ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod)]
 
 
 # reference decodes with grk_decompress options, -> mk_<name>.<tag>.dec.npy
