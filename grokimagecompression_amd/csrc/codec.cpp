@@ -204,6 +204,8 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->inv01 = g_dwt_opts.inv01;
     out->pair_group = g_dwt_opts.pair_group;
     out->inv01_min_samples = g_dwt_opts.inv01_min_samples;
+    out->f64_lift = g_dwt_opts.f64_lift;
+    out->pad_ = 0;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -216,6 +218,8 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
         return set_err(GRKGPU_EINVAL, "f01_rows must be 0, 2, 4 or 6");
     if (o->inv01 != 0 && o->inv01 != 2 && o->inv01 != 4) return set_err(GRKGPU_EINVAL, "inv01 must be 0, 2 or 4");
     if (o->pair_group < 0 || o->pair_group > 4096) return set_err(GRKGPU_EINVAL, "pair_group must be 0 .. 4096");
+    if (o->f64_lift != 0 && o->f64_lift != 1) return set_err(GRKGPU_EINVAL, "f64_lift must be 0 or 1");
+    g_dwt_opts.f64_lift = o->f64_lift;
     g_dwt_opts.inv01 = o->inv01;
     g_dwt_opts.pair_group = o->pair_group;
     g_dwt_opts.inv01_min_samples = o->inv01_min_samples;

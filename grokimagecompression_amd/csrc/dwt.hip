@@ -108,15 +108,46 @@ template <int OP> __device__ __forceinline__ int32_t lift(int32_t t, int32_t l, 
     }
 }
 
+// The forward 9/7 lifting held in f64 registers: every value is an integer
+// below 2^31 in magnitude, s c / 2^13 + 1/2 (s = l + r, c < 2^14) is exact in
+// a double, so floor(fma(s, c / 8192, 1/2)) is fixmul13(s, c) bit for bit,
+// and a subtracted step t - floor(.) is the reference's int32 difference (no
+// wrap below 2^31).  An f64 FMA + floor issue at the full VALU rate where
+// v_mad_i64_i32 issues at about a quarter (scripts/mulrate.hip).
+__device__ __forceinline__ double fixd(double s, double c13) { return __builtin_floor(__builtin_fma(s, c13, 0.5)); }
+template <int OP> __device__ __forceinline__ double liftd(double t, double l, double r) {
+    if constexpr (OP == 2) return t - fixd(l + r, 12994.0 / 8192.0);
+    else if constexpr (OP == 3) return t - fixd(l + r, 434.0 / 8192.0);
+    else if constexpr (OP == 4) return t + fixd(l + r, 7233.0 / 8192.0);
+    else return t + fixd(l + r, 3633.0 / 8192.0);
+}
+__device__ __forceinline__ double from_next(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)from_next((int32_t)(uint32_t)b), hi = (uint32_t)from_next((int32_t)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double from_prev(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)from_prev((int32_t)(uint32_t)b), hi = (uint32_t)from_prev((int32_t)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// value-type dispatch for the forward 9/7 (int32: v_mad_i64_i32, double: f64)
+template <int OP> __device__ __forceinline__ int32_t liftv(int32_t t, int32_t l, int32_t r) { return lift<OP>(t, l, r); }
+template <int OP> __device__ __forceinline__ double liftv(double t, double l, double r) { return liftd<OP>(t, l, r); }
+__device__ __forceinline__ int32_t scalev(int32_t v, int32_t k) { return fixmul13(v, k); }
+__device__ __forceinline__ double scalev(double v, int32_t k) { return fixd(v, (double)k / 8192.0); }
+__device__ __forceinline__ int32_t to_i32(int32_t v) { return v; }
+__device__ __forceinline__ int32_t to_i32(double v) { return (int32_t)v; }
+
 // vertical lifting step S (0-based) over the window rows of parity PAR (0
 // low, 1 high).  The rows a window keeps are [H, R - H), H = the number of
 // steps (the halo), so step S only needs rows [S + 1, R - 1 - S): the rows
 // further out feed nothing that is kept.
-template <int OP, int PAR, int S, int R>
-__device__ __forceinline__ void vstep(int32_t (&v)[R]) {
+template <int OP, int PAR, int S, int R, typename T>
+__device__ __forceinline__ void vstep(T (&v)[R]) {
     constexpr int K0 = ((S + 1) & 1) == PAR ? S + 1 : S + 2;
 #pragma unroll
-    for (int k = K0; k + 1 + S < R; k += 2) v[k] = lift<OP>(v[k], v[k - 1], v[k + 1]);
+    for (int k = K0; k + 1 + S < R; k += 2) v[k] = liftv<OP>(v[k], v[k - 1], v[k + 1]);
 }
 
 // Linear workgroup id -> position in an order where each XCD (workgroups are
@@ -241,8 +272,8 @@ __device__ __forceinline__ void fused_load(const DwtJob &J, int32_t (&lo)[R], in
 }
 
 // Vertical lifting of a window (position = window row; even rows are low pass).
-template <bool IRREV, int R>
-__device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R], int rh, int casy) {
+template <bool IRREV, int R, typename T = int32_t>
+__device__ __forceinline__ void fwd_vertical(T (&lo)[R], T (&hi)[R], int rh, int casy) {
     if (rh > 1) {
         if constexpr (!IRREV) {
             vstep<0, 1, 0>(lo); vstep<0, 1, 0>(hi);
@@ -253,17 +284,19 @@ __device__ __forceinline__ void fwd_vertical(int32_t (&lo)[R], int32_t (&hi)[R],
             vstep<4, 1, 2>(lo); vstep<4, 1, 2>(hi);
             vstep<5, 0, 3>(lo); vstep<5, 0, 3>(hi);
         }
-    } else if (!IRREV && casy) {  // single row, odd origin: S0 <<= 1 (dwt53.cpp:161)
+    } else if constexpr (!IRREV) {
+        if (casy) {  // single row, odd origin: S0 <<= 1 (dwt53.cpp:161)
 #pragma unroll
-        for (int r = 0; r < R; ++r) { lo[r] = (int32_t)((uint32_t)lo[r] << 1); hi[r] = (int32_t)((uint32_t)hi[r] << 1); }
+            for (int r = 0; r < R; ++r) { lo[r] = (int32_t)((uint32_t)lo[r] << 1); hi[r] = (int32_t)((uint32_t)hi[r] << 1); }
+        }
     }
 }
 
 // Horizontal lifting of the window's core rows, then the stores into the
 // LL buffer and the Mallat bands.
-template <bool IRREV, int TH, int WIN = DWT_WIN>
-__device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&lo)[DwtGeo<IRREV, TH>::R],
-                                                     int32_t (&hi)[DwtGeo<IRREV, TH>::R], int ty, int yw, int gx0,
+template <bool IRREV, int TH, int WIN = DWT_WIN, typename T = int32_t>
+__device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, T (&lo)[DwtGeo<IRREV, TH>::R],
+                                                     T (&hi)[DwtGeo<IRREV, TH>::R], int ty, int yw, int gx0,
                                                      int lane) {
     using G = DwtGeo<IRREV, TH, WIN>;
     const int rw = J.rw, rh = J.rh, casx = J.casx, casy = J.casy;
@@ -284,26 +317,28 @@ __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&
     const bool rows_all = ylo >= 0 && yhi <= rh;      // wave-uniform: no per-row checks
 #pragma unroll
     for (int r = G::HALO; r < G::HALO + G::TH; ++r) {
-        int32_t L = lo[r], H = hi[r];
+        T L = lo[r], H = hi[r];
         if (IRREV && rh > 1) {
             const int32_t k = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
-            L = fixmul13(L, k); H = fixmul13(H, k);
+            L = scalev(L, k); H = scalev(H, k);
         }
         if (rw > 1) {
             if constexpr (!IRREV) {
                 H = lift<0>(H, L, from_next(L));
                 L = lift<1>(L, from_prev(H), H);
             } else {
-                H = lift<2>(H, L, from_next(L));
-                L = lift<3>(L, from_prev(H), H);
-                H = lift<4>(H, L, from_next(L));
-                L = lift<5>(L, from_prev(H), H);
-                H = fixmul13(H, 5039);
-                L = fixmul13(L, 6659);
+                H = liftv<2>(H, L, from_next(L));
+                L = liftv<3>(L, from_prev(H), H);
+                H = liftv<4>(H, L, from_next(L));
+                L = liftv<5>(L, from_prev(H), H);
+                H = scalev(H, 5039);
+                L = scalev(L, 6659);
             }
-        } else if (!IRREV && casx) {
-            L = (int32_t)((uint32_t)L << 1);
-            H = (int32_t)((uint32_t)H << 1);
+        } else if constexpr (!IRREV) {
+            if (casx) {
+                L = (int32_t)((uint32_t)L << 1);
+                H = (int32_t)((uint32_t)H << 1);
+            }
         }
         if (!rows_all) {
             const int gy = yw + r;
@@ -311,19 +346,19 @@ __device__ __forceinline__ void fwd_horizontal_store(const DwtJob &J, int32_t (&
         }
         if ((r & 1) == 0) {  // low row -> LL | HL
             const int iy = lbase + r / 2;
-            st32(L, outb, vl, iy * ost);
-            st32(H, bandb, vh, iy * bst);
+            st32(to_i32(L), outb, vl, iy * ost);
+            st32(to_i32(H), bandb, vh, iy * bst);
         } else {             // high row -> LH | HH
             const int so = (hbase + (r - 1) / 2) * bst;
-            st32(L, bandb, vl, so);
-            st32(H, bandb, vh, so);
+            st32(to_i32(L), bandb, vl, so);
+            st32(to_i32(H), bandb, vh, so);
         }
     }
 }
 
 // FUSED: 0 = reads `in`; 1 = DC shift (+ MCT for a component of an MCT
 // triple) fused into the loads (fused_load: 3 planes per MCT component).
-template <bool IRREV, int TH, int FUSED = 0, typename S = int32_t>
+template <bool IRREV, int TH, int FUSED = 0, typename S = int32_t, typename T = int32_t>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__restrict__ jobs, int lay) {
     using G = DwtGeo<IRREV, TH>;
     constexpr int R = G::R;
@@ -336,8 +371,9 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
     const int yw = ty * G::TH - casy - G::HALO;
     const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
 
-    int32_t lo[R], hi[R];  // column 2l (low pass) and 2l+1 (high pass)
-    if (FUSED == 1) {
+    T lo[R], hi[R];  // column 2l (low pass) and 2l+1 (high pass)
+    if constexpr (FUSED == 1) {
+        static_assert(sizeof(T) == 4, "fused loads: int32 lifting");
         fused_load<IRREV, R, S>(J, lo, hi, xw, yw, gx0, gx1);
     } else {
         const rsrc_t in = mkbuf(J.in, J.in_bytes);
@@ -349,25 +385,25 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd(const DwtJob *__rest
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, base + r * st, 0);
-                lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
+                lo[r] = (T)(int32_t)p[0]; hi[r] = (T)(int32_t)p[1];
             }
         } else if (vec) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, mirror_idx(yw + r, rh) * st, 0);
-                lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
+                lo[r] = (T)(int32_t)p[0]; hi[r] = (T)(int32_t)p[1];
             }
         } else {
             const int o0 = mirror_idx(gx0, rw) * 4, o1 = mirror_idx(gx1, rw) * 4;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int so = mirror_idx(yw + r, rh) * st;
-                lo[r] = ld32(in, o0, so); hi[r] = ld32(in, o1, so);
+                lo[r] = (T)ld32(in, o0, so); hi[r] = (T)ld32(in, o1, so);
             }
         }
     }
-    fwd_vertical<IRREV, R>(lo, hi, rh, casy);
-    fwd_horizontal_store<IRREV, TH>(J, lo, hi, ty, yw, gx0, lane);
+    fwd_vertical<IRREV, R, T>(lo, hi, rh, casy);
+    fwd_horizontal_store<IRREV, TH, DWT_WIN, T>(J, lo, hi, ty, yw, gx0, lane);
 }
 
 // Forward level 0 of an MCT component triple in ONE wavefront per window:
@@ -625,7 +661,7 @@ int dwt01_tiles(int irrev, int ny, int rw1, int rh1, int casx1, int casy1, int *
     return *tiles_x * ((rh1 + casy1 + th - 1) / th);
 }
 
-template <bool IRREV, int NY>
+template <bool IRREV, int NY, typename T = int32_t>
 __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__restrict__ jobs0,
                                                              const DwtJob *__restrict__ jobs1, int lay) {
     using F = F01Geo<IRREV, NY>;
@@ -671,36 +707,36 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
         const int lcol = lane_core ? pc - xw1 : 0;  // LDS column of this lane's LL sample
         for (int jy = w >> 1; jy < NY; jy += DWT_WAVES / 2) {
             const int yw = 2 * (yw1 + (F01_TH0 / 2) * jy) + casy - H;
-            int32_t lo[R0], hi[R0];
+            T lo[R0], hi[R0];
             const bool rows_in = yw >= 0 && yw + R0 <= rh;  // wave-uniform
             if (vec && rows_in) {
                 const int base = yw * st;
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
                     const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, gx0 * 4, base + r * st, 0);
-                    lo[r] = (int32_t)p[0]; hi[r] = (int32_t)p[1];
+                    lo[r] = (T)(int32_t)p[0]; hi[r] = (T)(int32_t)p[1];
                 }
             } else {
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
                     const int so = mirror_idx(yw + r, rh) * st;
-                    lo[r] = ld32(in, o0, so); hi[r] = ld32(in, o1, so);
+                    lo[r] = (T)ld32(in, o0, so); hi[r] = (T)ld32(in, o1, so);
                 }
             }
-            fwd_vertical<IRREV, R0>(lo, hi, rh, casy);
+            fwd_vertical<IRREV, R0, T>(lo, hi, rh, casy);
             const int prow0 = yw1 + (F01_TH0 / 2) * jy;  // pair row of window row H
 #pragma unroll
             for (int r = H; r < H + F01_TH0; ++r) {
-                int32_t Lv = lo[r], Hv = hi[r];
+                T Lv = lo[r], Hv = hi[r];
                 if constexpr (IRREV) {
                     const int32_t kk = (r & 1) ? 5039 : 6659;  // vertical scale: high rows K/2, low rows 1/K
-                    Lv = fixmul13(Lv, kk); Hv = fixmul13(Hv, kk);
-                    Hv = lift<2>(Hv, Lv, from_next(Lv));
-                    Lv = lift<3>(Lv, from_prev(Hv), Hv);
-                    Hv = lift<4>(Hv, Lv, from_next(Lv));
-                    Lv = lift<5>(Lv, from_prev(Hv), Hv);
-                    Hv = fixmul13(Hv, 5039);
-                    Lv = fixmul13(Lv, 6659);
+                    Lv = scalev(Lv, kk); Hv = scalev(Hv, kk);
+                    Hv = liftv<2>(Hv, Lv, from_next(Lv));
+                    Lv = liftv<3>(Lv, from_prev(Hv), Hv);
+                    Hv = liftv<4>(Hv, Lv, from_next(Lv));
+                    Lv = liftv<5>(Lv, from_prev(Hv), Hv);
+                    Hv = scalev(Hv, 5039);
+                    Lv = scalev(Lv, 6659);
                 } else {
                     Hv = lift<0>(Hv, Lv, from_next(Lv));
                     Lv = lift<1>(Lv, from_prev(Hv), Hv);
@@ -709,12 +745,12 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
                 const int gy = yw + r;
                 const bool rok = prow >= Q0 && prow < Q1 && gy >= 0 && gy < rh;  // wave-uniform
                 if ((r & 1) == 0) {
-                    if (lane_core) ll[prow - yw1][lcol] = Lv;
-                    if (rok) st32(Hv, bandb, vh, prow * bst);  // HL
+                    if (lane_core) ll[prow - yw1][lcol] = to_i32(Lv);
+                    if (rok) st32(to_i32(Hv), bandb, vh, prow * bst);  // HL
                 } else if (rok) {
                     const int so = (J0.sny + prow + casy) * bst;  // LH | HH row (pair row + casy)
-                    st32(Lv, bandb, vl, so);
-                    st32(Hv, bandb, vh, so);
+                    st32(to_i32(Lv), bandb, vl, so);
+                    st32(to_i32(Hv), bandb, vh, so);
                 }
             }
         }
@@ -727,15 +763,15 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
         const int gx0 = xw1 + 2 * lane;
         const int c0 = min(max(mirror_idx(gx0, rw1) - xw1, 0), F::W1 - 1);
         const int c1 = min(max(mirror_idx(gx0 + 1, rw1) - xw1, 0), F::W1 - 1);
-        int32_t lo[RW], hi[RW];
+        T lo[RW], hi[RW];
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
             const int rr = min(max(mirror_idx(yw + r, rh1) - yw1, 0), F::R1 - 1);
-            lo[r] = ll[rr][c0];
-            hi[r] = ll[rr][c1];
+            lo[r] = (T)ll[rr][c0];
+            hi[r] = (T)ll[rr][c1];
         }
-        fwd_vertical<IRREV, RW>(lo, hi, rh1, casy1);
-        fwd_horizontal_store<IRREV, F::THW, F::W1>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
+        fwd_vertical<IRREV, RW, T>(lo, hi, rh1, casy1);
+        fwd_horizontal_store<IRREV, F::THW, F::W1, T>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
     }
 }
 
@@ -959,7 +995,9 @@ static void launch_th(const DwtJob *jobs, dim3 grid, dim3 block, int irrev, int 
         return;
     }
     if (!inverse) {
-        if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH>), grid, block, 0, s, jobs, lay);
+        if (irrev && dwt_options().f64_lift)
+            hipLaunchKernelGGL((k_dwt_fwd<true, TH, 0, int32_t, double>), grid, block, 0, s, jobs, lay);
+        else if (irrev) hipLaunchKernelGGL((k_dwt_fwd<true, TH>), grid, block, 0, s, jobs, lay);
         else hipLaunchKernelGGL((k_dwt_fwd<false, TH>), grid, block, 0, s, jobs, lay);
     } else {
         if (irrev) hipLaunchKernelGGL((k_dwt_inv<true, TH>), grid, block, 0, s, jobs, lay);
@@ -977,7 +1015,10 @@ hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t n
     switch (ny) {
         case 2: hipLaunchKernelGGL((k_dwt_fwd01<true, 2>), g, b, 0, s, jobs0, jobs1, lay); break;
         case 6: hipLaunchKernelGGL((k_dwt_fwd01<true, 6>), g, b, 0, s, jobs0, jobs1, lay); break;
-        default: hipLaunchKernelGGL((k_dwt_fwd01<true, 4>), g, b, 0, s, jobs0, jobs1, lay); break;
+        default:
+            if (dwt_options().f64_lift) hipLaunchKernelGGL((k_dwt_fwd01<true, 4, double>), g, b, 0, s, jobs0, jobs1, lay);
+            else hipLaunchKernelGGL((k_dwt_fwd01<true, 4>), g, b, 0, s, jobs0, jobs1, lay);
+            break;
     }
     return hipGetLastError();
 }

@@ -183,7 +183,11 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    size); 0: one launch per level.
  *   pair_group       workgroup order of the fused level pairs (k_dwt_fwd01,
  *                    k_dwt_inv01): 0 (default) row-major; G > 0: groups of G
- *                    workgroup columns, each walked top to bottom. */
+ *                    workgroup columns, each walked top to bottom.
+ *   f64_lift         forward 9/7 lifting arithmetic (fused pair and per-level
+ *                    kernel, not the fused DC-shift loads): 0 the
+ *                    64-bit integer multiply (v_mad_i64_i32), 1 f64 FMA +
+ *                    floor (bit-identical results). */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -192,6 +196,8 @@ typedef struct {
     int32_t inv01;
     int32_t pair_group;
     uint64_t inv01_min_samples;
+    int32_t f64_lift;
+    int32_t pad_;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */

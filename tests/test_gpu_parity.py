@@ -183,22 +183,29 @@ def test_device_resident_roundtrip(codec):
             assert np.array_equal(ref, img)
 
 
-@pytest.mark.parametrize("irrev", [False, True])
+@pytest.mark.parametrize("irrev", [False, True, "f64"])
 @pytest.mark.parametrize("shape_off", [((64, 64), (0, 0)), ((77, 100), (3, 5)), ((1, 37), (0, 1)),
                                        ((45, 1), (1, 0)), ((129, 200), (1, 1)), ((513, 257), (0, 3)),
                                        ((2, 3), (1, 1)), ((3, 130), (1, 0)), ((4, 5), (0, 1)), ((250, 121), (0, 0)),
                                        ((37, 260), (1, 1)), ((300, 497), (2, 2))])
 @pytest.mark.parametrize("numres", [1, 2, 6, 9])
 def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
+    """Per-level forward / inverse launches against the oracle; "f64": the
+    9/7 forward lifting in f64 FMA + floor (f64_lift), at the magnitude of
+    16-bit samples after the << 11 (2^26)."""
     import torch
     import grokimagecompression_amd as grk
     (h, w), (x0, y0) = shape_off
+    f64 = irrev == "f64"
+    irrev = bool(irrev)
     rng = np.random.default_rng(h * 1000 + w + numres)
-    a = rng.integers(-(1 << 20) if irrev else -4096, 1 << 20 if irrev else 4096, size=(h, w)).astype(np.int32)
+    mag = (1 << 26) if f64 else (1 << 20) if irrev else 4096
+    a = rng.integers(-mag, mag, size=(h, w)).astype(np.int32)
     ref = oracle.dwt_fwd(a, x0, y0, numres, irrev)
     t = torch.from_numpy(a).cuda()
-    grk.dwt_fwd(t, x0, y0, numres, irrev)
-    torch.cuda.synchronize()
+    with grk.dwt_options(f64_lift=int(f64), f01_rows=0 if f64 else 4):
+        grk.dwt_fwd(t, x0, y0, numres, irrev)
+        torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), ref)
     # inverse: 5/3 on integers (exact reconstruction), 9/7 on floats
     if not irrev:
@@ -214,7 +221,7 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
         assert np.array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix", "g3"])
+@pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix", "g3", "d"])
 @pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
                                        ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1))])
@@ -230,14 +237,18 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
     import grokimagecompression_amd as grk
     (h, w), (x0, y0) = shape_off
     rng = np.random.default_rng(h * 31 + w + numres)
-    a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
+    # "d" at the magnitude of 16-bit samples after the 9/7 << 11 (2^26)
+    mag = 1 << (26 if ny == "d" else 20)
+    a = rng.integers(-mag, mag, size=(h, w)).astype(np.int32)
     ref = oracle.dwt_fwd(a, x0, y0, numres, True)
     t = torch.from_numpy(a).cuda()
     # fuse every qualifying pair, not only chip-filling ones ("mix": pairs of
     # >= 2^16 samples with 4 row windows, smaller ones with 2)
     # "g3": workgroups walk groups of 3 columns top-down (pair_group)
+    # "d": the f64 FMA + floor lifting (f64_lift)
     opts = dict(f01_rows=4, f01_min_samples=1 << 16, f01_small_min_samples=0) if ny == "mix" else \
-        dict(f01_rows=4, f01_min_samples=0, pair_group=3) if ny == "g3" else dict(f01_rows=int(ny), f01_min_samples=0)
+        dict(f01_rows=4, f01_min_samples=0, pair_group=3) if ny == "g3" else \
+        dict(f01_rows=4, f01_min_samples=0, f64_lift=1) if ny == "d" else dict(f01_rows=int(ny), f01_min_samples=0)
     with grk.dwt_options(**opts):
         grk.dwt_fwd(t, x0, y0, numres, True)
         torch.cuda.synchronize()
