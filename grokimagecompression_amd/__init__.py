@@ -32,7 +32,8 @@ class GrkGpuError(RuntimeError):
 
 class ImageDesc(ctypes.Structure):
     _fields_ = [("x0", ctypes.c_uint32), ("y0", ctypes.c_uint32), ("x1", ctypes.c_uint32), ("y1", ctypes.c_uint32),
-                ("numcomps", ctypes.c_uint32), ("prec", ctypes.c_uint32 * MAXC), ("sgnd", ctypes.c_int32 * MAXC)]
+                ("numcomps", ctypes.c_uint32), ("prec", ctypes.c_uint32 * MAXC), ("sgnd", ctypes.c_int32 * MAXC),
+                ("dx", ctypes.c_uint32 * MAXC), ("dy", ctypes.c_uint32 * MAXC)]
 
 
 class DParams(ctypes.Structure):
@@ -478,6 +479,49 @@ class Codec:
         return self.compress_tiles(img, prec, params or CParams.make(), 0, 0xFFFFFFFF, PART_ALL, offset, sgnd,
                                    view=view)
 
+    def compress_subsampled(self, planes, prec, size, subsampling, params=None, offset=(0, 0), sgnd=False):
+        """Subsampled components (SIZ XRsiz / YRsiz): planes[k] is component
+        k's (h_k, w_k) array on its grid, component k subsampled by
+        subsampling[k] = (dx, dy) of an image size = (w, h) at `offset` on the
+        reference grid (w_k = ceil((x0 + w) / dx) - ceil(x0 / dx)); host numpy
+        planes, int32 or their 8 / 16-bit samples.  MCT is disabled when the
+        first three components differ in subsampling (j2k.cpp:1963-1971)."""
+        c = len(planes)
+        if len(subsampling) != c:
+            raise GrkGpuError("one (dx, dy) per component")
+        d = ImageDesc()
+        d.x0, d.y0 = offset
+        d.x1, d.y1 = offset[0] + size[0], offset[1] + size[1]
+        d.numcomps = c
+        pl = Planes()
+        keep = []
+        fmts = set()
+        for k, (a, (dx, dy)) in enumerate(zip(planes, subsampling)):
+            cw = -(-d.x1 // dx) - (-(-d.x0 // dx))
+            ch = -(-d.y1 // dy) - (-(-d.y0 // dy))
+            a = np.asarray(a)
+            if a.shape != (ch, cw):
+                raise GrkGpuError("component %d: plane %s, its grid needs %s" % (k, a.shape, (ch, cw)))
+            if a.dtype not in _NP_FMT or not _fmt_fits(_NP_FMT[a.dtype], prec, sgnd):
+                a = a.astype(np.int32)
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            fmts.add(_NP_FMT[a.dtype])
+            d.prec[k], d.sgnd[k], d.dx[k], d.dy[k] = prec, 1 if sgnd else 0, dx, dy
+            pl.planes[k] = a.ctypes.data
+        if len(fmts) != 1:
+            keep = [a.astype(np.int32) for a in keep]
+            for k, a in enumerate(keep):
+                pl.planes[k] = a.ctypes.data
+            fmts = {SAMPLE_I32}
+        pl.sample_fmt = fmts.pop()
+        pl.on_device = 0
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _check(lib().grkgpu_compress_ex(self._ctx, ctypes.byref(d), ctypes.byref(params or CParams.make()),
+                                        ctypes.byref(pl), 0, 0xFFFFFFFF, PART_ALL, ctypes.byref(out), ctypes.byref(n)))
+        return ctypes.string_at(out, n.value)
+
     def compress_tiles(self, img, prec, params, tile_begin, tile_end, parts=PART_TILES, offset=(0, 0), sgnd=False,
                        row0=None, height=None, view=False):
         """Encode tiles [tile_begin, tile_end) of img; returns their tile-parts
@@ -537,6 +581,20 @@ class Codec:
             if d.x1 <= d.x0 or d.y1 <= d.y0:
                 raise GrkGpuError("decode window outside the image")
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
+        if any(d.dx[k] != 1 or d.dy[k] != 1 for k in range(c)):
+            # subsampled components: a list of host planes, each on its grid
+            if out is not None or device_out:
+                raise GrkGpuError("subsampled components decode to host planes only")
+            cd = lambda v, s: -(-v // s)  # noqa: E731
+            outs = [np.empty((cd(d.y1, d.dy[k]) - cd(d.y0, d.dy[k]), cd(d.x1, d.dx[k]) - cd(d.x0, d.dx[k])),
+                             dtype=np.int32) for k in range(c)]
+            ptrs = (ctypes.c_void_p * c)(*[a.ctypes.data for a in outs])
+            bp, bn, keep = _buf_ptr(buf)
+            dp = DParams(cp_reduce=reduce, cp_layer=layers)
+            if window is not None:
+                dp.DA_x0, dp.DA_y0, dp.DA_x1, dp.DA_y1 = [int(v) for v in window]
+            _check(lib().grkgpu_decompress_ex(self._ctx, bp, bn, ctypes.byref(dp), None, ptrs, 0))
+            return outs
         if out is not None:
             on_dev = _check_out(out, (c, h, w), self.device)
         else:

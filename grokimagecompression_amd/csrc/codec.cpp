@@ -370,7 +370,11 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     }
     if (p->cp_disto_alloc && p->cp_fixed_quality) return set_err(GRKGPU_EINVAL, "-r and -q cannot be used together");
     {  // max codestream size vs layer rates (j2k.cpp:1663-1689)
-        const double image_bytes = ((double)img->numcomps * (img->x1 - img->x0) * (img->y1 - img->y0) * img->prec[0]) / 8;
+        // component 0's plane size, divided by its subsampling once more (sic)
+        const uint32_t dx0 = img->dx[0] ? img->dx[0] : 1, dy0 = img->dy[0] ? img->dy[0] : 1;
+        const Rect c0 = comp_rect({img->x0, img->y0, img->x1, img->y1}, dx0, dy0);
+        const double image_bytes =
+            ((double)img->numcomps * c0.w() * c0.h() * img->prec[0]) / (8.0 * dx0 * dy0);
         const uint32_t L = p->tcp_numlayers;
         if (p->max_cs_size == 0) {
             if (p->tcp_rates[L - 1] > 0) p->max_cs_size = (uint64_t)floor(image_bytes / p->tcp_rates[L - 1]);
@@ -396,6 +400,9 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
         cp.prec[k] = img->prec[k];
         cp.sgnd[k] = img->sgnd[k] ? 1 : 0;
         cp.shift[k] = cp.sgnd[k] ? 0 : (1 << (cp.prec[k] - 1));
+        cp.dx[k] = img->dx[k] ? img->dx[k] : 1;
+        cp.dy[k] = img->dy[k] ? img->dy[k] : 1;
+        if (cp.dx[k] > 255 || cp.dy[k] > 255) return set_err(GRKGPU_EINVAL, "component subsampling must be 1..255");
     }
     cp.numres = p->numresolution;
     cp.cblkw = (uint32_t)floorlog2((int32_t)p->cblockw_init);
@@ -403,6 +410,9 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     cp.irrev = p->irreversible ? 1 : 0;
     cp.mct = p->tcp_mct < 0 ? (img->numcomps >= 3 ? 1 : 0) : (p->tcp_mct ? 1 : 0);
     if (cp.mct && img->numcomps < 3) cp.mct = 0;
+    // "Cannot perform MCT on components with different sizes. Disabling MCT." (j2k.cpp:1963-1971)
+    if (cp.mct && (cp.dx[1] != cp.dx[0] || cp.dx[2] != cp.dx[0] || cp.dy[1] != cp.dy[0] || cp.dy[2] != cp.dy[0]))
+        cp.mct = 0;
     if (p->tile_size_on) {
         if (!p->cp_tdx || !p->cp_tdy) return set_err(GRKGPU_EINVAL, "zero tile size");
         if (p->cp_tx0 > img->x0 || p->cp_ty0 > img->y0 || (uint64_t)p->cp_tx0 + p->cp_tdx <= img->x0 ||
@@ -929,6 +939,26 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     if ((uint64_t)col0 + ncols > iw) return set_err(GRKGPU_EINVAL, "column range outside the image");
     const uint32_t pw = ncols;                    // row stride of the caller's planes (samples)
     const uint64_t plane = (uint64_t)pw * nrows;  // samples per plane held by the caller
+    // subsampled components (SIZ XRsiz / YRsiz): each plane on its own grid
+    bool subs = false;
+    for (uint32_t k = 0; k < nc; ++k) subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+    if (subs && (row0 || col0 || nrows != ih || ncols != iw))
+        return set_err(GRKGPU_EUNSUPPORTED, "row / column shards of subsampled images are not supported");
+    // the rectangle each caller plane covers (component grid), its stride,
+    // and its offset in the staging buffer (samples)
+    Rect prect[GRKGPU_MAX_COMPS];
+    uint64_t poff[GRKGPU_MAX_COMPS + 1];
+    poff[0] = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+        prect[k] = subs ? comp_rect(cp.image, cp.dx[k], cp.dy[k])
+                        : Rect{cp.image.x0 + col0, cp.image.y0 + row0, cp.image.x0 + col0 + ncols,
+                               cp.image.y0 + row0 + nrows};
+        poff[k + 1] = poff[k] + (uint64_t)prect[k].w() * prect[k].h();
+    }
+    // element offset of tile-component tc's first sample in plane k
+    auto plane_org = [&](uint32_t k, const TileComp &tc) {
+        return (uint64_t)(tc.r.y0 - prect[k].y0) * prect[k].w() + (tc.r.x0 - prect[k].x0);
+    };
 
     // geometry for every tile of the shard, arena offsets, block table
     const uint32_t ntiles = te - tb;
@@ -968,16 +998,16 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
             tc.arena_off = arena;
-            uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
+            uint64_t area = (uint64_t)tc.r.w() * tc.r.h();
             arena += (area + 63) & ~63ull;
             lloff[t * nc + k] = llarena;
             llarena += ll_geom(tc).elems;
             for_each_cblk(tc, [&](Band &band, Cblk &cb) {
                 cb.gidx = (uint32_t)eb.size();
                 EncBlock b;
-                b.coef_off = tc.arena_off + (uint64_t)cb.by * tile.r.w() + cb.bx;
+                b.coef_off = tc.arena_off + (uint64_t)cb.by * tc.r.w() + cb.bx;
                 b.out_off = 0;
-                b.stride = tile.r.w();
+                b.stride = tc.r.w();
                 b.w = cb.r.w();
                 b.h = cb.r.h();
                 b.orient = band.bandno;
@@ -1032,10 +1062,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     if (planes_on_device) {
         for (uint32_t k = 0; k < nc; ++k) src.p[k] = planes[k];
     } else {
-        HIPCHK(c->img.ensure(plane * nc * sb + 256));
+        HIPCHK(c->img.ensure(poff[nc] * sb + 256));
         for (uint32_t k = 0; k < nc; ++k) {
-            src.p[k] = c->img.as<uint8_t>() + plane * sb * k;
-            HIPCHK(hipMemcpyAsync((void *)src.p[k], planes[k], plane * sb, hipMemcpyHostToDevice, s));
+            src.p[k] = c->img.as<uint8_t>() + poff[k] * sb;
+            HIPCHK(hipMemcpyAsync((void *)src.p[k], planes[k], (poff[k + 1] - poff[k]) * sb, hipMemcpyHostToDevice,
+                                  s));
         }
     }
     auto src_at = [&](uint32_t k, uint64_t off) { return (const void *)((const uint8_t *)src.p[k] + off * sb); };
@@ -1071,7 +1102,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], cp.irrev, false);
             if (!fuse || dplan.levels.empty() || dplan.levels[0].size() == before) continue;
             DwtJob &j = dplan.levels[0].back();
-            const uint64_t org = (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * pw + (tile.r.x0 - cp.image.x0 - col0);
+            const uint64_t org = plane_org(k, tc);  // fused: no subsampling, every plane alike
             const bool mct3 = cp.mct && nc >= 3 && k < 3;
             for (uint32_t i = 0; i < 3; ++i) {
                 const uint32_t pk = mct3 ? i : k;
@@ -1091,10 +1122,24 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
         if (fuse) break;
+        if (subs) {  // one launch per tile-component, each on its own grid (no MCT, j2k.cpp:1963-1971)
+            for (uint32_t k = 0; k < nc; ++k) {
+                const TileComp &tc = tile.comps[k];
+                SrcPlanes tsrc{};
+                PlanePtrs tdst{};
+                ShiftArr sk{};
+                tsrc.p[0] = src_at(k, plane_org(k, tc));
+                tdst.p[0] = c->work.as<int32_t>() + tc.arena_off;
+                sk.v[0] = sh.v[k];
+                HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, prect[k].w(), tdst, tc.r.w(), tc.r.h(), 1, sk, 0, cp.irrev,
+                                              s));
+            }
+            continue;
+        }
         SrcPlanes tsrc{};
         PlanePtrs tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
-            tsrc.p[k] = src_at(k, (uint64_t)(tile.r.y0 - cp.image.y0 - row0) * pw + (tile.r.x0 - cp.image.x0 - col0));
+            tsrc.p[k] = src_at(k, plane_org(k, tile.comps[k]));
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
         HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
@@ -1273,7 +1318,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     }
     // j2k_update_rates (j2k.cpp:2806-2926): layer ratios -> byte budgets per tile
     const double header_size = (double)mainhdr.size();
-    const double bits_empty = 8.0, size_pixel = (double)nc * cp.prec[0];
+    const double bits_empty = 8.0 * cp.dx[0] * cp.dy[0], size_pixel = (double)nc * cp.prec[0];
     const uint32_t width = iw, height = ih;
     auto tile_rates = [&](const Rect &tr, uint32_t ntp, double *rates) {
         const double offset = (double)(cp.tp_on ? (float)((ntp - 1) * 14) : 0.0f) / L;
@@ -1633,7 +1678,12 @@ extern "C" int grkgpu_read_header(const uint8_t *cs, size_t len, grkgpu_image_de
     memset(img, 0, sizeof(*img));
     img->x0 = cp.image.x0; img->y0 = cp.image.y0; img->x1 = cp.image.x1; img->y1 = cp.image.y1;
     img->numcomps = cp.numcomps;
-    for (uint32_t k = 0; k < cp.numcomps; ++k) { img->prec[k] = cp.prec[k]; img->sgnd[k] = cp.sgnd[k]; }
+    for (uint32_t k = 0; k < cp.numcomps; ++k) {
+        img->prec[k] = cp.prec[k];
+        img->sgnd[k] = cp.sgnd[k];
+        img->dx[k] = cp.dx[k];
+        img->dy[k] = cp.dy[k];
+    }
     return GRKGPU_OK;
 }
 
@@ -1750,12 +1800,27 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th;
-    const uint32_t iw = ix1 - ix0, ih = iy1 - iy0;
-    const uint64_t plane = (uint64_t)iw * ih;
+    const uint32_t iw = ix1 - ix0;
     if (te > ntiles) te = ntiles;
     if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
     const bool whole = tb == 0 && te == ntiles;
     if (reduce && !whole) return set_err(GRKGPU_EINVAL, "reduced decode of a tile range is not supported");
+    // subsampled components: component k's output plane is the output
+    // rectangle on its grid (ceil(x / dx), the nested ceilings of a reduced
+    // decode commute), rows of its own width
+    bool subs = false;
+    for (uint32_t k = 0; k < nc; ++k) subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+    if (subs && !whole) return set_err(GRKGPU_EUNSUPPORTED, "tile-range decode of subsampled images is not supported");
+    Rect orect[GRKGPU_MAX_COMPS];
+    uint64_t ooff[GRKGPU_MAX_COMPS + 1];
+    ooff[0] = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+        orect[k] = comp_rect({ix0, iy0, ix1, iy1}, cp.dx[k], cp.dy[k]);
+        ooff[k + 1] = ooff[k] + (uint64_t)orect[k].w() * orect[k].h();
+    }
+    // the window on each component's grid
+    Rect cwin[GRKGPU_MAX_COMPS];
+    for (uint32_t k = 0; k < nc; ++k) cwin[k] = comp_rect(wr, cp.dx[k], cp.dy[k]);
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
     // and the coding-parameter markers of their headers (COD / COC / QCD /
@@ -1887,10 +1952,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                     if (cc.cblksty != cp.cblksty || reduce >= cc.numres || cc.cblkw > 6 || cc.cblkh > 6) ok = false;
                     troi[lt][k] = tcp.roishift[k];
                 }
-                // MCT over components of different wavelets: the reference
-                // picks the transform by component 0's alone
+                // MCT over components of different wavelets (the reference
+                // picks the transform by component 0's alone) or sizes
                 if (tcp.mct && nc >= 3 && (tcp.comp[1].irrev != tcp.comp[0].irrev ||
-                                           tcp.comp[2].irrev != tcp.comp[0].irrev))
+                                           tcp.comp[2].irrev != tcp.comp[0].irrev || cp.dx[1] != cp.dx[0] ||
+                                           cp.dx[2] != cp.dx[0] || cp.dy[1] != cp.dy[0] || cp.dy[2] != cp.dy[0]))
                     ok = false;
                 tmct[lt] = tcp.mct;
                 if (!ok) { terr[lt] = 4; continue; }
@@ -1969,7 +2035,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         if (tile.comps.empty()) continue;
         for (uint32_t k = 0; k < nc; ++k) {
             tile.comps[k].arena_off = arena;
-            uint64_t area = (uint64_t)tile.r.w() * tile.r.h();
+            uint64_t area = (uint64_t)tile.comps[k].r.w() * tile.comps[k].r.h();
             arena += (area + 63) & ~63ull;
             lloff[lt * nc + k] = llarena;
             llarena += ll_geom(tile.comps[k]).elems;
@@ -1978,11 +2044,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         const std::vector<uint8_t> &tilebuf = tbufs[lt];
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
-            const BandNeed need = win ? window_need(tc, wr) : BandNeed();
+            const BandNeed need = win ? window_need(tc, cwin[k]) : BandNeed();
             for_each_cblk(tc, [&](Band &band, Cblk &cb) {
                 DecBlock d{};
-                d.dst_off = tc.arena_off + (uint64_t)cb.by * tile.r.w() + cb.bx;
-                d.dstride = tile.r.w();
+                d.dst_off = tc.arena_off + (uint64_t)cb.by * tc.r.w() + cb.bx;
+                d.dstride = tc.r.w();
                 d.w = cb.r.w();
                 d.h = cb.r.h();
                 d.orient = band.bandno;
@@ -2074,7 +2140,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             // a window decode reconstructs, per level, only the windows over
             // the region the window's samples depend on
             std::vector<Rect> rn;
-            if (win) window_need(tc, wr, &rn);
+            if (win) window_need(tc, cwin[k], &rn);
             dwt_plan_tc(dplan[tc.irrev], tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], tc.irrev, true, tc.numres - reduce,
                         win ? &rn : nullptr);
@@ -2100,8 +2166,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (planes_on_device) {
         for (uint32_t k = 0; k < nc; ++k) dst.p[k] = planes[k];
     } else {
-        HIPCHK(c->img.ensure(plane * nc * 4 + 256));
-        for (uint32_t k = 0; k < nc; ++k) dst.p[k] = c->img.as<int32_t>() + plane * k;
+        HIPCHK(c->img.ensure(ooff[nc] * 4 + 256));
+        for (uint32_t k = 0; k < nc; ++k) dst.p[k] = c->img.as<int32_t>() + ooff[k];
     }
     ShiftArr sh{}, mn{}, mx{};
     for (uint32_t k = 0; k < nc; ++k) {
@@ -2111,6 +2177,24 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     }
     for (auto &tile : tiles) {
         if (tile.comps.empty()) continue;  // outside the window
+        if (subs) {  // each tile-component on its own grid, no MCT
+            for (uint32_t k = 0; k < nc; ++k) {
+                const TileComp &tc = tile.comps[k];
+                const Rect tr = tc.res[tc.numres - 1 - reduce].r;
+                const Rect out = intersect(tr, orect[k]);
+                if (out.empty()) continue;
+                PlanePtrs tsrc{}, tdst{};
+                ShiftArr sk{}, mnk{}, mxk{};
+                tsrc.p[0] = c->work.as<int32_t>() + tc.arena_off + (uint64_t)(out.y0 - tr.y0) * tr.w() + (out.x0 - tr.x0);
+                tdst.p[0] = dst.p[k] + (uint64_t)(out.y0 - orect[k].y0) * orect[k].w() + (out.x0 - orect[k].x0);
+                sk.v[0] = sh.v[k];
+                mnk.v[0] = mn.v[k];
+                mxk.v[0] = mx.v[k];
+                HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, orect[k].w(), 1, sk, mnk, mxk, 0,
+                                              tc.irrev, s));
+            }
+            continue;
+        }
         PlanePtrs tsrc{}, tdst{};
         const Rect tr = tile.comps[0].res[tile.comps[0].numres - 1 - reduce].r;  // the tile at the decoded resolution
         const Rect out = win ? intersect(tr, wr) : tr;        // its part of the output
@@ -2129,7 +2213,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (!planes_on_device) {
         if (whole) {
             for (uint32_t k = 0; k < nc; ++k)
-                HIPCHK(hipMemcpyAsync(planes[k], dst.p[k], plane * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(planes[k], dst.p[k], (ooff[k + 1] - ooff[k]) * 4, hipMemcpyDeviceToHost, s));
         } else {  // only the shard's tiles
             for (auto &tile : tiles)
                 for (uint32_t k = 0; k < nc; ++k) {

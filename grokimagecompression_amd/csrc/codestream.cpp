@@ -145,8 +145,14 @@ void TagTree::setvalue(uint32_t leaf, int64_t v) {
     while (n >= 0 && nodes[n].value > v) { nodes[n].value = v; n = nodes[n].parent; }
 }
 
-void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32_t compno, bool encoder) {
+Rect comp_rect(const Rect &r, uint32_t dx, uint32_t dy) {
+    return {ceildiv(r.x0, dx), ceildiv(r.y0, dy), ceildiv(r.x1, dx), ceildiv(r.y1, dy)};
+}
+
+void build_tilecomp(TileComp &tc, const Rect &tile_r, const CodingParams &cp, uint32_t compno, bool encoder) {
     const CompParams &cc = cp.comp[compno];  // the component's COD / COC and QCD / QCC
+    // the tile-component on the component's subsampled grid (TileComponent.cpp:193-196)
+    const Rect tr = comp_rect(tile_r, cp.dx[compno], cp.dy[compno]);
     tc.r = tr;
     tc.numres = cc.numres;
     tc.irrev = cc.irrev;
@@ -242,7 +248,11 @@ void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at, uint
     cs.put32(cp.image.x1); cs.put32(cp.image.y1); cs.put32(cp.image.x0); cs.put32(cp.image.y0);
     cs.put32(cp.tdx); cs.put32(cp.tdy); cs.put32(cp.tx0); cs.put32(cp.ty0);
     cs.put16(nc);
-    for (uint32_t k = 0; k < nc; ++k) { cs.put8((cp.prec[k] - 1) + ((uint32_t)cp.sgnd[k] << 7)); cs.put8(1); cs.put8(1); }
+    for (uint32_t k = 0; k < nc; ++k) {
+        cs.put8((cp.prec[k] - 1) + ((uint32_t)cp.sgnd[k] << 7));
+        cs.put8(cp.dx[k]);
+        cs.put8(cp.dy[k]);
+    }
     // COD (j2k_write_cod + j2k_write_SPCod_SPCoc, j2k.cpp:3723-3770, 6905-6950)
     cs.put16(0xFF52); cs.put16(12 + (prt ? cp.numres : 0));
     cs.put8(cp.csty); cs.put8(cp.prog); cs.put16(cp.numlayers); cs.put8((uint32_t)cp.mct);
@@ -635,7 +645,9 @@ bool parse_main_header(const uint8_t *cs, size_t len, CodingParams &cp, size_t &
                 cp.prec[k] = (p[36 + 3 * k] & 0x7f) + 1u;
                 cp.sgnd[k] = p[36 + 3 * k] >> 7;
                 if (cp.prec[k] > 16) { err = "precision above 16 bits not supported"; return false; }
-                if (p[37 + 3 * k] != 1 || p[38 + 3 * k] != 1) { err = "subsampled components not supported"; return false; }
+                cp.dx[k] = p[37 + 3 * k];
+                cp.dy[k] = p[38 + 3 * k];
+                if (!cp.dx[k] || !cp.dy[k]) { err = "Invalid component subsampling dx / dy (should be between 1 and 255 according to the JPEG2000 norm)"; return false; }
             }
             if (cp.tdx == 0 || cp.tdy == 0) { err = "bad tile size"; return false; }
             if (cp.tx0 > cp.image.x0 || cp.ty0 > cp.image.y0 || (uint64_t)cp.tx0 + cp.tdx <= cp.image.x0 ||

@@ -63,6 +63,8 @@ struct CodingParams {
     Rect image;
     uint32_t prec[16] = {};
     int32_t sgnd[16] = {};
+    uint32_t dx[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};  // SIZ XRsiz / YRsiz: component subsampling
+    uint32_t dy[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
     uint32_t numres = 6, cblkw = 6, cblkh = 6;
     int32_t irrev = 0, mct = 0;
     uint32_t tdx = 0, tdy = 0, tx0 = 0, ty0 = 0, tw = 1, th = 1;
@@ -185,7 +187,9 @@ struct Tile {
     std::vector<TileComp> comps;
 };
 
-// geometry (TileComponent.cpp:165-507)
+// geometry (TileComponent.cpp:165-507); comp_rect: a rectangle of the
+// reference grid on a component's subsampled grid (ceil of each coordinate / dx, dy)
+Rect comp_rect(const Rect &r, uint32_t dx, uint32_t dy);
 void build_tilecomp(TileComp &tc, const Rect &tr, const CodingParams &cp, uint32_t compno, bool encoder);
 Rect tile_rect(const CodingParams &cp, uint32_t tileno);
 // QCD generation (HTParams.cpp:164-260)

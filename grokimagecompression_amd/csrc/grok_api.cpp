@@ -212,6 +212,17 @@ struct Codec {
 };
 
 uint32_t cdivpow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); }
+uint32_t cdiv(uint32_t v, uint32_t d) { return (uint32_t)(((uint64_t)v + d - 1) / d); }
+// a component's origin and size for an image / area [x0, x1) x [y0, y1) of
+// the reference grid, on its dx / dy grid at resolution reduce r
+// (j2k_read_header / j2k_set_decode_area: ceil(ceil(x / dx) / 2^r))
+void comp_geom(grk_image_comp &cp, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t r) {
+    const uint32_t dx = cp.dx ? cp.dx : 1, dy = cp.dy ? cp.dy : 1;
+    cp.x0 = cdivpow2(cdiv(x0, dx), r);
+    cp.y0 = cdivpow2(cdiv(y0, dy), r);
+    cp.w = cdivpow2(cdiv(x1, dx), r) - cp.x0;
+    cp.h = cdivpow2(cdiv(y1, dy), r) - cp.y0;
+}
 
 struct TileRect { uint32_t x0, y0, x1, y1; };
 // tile t of the grid (j2k tile geometry: tile (p, q) spans tx0 + p tdx .. clipped to the image)
@@ -230,7 +241,8 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     if (g->cblk_sty & ~0x3Fu) { GRK_ERROR("code-block style 0x%x: HT is not supported", g->cblk_sty); return false; }
     if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
     if (g->tcp_mct == 2 || g->mct_data) { GRK_ERROR("custom MCT is not supported"); return false; }
-    if (g->subsampling_dx != 1 || g->subsampling_dy != 1) { GRK_ERROR("subsampling is not supported"); return false; }
+    // subsampling_dx / _dy are the CLI image readers' (PNMFormat.cpp:397-417);
+    // the library takes each component's dx / dy from the image
     p->numresolution = g->numresolution;
     p->cblockw_init = g->cblockw_init;
     p->cblockh_init = g->cblockh_init;
@@ -285,11 +297,15 @@ bool image_desc(const grk_image *img, grkgpu_image_desc *d) {
     d->numcomps = img->numcomps;
     for (uint32_t k = 0; k < img->numcomps; ++k) {
         const grk_image_comp &c = img->comps[k];
-        if (c.dx != 1 || c.dy != 1) { GRK_ERROR("component %u is subsampled: not supported", k); return false; }
-        if (c.w != img->x1 - img->x0 || c.h != img->y1 - img->y0) {
-            GRK_ERROR("component %u size differs from the image", k);
+        if (!c.dx || !c.dy || c.dx > 255 || c.dy > 255) { GRK_ERROR("component %u: dx / dy must be 1..255", k); return false; }
+        // the component's plane: the image on its subsampled grid (TileComponent.cpp:150-163)
+        const uint32_t cw = cdiv(img->x1, c.dx) - cdiv(img->x0, c.dx), ch = cdiv(img->y1, c.dy) - cdiv(img->y0, c.dy);
+        if (c.w != cw || c.h != ch) {
+            GRK_ERROR("component %u size differs from the image's on its grid", k);
             return false;
         }
+        d->dx[k] = c.dx;
+        d->dy[k] = c.dy;
         if (!c.data) { GRK_ERROR("component %u has no data", k); return false; }
         d->prec[k] = c.prec;
         d->sgnd[k] = (int32_t)c.sgnd;
@@ -563,13 +579,11 @@ GRK_EXPORT bool grk_read_header(grk_codec *codec, grk_header_info *hi, grk_image
     const uint32_t r = c->dparams.cp_reduce;
     for (uint32_t k = 0; k < d.numcomps; ++k) {
         grk_image_comp &cp = img->comps[k];
-        cp.dx = cp.dy = 1;
+        cp.dx = d.dx[k];
+        cp.dy = d.dy[k];
         cp.prec = d.prec[k];
         cp.sgnd = (uint32_t)d.sgnd[k];
-        cp.x0 = cdivpow2(d.x0, r);
-        cp.y0 = cdivpow2(d.y0, r);
-        cp.w = cdivpow2(d.x1, r) - cp.x0;
-        cp.h = cdivpow2(d.y1, r) - cp.y0;
+        comp_geom(cp, d.x0, d.y0, d.x1, d.y1, r);
     }
     *image = img;
     if (hi) {
@@ -615,12 +629,7 @@ GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t
     c->win[0] = std::max(x0, d.x0); c->win[1] = std::max(y0, d.y0);
     c->win[2] = std::min(x1, d.x1); c->win[3] = std::min(y1, d.y1);
     image->x0 = c->win[0]; image->y0 = c->win[1]; image->x1 = c->win[2]; image->y1 = c->win[3];
-    for (uint32_t k = 0; k < image->numcomps; ++k) {
-        grk_image_comp &cp = image->comps[k];
-        cp.x0 = c->win[0]; cp.y0 = c->win[1];
-        cp.w = c->win[2] - c->win[0];
-        cp.h = c->win[3] - c->win[1];
-    }
+    for (uint32_t k = 0; k < image->numcomps; ++k) comp_geom(image->comps[k], c->win[0], c->win[1], c->win[2], c->win[3], 0);
     return true;
 }
 
@@ -719,6 +728,11 @@ GRK_EXPORT bool grk_read_tile_header(grk_codec *codec, uint16_t *tile_index, uin
                                      uint32_t *y0, uint32_t *x1, uint32_t *y1, uint32_t *nb_comps, bool *go_on) {
     Codec *c = (Codec *)codec;
     if (!c || !c->decompressor || !c->have_header || !tile_index || !data_size) return false;
+    for (uint32_t k = 0; k < c->desc.numcomps; ++k)
+        if (c->desc.dx[k] != 1 || c->desc.dy[k] != 1) {
+            GRK_ERROR("tile-by-tile decode of subsampled components is not supported (grk_decode decodes them)");
+            return false;
+        }
     const grkgpu_header_info &h = c->hinfo;
     if (!c->tile_order_ready) {
         for (uint32_t t : stream_tile_order(c->cs, h.tw * h.th)) {

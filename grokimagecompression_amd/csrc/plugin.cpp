@@ -570,6 +570,11 @@ int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const c
         log(grkgpu_last_error());
         return -1;
     }
+    for (uint32_t k = 0; k < d.numcomps; ++k)
+        if (d.dx[k] != 1 || d.dy[k] != 1) {
+            log("subsampled components; declined");
+            return -1;
+        }
     const uint32_t r = params->core.cp_reduce;
     grkgpu_dparams dp{r, params->core.cp_layer, params->DA_x0, params->DA_y0, params->DA_x1, params->DA_y1};
     const bool win = dp.DA_x0 || dp.DA_y0 || dp.DA_x1 || dp.DA_y1;

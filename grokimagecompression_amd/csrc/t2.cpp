@@ -71,12 +71,14 @@ TileGeom tile_geom(const CodingParams &cp, const Tile &tile) {
         PiComp &c = g.comps[k];
         const CompParams &cc = cp.comp[k];  // the component's COD / COC
         c.numres = cc.numres;
+        c.dx = cp.dx[k];
+        c.dy = cp.dy[k];
         g.max_res = std::max(g.max_res, cc.numres);
         for (uint32_t r = 0; r < cc.numres; ++r) {
             const uint32_t level = cc.numres - 1 - r;
             c.res[r].pdx = cc.prcw[r];
             c.res[r].pdy = cc.prch[r];
-            const uint64_t dx = (uint64_t)1 << (cc.prcw[r] + level), dy = (uint64_t)1 << (cc.prch[r] + level);
+            const uint64_t dx = (uint64_t)c.dx << (cc.prcw[r] + level), dy = (uint64_t)c.dy << (cc.prch[r] + level);
             if (dx < UINT_MAX) g.dx_min = std::min<uint32_t>(g.dx_min, (uint32_t)dx);
             if (dy < UINT_MAX) g.dy_min = std::min<uint32_t>(g.dy_min, (uint32_t)dy);
             if (tile.comps.empty()) continue;

@@ -62,12 +62,19 @@ enum {
     GRKGPU_ECORRUPT = -5
 };
 
-/* grk_image subset (grok.h:851-918): planar int32 components, dx = dy = 1 */
+/* grk_image subset (grok.h:851-918): planar components.  [x0, x1) x [y0, y1)
+ * is the image on the reference grid; component k is subsampled by dx[k],
+ * dy[k] (SIZ XRsiz / YRsiz; 0 reads as 1), so its plane covers
+ * [ceil(x0 / dx), ceil(x1 / dx)) x [ceil(y0 / dy), ceil(y1 / dy)) -- rows of
+ * that width, planes[k] holding only component k (grk_image_comp w, h,
+ * TileComponent.cpp:150-163).  A reduced / window decode reports the reduced
+ * / window rectangle here, and component planes follow the same rule. */
 typedef struct {
     uint32_t x0, y0, x1, y1;
     uint32_t numcomps;
     uint32_t prec[GRKGPU_MAX_COMPS];
     int32_t sgnd[GRKGPU_MAX_COMPS];
+    uint32_t dx[GRKGPU_MAX_COMPS], dy[GRKGPU_MAX_COMPS];
 } grkgpu_image_desc;
 
 /* One progression-order change (grk_poc, grok.h:393-410; grk_compress -P

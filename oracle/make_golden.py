@@ -223,9 +223,28 @@ def ref_decode(j2k, tmp, extra=()):
     with open(src, "wb") as f:
         f.write(j2k)
     r = subprocess.run([DRIVER, "dec", src, out] + list(extra), check=True, capture_output=True, text=True)
-    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.split())
+    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.splitlines()[0].split())
     dec = np.fromfile(out, dtype="<i4").reshape(nc, ch, cw)
     return dec, (x0, y0, x1, y1, prec, sgnd)
+
+
+def ref_decode_planes(j2k, tmp, extra=()):
+    """Reference decode of a stream whose components may differ in size
+    (subsampled) -> ([int32 (h_k, w_k) per component], [(dx, dy) per component])."""
+    src = os.path.join(tmp, "in.j2k")
+    out = os.path.join(tmp, "out.i32")
+    with open(src, "wb") as f:
+        f.write(j2k)
+    r = subprocess.run([DRIVER, "dec", src, out] + list(extra), check=True, capture_output=True, text=True)
+    f = list(map(int, r.stdout.splitlines()[1].split()[1:]))
+    raw = np.fromfile(out, dtype="<i4")
+    planes, subs, off = [], [], 0
+    for k in range(len(f) // 4):
+        w, h, dx, dy = f[4 * k:4 * k + 4]
+        planes.append(raw[off:off + w * h].reshape(h, w))
+        subs.append((dx, dy))
+        off += w * h
+    return planes, subs
 
 
 def run_case(name, shape, kind, seed, args, tmp, keep_dir=None):

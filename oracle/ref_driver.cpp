@@ -112,6 +112,11 @@ static GRK_PROG_ORDER prog(const char *s) {
     return GRK_PROG_UNKNOWN;
 }
 
+// -sub dx,dy/dx,dy/...: per-component subsampling of the grk_image the
+// driver builds (grk_image_cmptparm dx / dy; the CLI's -s sets one factor for
+// all components, grk_compress.cpp:1060, PNMFormat.cpp:397-417)
+static std::vector<std::pair<uint32_t, uint32_t>> g_sub;
+
 // grk_compress option subset -> parameters (citations in the header)
 static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
     grk_set_default_encoder_parameters(p);
@@ -132,6 +137,17 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
         else if (a == "-T") { if (sscanf(v, "%u,%u", &p->cp_tx0, &p->cp_ty0) != 2) return false; }
         else if (a == "-Y") p->tcp_mct = (uint8_t)atoi(v);
         else if (a == "-p") p->prog_order = prog(v);
+        else if (a == "-sub") {
+            g_sub.clear();
+            const char *s = v;
+            uint32_t dx, dy;
+            while (sscanf(s, "%u,%u", &dx, &dy) == 2) {
+                g_sub.push_back({dx, dy});
+                while (*s && *s != '/') s++;
+                if (!*s) break;
+                s++;
+            }
+        }
         else if (a == "-M") p->cblk_sty = (uint8_t)(atoi(v) & 0x7f);
         else if (a == "-u") { p->tp_flag = (uint8_t)v[0]; p->tp_on = 1; }
         else if (a == "-A") p->rateControlAlgorithm = (uint32_t)atoi(v);
@@ -204,6 +220,16 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
     return true;
 }
 
+static uint32_t cdivu(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// component k's plane size for a w x h image at the parameters' offset
+static void comp_size(const grk_cparameters *p, uint32_t w, uint32_t h, uint32_t k, uint32_t *cw, uint32_t *ch) {
+    const uint32_t dx = k < g_sub.size() ? g_sub[k].first : 1, dy = k < g_sub.size() ? g_sub[k].second : 1;
+    const uint32_t x0 = p->image_offset_x0, y0 = p->image_offset_y0;
+    *cw = cdivu(x0 + w, dx) - cdivu(x0, dx);
+    *ch = cdivu(y0 + h, dy) - cdivu(y0, dy);
+}
+
 static grk_image *make_image(const int32_t *planes, uint32_t w, uint32_t h, uint32_t c, uint32_t bits, uint32_t sgnd,
                              const grk_cparameters *p) {
     std::vector<grk_image_cmptparm> cm(c);
@@ -211,10 +237,11 @@ static grk_image *make_image(const int32_t *planes, uint32_t w, uint32_t h, uint
     for (uint32_t k = 0; k < c; ++k) {
         cm[k].prec = bits;
         cm[k].sgnd = sgnd;
-        cm[k].dx = 1;
-        cm[k].dy = 1;
-        cm[k].w = w;
-        cm[k].h = h;
+        cm[k].dx = k < g_sub.size() ? g_sub[k].first : 1;
+        cm[k].dy = k < g_sub.size() ? g_sub[k].second : 1;
+        comp_size(p, w, h, k, &cm[k].w, &cm[k].h);
+        cm[k].x0 = cdivu(p->image_offset_x0, cm[k].dx);
+        cm[k].y0 = cdivu(p->image_offset_y0, cm[k].dy);
     }
     grk_image *img = grk_image_create(c, cm.data(), c >= 3 ? GRK_CLRSPC_SRGB : GRK_CLRSPC_GRAY);
     if (!img) return nullptr;
@@ -222,7 +249,12 @@ static grk_image *make_image(const int32_t *planes, uint32_t w, uint32_t h, uint
     img->y0 = p->image_offset_y0;
     img->x1 = p->image_offset_x0 + w;
     img->y1 = p->image_offset_y0 + h;
-    for (uint32_t k = 0; k < c; ++k) memcpy(img->comps[k].data, planes + (size_t)k * w * h, (size_t)w * h * 4);
+    size_t off = 0;
+    for (uint32_t k = 0; k < c; ++k) {
+        const size_t n = (size_t)cm[k].w * cm[k].h;
+        memcpy(img->comps[k].data, planes + off, n * 4);
+        off += n;
+    }
     return img;
 }
 
@@ -616,7 +648,17 @@ int main(int argc, char **argv) {
         ai += 5;
         if (bench) { threads = (uint32_t)atoi(argv[ai]); reps = (uint32_t)atoi(argv[ai + 1]); ai += 2; }
         std::vector<uint8_t> in = read_file(argv[2]);
-        if (in.size() != (size_t)w * h * c * 4) { fprintf(stderr, "input size mismatch\n"); return 2; }
+        {
+            grk_cparameters p0;  // the offset and -sub decide the plane sizes
+            if (!parse_enc_opts(&p0, argc - ai, argv + ai)) return 2;
+            size_t need = 0;
+            for (uint32_t k = 0; k < c; ++k) {
+                uint32_t cw, ch;
+                comp_size(&p0, w, h, k, &cw, &ch);
+                need += (size_t)cw * ch * 4;
+            }
+            if (in.size() != need) { fprintf(stderr, "input size mismatch\n"); return 2; }
+        }
         grk_initialize(nullptr, threads);  // returns "plugin loaded": none is, CPU path
         std::vector<uint8_t> cs;
         double t_enc = 0, t_dec = 0;
@@ -709,6 +751,10 @@ int main(int argc, char **argv) {
         write_file(argv[3], out.data(), out.size() * 4);
         printf("%u %u %u %u %u %u %u %u %u\n", img->x0, img->y0, img->x1, img->y1, img->numcomps, img->comps[0].prec,
                img->comps[0].sgnd, img->comps[0].w, img->comps[0].h);
+        printf("comps");  // each component's plane (subsampled ones differ)
+        for (uint32_t k = 0; k < img->numcomps; ++k)
+            printf(" %u %u %u %u", img->comps[k].w, img->comps[k].h, img->comps[k].dx, img->comps[k].dy);
+        printf("\n");
         grk_destroy_codec(codec);
         grk_stream_destroy(st);
         grk_deinitialize();

@@ -78,7 +78,7 @@ def test_siz_field_checks():
     _rejects(_patch(cs, siz + 38, ">H", 4))           # Csiz does not match the marker length
     _rejects(_patch(cs, siz + 38, ">H", 0))           # no components
     _rejects(_patch(cs, siz + 40, ">B", 16))          # 17-bit precision: unsupported
-    _rejects(_patch(cs, siz + 41, ">B", 2))           # subsampled component
+    _rejects(_patch(cs, siz + 41, ">B", 0))           # XRsiz 0
     _rejects(_patch(cs, siz + 2, ">H", 20))           # marker too short
 
 
@@ -96,7 +96,7 @@ def test_cod_qcd_field_checks():
     _rejects(_patch(cs, p, ">B", 8))                  # unknown Scod bit
     _rejects(_patch(cs, cod + 2, ">H", 4))            # COD too short
     qcd = _marker(cs, 0xFF5C)
-    _rejects(_patch(cs, qcd + 4, ">B", 1))            # scalar-derived quantisation
+    _rejects(_patch(cs, qcd + 4, ">B", 1))            # scalar-derived: one step size, not the marker's 16
     _rejects(_patch(cs, qcd + 2, ">H", 2))            # QCD too short
 
 

@@ -61,6 +61,14 @@ def test_marker_fixtures_regenerate():
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
 
 
+def test_subsampled_fixtures_regenerate():
+    """tests/golden/sub_*: subsampled-component images encoded and decoded by
+    the reference (oracle/make_golden_sub.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "make_golden_sub.py"), "--check"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
 def test_cstr_info_matches_reference():
     """grk_get_cstr_info of our libgrok.so (ref_driver_mi355x: the same driver
     relinked against it; header parsing needs no GPU) prints exactly what the
