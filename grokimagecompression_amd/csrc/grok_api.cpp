@@ -209,6 +209,7 @@ struct Codec {
     int64_t cur_tile = -1;
     std::vector<int32_t> reduced;  // reduced-resolution decode of the whole image (cp_reduce > 0), decoded once
     grkgpu_image_desc reduced_desc{};
+    bool decoded = false;  // grk_decode has read every tile-part (what grk_get_cstr_index reports)
 };
 
 uint32_t cdivpow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); }
@@ -653,6 +654,7 @@ GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image
     }
     for (uint32_t k = 0; k < image->numcomps; ++k)
         image->comps[k].resno_decoded = c->hinfo.numresolutions - 1 - c->dparams.cp_reduce;
+    c->decoded = true;
     return true;
 }
 
@@ -1084,8 +1086,97 @@ GRK_EXPORT void grk_destroy_cstr_info(grk_codestream_info_v2 **p) {
     free(*p);
     *p = nullptr;
 }
-GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *) { return nullptr; }
-GRK_EXPORT void grk_destroy_cstr_index(grk_codestream_index **p) { if (p) *p = nullptr; }
+// grk_get_cstr_index (grok.cpp:694 -> j2k_get_cstr_index, j2k_dump.cpp:
+// 402-517): what the reference's decoder records while reading -- every
+// main-header marker (type, position, length incl. the marker code:
+// j2k.cpp:304-311, SOC 3150-3161), the first SOT's position
+// (main_head_end, :341-344), and per tile its tile-part markers (SOT, the
+// header markers, SOD with length 0: :739-749, 5443-5448) and tile-part
+// positions (SOT, SOD, SOT + Psot: :5276-5360, 5426-5441, 6696-6704).
+// codestream_size is only set when encoding (j2k_write_epc) and stays 0.
+// The copy is the reference's too: tileno and the current_* fields are not
+// copied (0), and since grk_malloc(0) is null, a tile without markers or
+// without a TNsot count makes the whole call return null -- as it does after
+// grk_read_header alone, before any tile-part is read.
+static void *malloc_nz(size_t n) { return n ? malloc(n) : nullptr; }
+GRK_EXPORT void grk_destroy_cstr_index(grk_codestream_index **p) {
+    if (!p || !*p) return;
+    grk_codestream_index *ix = *p;
+    for (uint32_t t = 0; ix->tile_index && t < ix->nb_of_tiles; ++t) {
+        free(ix->tile_index[t].marker);
+        free(ix->tile_index[t].tp_index);
+        free(ix->tile_index[t].packet_index);
+    }
+    free(ix->tile_index);
+    free(ix->marker);
+    free(ix);
+    *p = nullptr;
+}
+GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *codec) {
+    Codec *c = (Codec *)codec;
+    if (!c || !c->decompressor || !c->have_header || !c->decoded) return nullptr;
+    const std::vector<uint8_t> &cs = c->cs;
+    const size_t len = cs.size();
+    auto rd16 = [&](size_t q) { return q + 2 <= len ? (uint32_t)cs[q] << 8 | cs[q + 1] : 0u; };
+    std::vector<grk_marker_info> mh{{0xFF4F, 0, 2}};
+    size_t pos = 2;
+    while (pos + 4 <= len && rd16(pos) != 0xFF90) {
+        const uint32_t L = rd16(pos + 2);
+        mh.push_back({(uint16_t)rd16(pos), (uint64_t)pos, L + 2});
+        pos += 2 + L;
+    }
+    const size_t main_end = pos;
+    const uint32_t nt = c->hinfo.tw * c->hinfo.th;
+    std::vector<std::vector<grk_marker_info>> tm(nt);
+    std::vector<std::vector<grk_tp_index>> tp(nt);
+    std::vector<uint32_t> nb_tps(nt, 0);
+    while (pos + 12 <= len && rd16(pos) == 0xFF90) {
+        const uint32_t isot = rd16(pos + 4), psot = rd16(pos + 6) << 16 | rd16(pos + 8);
+        const uint32_t tpsot = cs[pos + 10], tnsot = cs[pos + 11];
+        if (isot >= nt) break;
+        const size_t sot = pos;
+        tm[isot].push_back({0xFF90, (uint64_t)sot, 12});
+        if (tnsot) nb_tps[isot] = tnsot;
+        if (tp[isot].size() < std::max<uint32_t>(nb_tps[isot], tpsot + 1)) tp[isot].resize(std::max<uint32_t>(nb_tps[isot], tpsot + 1), grk_tp_index{});
+        tp[isot][tpsot].start_pos = sot;
+        pos += 12;
+        while (pos + 4 <= len && rd16(pos) != 0xFF93) {
+            const uint32_t L = rd16(pos + 2);
+            tm[isot].push_back({(uint16_t)rd16(pos), (uint64_t)pos, L + 2});
+            pos += 2 + L;
+        }
+        tm[isot].push_back({0xFF93, (uint64_t)pos, 0});
+        const size_t end = psot ? std::min<size_t>(sot + psot, len) : (len >= 2 ? len - 2 : len);
+        tp[isot][tpsot].end_header = pos;
+        tp[isot][tpsot].end_pos = end;
+        if (!psot || end <= pos) break;
+        pos = end;
+    }
+    for (uint32_t t = 0; t < nt; ++t)
+        if (tm[t].empty() || !nb_tps[t]) return nullptr;  // grk_malloc(0) (j2k_dump.cpp:449-465, 481-498)
+    auto *ix = (grk_codestream_index *)calloc(1, sizeof(grk_codestream_index));
+    if (!ix) return nullptr;
+    ix->main_head_start = 0;
+    ix->main_head_end = main_end;
+    ix->codestream_size = 0;
+    ix->marknum = (uint32_t)mh.size();
+    ix->marker = (grk_marker_info *)malloc_nz(mh.size() * sizeof(grk_marker_info));
+    ix->nb_of_tiles = nt;
+    ix->tile_index = (grk_tile_index *)calloc(nt, sizeof(grk_tile_index));
+    if (!ix->marker || !ix->tile_index) { grk_destroy_cstr_index(&ix); return nullptr; }
+    memcpy(ix->marker, mh.data(), mh.size() * sizeof(grk_marker_info));
+    for (uint32_t t = 0; t < nt; ++t) {
+        grk_tile_index &ti = ix->tile_index[t];
+        ti.marknum = (uint32_t)tm[t].size();
+        ti.marker = (grk_marker_info *)malloc_nz(tm[t].size() * sizeof(grk_marker_info));
+        ti.nb_tps = nb_tps[t];
+        ti.tp_index = (grk_tp_index *)calloc(nb_tps[t], sizeof(grk_tp_index));
+        if (!ti.marker || !ti.tp_index) { grk_destroy_cstr_index(&ix); return nullptr; }
+        memcpy(ti.marker, tm[t].data(), tm[t].size() * sizeof(grk_marker_info));
+        memcpy(ti.tp_index, tp[t].data(), std::min<size_t>(nb_tps[t], tp[t].size()) * sizeof(grk_tp_index));
+    }
+    return ix;
+}
 
 // ---------------------------------------------------------------------------
 // plugin management: this library is the accelerated path, no plugin loads

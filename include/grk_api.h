@@ -54,7 +54,40 @@ typedef grkp_dparameters grk_dparameters;
 typedef grkp_decompress_parameters grk_decompress_parameters;
 typedef void *grk_codec;   /* grok.h:797 */
 typedef void *grk_stream;  /* grok.h:836 */
-typedef struct grk_codestream_index grk_codestream_index;
+
+/* Codestream index (grok.h:950-1214, filled by j2k_get_cstr_index,
+ * j2k_dump.cpp:402-517): marker and tile-part positions recorded while
+ * decoding; layouts checked by oracle/abi/. */
+typedef struct grk_packet_info {     /* grok.h:953-962 */
+    uint64_t start_pos, end_ph_pos, end_pos;
+    double disto;
+} grk_packet_info;
+typedef struct grk_marker_info {     /* grok.h:967-974 */
+    uint16_t type;
+    uint64_t pos;
+    uint32_t len;
+} grk_marker_info;
+typedef struct grk_tp_index {        /* grok.h:1161-1168 */
+    uint64_t start_pos, end_header, end_pos;
+} grk_tp_index;
+typedef struct grk_tile_index {      /* grok.h:1173-1194 */
+    uint16_t tileno;
+    uint32_t nb_tps, current_nb_tps, current_tpsno;
+    grk_tp_index *tp_index;
+    uint32_t marknum;
+    grk_marker_info *marker;
+    uint32_t maxmarknum;
+    uint32_t nb_packet;
+    grk_packet_info *packet_index;
+} grk_tile_index;
+typedef struct grk_codestream_index { /* grok.h:1199-1214 */
+    uint64_t main_head_start, main_head_end, codestream_size;
+    uint32_t marknum;
+    grk_marker_info *marker;
+    uint32_t maxmarknum;
+    uint32_t nb_of_tiles;
+    grk_tile_index *tile_index;
+} grk_codestream_index;
 
 /* Codestream info of the main header (grok.h:1080-1156, filled by
  * j2k_get_cstr_info, j2k_dump.cpp:326-400); layouts checked by oracle/abi/. */

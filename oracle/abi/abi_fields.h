@@ -67,7 +67,15 @@
     S(TILEINFO2) F(TILEINFO2, tileno) F(TILEINFO2, csty) F(TILEINFO2, prg) F(TILEINFO2, numlayers)           \
     F(TILEINFO2, mct) F(TILEINFO2, tccp_info)                                                                \
     S(CSINFO) F(CSINFO, tx0) F(CSINFO, ty0) F(CSINFO, tdx) F(CSINFO, tdy) F(CSINFO, tw) F(CSINFO, th)         \
-    F(CSINFO, nbcomps) F(CSINFO, m_default_tile_info) F(CSINFO, tile_info)
+    F(CSINFO, nbcomps) F(CSINFO, m_default_tile_info) F(CSINFO, tile_info)                                   \
+    S(MARKER) F(MARKER, type) F(MARKER, pos) F(MARKER, len)                                                  \
+    S(TPIDX) F(TPIDX, start_pos) F(TPIDX, end_header) F(TPIDX, end_pos)                                      \
+    S(PKTINFO) F(PKTINFO, start_pos) F(PKTINFO, end_ph_pos) F(PKTINFO, end_pos) F(PKTINFO, disto)              \
+    S(TILEIDX) F(TILEIDX, tileno) F(TILEIDX, nb_tps) F(TILEIDX, current_nb_tps) F(TILEIDX, current_tpsno)      \
+    F(TILEIDX, tp_index) F(TILEIDX, marknum) F(TILEIDX, marker) F(TILEIDX, maxmarknum) F(TILEIDX, nb_packet)   \
+    F(TILEIDX, packet_index)                                                                                 \
+    S(CSIDX) F(CSIDX, main_head_start) F(CSIDX, main_head_end) F(CSIDX, codestream_size) F(CSIDX, marknum)    \
+    F(CSIDX, marker) F(CSIDX, maxmarknum) F(CSIDX, nb_of_tiles) F(CSIDX, tile_index)
 
 #define ABI_EMIT_S(tag) {#tag, "sizeof", sizeof(T_##tag)},
 #define ABI_EMIT_F(tag, field) {#tag, #field, offsetof(T_##tag, field)},

@@ -26,4 +26,9 @@ using T_DCBINFO = grk::PluginDecodeCallbackInfo;
 using T_TCCPINFO = grk_tccp_info;
 using T_TILEINFO2 = grk_tile_info_v2;
 using T_CSINFO = grk_codestream_info_v2;
+using T_MARKER = grk_marker_info;
+using T_TPIDX = grk_tp_index;
+using T_PKTINFO = grk_packet_info;
+using T_TILEIDX = grk_tile_index;
+using T_CSIDX = grk_codestream_index;
 extern const AbiEntry abi_ref[] = {ABI_FIELDS(ABI_EMIT_F, ABI_EMIT_S){nullptr, nullptr, 0}};

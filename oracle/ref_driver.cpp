@@ -57,6 +57,7 @@
 //       caller thread), encode + decode REPS times concurrently;
 //       exit 0 iff every encode equals EXPECT.j2k and every decode equals the
 //       first decode (lossless: the input).
+//   ref_driver index IN.j2k   (grk_get_cstr_index after grk_read_header and after grk_decode)
 //   ref_driver info IN.j2k
 //       grk_read_header, then grk_get_cstr_info printed field by field (the
 //       grk_dump path, grk_dump.cpp:494-500) and grk_destroy_cstr_info.
@@ -627,7 +628,7 @@ static int mt_mode(int argc, char **argv) {
 }
 
 int main(int argc, char **argv) {
-    if (argc < 4 && !(argc == 3 && std::string(argv[1]) == "info")) {
+    if (argc < 4 && !(argc == 3 && (std::string(argv[1]) == "info" || std::string(argv[1]) == "index"))) {
         fprintf(stderr, "usage: see oracle/ref_driver.cpp\n");
         return 2;
     }
@@ -722,6 +723,49 @@ int main(int argc, char **argv) {
         }
         grk_destroy_cstr_info(&ci);
         printf("destroyed %d\n", ci == nullptr);
+        grk_destroy_codec(codec);
+        grk_stream_destroy(st);
+        grk_deinitialize();
+        return 0;
+    }
+    if (mode == "index") {  // grk_get_cstr_index after grk_read_header, then after a full grk_decode
+        std::vector<uint8_t> cs = read_file(argv[2]);
+        grk_initialize(nullptr, 0);
+        grk_stream *st = grk_stream_create_mem_stream(cs.data(), cs.size(), false, true);
+        grk_codec *codec = grk_create_decompress(GRK_CODEC_J2K, st);
+        grk_set_error_handler(err_cb, nullptr);
+        grk_dparameters dp;
+        grk_set_default_decoder_parameters(&dp);
+        grk_header_info hi;
+        memset(&hi, 0, sizeof(hi));
+        grk_image *img = nullptr;
+        if (!(codec && grk_setup_decoder(codec, &dp) && grk_read_header(codec, &hi, &img))) return 1;
+        auto dump = [](grk_codestream_index *ix, const char *when) {
+            if (!ix) { printf("%s none\n", when); return; }
+            printf("%s main %llu %llu size %llu marknum %u\n", when, (unsigned long long)ix->main_head_start,
+                   (unsigned long long)ix->main_head_end, (unsigned long long)ix->codestream_size, ix->marknum);
+            for (uint32_t i = 0; i < ix->marknum && ix->marker; ++i)
+                printf(" m %04x %llu %u\n", ix->marker[i].type, (unsigned long long)ix->marker[i].pos, ix->marker[i].len);
+            printf(" tiles %u %d\n", ix->nb_of_tiles, ix->tile_index != nullptr);
+            for (uint32_t t = 0; ix->tile_index && t < ix->nb_of_tiles; ++t) {
+                const grk_tile_index &ti = ix->tile_index[t];
+                printf(" tile %u tileno %u marknum %u nb_tps %u nb_packet %u\n", t, ti.tileno, ti.marknum, ti.nb_tps,
+                       ti.nb_packet);
+                for (uint32_t i = 0; i < ti.marknum && ti.marker; ++i)
+                    printf("  m %04x %llu %u\n", ti.marker[i].type, (unsigned long long)ti.marker[i].pos, ti.marker[i].len);
+                for (uint32_t i = 0; i < ti.nb_tps && ti.tp_index; ++i)
+                    printf("  tp %llu %llu %llu\n", (unsigned long long)ti.tp_index[i].start_pos,
+                           (unsigned long long)ti.tp_index[i].end_header, (unsigned long long)ti.tp_index[i].end_pos);
+            }
+        };
+        grk_codestream_index *ix = grk_get_cstr_index(codec);
+        dump(ix, "header");
+        grk_destroy_cstr_index(&ix);
+        if (!(grk_decode(codec, nullptr, img) && grk_end_decompress(codec))) return 1;
+        ix = grk_get_cstr_index(codec);
+        dump(ix, "decoded");
+        grk_destroy_cstr_index(&ix);
+        printf("destroyed %d\n", ix == nullptr);
         grk_destroy_codec(codec);
         grk_stream_destroy(st);
         grk_deinitialize();

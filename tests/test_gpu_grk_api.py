@@ -77,8 +77,59 @@ def _dec(name, tmp_path, extra=()):
     r = subprocess.run([DRIVER, "dec", f"{GOLD}/{name}.j2k", str(out)] + list(extra), capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr
-    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.split())
+    x0, y0, x1, y1, nc, prec, sgnd, cw, ch = map(int, r.stdout.splitlines()[0].split())
     return np.fromfile(out, dtype="<i4").reshape(nc, ch, cw), (x0, y0, x1, y1, prec, sgnd)
+
+
+INDEX = json.load(open(f"{GOLD}/cstr_index.json"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(INDEX))
+def test_grk_cstr_index_matches_reference(name):
+    """grk_get_cstr_index through our libgrok.so: after grk_read_header and
+    after grk_decode, every field (main-header markers, the first SOT,
+    per-tile SOT / header markers / SOD, tile-part start / header end / end)
+    printed by the same driver equals the reference's output
+    (oracle/make_golden_index.py) for every golden codestream."""
+    _need_driver()
+    r = subprocess.run([DRIVER, "index", f"{GOLD}/{name}"], capture_output=True, text=True, timeout=120)
+    got = r.stdout if r.returncode == 0 else "error"
+    assert got == INDEX[name]
+
+
+SUB = json.load(open(f"{GOLD}/manifest_sub.json"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", sorted(SUB))
+def test_grk_api_subsampled_matches_reference(tag, tmp_path):
+    """Subsampled grk_images through grk_compress's library calls (driver -sub:
+    per-component grk_image_cmptparm dx / dy) and grk_decode: the same bytes
+    and the same per-component planes as the reference."""
+    _need_driver()
+    m = SUB[tag]
+    cd = lambda v, s: -(-v // s)  # noqa: E731
+    a = m["args"]
+    off = tuple(int(v) for v in a[a.index("-d") + 1].split(",")) if "-d" in a else (0, 0)
+    w, h = m["size"]
+    planes = [synth.synth_image(cd(off[1] + h, dy) - cd(off[1], dy), cd(off[0] + w, dx) - cd(off[0], dx), 1,
+                                m["bits"], m["seed"] + k, m["kind"])[0] for k, (dx, dy) in enumerate(m["subsampling"])]
+    src, out = tmp_path / "in.i32", tmp_path / "out.j2k"
+    with open(src, "wb") as f:
+        for p in planes:
+            f.write(np.ascontiguousarray(p, dtype="<i4").tobytes())
+    sub = "/".join("%d,%d" % tuple(s) for s in m["subsampling"])
+    r = subprocess.run([DRIVER, "enc", str(src), str(out), str(w), str(h), str(len(planes)), str(m["bits"]), "0"] +
+                       a + ["-sub", sub], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == open(f"{GOLD}/{tag}.j2k", "rb").read()
+    dec = tmp_path / "out.i32"
+    r = subprocess.run([DRIVER, "dec", f"{GOLD}/{tag}.j2k", str(dec)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    z = np.load(f"{GOLD}/{tag}.dec.npz")
+    ref = np.concatenate([z["c%d" % k].ravel() for k in range(len(planes))])
+    assert np.array_equal(np.fromfile(dec, dtype="<i4"), ref)
 
 
 @pytest.mark.gpu

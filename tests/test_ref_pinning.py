@@ -69,6 +69,14 @@ def test_subsampled_fixtures_regenerate():
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
 
 
+def test_index_fixtures_regenerate():
+    """tests/golden/cstr_index.json: the reference's grk_get_cstr_index of
+    every golden (oracle/make_golden_index.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "make_golden_index.py"), "--check"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
 def test_cstr_info_matches_reference():
     """grk_get_cstr_info of our libgrok.so (ref_driver_mi355x: the same driver
     relinked against it; header parsing needs no GPU) prints exactly what the
