@@ -68,7 +68,16 @@ class CParams(ctypes.Structure):
                 ("POC", Poc * 32), ("tp_on", ctypes.c_int32), ("tp_flag", ctypes.c_int32), ("rsiz", ctypes.c_uint32),
                 ("framerate", ctypes.c_uint32), ("max_cs_size", ctypes.c_uint64), ("max_comp_size", ctypes.c_uint64),
                 ("cblk_sty", ctypes.c_uint32), ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
-                ("pad_", ctypes.c_uint32)]
+                ("pad_", ctypes.c_uint32), ("mct_ncomp", ctypes.c_uint32), ("mct_matrix", ctypes.c_float * (MAXC * MAXC)),
+                ("mct_dc_shift", ctypes.c_int32 * MAXC)]
+
+    def set_mct(self, matrix, dc_shift):
+        """grk_set_MCT: a custom array-based MCT (grkgpu_set_mct)."""
+        n = len(dc_shift)
+        m = (ctypes.c_float * (n * n))(*[float(v) for v in np.asarray(matrix, dtype=np.float32).ravel()])
+        s = (ctypes.c_int32 * n)(*[int(v) for v in dc_shift])
+        _check(lib().grkgpu_set_mct(ctypes.byref(self), m, s, n))
+        return self
 
     @classmethod
     def make(cls, numresolution=6, cblk=(64, 64), irreversible=False, mct=-1, tiles=None, tile_offset=(0, 0)):
@@ -113,6 +122,9 @@ class CParams(ctypes.Structure):
                     p.cp_tx0, p.cp_ty0 = (int(x) for x in v.split(","))
                 elif a == "-Y":
                     p.tcp_mct = int(v)
+                elif a == "-mct":  # oracle/ref_driver's grk_set_MCT: m00,m01,...:s0,s1,...
+                    mv, sv = v.split(":")
+                    p.set_mct([float(x) for x in mv.split(",")], [int(x) for x in sv.split(",")])
                 elif a == "-d":
                     off = tuple(int(x) for x in v.split(","))
                 elif a == "-p":
@@ -239,6 +251,7 @@ def lib():
         L.grkgpu_set_dwt_options.argtypes = [P(DwtOptions)]
         L.grkgpu_get_launch_times.argtypes = [VP, P(LaunchTime), U32, P(U32)]
         L.grkgpu_default_cparams.argtypes = [P(CParams)]
+        L.grkgpu_set_mct.argtypes = [P(CParams), VP, VP, U32]
         L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
                                       P(ctypes.c_size_t)]
         L.grkgpu_compress_view.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int,

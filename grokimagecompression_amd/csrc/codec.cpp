@@ -141,6 +141,17 @@ int grkgpu_device_count(void) {
     return n;
 }
 
+int grkgpu_set_mct(grkgpu_cparams *p, const float *matrix, const int32_t *dc_shift, uint32_t n) {
+    if (!p || !matrix || !dc_shift || !n || n > GRKGPU_MAX_COMPS) return set_err(GRKGPU_EINVAL, "custom MCT: 1..16 components");
+    p->rsiz = (p->rsiz & RSIZ_PART2) ? (p->rsiz | RSIZ_EXT_MCT) : (RSIZ_PART2 | RSIZ_EXT_MCT);  // grok.cpp:612-617
+    p->irreversible = 1;
+    p->tcp_mct = 2;
+    p->mct_ncomp = n;
+    memcpy(p->mct_matrix, matrix, sizeof(float) * n * n);
+    memcpy(p->mct_dc_shift, dc_shift, sizeof(int32_t) * n);
+    return GRKGPU_OK;
+}
+
 // grk_set_default_encoder_parameters (grok.cpp) + grk_compress's defaults
 void grkgpu_default_cparams(grkgpu_cparams *p) {
     memset(p, 0, sizeof(*p));
@@ -387,8 +398,10 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     if (p->rsiz == GRKGPU_PROFILE_CINEMA_2K || p->rsiz == GRKGPU_PROFILE_CINEMA_4K) {
         if (cinema_compliant(img, p->rsiz)) set_cinema_parameters(p, img);
         else p->rsiz = 0;  // "Non-profile-3/4 codestream will be generated"
+    } else if (p->rsiz & RSIZ_PART2) {  // j2k.cpp:1720-1731: Part 2 with the MCT extension only
+        if (p->rsiz != (RSIZ_PART2 | RSIZ_EXT_MCT)) p->rsiz = 0;
     } else if (p->rsiz != 0) {
-        return set_err(GRKGPU_EUNSUPPORTED, "only the 2K / 4K digital cinema profiles are supported");
+        return set_err(GRKGPU_EUNSUPPORTED, "only the 2K / 4K digital cinema profiles and Part-2 MCT are supported");
     }
     if (p->numresolution < 1 || p->numresolution > 33) return set_err(GRKGPU_EINVAL, "numresolution must be 1..33");
     auto pow2 = [](uint32_t v) { return v >= 4 && v <= 64 && (v & (v - 1)) == 0; };
@@ -408,11 +421,39 @@ static int setup_params(const grkgpu_image_desc *img, const grkgpu_cparams *pin,
     cp.cblkw = (uint32_t)floorlog2((int32_t)p->cblockw_init);
     cp.cblkh = (uint32_t)floorlog2((int32_t)p->cblockh_init);
     cp.irrev = p->irreversible ? 1 : 0;
-    cp.mct = p->tcp_mct < 0 ? (img->numcomps >= 3 ? 1 : 0) : (p->tcp_mct ? 1 : 0);
-    if (cp.mct && img->numcomps < 3) cp.mct = 0;
+    cp.mct = p->tcp_mct < 0 ? (img->numcomps >= 3 ? 1 : 0) : (p->tcp_mct == 2 ? 2 : p->tcp_mct ? 1 : 0);
+    if (cp.mct == 1 && img->numcomps < 3) cp.mct = 0;
+    if (p->mct_ncomp) {  // grk_set_MCT's mct_data (j2k.cpp:1899-1961)
+        const uint32_t n = img->numcomps;
+        if (p->mct_ncomp != n) return set_err(GRKGPU_EINVAL, "custom MCT matrix size differs from the component count");
+        if (!p->irreversible) return set_err(GRKGPU_EUNSUPPORTED, "a custom MCT needs the 9/7 wavelet (grk_set_MCT sets it)");
+        cp.mct = 2;
+        for (uint32_t i = 0; i < n * n; ++i)  // (int32)(m * 2^13), mct.cpp:452-454
+            cp.mct_coding[i] = (int32_t)(p->mct_matrix[i] * (float)(1 << 13));
+        float m[16 * 16];
+        memcpy(m, p->mct_matrix, sizeof(float) * n * n);
+        if (!mct_invert(m, cp.mct_decoding, n))
+            return set_err(GRKGPU_EINVAL, "Failed to inverse encoder MCT decoding matrix");
+        for (uint32_t i = 0; i < n; ++i) {  // mct::calculate_norms (mct.cpp:409-427): column norms of the inverse
+            double s = 0;
+            for (uint32_t j = 0; j < n; ++j) {
+                const float v = cp.mct_decoding[(size_t)j * n + i];
+                s += (double)(v * v);
+            }
+            cp.mct_norms[i] = sqrt(s);
+        }
+    } else if (cp.mct == 2) {
+        return set_err(GRKGPU_EINVAL, "tcp_mct 2 without a custom matrix (grkgpu_set_mct)");
+    }
     // "Cannot perform MCT on components with different sizes. Disabling MCT." (j2k.cpp:1963-1971)
-    if (cp.mct && (cp.dx[1] != cp.dx[0] || cp.dx[2] != cp.dx[0] || cp.dy[1] != cp.dy[0] || cp.dy[2] != cp.dy[0]))
+    if (cp.mct == 1 && (cp.dx[1] != cp.dx[0] || cp.dx[2] != cp.dx[0] || cp.dy[1] != cp.dy[0] || cp.dy[2] != cp.dy[0]))
         cp.mct = 0;
+    if (cp.mct == 2) {
+        for (uint32_t k = 1; k < img->numcomps; ++k)
+            if (cp.dx[k] != cp.dx[0] || cp.dy[k] != cp.dy[0])
+                return set_err(GRKGPU_EUNSUPPORTED, "a custom MCT over components of different sizes");
+        for (uint32_t k = 0; k < img->numcomps; ++k) cp.shift[k] = p->mct_dc_shift[k];  // j2k.cpp:1952-1955
+    }
     if (p->tile_size_on) {
         if (!p->cp_tdx || !p->cp_tdy) return set_err(GRKGPU_EINVAL, "zero tile size");
         if (p->cp_tx0 > img->x0 || p->cp_ty0 > img->y0 || (uint64_t)p->cp_tx0 + p->cp_tdx <= img->x0 ||
@@ -1083,17 +1124,17 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     // and single components, DC shift in the loads).  Requires every
     // tile-component to be decomposed at least once and to span its tile.
     const int fo = dwt_options().fuse_level0;
-    bool fuse = fo >= 0 ? fo != 0 : (!cp.irrev && cp.mct && nc == 3);
+    bool fuse = fo >= 0 ? fo != 0 : (!cp.irrev && cp.mct == 1 && nc == 3);
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
             fuse = fuse && tc.numres >= 2 && tc.r.w() == tile.r.w() && tc.r.h() == tile.r.h();
         }
-    if (cp.mct && nc != 3) fuse = false;  // MCT over more than 3 components: separate pass
+    if ((cp.mct && nc != 3) || cp.mct == 2) fuse = false;  // MCT over more than 3 components, custom MCT: separate pass
     if (fmt == SMP_I8 || fmt == SMP_I16) fuse = false;  // the fused loads read int32, u16 or u8 samples
     DwtPlan dplan;
     dplan.fused0 = fuse;
-    dplan.mct3 = fuse && cp.mct && nc == 3;
+    dplan.mct3 = fuse && cp.mct == 1 && nc == 3;
     for (auto &tile : tiles)
         for (uint32_t k = 0; k < nc; ++k) {
             const TileComp &tc = tile.comps[k];
@@ -1103,7 +1144,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             if (!fuse || dplan.levels.empty() || dplan.levels[0].size() == before) continue;
             DwtJob &j = dplan.levels[0].back();
             const uint64_t org = plane_org(k, tc);  // fused: no subsampling, every plane alike
-            const bool mct3 = cp.mct && nc >= 3 && k < 3;
+            const bool mct3 = cp.mct == 1 && nc >= 3 && k < 3;
             for (uint32_t i = 0; i < 3; ++i) {
                 const uint32_t pk = mct3 ? i : k;
                 j.src[i] = src_at(pk, org);
@@ -1142,7 +1183,13 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             tsrc.p[k] = src_at(k, plane_org(k, tile.comps[k]));
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
-        HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+        if (cp.mct == 2) {
+            MctMatrix mm{};
+            memcpy(mm.c, cp.mct_coding, sizeof(int32_t) * nc * nc);
+            HIPCHK(launch_dcshift_mct_custom(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, mm, s));
+        } else {
+            HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+        }
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
     c->ltimes.clear();
@@ -1187,8 +1234,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         static const double kRev[3] = {1.732, .8292, .8292}, kIrrev[3] = {1.732, 1.805, 1.573};
         mct_norms = cp.irrev ? kIrrev : kRev;
         mct_numcomps = 3;
-    } else {
+    } else {  // custom MCT: the inverse's column norms (TileProcessor.cpp:1548-1551); else none
         mct_numcomps = nc;
+        if (cp.mct == 2) mct_norms = cp.mct_norms;
     }
     // per-block pass records: validate and lay the blocks' passes out (prefix
     // sum), then fill them on the host pool (blocks are independent)

@@ -287,6 +287,96 @@ void write_main_header(ByteBuf &cs, const CodingParams &cp, size_t *tlm_at, uint
     static const char kCom[] = "Created by Grok     version 5.1.0";  // j2k.cpp:1798
     cs.put16(0xFF64); cs.put16(4 + (uint32_t)strlen(kCom)); cs.put16(1);
     cs.putn((const uint8_t *)kCom, strlen(kCom));
+    if ((cp.rsiz & (RSIZ_PART2 | RSIZ_EXT_MCT)) == (RSIZ_PART2 | RSIZ_EXT_MCT)) write_mct_group(cs, cp);
+}
+
+// The Part-2 array-based MCT marker group (j2k_write_mct_data_group,
+// j2k.cpp:5615-5652, with the records j2k_setup_mct_encoding makes,
+// :2580-2741): CBD (component bit depths), an MCT record holding the
+// decoding matrix (index 1, decorrelation array, float elements), one
+// holding the DC shifts (index 2, offset array, float), an MCC collection
+// (index 3, irreversible, array 1 + offsets 2, components in order) and MCO
+// naming it.  Floats big-endian, as grk_write_float writes them.
+static void put_float(ByteBuf &cs, float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    cs.put32(u);
+}
+void write_mct_group(ByteBuf &cs, const CodingParams &cp) {
+    const uint32_t n = cp.numcomps;
+    cs.put16(0xFF78); cs.put16(4 + n); cs.put16(n);  // CBD (j2k_write_cbd, :6476-6510)
+    for (uint32_t k = 0; k < n; ++k) cs.put8(((uint32_t)cp.sgnd[k] << 7) | (cp.prec[k] - 1));
+    enum { ARRAY_DECORRELATION = 1, ARRAY_OFFSET = 2, ELEM_FLOAT = 2 };
+    auto mct_head = [&](uint32_t index, uint32_t array, uint32_t nbytes) {  // j2k_write_mct_record (:5779-5822)
+        cs.put16(0xFF74); cs.put16(8 + nbytes);
+        cs.put16(0);                                                   // Zmct
+        cs.put16((index & 0xff) | (array << 8) | (ELEM_FLOAT << 10));  // Imct
+        cs.put16(0);                                                   // Ymct
+    };
+    mct_head(1, ARRAY_DECORRELATION, 4 * n * n);
+    for (uint32_t i = 0; i < n * n; ++i) put_float(cs, cp.mct_decoding[i]);
+    mct_head(2, ARRAY_OFFSET, 4 * n);
+    for (uint32_t k = 0; k < n; ++k) put_float(cs, (float)cp.shift[k]);
+    // MCC (j2k_write_mcc_record, :5961-6070): one collection, 1- or 2-byte component indices
+    const uint32_t cb = n > 255 ? 2 : 1, mask = n > 255 ? 0x8000 : 0;
+    cs.put16(0xFF75); cs.put16(17 + 2 * n * cb);
+    cs.put16(0); cs.put8(3); cs.put16(0); cs.put16(1); cs.put8(1);
+    for (int side = 0; side < 2; ++side) {
+        cs.put16(n | mask);
+        for (uint32_t k = 0; k < n; ++k) { if (cb == 2) cs.put16(k); else cs.put8(k); }
+    }
+    const uint32_t tmcc = (0u << 16) | (2u << 8) | 1u;  // irreversible, offsets = record 2, matrix = record 1
+    cs.put8(tmcc >> 16); cs.put8((tmcc >> 8) & 0xff); cs.put8(tmcc & 0xff);
+    cs.put16(0xFF77); cs.put16(3); cs.put8(1); cs.put8(3);  // MCO (j2k_write_mco, :6298-6333)
+}
+
+// matrix_inversion_f (mct/invert.cpp:78-286), restated: an LU decomposition
+// with row pivoting on the largest |value| of each column (in float, a
+// separate multiply and subtract per update), then one forward / back
+// substitution per unit vector.  false for a singular matrix.
+bool mct_invert(const float *src_in, float *dst, uint32_t n) {
+    std::vector<float> a(src_in, src_in + (size_t)n * n);
+    std::vector<uint32_t> perm(n);
+    for (uint32_t i = 0; i < n; ++i) perm[i] = i;
+    for (uint32_t k = 0; k + 1 < n; ++k) {
+        float p = 0.0f;
+        uint32_t k2 = 0;
+        for (uint32_t i = k; i < n; ++i) {
+            const float v = a[(size_t)i * n + k];
+            const float m = v > 0 ? v : -v;
+            if (m > p) { p = m; k2 = i; }
+        }
+        if (p == 0.0f) return false;
+        if (k2 != k) {
+            std::swap(perm[k], perm[k2]);
+            for (uint32_t j = 0; j < n; ++j) std::swap(a[(size_t)k * n + j], a[(size_t)k2 * n + j]);
+        }
+        const float d = a[(size_t)k * n + k];
+        for (uint32_t i = k + 1; i < n; ++i) {
+            const float f = a[(size_t)i * n + k] / d;
+            a[(size_t)i * n + k] = f;
+            for (uint32_t j = k + 1; j < n; ++j) {
+                const float prod = f * a[(size_t)k * n + j];
+                a[(size_t)i * n + j] = a[(size_t)i * n + j] - prod;
+            }
+        }
+    }
+    std::vector<float> y(n), x(n), e(n);
+    for (uint32_t col = 0; col < n; ++col) {
+        for (uint32_t i = 0; i < n; ++i) e[i] = i == col ? 1.0f : 0.0f;
+        for (uint32_t i = 0; i < n; ++i) {  // L y = P e (unit lower triangle)
+            float sum = 0.0f;
+            for (uint32_t j = 0; j < i; ++j) { const float t = a[(size_t)i * n + j] * y[j]; sum = sum + t; }
+            y[i] = e[perm[i]] - sum;
+        }
+        for (int32_t k = (int32_t)n - 1; k >= 0; --k) {  // U x = y
+            float sum = 0.0f;
+            for (uint32_t j = (uint32_t)k + 1; j < n; ++j) { const float t = a[(size_t)k * n + j] * x[j]; sum = sum + t; }
+            x[k] = (y[k] - sum) / a[(size_t)k * n + k];
+        }
+        for (uint32_t i = 0; i < n; ++i) dst[(size_t)i * n + col] = x[i];
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -524,6 +614,7 @@ bool parse_cod(const uint8_t *p, uint32_t size, CodingParams &cp, std::string &e
     if (p[0] & ~7u) { err = "unknown Scod bits"; return false; }
     cp.csty = p[0];
     cp.prog = p[1]; cp.numlayers = rd16(p + 2); cp.mct = p[4];
+    if (cp.mct > 1) { err = "Invalid MCT value: should be either 0 or 1"; return false; }  // j2k.cpp:3869-3872
     if (cp.numlayers == 0) { err = "Invalid number of layers in COD marker"; return false; }
     if (cp.prog > 4) { err = "Unknown progression order in COD marker"; return false; }
     CompParams c;

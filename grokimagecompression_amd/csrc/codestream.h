@@ -34,6 +34,7 @@ struct PocSpec {
 
 constexpr uint32_t CSTY_PRT = 1, CSTY_SOP = 2, CSTY_EPH = 4;  // Scod bits (j2k.h J2K_CP_CSTY_*)
 constexpr uint16_t RSIZ_CINEMA_2K = 3, RSIZ_CINEMA_4K = 4;     // grok.h:160-161
+constexpr uint16_t RSIZ_PART2 = 0x8000, RSIZ_EXT_MCT = 0x0100;  // GRK_PROFILE_PART2, GRK_EXTENSION_MCT
 
 // Coding style and quantisation of one component (the reference's grk_tccp):
 // COD / COC and QCD / QCC of the main header or of a tile's first tile-part
@@ -96,6 +97,12 @@ struct CodingParams {
     // marker, j2k.cpp:1997-2001 / 5482-5604): adds to every band's bit-plane
     // count, and the decoder shifts decoded magnitudes >= 2^roishift down
     uint8_t roishift[16] = {};
+    // custom array-based MCT (mct == 2, Part 2; j2k.cpp:1899-1961): the
+    // encoding matrix in 13-bit fixed point, its float inverse (written to
+    // the codestream) and the inverse's column norms (rate-control weights)
+    int32_t mct_coding[16 * 16] = {};
+    float mct_decoding[16 * 16] = {};
+    double mct_norms[16] = {};
     // per component (decoder: COC / QCC resolved; encoder: sync_comps)
     CompParams comp[16];
     bool coc_set[16] = {}, qcc_set[16] = {};  // main-header COC / QCC seen
@@ -105,6 +112,9 @@ struct CodingParams {
         for (int i = 0; i < 33; ++i) prcw[i] = prch[i] = 15;
     }
 };
+
+// Part-2 MCT: matrix_inversion_f restated (false: singular)
+bool mct_invert(const float *src, float *dst, uint32_t n);
 
 // COD's coding style / QCD's quantisation -> component k (the global fields)
 void comp_style_from_cod(CodingParams &cp, uint32_t k);
@@ -207,6 +217,9 @@ struct ByteBuf {
     }
     size_t size() const { return v.size(); }
 };
+// the Part-2 MCT marker group (CBD, MCT x 2, MCC, MCO) of a custom-MCT encode
+void write_mct_group(ByteBuf &cs, const CodingParams &cp);
+
 
 // The codestream is assembled on the device: the host writes headers into a
 // small blob and a plan of (source, length) runs; a gather kernel copies the

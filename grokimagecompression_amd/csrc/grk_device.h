@@ -62,6 +62,12 @@ hipError_t launch_dcshift_mct_fwd(const SrcPlanes &src, int32_t fmt, uint32_t ss
 // src rows at sstride elements (a window of a tile buffer), dst rows at dstride;
 // irrev: bit k set = component k holds 9/7 (float) samples; MCT follows
 // component 0's wavelet
+// DC shift + custom MCT (Part 2) of one tile: m.c = the n x n encoding matrix in
+// 13-bit fixed point (row-major)
+struct MctMatrix { int32_t c[GRK_MAX_COMPS * GRK_MAX_COMPS]; };
+hipError_t launch_dcshift_mct_custom(const SrcPlanes &src, int32_t fmt, uint32_t sstride, const PlanePtrs &dst,
+                                     uint32_t tw, uint32_t th, uint32_t ncomp, const ShiftArr &shift,
+                                     const MctMatrix &m, hipStream_t s);
 hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32_t tw, uint32_t th,
                                   const PlanePtrs &dst, uint32_t dstride, uint32_t ncomp, const ShiftArr &shift,
                                   const ShiftArr &mn, const ShiftArr &mx, int32_t mct, int32_t irrev, hipStream_t s);

@@ -241,14 +241,20 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     grkgpu_default_cparams(p);
     if (g->cblk_sty & ~0x3Fu) { GRK_ERROR("code-block style 0x%x: HT is not supported", g->cblk_sty); return false; }
     if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
-    if (g->tcp_mct == 2 || g->mct_data) { GRK_ERROR("custom MCT is not supported"); return false; }
+    if (g->mct_data) {  // grk_set_MCT: numcomps x numcomps matrix, then numcomps DC shifts (j2k.cpp:1899-1956)
+        if (numcomps > GRKGPU_MAX_COMPS) return false;
+        p->mct_ncomp = numcomps;
+        memcpy(p->mct_matrix, g->mct_data, sizeof(float) * numcomps * numcomps);
+        memcpy(p->mct_dc_shift, (const uint8_t *)g->mct_data + sizeof(float) * numcomps * numcomps,
+               sizeof(int32_t) * numcomps);
+    }
     // subsampling_dx / _dy are the CLI image readers' (PNMFormat.cpp:397-417);
     // the library takes each component's dx / dy from the image
     p->numresolution = g->numresolution;
     p->cblockw_init = g->cblockw_init;
     p->cblockh_init = g->cblockh_init;
     p->irreversible = g->irreversible ? 1 : 0;
-    p->tcp_mct = g->tcp_mct == 255 ? -1 : (g->tcp_mct && numcomps >= 3 ? 1 : 0);
+    p->tcp_mct = g->tcp_mct == 255 ? -1 : g->tcp_mct == 2 ? 2 : (g->tcp_mct && numcomps >= 3 ? 1 : 0);
     p->tile_size_on = g->tile_size_on ? 1 : 0;
     p->cp_tdx = g->cp_tdx;
     p->cp_tdy = g->cp_tdy;
@@ -1010,9 +1016,21 @@ GRK_EXPORT bool grk_write_tile(grk_codec *codec, uint16_t tile_index, uint8_t *d
     return true;
 }
 
-GRK_EXPORT bool grk_set_MCT(grk_cparameters *, float *, int32_t *, uint32_t) {
-    GRK_ERROR("custom MCT is not supported");
-    return false;
+// grk_set_MCT (grok.cpp:606-630): Part-2 MCT extension in rsiz, 9/7,
+// tcp_mct = 2, mct_data = the n x n encoding matrix followed by n DC shifts
+// (owned by the parameters, as there)
+GRK_EXPORT bool grk_set_MCT(grk_cparameters *parameters, float *matrix, int32_t *dc_shift, uint32_t n) {
+    if (!parameters || !matrix || !dc_shift) return false;
+    const size_t msize = (size_t)n * n * sizeof(float), ssize = (size_t)n * sizeof(int32_t);
+    if ((parameters->rsiz & 0x8000) != 0) parameters->rsiz |= 0x0100;
+    else parameters->rsiz = 0x8000 | 0x0100;
+    parameters->irreversible = true;
+    parameters->tcp_mct = 2;
+    parameters->mct_data = malloc(msize + ssize);
+    if (!parameters->mct_data) return false;
+    memcpy(parameters->mct_data, matrix, msize);
+    memcpy((uint8_t *)parameters->mct_data + msize, dc_shift, ssize);
+    return true;
 }
 
 // ---------------------------------------------------------------------------

@@ -68,6 +68,28 @@ __global__ void k_dcshift_mct_fwd(SrcPlanes src, uint32_t sstride, PlanePtrs dst
     }
 }
 
+// DC shift + custom array-based MCT (Part 2): TileProcessor.cpp:1449-1471
+// then mct::encode_custom (mct.cpp:429-475) -- (x - shift) << 11, then per
+// output component j the int32 sum over k of int_fix_mul(C[j][k], x_k), C the
+// encoding matrix in 13-bit fixed point, in the reference's order.
+template <typename S>
+__global__ void k_dcshift_mct_custom(SrcPlanes src, uint32_t sstride, PlanePtrs dst, uint32_t tw, uint32_t th,
+                                     uint32_t ncomp, ShiftArr shift, MctMatrix m) {
+    uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t y = blockIdx.y;
+    if (x >= tw || y >= th) return;
+    size_t si = (size_t)y * sstride + x, di = (size_t)y * tw + x;
+    int32_t v[GRK_MAX_COMPS];
+    for (uint32_t c = 0; c < ncomp; ++c)
+        v[c] = (int32_t)((uint32_t)((int32_t)((const S *)src.p[c])[si] - shift.v[c]) << 11);
+    for (uint32_t j = 0; j < ncomp; ++j) {
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < ncomp; ++k)
+            acc += (uint32_t)(int32_t)(((int64_t)m.c[j * ncomp + k] * (int64_t)v[k] + 4096) >> 13);
+        put<true>(&dst.p[j][di], (int32_t)acc);
+    }
+}
+
 // Inverse MCT + DC shift + clamp, tile buffers -> image planes.
 __global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t sstride, uint32_t tw, uint32_t th, PlanePtrs dst,
                                   uint32_t dstride, uint32_t ncomp, ShiftArr shift, ShiftArr minv, ShiftArr maxv,
@@ -571,6 +593,25 @@ hipError_t launch_dcshift_mct_fwd(const SrcPlanes &src, int32_t fmt, uint32_t ss
         default: return hipErrorInvalidValue;
     }
 #undef GRK_DCS
+    return hipGetLastError();
+}
+
+hipError_t launch_dcshift_mct_custom(const SrcPlanes &src, int32_t fmt, uint32_t sstride, const PlanePtrs &dst,
+                                     uint32_t tw, uint32_t th, uint32_t ncomp, const ShiftArr &shift,
+                                     const MctMatrix &m, hipStream_t s) {
+    if (ncomp > GRK_MAX_COMPS) return hipErrorInvalidValue;
+    dim3 grid((tw + 255) / 256, th);
+#define GRK_DCC(S) hipLaunchKernelGGL((k_dcshift_mct_custom<S>), grid, dim3(256), 0, s, src, sstride, dst, tw, th, ncomp, \
+                                      shift, m)
+    switch (fmt) {
+        case SMP_I32: GRK_DCC(int32_t); break;
+        case SMP_U8: GRK_DCC(uint8_t); break;
+        case SMP_I8: GRK_DCC(int8_t); break;
+        case SMP_U16: GRK_DCC(uint16_t); break;
+        case SMP_I16: GRK_DCC(int16_t); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef GRK_DCC
     return hipGetLastError();
 }
 

@@ -97,7 +97,8 @@ typedef struct {
     uint32_t numresolution;                /* default 6 */
     uint32_t cblockw_init, cblockh_init;   /* default 64, 64 (powers of 2, <= 64) */
     int32_t irreversible;                  /* 0: 5/3, 1: 9/7 (-I) */
-    int32_t tcp_mct;                       /* -1: auto (RGB->YCC iff >= 3 comps), 0, 1 */
+    int32_t tcp_mct;                       /* -1: auto (RGB->YCC iff >= 3 comps), 0, 1; 2: the custom
+                                              matrix below (grkgpu_set_mct) */
     int32_t tile_size_on;
     uint32_t cp_tdx, cp_tdy, cp_tx0, cp_ty0;
     /* quality layers and rate control (grk_compress -r / -q / -A) */
@@ -126,6 +127,12 @@ typedef struct {
     int32_t roi_compno;
     uint32_t roi_shift;
     uint32_t pad_;
+    /* custom (Part 2 array-based) MCT, grk_set_MCT's mct_data: mct_ncomp x
+     * mct_ncomp encoding matrix (row-major) and per-component DC shifts;
+     * mct_ncomp 0 = none */
+    uint32_t mct_ncomp;
+    float mct_matrix[GRKGPU_MAX_COMPS * GRKGPU_MAX_COMPS];
+    int32_t mct_dc_shift[GRKGPU_MAX_COMPS];
 } grkgpu_cparams;
 
 typedef struct grkgpu_ctx grkgpu_ctx;
@@ -210,6 +217,13 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */
 int grkgpu_get_launch_times(grkgpu_ctx *ctx, grkgpu_launch_time *out, uint32_t max, uint32_t *n);
 void grkgpu_default_cparams(grkgpu_cparams *p);
+/* grk_set_MCT (grok.cpp:606-630): a custom array-based MCT -- rsiz gains the
+ * Part-2 MCT extension (0x8000 | 0x0100), 9/7, tcp_mct = 2, the n x n
+ * encoding matrix (row-major, applied in 13-bit fixed point,
+ * mct.cpp:429-475) and the per-component DC shifts.  The codestream then
+ * carries its inverse (float, j2k.cpp:1932) in CBD / MCT / MCC / MCO marker
+ * segments (j2k.cpp:5615-6333). */
+int grkgpu_set_mct(grkgpu_cparams *p, const float *matrix, const int32_t *dc_shift, uint32_t n);
 
 /* Whole-codestream encode.  planes[c] = (y1-y0)*(x1-x0) int32 samples, on
  * the device when planes_on_device != 0, else host memory.  The .j2k

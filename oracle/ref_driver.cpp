@@ -117,6 +117,10 @@ static GRK_PROG_ORDER prog(const char *s) {
 // driver builds (grk_image_cmptparm dx / dy; the CLI's -s sets one factor for
 // all components, grk_compress.cpp:1060, PNMFormat.cpp:397-417)
 static std::vector<std::pair<uint32_t, uint32_t>> g_sub;
+// -mct m00,m01,...:s0,s1,...: a custom MCT through grk_set_MCT (grok.cpp:606),
+// row-major n x n encoding matrix and n DC shifts
+static std::vector<float> g_mct;
+static std::vector<int32_t> g_mct_shift;
 
 // grk_compress option subset -> parameters (citations in the header)
 static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
@@ -138,6 +142,21 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
         else if (a == "-T") { if (sscanf(v, "%u,%u", &p->cp_tx0, &p->cp_ty0) != 2) return false; }
         else if (a == "-Y") p->tcp_mct = (uint8_t)atoi(v);
         else if (a == "-p") p->prog_order = prog(v);
+        else if (a == "-mct") {
+            g_mct.clear();
+            g_mct_shift.clear();
+            const char *s = v;
+            while (*s && *s != ':') {
+                g_mct.push_back(strtof(s, (char **)&s));
+                if (*s == ',') s++;
+            }
+            if (*s == ':') s++;
+            while (*s) {
+                g_mct_shift.push_back((int32_t)strtol(s, (char **)&s, 10));
+                if (*s == ',') s++;
+                else break;
+            }
+        }
         else if (a == "-sub") {
             g_sub.clear();
             const char *s = v;
@@ -217,6 +236,11 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
         p->tcp_rates[0] = 0;
         p->tcp_numlayers = 1;
         p->cp_disto_alloc = 1;
+    }
+    if (!g_mct.empty()) {
+        const uint32_t n = (uint32_t)g_mct_shift.size();
+        if (n * n != g_mct.size()) { fprintf(stderr, "-mct: n*n matrix entries and n shifts\n"); return false; }
+        if (!grk_set_MCT(p, g_mct.data(), g_mct_shift.data(), n)) return false;
     }
     return true;
 }

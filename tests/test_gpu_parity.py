@@ -87,6 +87,30 @@ def test_decode_marker_fixtures_match_reference(codec, tag):
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
 
+MCT = json.load(open(f"{GOLD}/manifest_mct.json"))
+
+
+@pytest.mark.parametrize("tag", sorted(MCT))
+def test_custom_mct_encode_matches_reference(codec, tag):
+    """Custom array-based MCT (grk_set_MCT; oracle/make_golden_mct.py): the
+    13-bit fixed-point encoding matrix applied on the GPU after the DC shift
+    (mct.cpp:429-475), the float inverse (matrix_inversion_f restated) in the
+    CBD / MCT / MCC / MCO segments, Part-2 rsiz, rate control weighted by the
+    inverse's column norms -- byte-identical to the reference.  Decoding is
+    refused as the reference refuses it (COD MCT byte 2, j2k.cpp:3869)."""
+    import grokimagecompression_amd as grk
+    m = MCT[tag]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    b = codec.compress(img, bits, p, offset=off)
+    gold = open(f"{GOLD}/{tag}.j2k", "rb").read()
+    assert len(b) == len(gold)
+    assert b == gold
+    assert m["dec"] == "error"
+    with pytest.raises(grk.GrkGpuError):
+        codec.decompress(gold)
+
+
 SUB = json.load(open(f"{GOLD}/manifest_sub.json"))
 
 
