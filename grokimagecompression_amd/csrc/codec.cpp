@@ -981,8 +981,11 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     const uint32_t pw = ncols;                    // row stride of the caller's planes (samples)
     const uint64_t plane = (uint64_t)pw * nrows;  // samples per plane held by the caller
     // subsampled components (SIZ XRsiz / YRsiz): each plane on its own grid
-    bool subs = false;
-    for (uint32_t k = 0; k < nc; ++k) subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+    bool subs = false, mixed = false;  // mixed: components on different grids
+    for (uint32_t k = 0; k < nc; ++k) {
+        subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+        mixed = mixed || cp.dx[k] != cp.dx[0] || cp.dy[k] != cp.dy[0];
+    }
     if (subs && (row0 || col0 || nrows != ih || ncols != iw))
         return set_err(GRKGPU_EUNSUPPORTED, "row / column shards of subsampled images are not supported");
     // the rectangle each caller plane covers (component grid), its stride,
@@ -1163,7 +1166,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(dwt_upload(dplan, c->dwtjobs, c->h_dwtjobs, cp.irrev, s));
     for (auto &tile : tiles) {
         if (fuse) break;
-        if (subs) {  // one launch per tile-component, each on its own grid (no MCT, j2k.cpp:1963-1971)
+        if (mixed) {  // one launch per tile-component, each on its own grid (no MCT, j2k.cpp:1963-1971)
             for (uint32_t k = 0; k < nc; ++k) {
                 const TileComp &tc = tile.comps[k];
                 SrcPlanes tsrc{};
@@ -1177,18 +1180,22 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             }
             continue;
         }
+        // every component on one grid (no subsampling, or the same dx / dy
+        // for all): one launch over the tile, MCT included
         SrcPlanes tsrc{};
         PlanePtrs tdst{};
         for (uint32_t k = 0; k < nc; ++k) {
             tsrc.p[k] = src_at(k, plane_org(k, tile.comps[k]));
             tdst.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off;
         }
+        const Rect &tcr = tile.comps[0].r;
+        const uint32_t spw = prect[0].w();
         if (cp.mct == 2) {
             MctMatrix mm{};
             memcpy(mm.c, cp.mct_coding, sizeof(int32_t) * nc * nc);
-            HIPCHK(launch_dcshift_mct_custom(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, mm, s));
+            HIPCHK(launch_dcshift_mct_custom(tsrc, fmt, spw, tdst, tcr.w(), tcr.h(), nc, sh, mm, s));
         } else {
-            HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, pw, tdst, tile.r.w(), tile.r.h(), nc, sh, cp.mct, cp.irrev, s));
+            HIPCHK(launch_dcshift_mct_fwd(tsrc, fmt, spw, tdst, tcr.w(), tcr.h(), nc, sh, cp.mct, cp.irrev, s));
         }
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
@@ -1856,8 +1863,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     // subsampled components: component k's output plane is the output
     // rectangle on its grid (ceil(x / dx), the nested ceilings of a reduced
     // decode commute), rows of its own width
-    bool subs = false;
-    for (uint32_t k = 0; k < nc; ++k) subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+    bool subs = false, mixed = false;  // mixed: components on different grids
+    for (uint32_t k = 0; k < nc; ++k) {
+        subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
+        mixed = mixed || cp.dx[k] != cp.dx[0] || cp.dy[k] != cp.dy[0];
+    }
     if (subs && !whole) return set_err(GRKGPU_EUNSUPPORTED, "tile-range decode of subsampled images is not supported");
     Rect orect[GRKGPU_MAX_COMPS];
     uint64_t ooff[GRKGPU_MAX_COMPS + 1];
@@ -2225,7 +2235,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     }
     for (auto &tile : tiles) {
         if (tile.comps.empty()) continue;  // outside the window
-        if (subs) {  // each tile-component on its own grid, no MCT
+        if (mixed) {  // each tile-component on its own grid, no MCT
             for (uint32_t k = 0; k < nc; ++k) {
                 const TileComp &tc = tile.comps[k];
                 const Rect tr = tc.res[tc.numres - 1 - reduce].r;
@@ -2243,18 +2253,21 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             }
             continue;
         }
+        // every component on one grid: one launch, MCT included (orect[k]
+        // is the output on that grid -- the image itself without subsampling)
         PlanePtrs tsrc{}, tdst{};
         const Rect tr = tile.comps[0].res[tile.comps[0].numres - 1 - reduce].r;  // the tile at the decoded resolution
-        const Rect out = win ? intersect(tr, wr) : tr;        // its part of the output
+        const Rect out = intersect(tr, orect[0]);             // its part of the output
         if (out.empty()) continue;
+        const uint32_t ow = orect[0].w();
         for (uint32_t k = 0; k < nc; ++k) {
             tsrc.p[k] = c->work.as<int32_t>() + tile.comps[k].arena_off + (uint64_t)(out.y0 - tr.y0) * tr.w() +
                         (out.x0 - tr.x0);
-            tdst.p[k] = dst.p[k] + (uint64_t)(out.y0 - iy0) * iw + (out.x0 - ix0);
+            tdst.p[k] = dst.p[k] + (uint64_t)(out.y0 - orect[0].y0) * ow + (out.x0 - orect[0].x0);
         }
         int32_t wmask = 0;  // components holding 9/7 (float) samples
         for (uint32_t k = 0; k < nc; ++k) wmask |= tile.comps[k].irrev << k;
-        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, iw, nc, sh, mn, mx,
+        HIPCHK(launch_mct_inv_dcshift(tsrc, tr.w(), out.w(), out.h(), tdst, ow, nc, sh, mn, mx,
                                       tmct[tile.index - tb], wmask, s));
     }
     HIPCHK(hipEventRecord(c->ev[4], s));

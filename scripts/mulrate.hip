@@ -25,6 +25,34 @@ __device__ __forceinline__ int32_t fmdot(int32_t a, int32_t b) {
     return (int32_t)(((uint32_t)Y << 3) + (X >> 13));
 }
 
+// the lift held in doubles: s c / 2^13 + 1/2 is exact (|s| < 2^31, c < 2^15),
+// so floor() of it is fixmul13; values stay integers in f64 registers
+__device__ __forceinline__ double lift_f64(double t, double s, double c13) {
+    return t - __builtin_floor(__builtin_fma(s, c13, 0.5));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void kd(int32_t *out, int32_t seed, int iters) {
+    constexpr double c13 = 12994.0 / 8192.0;
+    double x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (double)(seed + threadIdx.x * 8 + i);
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if constexpr (MODE == 4) x[i] = lift_f64(x[i], x[i] + 77.0, c13);
+            else {  // int32 storage, converted around the f64 multiply
+                const int32_t xi = (int32_t)x[i];
+                x[i] = (double)(xi - (int32_t)__builtin_floor(__builtin_fma((double)(xi + 77), c13, 0.5)));
+            }
+        }
+    }
+    int32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += (int32_t)x[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k(int32_t *out, int32_t seed, int iters) {
     constexpr int32_t c = 12994;  // a lifting constant (compile-time, as in dwt.hip)
@@ -53,14 +81,16 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *names[4] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain", "dot2 fixmul13"};
-    for (int mode = 0; mode < 4; ++mode) {
+    const char *names[5] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain", "dot2 fixmul13",
+                            "f64 lift (fma + floor)"};
+    for (int mode = 0; mode < 5; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             hipEventRecord(e0, 0);
             if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
-            else hipLaunchKernelGGL(k<3>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else hipLaunchKernelGGL(kd<4>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             hipEventRecord(e1, 0);
             hipEventSynchronize(e1);
             float ms = 0;
