@@ -216,7 +216,7 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->pair_group = g_dwt_opts.pair_group;
     out->inv01_min_samples = g_dwt_opts.inv01_min_samples;
     out->f64_lift = g_dwt_opts.f64_lift;
-    out->pad_ = 0;
+    out->t1_dec_sort = g_dwt_opts.t1_dec_sort;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -231,6 +231,8 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->pair_group < 0 || o->pair_group > 4096) return set_err(GRKGPU_EINVAL, "pair_group must be 0 .. 4096");
     if (o->f64_lift != 0 && o->f64_lift != 1) return set_err(GRKGPU_EINVAL, "f64_lift must be 0 or 1");
     g_dwt_opts.f64_lift = o->f64_lift;
+    if (o->t1_dec_sort != 0 && o->t1_dec_sort != 1) return set_err(GRKGPU_EINVAL, "t1_dec_sort must be 0 or 1");
+    g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
     g_dwt_opts.inv01 = o->inv01;
     g_dwt_opts.pair_group = o->pair_group;
     g_dwt_opts.inv01_min_samples = o->inv01_min_samples;
@@ -2156,6 +2158,33 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (too_deep) return set_err(GRKGPU_ECORRUPT, "unsupported bpno_plus_one >= 31 (code-block bit-planes + ROI shift)");
     const uint32_t nblk = (uint32_t)db.size();
     seg_first.push_back((uint32_t)dsegs.size());
+    if (dwt_options().t1_dec_sort && nblk > 64) {
+        // lanes of a wavefront run until its slowest block is done: hand them
+        // blocks of similar work (pass count, then coded bytes), heaviest first
+        std::vector<uint32_t> ord(nblk);
+        for (uint32_t i = 0; i < nblk; ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+            const DecBlock &x = db[a], &y = db[b];
+            return x.numpasses != y.numpasses ? x.numpasses > y.numpasses : x.len > y.len;
+        });
+        std::vector<DecBlock> db2(nblk);
+        std::vector<DecSeg> segs2;
+        segs2.reserve(dsegs.size());
+        std::vector<uint32_t> first2(nblk + 1);
+        std::vector<uint8_t> roi2(droi.size());
+        for (uint32_t j = 0; j < nblk; ++j) {
+            const uint32_t i = ord[j];
+            db2[j] = db[i];
+            first2[j] = (uint32_t)segs2.size();
+            segs2.insert(segs2.end(), dsegs.begin() + seg_first[i], dsegs.begin() + seg_first[i + 1]);
+            if (!droi.empty()) roi2[j] = droi[i];
+        }
+        first2[nblk] = (uint32_t)segs2.size();
+        db.swap(db2);
+        dsegs.swap(segs2);
+        seg_first.swap(first2);
+        droi.swap(roi2);
+    }
     double t_t2 = now_ms();
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));

@@ -201,7 +201,11 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *   f64_lift         forward 9/7 lifting arithmetic (fused pair and per-level
  *                    kernel, not the fused DC-shift loads): 0 the
  *                    64-bit integer multiply (v_mad_i64_i32), 1 f64 FMA +
- *                    floor (bit-identical results). */
+ *                    floor (bit-identical results).
+ *   t1_dec_sort      T1 decode: 1 = code-blocks handed to the lanes in
+ *                    decreasing order of expected work (passes, bytes), so a
+ *                    wavefront's 64 lanes finish close together; 0 = stream
+ *                    order.  Same output either way. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -211,7 +215,7 @@ typedef struct {
     int32_t pair_group;
     uint64_t inv01_min_samples;
     int32_t f64_lift;
-    int32_t pad_;
+    int32_t t1_dec_sort;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */
