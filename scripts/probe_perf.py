@@ -10,7 +10,13 @@ import torch
 import grokimagecompression_amd as grk
 import synth
 
-configs = [a for a in sys.argv[1:]] or ["4k", "8k"]
+# arguments: configs ("512", "4k", "8k", "16k") and plan options key=value
+# (grkgpu_dwt_options fields, e.g. t1_dec_sort=1 f64_lift=1) for the whole run
+opts = dict(a.split("=") for a in sys.argv[1:] if "=" in a)
+configs = [a for a in sys.argv[1:] if "=" not in a] or ["4k", "8k"]
+if opts:
+    grk.dwt_options(**{k: int(v) for k, v in opts.items()}).__enter__()
+    print("options", opts, flush=True)
 codec = grk.Codec(0)
 dcodec = grk.Codec(0)  # decode context: reads the encoder's pinned output in place
 for cfg in configs:
