@@ -217,6 +217,8 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->inv01_min_samples = g_dwt_opts.inv01_min_samples;
     out->f64_lift = g_dwt_opts.f64_lift;
     out->t1_dec_sort = g_dwt_opts.t1_dec_sort;
+    out->t1_dec_bpw = g_dwt_opts.t1_dec_bpw;
+    out->pad_ = 0;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -233,6 +235,9 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     g_dwt_opts.f64_lift = o->f64_lift;
     if (o->t1_dec_sort != 0 && o->t1_dec_sort != 1) return set_err(GRKGPU_EINVAL, "t1_dec_sort must be 0 or 1");
     g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
+    if (o->t1_dec_bpw < 0 || o->t1_dec_bpw > 64 || (o->t1_dec_bpw & (o->t1_dec_bpw - 1)))
+        return set_err(GRKGPU_EINVAL, "t1_dec_bpw must be 0 or a power of two <= 64");
+    g_dwt_opts.t1_dec_bpw = o->t1_dec_bpw;
     g_dwt_opts.inv01 = o->inv01;
     g_dwt_opts.pair_group = o->pair_group;
     g_dwt_opts.inv01_min_samples = o->inv01_min_samples;

@@ -113,6 +113,7 @@ struct DwtOptions {
     int32_t pair_group = 0;  // fused level pairs: workgroups walk groups of this many columns top-down (0: row-major)
     int32_t f64_lift = 0;    // forward 9/7 fused pair: lifting in f64 FMA + floor instead of v_mad_i64_i32
     int32_t t1_dec_sort = 0; // T1 decode: blocks in decreasing order of expected work
+    int32_t t1_dec_bpw = 0;  // T1 decode: blocks per wavefront (0: by block count)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose

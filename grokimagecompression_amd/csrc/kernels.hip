@@ -698,7 +698,7 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
                        seg_first);
-    const uint32_t bpw = t1_blocks_per_wave(n);
+    const uint32_t bpw = dwt_options().t1_dec_bpw ? (uint32_t)dwt_options().t1_dec_bpw : t1_blocks_per_wave(n);
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
                            n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi, bpw);

@@ -205,7 +205,9 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *   t1_dec_sort      T1 decode: 1 = code-blocks handed to the lanes in
  *                    decreasing order of expected work (passes, bytes), so a
  *                    wavefront's 64 lanes finish close together; 0 = stream
- *                    order.  Same output either way. */
+ *                    order.  Same output either way.
+ *   t1_dec_bpw       T1 decode: code-blocks per wavefront (1, 2, 4 .. 64);
+ *                    0 (default) = by block count (64 from 4096 blocks). */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -216,6 +218,8 @@ typedef struct {
     uint64_t inv01_min_samples;
     int32_t f64_lift;
     int32_t t1_dec_sort;
+    int32_t t1_dec_bpw;
+    int32_t pad_;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */

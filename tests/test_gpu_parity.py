@@ -60,6 +60,9 @@ def test_decode_sorted_blocks_match_reference(codec, name):
     with grk.dwt_options(t1_dec_sort=1):
         d = codec.decompress(gold)
     assert np.array_equal(d, ref)
+    with grk.dwt_options(t1_dec_sort=1, t1_dec_bpw=16):  # 16 blocks per wavefront
+        d = codec.decompress(gold)
+    assert np.array_equal(d, ref)
 
 
 GBITS = sorted(json.load(open(f"{GOLD}/manifest_gbits.json")))
