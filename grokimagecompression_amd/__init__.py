@@ -580,20 +580,15 @@ class Codec:
         in every coordinate.  window = (x0, y0, x1, y1) in image coordinates:
         only that region (grk_set_decode_area), clipped to the image.
         layers > 0: only the first `layers` quality layers (grk_decompress -l)."""
-        if reduce and window is not None:
-            # the window ABI has no reduce parameter (grkgpu_decompress_window
-            # decodes at full resolution); refuse rather than mix coordinate
-            # systems (codec.cpp decompress_impl rejects the same combination)
-            raise GrkGpuError("window decode at a reduced resolution is not supported")
         d = read_header(buf)
-        if reduce:
-            cd = lambda v: -(-v >> reduce)  # noqa: E731
-            d.x0, d.y0, d.x1, d.y1 = cd(d.x0), cd(d.y0), cd(d.x1), cd(d.y1)
-        if window is not None:
+        if window is not None:  # the window (reference grid) clipped to the image
             wx0, wy0, wx1, wy1 = window
             d.x0, d.y0, d.x1, d.y1 = max(d.x0, wx0), max(d.y0, wy0), min(d.x1, wx1), min(d.y1, wy1)
             if d.x1 <= d.x0 or d.y1 <= d.y0:
                 raise GrkGpuError("decode window outside the image")
+        if reduce:  # then at the decoded resolution, ceil(x / 2^reduce) (j2k_set_decode_area)
+            cd = lambda v: -(-v >> reduce)  # noqa: E731
+            d.x0, d.y0, d.x1, d.y1 = cd(d.x0), cd(d.y0), cd(d.x1), cd(d.y1)
         c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
         if any(d.dx[k] != 1 or d.dy[k] != 1 for k in range(c)):
             # subsampled components: a list of host planes, each on its grid

@@ -919,12 +919,14 @@ static void for_each_cblk(TileComp &tc, F f, uint32_t maxres = 0xffffffffu, cons
 // its support only).
 // resneed (optional): per resolution the region of its samples the window
 // needs (the inverse DWT levels run only over these).
-static BandNeed window_need(const TileComp &tc, const Rect &win, std::vector<Rect> *resneed = nullptr) {
+static BandNeed window_need(const TileComp &tc, const Rect &win, std::vector<Rect> *resneed = nullptr,
+                            uint32_t reduce = 0) {
     constexpr uint32_t M = 4;
     BandNeed need(tc.numres);
-    Rect n = intersect(win, tc.res[tc.numres - 1].r);
+    // win: on the component's grid at resolution numres - 1 - reduce
+    Rect n = intersect(win, tc.res[tc.numres - 1 - reduce].r);
     if (resneed) resneed->assign(tc.numres, Rect{});
-    for (int32_t r = (int32_t)tc.numres - 1; r >= 0; --r) {
+    for (int32_t r = (int32_t)tc.numres - 1 - (int32_t)reduce; r >= 0; --r) {
         const Resolution &res = tc.res[r];
         if (resneed) (*resneed)[r] = n;
         if (r == 0) {
@@ -1848,13 +1850,15 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         return set_err(GRKGPU_EINVAL, "reduce must be smaller than the number of resolutions");
     Rect wr{};  // window, clipped to the image
     if (win) {
-        if (reduce) return set_err(GRKGPU_EINVAL, "window decode at a reduced resolution is not supported");
         wr = intersect(*win, cp.image);
         if (wr.empty()) return set_err(GRKGPU_EINVAL, "decode window outside the image");
     }
-    // output image geometry (reduced when reduce > 0, the window when win)
-    const uint32_t ix0 = win ? wr.x0 : ceil_pow2(cp.image.x0, reduce), iy0 = win ? wr.y0 : ceil_pow2(cp.image.y0, reduce);
-    const uint32_t ix1 = win ? wr.x1 : ceil_pow2(cp.image.x1, reduce), iy1 = win ? wr.y1 : ceil_pow2(cp.image.y1, reduce);
+    // output image geometry: the image or the window (reference grid), at the
+    // decoded resolution ceil(x / 2^reduce) (j2k_set_decode_area, j2k.cpp:1464-1476)
+    const Rect full = win ? wr : cp.image;
+    const uint32_t ix0 = ceil_pow2(full.x0, reduce), iy0 = ceil_pow2(full.y0, reduce);
+    const uint32_t ix1 = ceil_pow2(full.x1, reduce), iy1 = ceil_pow2(full.y1, reduce);
+    if (win && (ix1 <= ix0 || iy1 <= iy0)) return set_err(GRKGPU_EINVAL, "decode window empty at this resolution");
     if (img && (reduce || win)) {
         img->x0 = ix0; img->y0 = iy0;
         img->x1 = ix1; img->y1 = iy1;
@@ -1884,8 +1888,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         ooff[k + 1] = ooff[k] + (uint64_t)orect[k].w() * orect[k].h();
     }
     // the window on each component's grid
+    // the window on each component's grid at the decoded resolution
     Rect cwin[GRKGPU_MAX_COMPS];
-    for (uint32_t k = 0; k < nc; ++k) cwin[k] = comp_rect(wr, cp.dx[k], cp.dy[k]);
+    for (uint32_t k = 0; k < nc; ++k) cwin[k] = comp_rect({ix0, iy0, ix1, iy1}, cp.dx[k], cp.dy[k]);
 
     // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
     // and the coding-parameter markers of their headers (COD / COC / QCD /
@@ -1973,7 +1978,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             tile.index = t;
             tile.r = tile_rect(cp, t);
             for (uint32_t k = 0; k < 16; ++k) troi[lt][k] = cp.roishift[k];
-            if (win && !overlap(tile.r, wr)) continue;  // left without components: skipped below
+            if (win && !overlap(comp_rect(tile.r, 1u << reduce, 1u << reduce), {ix0, iy0, ix1, iy1}))
+                continue;  // left without components: skipped below
             // the tile's coding parameters: the main header's, then its
             // tile-part headers' markers (precedence tile COC > tile COD >
             // main COC > main COD; QCC / QCD alike); POC entries appended
@@ -2109,7 +2115,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         const std::vector<uint8_t> &tilebuf = tbufs[lt];
         for (uint32_t k = 0; k < nc; ++k) {
             TileComp &tc = tile.comps[k];
-            const BandNeed need = win ? window_need(tc, cwin[k]) : BandNeed();
+            const BandNeed need = win ? window_need(tc, cwin[k], nullptr, reduce) : BandNeed();
             for_each_cblk(tc, [&](Band &band, Cblk &cb) {
                 DecBlock d{};
                 d.dst_off = tc.arena_off + (uint64_t)cb.by * tc.r.w() + cb.bx;
@@ -2232,7 +2238,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             // a window decode reconstructs, per level, only the windows over
             // the region the window's samples depend on
             std::vector<Rect> rn;
-            if (win) window_need(tc, cwin[k], &rn);
+            if (win) window_need(tc, cwin[k], &rn, reduce);
             dwt_plan_tc(dplan[tc.irrev], tc, c->work.as<int32_t>() + tc.arena_off, c->coef.as<int32_t>() + tc.arena_off,
                         c->ll.as<int32_t>() + lloff[(tile.index - tb) * nc + k], tc.irrev, true, tc.numres - reduce,
                         win ? &rn : nullptr);

@@ -628,15 +628,19 @@ GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t
         GRK_ERROR("decode area (%u,%u,%u,%u) outside the image", x0, y0, x1, y1);
         return false;
     }
-    if (c->dparams.cp_reduce) {
-        GRK_ERROR("a decode area at a reduced resolution is not supported");
-        return false;
-    }
     c->window = true;
     c->win[0] = std::max(x0, d.x0); c->win[1] = std::max(y0, d.y0);
     c->win[2] = std::min(x1, d.x1); c->win[3] = std::min(y1, d.y1);
     image->x0 = c->win[0]; image->y0 = c->win[1]; image->x1 = c->win[2]; image->y1 = c->win[3];
-    for (uint32_t k = 0; k < image->numcomps; ++k) comp_geom(image->comps[k], c->win[0], c->win[1], c->win[2], c->win[3], 0);
+    // update_image_dimensions (image.cpp:207-246): the component origin on its
+    // grid at full resolution, its size at the decoded one
+    const uint32_t r = c->dparams.cp_reduce;
+    for (uint32_t k = 0; k < image->numcomps; ++k) {
+        grk_image_comp &cp = image->comps[k];
+        comp_geom(cp, c->win[0], c->win[1], c->win[2], c->win[3], r);
+        cp.x0 = cdiv(c->win[0], cp.dx ? cp.dx : 1);
+        cp.y0 = cdiv(c->win[1], cp.dy ? cp.dy : 1);
+    }
     return true;
 }
 

@@ -578,14 +578,17 @@ int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const c
     const uint32_t r = params->core.cp_reduce;
     grkgpu_dparams dp{r, params->core.cp_layer, params->DA_x0, params->DA_y0, params->DA_x1, params->DA_y1};
     const bool win = dp.DA_x0 || dp.DA_y0 || dp.DA_x1 || dp.DA_y1;
-    // decoded region: reduced coordinates ceil(x / 2^r), or the window clipped to the image
+    // decoded region: the image or the window clipped to it (reference grid),
+    // at the decoded resolution ceil(x / 2^r) (update_image_dimensions, image.cpp:207-246)
     auto cdiv = [r](uint32_t v) { return (uint32_t)(((uint64_t)v + (1ull << r) - 1) >> r); };
-    uint32_t x0 = cdiv(d.x0), y0 = cdiv(d.y0), x1 = cdiv(d.x1), y1 = cdiv(d.y1);
+    uint32_t fx0 = d.x0, fy0 = d.y0, fx1 = d.x1, fy1 = d.y1;
     if (win) {
-        x0 = std::max(d.x0, dp.DA_x0); y0 = std::max(d.y0, dp.DA_y0);
-        x1 = std::min(d.x1, dp.DA_x1); y1 = std::min(d.y1, dp.DA_y1);
-        if (x1 <= x0 || y1 <= y0) return -1;
+        fx0 = std::max(d.x0, dp.DA_x0); fy0 = std::max(d.y0, dp.DA_y0);
+        fx1 = std::min(d.x1, dp.DA_x1); fy1 = std::min(d.y1, dp.DA_y1);
+        if (fx1 <= fx0 || fy1 <= fy0) return -1;
     }
+    const uint32_t x0 = cdiv(fx0), y0 = cdiv(fy0), x1 = cdiv(fx1), y1 = cdiv(fy1);
+    if (x1 <= x0 || y1 <= y0) return -1;
     const uint32_t w = x1 - x0, h = y1 - y0, nc = d.numcomps;
     std::vector<int32_t> samples((size_t)w * h * nc);
     std::vector<int32_t *> planes(nc);
@@ -599,12 +602,12 @@ int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const c
     int32_t rc = cb(&info);
     if (rc == 0 && info.image && info.image->numcomps == nc) {
         grkp_image *img = info.image;
-        if (win) {  // grk_set_decode_area's image bounds (j2k.cpp j2k_set_decode_area)
-            img->x0 = x0; img->y0 = y0; img->x1 = x1; img->y1 = y1;
+        if (win) {  // grk_set_decode_area's image bounds: the window (TileProcessor.cpp:109-240)
+            img->x0 = fx0; img->y0 = fy0; img->x1 = fx1; img->y1 = fy1;
         }
         for (uint32_t k = 0; k < nc && rc == 0; ++k) {
             grkp_image_comp &cm = img->comps[k];
-            cm.x0 = x0; cm.y0 = y0; cm.w = w; cm.h = h;
+            cm.x0 = win ? fx0 : x0; cm.y0 = win ? fy0 : y0; cm.w = w; cm.h = h;
             if (!comp_alloc(&cm)) rc = -1;
             else memcpy(cm.data, planes[k], (size_t)w * h * 4);
         }

@@ -161,9 +161,10 @@ DEC_VARIANTS = {
     "rgb8_poc_r15_I": [["-l", "1"]],
     "rgb8_prec_r20_rpcl": [["-l", "1"], ["-r", "1"]],
     "g12_prec_r12_A1": [["-r", "2"]],
-    "rgb8_128x96": [["-r", "1"]],
-    "rgb12_I": [["-r", "2"]],
-    "g8_off_tiles": [["-r", "2"]],
+    "rgb8_128x96": [["-r", "1"], ["-r", "1", "-d", "10,6,91,77"], ["-r", "2", "-d", "17,9,128,96"]],
+    "rgb12_I": [["-r", "2"], ["-r", "1", "-d", "9,13,70,61"]],
+    "g8_off_tiles": [["-r", "2"], ["-r", "1", "-d", "40,30,170,121"]],
+    "g16_128": [["-r", "2", "-d", "33,20,100,99"]],
     "rgb12_cinema4k": [["-r", "1"]],
     "rgb8_prec_cprl": [["-r", "1"]],
     "g16_I": [["-r", "3"]],
@@ -179,7 +180,7 @@ DEC_VARIANTS = {
 
 
 def variant_tag(args):
-    return "".join(a.lstrip("-") for a in args)
+    return "".join(a.lstrip("-") for a in args).replace(",", "_")
 
 
 # BASELINE.json configs (hash-only)

@@ -241,8 +241,9 @@ def test_decode_options_match_reference(codec, name, tag):
     a = v["args"]
     reduce = int(a[a.index("-r") + 1]) if "-r" in a else 0
     layers = int(a[a.index("-l") + 1]) if "-l" in a else 0
+    window = tuple(int(x) for x in a[a.index("-d") + 1].split(",")) if "-d" in a else None
     ref = np.load(f"{GOLD}/{name}.{tag}.dec.npy")
-    d = codec.decompress(open(f"{GOLD}/{name}.j2k", "rb").read(), reduce=reduce, layers=layers)
+    d = codec.decompress(open(f"{GOLD}/{name}.j2k", "rb").read(), reduce=reduce, layers=layers, window=window)
     assert d.shape == ref.shape
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
