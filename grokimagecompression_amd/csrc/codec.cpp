@@ -1954,6 +1954,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     std::vector<DecBlock> db;
     std::vector<DecSeg> dsegs;        // codeword segments of all blocks
     std::vector<uint8_t> droi;        // per-block ROI shift (empty: no ROI)
+    std::vector<uint8_t> dsty;        // per-block code-block style (COD / COC of its tile-component)
     std::vector<uint32_t> seg_first;  // per block: first segment (+ the total at the end)
     std::vector<uint8_t> extra;  // concatenated multi-chunk segments
     bool too_deep = false;
@@ -1970,6 +1971,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     // reduce >= its resolutions)
     std::vector<int> terr(nsh, 0);
     std::vector<std::array<uint8_t, 16>> troi(nsh);  // per tile: ROI shift of each component
+    std::vector<std::array<uint8_t, 16>> tsty(nsh);  // per tile: code-block style of each component
     std::vector<int32_t> tmct(nsh, cp.mct);            // per tile: MCT (a tile COD may change it)
     host_parallel_for(nsh, 1, [&](size_t l0, size_t l1) {
         for (size_t lt = l0; lt < l1; ++lt) {
@@ -2020,8 +2022,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 if (!check_qcd_steps(tcp, cp.qcc_set, tqcd, tqcc, e)) { terr[lt] = 5; continue; }
                 for (uint32_t k = 0; k < nc; ++k) {
                     const CompParams &cc = tcp.comp[k];
-                    if (cc.cblksty != cp.cblksty || reduce >= cc.numres || cc.cblkw > 6 || cc.cblkh > 6) ok = false;
+                    if ((cc.cblksty & ~0x3Fu) || reduce >= cc.numres || cc.cblkw > 6 || cc.cblkh > 6) ok = false;
                     troi[lt][k] = tcp.roishift[k];
+                    tsty[lt][k] = (uint8_t)cc.cblksty;
                 }
                 // MCT over components of different wavelets (the reference
                 // picks the transform by component 0's alone) or sizes
@@ -2080,7 +2083,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
                 const bool skip = max_layers && pk.layno >= max_layers;
                 int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
-                                             base + off, tcp.csty, &packno, skip, tcp.cblksty,
+                                             base + off, tcp.csty, &packno, skip, tcp.comp[pk.compno].cblksty,
                                              tpacked_on[lt] ? &packed : nullptr);
                 if (used < 0) { terr[lt] = 2; break; }
                 off += (size_t)used;
@@ -2125,6 +2128,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 d.orient = band.bandno;
                 d.irrev = tc.irrev;
                 d.step = band.stepsize;
+                dsty.push_back(tsty[lt][k]);
                 // passes beyond the last bit-plane are not decoded (t1_decode_cblk
                 // stops at bpno < 0, t1.cpp:1086-1090)
                 d.numpasses = std::min<uint32_t>(cb.numpasses, cb.numbps ? 3 * cb.numbps - 2 : 0);
@@ -2169,12 +2173,18 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (too_deep) return set_err(GRKGPU_ECORRUPT, "unsupported bpno_plus_one >= 31 (code-block bit-planes + ROI shift)");
     const uint32_t nblk = (uint32_t)db.size();
     seg_first.push_back((uint32_t)dsegs.size());
-    if (dwt_options().t1_dec_sort && nblk > 64) {
-        // lanes of a wavefront run until its slowest block is done: hand them
-        // blocks of similar work (pass count, then coded bytes), heaviest first
+    bool mixed_sty = false;  // tile-components of different code-block styles: one decode launch per style
+    for (uint32_t i = 1; i < nblk; ++i) mixed_sty = mixed_sty || dsty[i] != dsty[0];
+    const bool sort_work = dwt_options().t1_dec_sort && nblk > 64;
+    if (sort_work || mixed_sty) {
+        // blocks grouped by style (a launch each), and -- t1_dec_sort -- since
+        // lanes of a wavefront run until its slowest block is done, blocks of
+        // similar work (pass count, then coded bytes) together, heaviest first
         std::vector<uint32_t> ord(nblk);
         for (uint32_t i = 0; i < nblk; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+            if (dsty[a] != dsty[b]) return dsty[a] < dsty[b];
+            if (!sort_work) return false;
             const DecBlock &x = db[a], &y = db[b];
             return x.numpasses != y.numpasses ? x.numpasses > y.numpasses : x.len > y.len;
         });
@@ -2182,10 +2192,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         std::vector<DecSeg> segs2;
         segs2.reserve(dsegs.size());
         std::vector<uint32_t> first2(nblk + 1);
-        std::vector<uint8_t> roi2(droi.size());
+        std::vector<uint8_t> roi2(droi.size()), sty2(nblk);
         for (uint32_t j = 0; j < nblk; ++j) {
             const uint32_t i = ord[j];
             db2[j] = db[i];
+            sty2[j] = dsty[i];
             first2[j] = (uint32_t)segs2.size();
             segs2.insert(segs2.end(), dsegs.begin() + seg_first[i], dsegs.begin() + seg_first[i + 1]);
             if (!droi.empty()) roi2[j] = droi[i];
@@ -2195,6 +2206,19 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         dsegs.swap(segs2);
         seg_first.swap(first2);
         droi.swap(roi2);
+        dsty.swap(sty2);
+    }
+    // launch ranges: one per code-block style, each with its own scratch
+    // groups (64 blocks each) so the ranges need no alignment
+    struct StyRange { uint32_t b0, n, sty; uint64_t scr0; };
+    std::vector<StyRange> sranges;
+    uint64_t scr_records = 0;
+    for (uint32_t i = 0; i < nblk;) {
+        uint32_t j = i;
+        while (j < nblk && dsty[j] == dsty[i]) ++j;
+        sranges.push_back({i, j - i, dsty[i], scr_records});
+        scr_records += t1_scratch_records(j - i);
+        i = j;
     }
     double t_t2 = now_ms();
     HIPCHK(c->cs.ensure(len + extra.size() + 256));
@@ -2202,7 +2226,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
     // the decoder's lane-interleaved groups span 64 records each (t1_lane.h)
-    HIPCHK(c->scratch.ensure((size_t)t1_scratch_records(nblk) * sizeof(T1Scratch) + 256));
+    HIPCHK(c->scratch.ensure((size_t)scr_records * sizeof(T1Scratch) + 256));
     // per-segment unstuffed-stream regions (16-byte units)
     uint64_t uwords = 0;
     for (auto &sg : dsegs) {
@@ -2250,10 +2274,12 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     // 9/7 float lifting free of stale NaNs)
     if (win && arena) HIPCHK(hipMemsetAsync(c->coef.p, 0, arena * 4, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
-    HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>(), nblk, c->cs.as<uint8_t>(), c->scratch.as<T1Scratch>(),
-                            c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(), 0, c->segs.as<DecSeg>(),
-                            (const uint32_t *)(c->segs.as<uint8_t>() + segbytes), cp.cblksty,
-                            roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes : nullptr));
+    for (const StyRange &g : sranges)
+        HIPCHK(launch_t1_decode(c->blocks.as<DecBlock>() + g.b0, g.n, c->cs.as<uint8_t>(),
+                                c->scratch.as<T1Scratch>() + g.scr0, c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(),
+                                0, c->segs.as<DecSeg>(),
+                                (const uint32_t *)(c->segs.as<uint8_t>() + segbytes) + g.b0, g.sty,
+                                roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes + g.b0 : nullptr));
     HIPCHK(hipEventRecord(c->ev[2], s));
     c->ltimes.clear();
     LaunchLog llog{&c->lev, &c->ltimes};

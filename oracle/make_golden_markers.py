@@ -340,15 +340,33 @@ def case_coc_then_cod(tmp):
     return write(out, tps), img
 
 
+def case_mixed_cblksty(tmp):
+    """Main COC(1) and COC(2) carrying code-block styles other than the
+    COD's: component 0 plain, component 1 every mode switch (-M 63),
+    component 2 RESET + vertically causal + SEGSYM (-M 42); two layers."""
+    img = synth(72, 100, 3, 8, 314)
+    opts = [P0 + ["-r", "20,4"], P0 + ["-r", "20,4", "-M", "63"], P0 + ["-r", "20,4", "-M", "42"]]
+    g = rgb_from_greys([img[0], img[1], img[2]], opts, 8, tmp)
+    ref, _ = parse(enc(img, 8, ["-p", "CPRL", "-Y", "0"] + opts[0], tmp))
+    main = []
+    for m, pl in ref:
+        main.append((m, pl))
+        if m == COD:
+            main += [(COC, coc_of(find(g[k][0], COD)[0], k)) for k in (1, 2)]
+    body = b"".join(gk[1][0]["body"] for gk in g)
+    return write(main, [dict(isot=0, tpsot=0, tnsot=1, hdr=[], body=body)]), None
+
+
 CASES = [("tile_cod", case_tile_cod), ("main_coc", case_main_coc), ("tile_coc", case_tile_coc),
          ("tp_cod_copy", case_tp_cod_copy), ("tile_rgn", case_tile_rgn), ("ppt", case_ppt), ("ppm", case_ppm), ("ppt_tparts", case_ppt_tparts),
          ("ppm_1tile", case_ppm_1tile), ("mixed_wavelet", case_mixed_wavelet), ("siqnt", case_siqnt),
-         ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod)]
+         ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod), ("mixed_cblksty", case_mixed_cblksty)]
 
 
 # reference decodes with grk_decompress options, -> mk_<name>.<tag>.dec.npy
 VARIANTS = {"tile_coc": [["-r", "1"]], "main_coc": [["-r", "1"]], "tile_cod": [["-r", "2"]],
-            "ppt_tparts": [["-r", "1"], ["-l", "1"]], "ppm": [["-l", "1"]], "mixed_wavelet": [["-r", "1"]]}
+            "ppt_tparts": [["-r", "1"], ["-l", "1"]], "ppm": [["-l", "1"]], "mixed_wavelet": [["-r", "1"]],
+            "mixed_cblksty": [["-l", "1"], ["-r", "1"]]}
 
 
 def variant_tag(a):

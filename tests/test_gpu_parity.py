@@ -211,7 +211,22 @@ def test_decode_marker_fixture_options_match_reference(codec, tag, vt):
     assert int(np.abs(d.astype(np.int64) - ref).max()) == 0
 
 
-@pytest.mark.parametrize("tag", ["mk_tile_coc", "mk_ppt_tparts", "mk_main_coc"])
+def test_decode_mixed_cblksty_sorted(codec):
+    """Components of different code-block styles (COC): the blocks go to one
+    decode launch per style; with t1_dec_sort the work order is kept inside
+    each style group.  Equal to the reference's decode either way."""
+    import grokimagecompression_amd as grk
+    cs = open(f"{GOLD}/mk_mixed_cblksty.j2k", "rb").read()
+    ref = np.load(f"{GOLD}/mk_mixed_cblksty.dec.npy")
+    for opts in ({}, {"t1_dec_sort": 1}, {"t1_dec_sort": 1, "t1_dec_bpw": 16}):
+        with grk.dwt_options(**opts):
+            assert np.array_equal(codec.decompress(cs), ref)
+    ref = np.load(f"{GOLD}/mk_mixed_cblksty.r1.dec.npy")
+    with grk.dwt_options(t1_dec_sort=1):
+        assert np.array_equal(codec.decompress(cs, reduce=1), ref)
+
+
+@pytest.mark.parametrize("tag", ["mk_tile_coc", "mk_ppt_tparts", "mk_main_coc", "mk_mixed_cblksty"])
 def test_marker_fixtures_reduce_and_window(codec, tag):
     """The per-component / packed-header streams through -r 1 and a window:
     the window equals the crop of the full decode, and -r 1 equals a reduced
