@@ -14,9 +14,12 @@
 #include <float.h>
 #include <limits.h>
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 
 namespace grkgpu {
@@ -733,6 +736,18 @@ bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ui
 //    only the precincts holding a block whose layer record changed since the
 //    last probe are simulated again; the packet order for a layer count is
 //    built once.
+// GRKGPU_T2_TRACE=1: per-tile breakdown of the rate allocation on stderr
+struct RateTrace {
+    bool on = false;
+    double hull = 0, form = 0, sim = 0;
+    uint32_t probes = 0;
+    uint64_t redo = 0, precs = 0;
+};
+thread_local RateTrace g_rt;
+double t2_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct RateProbe {
     // per block, in te.blist order
     std::vector<uint32_t> prec;        // precinct id
@@ -878,6 +893,7 @@ bool simulate_tile(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t 
     for (uint32_t p = 0; p < rp.nprec; ++p)
         if (rp.dirty[p] && rp.head[p + 1] > rp.head[p]) todo.push_back(p);
     std::fill(rp.dirty.begin(), rp.dirty.end(), 0);
+    g_rt.precs += todo.size();
     if (todo.size() > 16) {
         host_parallel_for(todo.size(), 8, [&](size_t a, size_t b) {
             for (size_t i = a; i < b; ++i) probe_precinct(cp, te, rp, todo[i]);
@@ -1070,6 +1086,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         }
     }
     std::vector<uint8_t> changed(redo.size());
+    g_rt.redo += redo.size();
     if (redo.size() > 2048) {
         host_parallel_for(redo.size(), 256, [&](size_t a, size_t b) {
             for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j]);
@@ -1242,6 +1259,7 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
     const bool sl = single_lossless(cp, te);
     uint32_t min_slope = USHRT_MAX;
     if (!sl) {  // per-block convex hulls (independent), then the smallest slope
+        const double h0 = g_rt.on ? t2_ms() : 0;
         blocks_parallel(te, [&](Cblk &c) {
             EncCblkState &s = (*te.cblk)[c.gidx];
             convex_hull(te.passes->data() + s.pass0, s.numpasses);
@@ -1252,6 +1270,7 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
             for (uint32_t pn = 0; pn < s.numpasses; ++pn)
                 if (P[pn].slope && P[pn].slope < min_slope) min_slope = P[pn].slope;
         }
+        if (g_rt.on) g_rt.hull += t2_ms() - h0;
     }
     if (sl) {
         makelayer_final(cp, te, 0);
@@ -1270,14 +1289,23 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
             for (uint32_t i = 0; i < 128; ++i) {
                 const uint32_t thresh = (lower + upper) >> 1;
                 if (prevthresh != 0 && prevthresh == thresh) break;
+                const double f0 = g_rt.on ? t2_ms() : 0;
                 form_layer<true>(cp, te, layno, (uint16_t)thresh, false, cp.fixed_quality != 0, rp);
+                ++g_rt.probes;
                 prevthresh = thresh;
                 if (cp.fixed_quality) {
                     const double achieved = layno == 0 ? te.distolayer[0] : cumdisto[layno - 1] + te.distolayer[layno];
                     if (achieved < distotarget) { upper = thresh; continue; }
                     lower = thresh;
                 } else {
-                    if (!simulate_tile(cp, te, layno + 1, maxlen, rp)) { lower = thresh; continue; }
+                    const double f1 = g_rt.on ? t2_ms() : 0;
+                    const bool fits = simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    if (g_rt.on) {
+                        const double f2 = t2_ms();
+                        g_rt.form += f1 - f0;
+                        g_rt.sim += f2 - f1;
+                    }
+                    if (!fits) { lower = thresh; continue; }
                     upper = thresh;
                 }
             }
@@ -1298,8 +1326,16 @@ bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
     te.blist.clear();
     for_each_block(te, [&](Cblk &c) { te.blist.push_back(&c); });
     if (!(cp.disto_alloc || cp.fixed_quality)) return true;
-    if (cp.rate_algo == 0) return pcrd_simple(cp, te, len);
-    return pcrd_feasible(cp, te, len);
+    static const bool trace = getenv("GRKGPU_T2_TRACE") && atoi(getenv("GRKGPU_T2_TRACE"));
+    g_rt = RateTrace{};
+    g_rt.on = trace;
+    const double t0 = trace ? t2_ms() : 0;
+    const bool ok = cp.rate_algo == 0 ? pcrd_simple(cp, te, len) : pcrd_feasible(cp, te, len);
+    if (trace)
+        fprintf(stderr, "[t2] tile %u blocks %zu: rate %.3f ms = hull %.3f + probes %u (form %.3f, sim %.3f; "
+                "%llu block evals, %llu precinct sims)\n", te.tile->index, te.blist.size(), t2_ms() - t0, g_rt.hull,
+                g_rt.probes, g_rt.form, g_rt.sim, (unsigned long long)g_rt.redo, (unsigned long long)g_rt.precs);
+    return ok;
 }
 
 // ---------------------------------------------------------------------------
