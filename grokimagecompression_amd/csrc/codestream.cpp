@@ -327,7 +327,7 @@ void write_mct_group(ByteBuf &cs, const CodingParams &cp) {
     }
     const uint32_t tmcc = (0u << 16) | (2u << 8) | 1u;  // irreversible, offsets = record 2, matrix = record 1
     cs.put8(tmcc >> 16); cs.put8((tmcc >> 8) & 0xff); cs.put8(tmcc & 0xff);
-    cs.put16(0xFF77); cs.put16(3); cs.put8(1); cs.put8(3);  // MCO (j2k_write_mco, :6298-6333)
+    cs.put16(0xFF77); cs.put16(4); cs.put8(1); cs.put8(3);  // MCO (j2k_write_mco, :6298-6333)
 }
 
 // matrix_inversion_f (mct/invert.cpp:78-286), restated: an LU decomposition
