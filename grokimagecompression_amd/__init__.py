@@ -576,8 +576,8 @@ class Codec:
     def decompress(self, buf, device_out=False, out=None, reduce=0, window=None, layers=0):
         """Decode a .j2k codestream -> (c,h,w) int32 (numpy, or torch.cuda when
         device_out / out is a cuda tensor).  reduce > 0: the image at
-        resolution numres-1-reduce (grk_decompress -r), ceil(x / 2^reduce)
-        in every coordinate.  window = (x0, y0, x1, y1) in image coordinates:
+        resolution numres-1-reduce (grk_decompress -r), ceil(size / 2^reduce)
+        samples a side (a window: ceil(x1 / 2^reduce) - ceil(x0 / 2^reduce)).  window = (x0, y0, x1, y1) in image coordinates:
         only that region (grk_set_decode_area), clipped to the image.
         layers > 0: only the first `layers` quality layers (grk_decompress -l)."""
         d = read_header(buf)
@@ -586,17 +586,25 @@ class Codec:
             d.x0, d.y0, d.x1, d.y1 = max(d.x0, wx0), max(d.y0, wy0), min(d.x1, wx1), min(d.y1, wy1)
             if d.x1 <= d.x0 or d.y1 <= d.y0:
                 raise GrkGpuError("decode window outside the image")
-        if reduce:  # then at the decoded resolution, ceil(x / 2^reduce) (j2k_set_decode_area)
-            cd = lambda v: -(-v >> reduce)  # noqa: E731
-            d.x0, d.y0, d.x1, d.y1 = cd(d.x0), cd(d.y0), cd(d.x1), cd(d.y1)
-        c, h, w = d.numcomps, d.y1 - d.y0, d.x1 - d.x0
+        # planes at the decoded resolution: a window's extent
+        # ceil(x1 / 2^r) - ceil(x0 / 2^r) (update_image_dimensions); the whole
+        # image's ceil(size / 2^r) (grk_image_comp_header_update), the
+        # decoded samples placed from ceil(x0 / 2^r) and the rest zero
+        cd = lambda v, s: -(-v // s)  # noqa: E731
+        R = 1 << reduce
+
+        def extent(a0, a1, s):
+            if window is not None:
+                return cd(cd(a1, s), R) - cd(cd(a0, s), R)
+            return cd(cd(a1, s) - cd(a0, s), R)
+        c = d.numcomps
+        h, w = extent(d.y0, d.y1, 1), extent(d.x0, d.x1, 1)
         if any(d.dx[k] != 1 or d.dy[k] != 1 for k in range(c)):
             # subsampled components: a list of host planes, each on its grid
             if out is not None or device_out:
                 raise GrkGpuError("subsampled components decode to host planes only")
-            cd = lambda v, s: -(-v // s)  # noqa: E731
-            outs = [np.empty((cd(d.y1, d.dy[k]) - cd(d.y0, d.dy[k]), cd(d.x1, d.dx[k]) - cd(d.x0, d.dx[k])),
-                             dtype=np.int32) for k in range(c)]
+            outs = [np.empty((extent(d.y0, d.y1, d.dy[k]), extent(d.x0, d.x1, d.dx[k])), dtype=np.int32)
+                    for k in range(c)]
             ptrs = (ctypes.c_void_p * c)(*[a.ctypes.data for a in outs])
             bp, bn, keep = _buf_ptr(buf)
             dp = DParams(cp_reduce=reduce, cp_layer=layers)

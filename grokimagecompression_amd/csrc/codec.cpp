@@ -1859,14 +1859,21 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     const uint32_t ix0 = ceil_pow2(full.x0, reduce), iy0 = ceil_pow2(full.y0, reduce);
     const uint32_t ix1 = ceil_pow2(full.x1, reduce), iy1 = ceil_pow2(full.y1, reduce);
     if (win && (ix1 <= ix0 || iy1 <= iy0)) return set_err(GRKGPU_EINVAL, "decode window empty at this resolution");
+    // Without a window the planes take grk_image_comp_header_update's sizes,
+    // ceil(size / 2^reduce) (image.cpp:124-155), while the tiles land from
+    // ceil(x0 / 2^reduce) (TileProcessor.cpp:1729-1734): with an odd origin
+    // that is one row / column more than the decoded samples, left zero.
+    // A window takes update_image_dimensions' (image.cpp:207-246) exact extent.
+    const uint32_t ox1 = win ? ix1 : ix0 + ceil_pow2(full.w(), reduce);
+    const uint32_t oy1 = win ? iy1 : iy0 + ceil_pow2(full.h(), reduce);
     if (img && (reduce || win)) {
         img->x0 = ix0; img->y0 = iy0;
-        img->x1 = ix1; img->y1 = iy1;
+        img->x1 = ox1; img->y1 = oy1;
     }
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th;
-    const uint32_t iw = ix1 - ix0;
+    const uint32_t iw = ox1 - ix0;
     if (te > ntiles) te = ntiles;
     if (tb > te) return set_err(GRKGPU_EINVAL, "bad tile range");
     const bool whole = tb == 0 && te == ntiles;
@@ -1883,11 +1890,18 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     Rect orect[GRKGPU_MAX_COMPS];
     uint64_t ooff[GRKGPU_MAX_COMPS + 1];
     ooff[0] = 0;
+    bool opad = false;  // planes extending past the decoded samples (zero filled)
     for (uint32_t k = 0; k < nc; ++k) {
         orect[k] = comp_rect({ix0, iy0, ix1, iy1}, cp.dx[k], cp.dy[k]);
+        if (!win) {  // ceil(ceil(size on the component grid) / 2^reduce)
+            const Rect cr = comp_rect(cp.image, cp.dx[k], cp.dy[k]);
+            const Rect sized{orect[k].x0, orect[k].y0, orect[k].x0 + ceil_pow2(cr.w(), reduce),
+                             orect[k].y0 + ceil_pow2(cr.h(), reduce)};
+            opad = opad || sized.x1 != orect[k].x1 || sized.y1 != orect[k].y1;
+            orect[k] = sized;
+        }
         ooff[k + 1] = ooff[k] + (uint64_t)orect[k].w() * orect[k].h();
     }
-    // the window on each component's grid
     // the window on each component's grid at the decoded resolution
     Rect cwin[GRKGPU_MAX_COMPS];
     for (uint32_t k = 0; k < nc; ++k) cwin[k] = comp_rect({ix0, iy0, ix1, iy1}, cp.dx[k], cp.dy[k]);
@@ -2293,6 +2307,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         HIPCHK(c->img.ensure(ooff[nc] * 4 + 256));
         for (uint32_t k = 0; k < nc; ++k) dst.p[k] = c->img.as<int32_t>() + ooff[k];
     }
+    if (opad)
+        for (uint32_t k = 0; k < nc; ++k)
+            HIPCHK(hipMemsetAsync(dst.p[k], 0, (ooff[k + 1] - ooff[k]) * 4, s));
     ShiftArr sh{}, mn{}, mx{};
     for (uint32_t k = 0; k < nc; ++k) {
         sh.v[k] = cp.shift[k];

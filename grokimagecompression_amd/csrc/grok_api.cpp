@@ -590,7 +590,12 @@ GRK_EXPORT bool grk_read_header(grk_codec *codec, grk_header_info *hi, grk_image
         cp.dy = d.dy[k];
         cp.prec = d.prec[k];
         cp.sgnd = (uint32_t)d.sgnd[k];
-        comp_geom(cp, d.x0, d.y0, d.x1, d.y1, r);
+        // grk_image_comp_header_update (image.cpp:124-155): the origin on the
+        // component grid, the size at the decoded resolution
+        cp.x0 = cdiv(d.x0, cp.dx);
+        cp.y0 = cdiv(d.y0, cp.dy);
+        cp.w = cdivpow2(cdiv(d.x1, cp.dx) - cp.x0, r);
+        cp.h = cdivpow2(cdiv(d.y1, cp.dy) - cp.y0, r);
     }
     *image = img;
     if (hi) {
@@ -815,8 +820,8 @@ GRK_EXPORT bool grk_decode_tile_data(grk_codec *codec, uint16_t tile_index, uint
                 grkgpu_image_desc d{};
                 grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
                 const uint32_t r = c->dparams.cp_reduce;
-                const uint32_t rw = cdivpow2(c->desc.x1, r) - cdivpow2(c->desc.x0, r);
-                const uint32_t rh = cdivpow2(c->desc.y1, r) - cdivpow2(c->desc.y0, r);
+                const uint32_t rw = cdivpow2(c->desc.x1 - c->desc.x0, r);  // the core's plane size
+                const uint32_t rh = cdivpow2(c->desc.y1 - c->desc.y0, r);
                 c->reduced.resize((size_t)rw * rh * nc);
                 std::vector<int32_t *> planes(nc);
                 for (uint32_t k = 0; k < nc; ++k) planes[k] = c->reduced.data() + (size_t)k * rw * rh;

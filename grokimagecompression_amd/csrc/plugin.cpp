@@ -589,7 +589,9 @@ int32_t decode_file(grkgpu_ctx *ctx, grkp_decompress_parameters *params, const c
     }
     const uint32_t x0 = cdiv(fx0), y0 = cdiv(fy0), x1 = cdiv(fx1), y1 = cdiv(fy1);
     if (x1 <= x0 || y1 <= y0) return -1;
-    const uint32_t w = x1 - x0, h = y1 - y0, nc = d.numcomps;
+    // the core's planes: a window's extent, or the image's ceil(size / 2^r)
+    // (grk_image_comp_header_update; see grkgpu_image_desc)
+    const uint32_t w = win ? x1 - x0 : cdiv(fx1 - fx0), h = win ? y1 - y0 : cdiv(fy1 - fy0), nc = d.numcomps;
     std::vector<int32_t> samples((size_t)w * h * nc);
     std::vector<int32_t *> planes(nc);
     for (uint32_t k = 0; k < nc; ++k) planes[k] = samples.data() + (size_t)k * w * h;

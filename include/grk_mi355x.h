@@ -68,7 +68,11 @@ enum {
  * [ceil(x0 / dx), ceil(x1 / dx)) x [ceil(y0 / dy), ceil(y1 / dy)) -- rows of
  * that width, planes[k] holding only component k (grk_image_comp w, h,
  * TileComponent.cpp:150-163).  A reduced / window decode reports the reduced
- * / window rectangle here, and component planes follow the same rule. */
+ * / window rectangle here, and component planes follow the same rule, except
+ * that a reduced decode of the whole image sizes its planes as the reference
+ * does (grk_image_comp_header_update, image.cpp:124-155): ceil(size / 2^r),
+ * with x1 = x0 + that -- one more row / column than the decoded samples when
+ * the origin is not a multiple of 2^r, left zero. */
 typedef struct {
     uint32_t x0, y0, x1, y1;
     uint32_t numcomps;
@@ -377,9 +381,10 @@ int grkgpu_decompress(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, grkgpu_ima
                       int32_t *const *planes, int planes_on_device);
 /* Reduced-resolution decode (grk_decompress -r; grk_decompress_parameters
  * cp_reduce, grok.h:698-702, applied in j2k.cpp:1464-1476 and
- * TileComponent.cpp:199-204): the image at resolution numres-1-reduce, every
- * coordinate ceil(x / 2^reduce); img (if given) receives the reduced
- * geometry.  reduce must be < the number of resolutions (GRKGPU_EINVAL). */
+ * TileComponent.cpp:199-204): the image at resolution numres-1-reduce, the
+ * samples from ceil(x0 / 2^reduce), planes of ceil(size / 2^reduce) a side
+ * (see grkgpu_image_desc); img (if given) receives the reduced geometry.
+ * reduce must be < the number of resolutions (GRKGPU_EINVAL). */
 int grkgpu_decompress_reduced(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t reduce,
                               grkgpu_image_desc *img, int32_t *const *planes, int planes_on_device);
 /* Window decode (grk_set_decode_area, grok.h:1587; grk_decompress -d):
@@ -392,7 +397,8 @@ int grkgpu_decompress_window(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uin
 /* Decode with grk_decompress's options (grk_dparameters, grok.h:694-735):
  * cp_reduce (-r), cp_layer (-l, 0 = all layers) and the decode area (-d,
  * grk_set_decode_area; all four 0 = the whole image).  A window at a reduced
- * resolution is GRKGPU_EINVAL.  img (if given) receives the decoded geometry. */
+ * resolution spans ceil(x1 / 2^r) - ceil(x0 / 2^r) (update_image_dimensions,
+ * image.cpp:207-246).  img (if given) receives the decoded geometry. */
 typedef struct {
     uint32_t cp_reduce, cp_layer;
     uint32_t DA_x0, DA_y0, DA_x1, DA_y1;

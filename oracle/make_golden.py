@@ -149,9 +149,11 @@ CASES = [
 # case: stored as <case>.<tag>.dec.npy, tag = the options without dashes
 # ("l1", "r1l2"), with the decoded header in the manifest under "variants".
 # Not g8_off35 -r 1: at an odd image offset the reference sizes the reduced
-# component as ceil(w / 2^r) instead of ceil(x1 / 2^r) - ceil(x0 / 2^r)
-# (27 x 31 for a 26 x 30 image) and returns uninitialised samples in the
-# extra row / column -- its output differs from run to run.
+# component as ceil(w / 2^r) (grk_image_comp_header_update) while it decodes
+# ceil(x1 / 2^r) - ceil(x0 / 2^r) samples (27 x 31 planes holding 26 x 30)
+# and returns uninitialised samples in the extra row / column -- its output
+# differs from run to run.  Ours sizes the planes the same way and zeroes
+# the extra samples (tests/test_gpu_parity.py assert_reduced_plane).
 DEC_VARIANTS = {
     "g8_r40_20_10": [["-l", "1"], ["-l", "2"], ["-r", "1", "-l", "2"]],
     "rgb12_r30_10_1_I": [["-l", "1"], ["-l", "2"], ["-r", "2"]],

@@ -159,6 +159,28 @@ def test_grk_api_decode_options_match_reference(name, tag, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,r", [("g8_off35", 1), ("g8_off35", 2), ("g8_off_tiles", 1)])
+def test_grk_api_reduced_odd_origin(codec, name, r, tmp_path):
+    """-r of an image whose origin is not a multiple of 2^r: the components
+    sized ceil(size / 2^r), as grk_image_comp_header_update sizes them
+    (image.cpp:124-155), the image header unreduced, the decoded samples
+    from ceil(origin / 2^r) on and the extra row / column zero (the
+    reference's is uninitialised, so no fixture holds it).  The samples equal
+    the Python path's, itself checked against the oracle
+    (test_gpu_parity.py::test_reduced_decode_matches_oracle)."""
+    _need_driver()
+    d, hdr = _dec(name, tmp_path, ["-r", str(r)])
+    h, w, c, bits = MAN[name]["shape"]
+    cd = lambda v: -(-v >> r)  # noqa: E731
+    assert d.shape == (c, cd(h), cd(w))
+    ox, oy = map(int, MAN[name]["args"][MAN[name]["args"].index("-d") + 1].split(","))
+    assert hdr[:4] == (ox, oy, ox + w, oy + h)
+    assert np.array_equal(d, codec.decompress(open(f"{GOLD}/{name}.j2k", "rb").read(), reduce=r))
+    dh, dw = cd(oy + h) - cd(oy), cd(ox + w) - cd(ox)
+    assert not d[:, dh:].any() and not d[:, :, dw:].any()
+
+
+@pytest.mark.gpu
 def test_grk_api_decode_area(tmp_path):
     """grk_set_decode_area: the window of the reference's full decode."""
     _need_driver()
