@@ -218,7 +218,7 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->f64_lift = g_dwt_opts.f64_lift;
     out->t1_dec_sort = g_dwt_opts.t1_dec_sort;
     out->t1_dec_bpw = g_dwt_opts.t1_dec_bpw;
-    out->pad_ = 0;
+    out->mid_th = g_dwt_opts.mid_th;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -232,12 +232,15 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->inv01 != 0 && o->inv01 != 2 && o->inv01 != 4) return set_err(GRKGPU_EINVAL, "inv01 must be 0, 2 or 4");
     if (o->pair_group < 0 || o->pair_group > 4096) return set_err(GRKGPU_EINVAL, "pair_group must be 0 .. 4096");
     if (o->f64_lift != 0 && o->f64_lift != 1) return set_err(GRKGPU_EINVAL, "f64_lift must be 0 or 1");
-    g_dwt_opts.f64_lift = o->f64_lift;
     if (o->t1_dec_sort != 0 && o->t1_dec_sort != 1) return set_err(GRKGPU_EINVAL, "t1_dec_sort must be 0 or 1");
-    g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
     if (o->t1_dec_bpw < 0 || o->t1_dec_bpw > 64 || (o->t1_dec_bpw & (o->t1_dec_bpw - 1)))
         return set_err(GRKGPU_EINVAL, "t1_dec_bpw must be 0 or a power of two <= 64");
+    if (o->mid_th != 0 && o->mid_th != 8 && o->mid_th != 16 && o->mid_th != 24)
+        return set_err(GRKGPU_EINVAL, "mid_th must be 0, 8, 16 or 24");
+    g_dwt_opts.f64_lift = o->f64_lift;
+    g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
     g_dwt_opts.t1_dec_bpw = o->t1_dec_bpw;
+    g_dwt_opts.mid_th = o->mid_th;
     g_dwt_opts.inv01 = o->inv01;
     g_dwt_opts.pair_group = o->pair_group;
     g_dwt_opts.inv01_min_samples = o->inv01_min_samples;

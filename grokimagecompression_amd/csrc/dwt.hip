@@ -948,7 +948,9 @@ hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t n
 // for 5/3, 24 for 9/7 at >= 2^23 samples), short ones for small levels (more
 // wavefronts, shorter per-wave chains).
 int dwt_pick_th(int irrev, uint64_t level_samples, int, int) {
-    return level_samples >= ((uint64_t)1 << 23) ? (irrev ? 24 : 32) : 8;
+    if (level_samples >= ((uint64_t)1 << 23)) return irrev ? 24 : 32;
+    if (level_samples >= ((uint64_t)1 << 21) && dwt_options().mid_th) return dwt_options().mid_th;
+    return 8;
 }
 
 void dwt_job_tiles(int irrev, int code, DwtJob &j) {
@@ -1031,6 +1033,7 @@ hipError_t launch_dwt_jobs(const DwtJob *jobs_dev, uint32_t njobs, uint32_t max_
     const int fmt = (code >> DWT_FMT_SHIFT) & 7;  // image sample format of a fused level 0
     switch (code & 0xff) {
         case 8: launch_th<8>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
+        case 16: launch_th<16>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
         case 24: launch_th<24>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
         case 32: launch_th<32>(jobs_dev, grid, block, irrev, inverse, fused, fmt, s); break;
         default: return hipErrorInvalidValue;

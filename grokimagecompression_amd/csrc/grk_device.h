@@ -114,6 +114,7 @@ struct DwtOptions {
     int32_t f64_lift = 0;    // forward 9/7 fused pair: lifting in f64 FMA + floor instead of v_mad_i64_i32
     int32_t t1_dec_sort = 0; // T1 decode: blocks in decreasing order of expected work
     int32_t t1_dec_bpw = 0;  // T1 decode: blocks per wavefront (0: by block count)
+    int32_t mid_th = 0;      // window rows of a level of 2^21 .. 2^23 samples (0: 8)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose

@@ -211,7 +211,9 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    wavefront's 64 lanes finish close together; 0 = stream
  *                    order.  Same output either way.
  *   t1_dec_bpw       T1 decode: code-blocks per wavefront (1, 2, 4 .. 64);
- *                    0 (default) = by block count (64 from 4096 blocks). */
+ *                    0 (default) = by block count (64 from 4096 blocks).
+ *   mid_th           window rows (8, 16, 24) of the per-level DWT kernels for
+ *                    a level of 2^21 .. 2^23 samples; 0 (default) = 8. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -223,7 +225,7 @@ typedef struct {
     int32_t f64_lift;
     int32_t t1_dec_sort;
     int32_t t1_dec_bpw;
-    int32_t pad_;
+    int32_t mid_th;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */

@@ -366,6 +366,30 @@ def test_dwt_stage_vs_oracle(oracle, irrev, shape_off, numres):
         assert np.array_equal(t.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("irrev", [False, True])
+@pytest.mark.parametrize("th", [16, 24])
+def test_dwt_mid_th_vs_oracle(oracle, irrev, th):
+    """Levels of 2^21 .. 2^23 samples in taller windows (mid_th = 16 / 24
+    rows instead of 8), forward and inverse, against the oracle."""
+    import torch
+    import grokimagecompression_amd as grk
+    h, w, x0, y0, numres = 1501, 1499, 1, 0, 4
+    rng = np.random.default_rng(th + irrev)
+    a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32)
+    with grk.dwt_options(mid_th=th):
+        t = torch.from_numpy(a).cuda()
+        grk.dwt_fwd(t, x0, y0, numres, irrev)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), oracle.dwt_fwd(a, x0, y0, numres, irrev))
+        f = (rng.standard_normal((h, w)) * 100).astype(np.float32).view(np.int32) if irrev else \
+            oracle.dwt_fwd(a, x0, y0, numres, False)
+        ref = oracle.dwt_inv(f, x0, y0, numres, True) if irrev else a
+        t = torch.from_numpy(f.copy()).cuda()
+        grk.dwt_inv(t, x0, y0, numres, irrev)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("ny", ["2", "4", "6", "0", "mix", "g3", "d"])
 @pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
                                        ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
