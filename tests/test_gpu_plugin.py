@@ -194,9 +194,17 @@ def test_plugin_decode_window(name, win, tmp_path):
     assert np.array_equal(_planes(r, out), ref[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox])
 
 
-def test_plugin_decode_declines_window_at_reduce(tmp_path):
-    r, _ = _dec("rgb12_I", tmp_path, ["-r", "1", "-d", "0,0,20,20"])
-    assert r.returncode == 3, r.stderr
+def test_plugin_decode_window_at_reduce(codec, tmp_path):
+    """-r with -d: the window's samples at the reduced resolution,
+    ceil(x / 2^r) of its corners (update_image_dimensions), as the library's
+    own window decode gives them (itself checked against the reference's -r
+    -d fixtures, test_gpu_parity.py::test_decode_options_match_reference)."""
+    r, out = _dec("rgb12_I", tmp_path, ["-r", "1", "-d", "3,0,21,19"])
+    assert r.returncode == 0, r.stderr
+    d = _planes(r, out)
+    ref = codec.decompress(open(f"{GOLD}/rgb12_I.j2k", "rb").read(), reduce=1, window=(3, 0, 21, 19))
+    assert d.shape == ref.shape == (3, 10, 9)
+    assert np.array_equal(d, ref)
 
 
 # ---- batch route: grk_compress / grk_decompress with an image directory ----
