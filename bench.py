@@ -169,6 +169,7 @@ def main():
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (input H2D timed) leg")
     ap.add_argument("--concurrency", type=int, default=16, help="frames in flight per GPU: 1, or an even number (half 9/7, half 5/3)")
     ap.add_argument("--workload", default="8k", choices=["8k", "c5", "c4"])
+    ap.add_argument("--opt", default="", help="plan options k=v[,k=v] (grkgpu_dwt_options) for the whole run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +190,9 @@ def main():
 
     import grokimagecompression_amd as grk
     import synth
+
+    if args.opt:  # process-wide plan options for an A/B (entered for the whole run)
+        grk.dwt_options(**{k: int(v) for k, v in (kv.split("=", 1) for kv in args.opt.split(","))}).__enter__()
 
     if args.workload == "c4":
         return bench_c4(args, grk, synth, dist, world, rank, local)
@@ -427,6 +431,8 @@ def main():
             "codestream_bytes": {tags[0]: st["bytes" + tags[0]], tags[1]: st["bytes" + tags[1]]},
             "stage_ms": {k: r(st[k]) for k in ("enc" + tags[0], "dec" + tags[0], "enc" + tags[1], "dec" + tags[1])},
         }
+        if args.opt:
+            line["config"]["plan_options"] = args.opt
         print(json.dumps(line), flush=True)
     for c in codecs:
         c.close()

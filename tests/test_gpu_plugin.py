@@ -145,7 +145,7 @@ def _dec(name, tmp_path, extra=()):
 
 
 def _planes(r, out):
-    x0, y0, x1, y1, nc, prec, sgnd, w, h = map(int, r.stdout.split())
+    x0, y0, x1, y1, nc, prec, sgnd, w, h = map(int, r.stdout.splitlines()[0].split())
     return np.fromfile(out, dtype="<i4").reshape(nc, h, w)
 
 
@@ -232,7 +232,7 @@ def _ref_decode(j2k_path, tmp_path):
     out = tmp_path / "ref_dec.i32"
     r = subprocess.run([DRIVER, "dec", str(j2k_path), str(out)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    x0, y0, x1, y1, nc, prec, sgnd, w, h = map(int, r.stdout.split())
+    x0, y0, x1, y1, nc, prec, sgnd, w, h = map(int, r.stdout.splitlines()[0].split())
     return np.fromfile(out, dtype="<i4").reshape(nc, h, w)
 
 
