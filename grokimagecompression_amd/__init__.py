@@ -206,7 +206,8 @@ class DwtOptions(ctypes.Structure):
     _fields_ = [("fuse_level0", ctypes.c_int32), ("f01_rows", ctypes.c_int32), ("f01_min_samples", ctypes.c_uint64),
                 ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("pair_group", ctypes.c_int32),
                 ("inv01_min_samples", ctypes.c_uint64), ("f64_lift", ctypes.c_int32), ("t1_dec_sort", ctypes.c_int32),
-                ("t1_dec_bpw", ctypes.c_int32), ("mid_th", ctypes.c_int32)]
+                ("t1_dec_bpw", ctypes.c_int32), ("mid_th", ctypes.c_int32),
+                ("t1_enc_bpw", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 class LaunchTime(ctypes.Structure):

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <chrono>
 #include <memory>
@@ -202,6 +203,18 @@ int grkgpu_set_stream(grkgpu_ctx *c, void *stream) {
 namespace grkgpu {
 static DwtOptions g_dwt_opts;
 const DwtOptions &dwt_options() { return g_dwt_opts; }
+
+// Codec calls in progress in this process.  A call that has the GPU to itself
+// (a lone frame: grk_decompress of one image) cannot fill the chip with its
+// T1 lanes packed 64 blocks to a wavefront (24,669 blocks of an 8K frame =
+// 386 wavefronts for 1,024 SIMDs), so it spreads them (lone_bpw) and orders
+// them by work; concurrent calls (frame batches) keep full wavefronts.
+static std::atomic<int> g_active_calls{0};
+struct ActiveCall {
+    ActiveCall() { g_active_calls.fetch_add(1); }
+    ~ActiveCall() { g_active_calls.fetch_sub(1); }
+};
+static bool lone_call() { return g_active_calls.load() <= 1; }
 }  // namespace grkgpu
 
 extern "C" {
@@ -219,6 +232,8 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->t1_dec_sort = g_dwt_opts.t1_dec_sort;
     out->t1_dec_bpw = g_dwt_opts.t1_dec_bpw;
     out->mid_th = g_dwt_opts.mid_th;
+    out->t1_enc_bpw = g_dwt_opts.t1_enc_bpw;
+    out->pad_ = 0;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -232,11 +247,14 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->inv01 != 0 && o->inv01 != 2 && o->inv01 != 4) return set_err(GRKGPU_EINVAL, "inv01 must be 0, 2 or 4");
     if (o->pair_group < 0 || o->pair_group > 4096) return set_err(GRKGPU_EINVAL, "pair_group must be 0 .. 4096");
     if (o->f64_lift != 0 && o->f64_lift != 1) return set_err(GRKGPU_EINVAL, "f64_lift must be 0 or 1");
-    if (o->t1_dec_sort != 0 && o->t1_dec_sort != 1) return set_err(GRKGPU_EINVAL, "t1_dec_sort must be 0 or 1");
+    if (o->t1_dec_sort < -1 || o->t1_dec_sort > 1) return set_err(GRKGPU_EINVAL, "t1_dec_sort must be -1, 0 or 1");
     if (o->t1_dec_bpw < 0 || o->t1_dec_bpw > 64 || (o->t1_dec_bpw & (o->t1_dec_bpw - 1)))
         return set_err(GRKGPU_EINVAL, "t1_dec_bpw must be 0 or a power of two <= 64");
     if (o->mid_th != 0 && o->mid_th != 8 && o->mid_th != 16 && o->mid_th != 24)
         return set_err(GRKGPU_EINVAL, "mid_th must be 0, 8, 16 or 24");
+    if (o->t1_enc_bpw < 0 || o->t1_enc_bpw > 64 || (o->t1_enc_bpw & (o->t1_enc_bpw - 1)))
+        return set_err(GRKGPU_EINVAL, "t1_enc_bpw must be 0 or a power of two <= 64");
+    g_dwt_opts.t1_enc_bpw = o->t1_enc_bpw;
     g_dwt_opts.f64_lift = o->f64_lift;
     g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
     g_dwt_opts.t1_dec_bpw = o->t1_dec_bpw;
@@ -961,6 +979,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                          bool export_blocks = false, int force_dist = 0, uint32_t row0 = 0, uint32_t nrows = 0,
                          uint32_t col0 = 0, uint32_t ncols = 0) {
     if (!c || !planes) return set_err(GRKGPU_EINVAL, "null argument");
+    ActiveCall active;
     CodingParams cp;
     int rc = setup_params(img, p, cp);
     if (rc) return rc;
@@ -1840,6 +1859,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                            int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te,
                            uint32_t reduce = 0, const Rect *win = nullptr, uint32_t max_layers = 0) {
     if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
+    ActiveCall active;
     double t_start = now_ms();
     CodingParams cp;
     size_t pos = 0;
@@ -2192,7 +2212,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     seg_first.push_back((uint32_t)dsegs.size());
     bool mixed_sty = false;  // tile-components of different code-block styles: one decode launch per style
     for (uint32_t i = 1; i < nblk; ++i) mixed_sty = mixed_sty || dsty[i] != dsty[0];
-    const bool sort_work = dwt_options().t1_dec_sort && nblk > 64;
+    const bool lone = lone_call();
+    const bool sort_work = (dwt_options().t1_dec_sort == 1 || (dwt_options().t1_dec_sort < 0 && lone)) && nblk > 64;
     if (sort_work || mixed_sty) {
         // blocks grouped by style (a launch each), and -- t1_dec_sort -- since
         // lanes of a wavefront run until its slowest block is done, blocks of
@@ -2296,7 +2317,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                                 c->scratch.as<T1Scratch>() + g.scr0, c->coef.as<int32_t>(), s, c->ubuf.as<uint32_t>(),
                                 0, c->segs.as<DecSeg>(),
                                 (const uint32_t *)(c->segs.as<uint8_t>() + segbytes) + g.b0, g.sty,
-                                roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes + g.b0 : nullptr));
+                                roibytes ? c->segs.as<uint8_t>() + segbytes + sfbytes + g.b0 : nullptr,
+                                lone ? lone_bpw(nblk) : 0));
     HIPCHK(hipEventRecord(c->ev[2], s));
     c->ltimes.clear();
     LaunchLog llog{&c->lev, &c->ltimes};

@@ -112,9 +112,10 @@ struct DwtOptions {
     uint64_t inv01_min_samples = (uint64_t)1 << 23;  // ... when the larger has this many samples
     int32_t pair_group = 0;  // fused level pairs: workgroups walk groups of this many columns top-down (0: row-major)
     int32_t f64_lift = 0;    // forward 9/7 fused pair: lifting in f64 FMA + floor instead of v_mad_i64_i32
-    int32_t t1_dec_sort = 0; // T1 decode: blocks in decreasing order of expected work
+    int32_t t1_dec_sort = -1;  // T1 decode: blocks in decreasing order of expected work (-1: when lone, see lone_bpw)
     int32_t t1_dec_bpw = 0;  // T1 decode: blocks per wavefront (0: by block count)
     int32_t mid_th = 0;      // window rows of a level of 2^21 .. 2^23 samples (0: 8)
+    int32_t t1_enc_bpw = 0;  // T1 encode (MQ coder): blocks per wavefront (0: by block count)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -145,7 +146,7 @@ hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t n
 // cblksty: the CBLKSTY_* mode switches of the codestream (t1_lane.h), 0 = none
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t cblksty = 0);
+                            hipStream_t s, uint32_t cblksty = 0, uint32_t bpw = 0);
 // Per-pass distortion sums of the blocks k_t1_model coded (same sym /
 // sym_off layout): nmsedec[pass] of every block, in the pass order of
 // t1_encode_cblk (t1.cpp:1222-1260).
@@ -161,7 +162,12 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words,
                             const DecSeg *segs = nullptr, const uint32_t *seg_first = nullptr, uint32_t cblksty = 0,
-                            const uint8_t *roi = nullptr);
+                            const uint8_t *roi = nullptr, uint32_t bpw = 0);
+// blocks per wavefront (bpw, a power of two <= 64; 0 = the options' value or
+// the block-count rule) of the T1 kernels' lane-per-block launches, and the
+// rule for a call that has the GPU to itself (lone_bpw): enough wavefronts
+// to give every SIMD of the chip one and a half (1,536), not full lanes
+uint32_t lone_bpw(uint32_t nblocks);
 // 32-bit words of a block's unstuffed-stream region (header + words + carries)
 inline uint32_t t1_unstuff_region_words(uint32_t len) { return 4 + unstuff_word_cap(len) + unstuff_carry_cap(len); }
 hipError_t launch_gather(const uint8_t *hdr, const uint8_t *slab, const GatherItem *items, uint32_t n, uint8_t *dst,

@@ -639,6 +639,12 @@ constexpr int DEC_LANES = 64;
 // block's chain instead, and the 64 blocks of a wavefront execute the union of
 // their paths -- there one block per wavefront (n <= 1024: at most one
 // wavefront per SIMD), then 2, 4, ... up to 64 from 4096 blocks on.
+uint32_t lone_bpw(uint32_t n) {
+    uint32_t b = 1;
+    while (b < 64 && (uint64_t)n >= 1536ull * (2 * b)) b <<= 1;
+    return b;
+}
+
 static uint32_t t1_blocks_per_wave(uint32_t n) {
     uint32_t b = 1;
     while (b < 64 && (uint64_t)n > 1024ull * b) b <<= 1;
@@ -647,14 +653,16 @@ static uint32_t t1_blocks_per_wave(uint32_t n) {
 
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t cblksty) {
+                            hipStream_t s, uint32_t cblksty, uint32_t bpw_req) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
     if (maxdepth > 32) maxdepth = 32;
     uint64_t threads = (uint64_t)n * maxdepth;
     hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
                        scratch, sym, sym_off, res, cblksty);
-    const uint32_t bpw = t1_blocks_per_wave(n);
+    const uint32_t bpw = dwt_options().t1_enc_bpw ? (uint32_t)dwt_options().t1_enc_bpw
+                         : bpw_req                ? bpw_req
+                                                  : t1_blocks_per_wave(n);
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
                            scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty, bpw);
@@ -694,11 +702,13 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coe
 
 hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *data, T1Scratch *scratch,
                             int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words, const DecSeg *segs,
-                            const uint32_t *seg_first, uint32_t cblksty, const uint8_t *roi) {
+                            const uint32_t *seg_first, uint32_t cblksty, const uint8_t *roi, uint32_t bpw_req) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
                        seg_first);
-    const uint32_t bpw = dwt_options().t1_dec_bpw ? (uint32_t)dwt_options().t1_dec_bpw : t1_blocks_per_wave(n);
+    const uint32_t bpw = dwt_options().t1_dec_bpw ? (uint32_t)dwt_options().t1_dec_bpw
+                         : bpw_req                ? bpw_req
+                                                  : t1_blocks_per_wave(n);
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
                            n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi, bpw);

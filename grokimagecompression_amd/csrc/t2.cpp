@@ -1151,6 +1151,7 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
     double min_slope = DBL_MAX, max_slope = -1;
     if (single_lossless(cp, te)) return true;
     const std::vector<EncPass> &P = *te.passes;
+    const double h0 = g_rt.on ? t2_ms() : 0;
     {  // min / max over every pass of every block (order-free), per chunk then combined
         std::mutex mu;
         host_parallel_for(te.blist.size(), 512, [&](size_t b0, size_t b1) {
@@ -1177,6 +1178,7 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
     const double maxSE = tile_max_se(cp, te);
     RateProbe rp;
     probe_init(cp, te, rp);
+    if (g_rt.on) g_rt.hull += t2_ms() - h0;
     double upper = max_slope;
     for (uint32_t layno = 0; layno < cp.numlayers; ++layno) {
         if (layer_needs_rate_control(cp, layno)) {
@@ -1187,7 +1189,10 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
             double thresh = 0;
             for (uint32_t i = 0; i < 128; ++i) {
                 thresh = (upper == -1) ? lower : (lower + upper) / 2;
+                const double f0 = g_rt.on ? t2_ms() : 0;
                 form_layer<false>(cp, te, layno, thresh, false, cp.fixed_quality != 0, rp);
+                ++g_rt.probes;
+                if (g_rt.on) g_rt.form += t2_ms() - f0;
                 if (prevthresh != -1 && (fabs(prevthresh - thresh)) < 0.001) break;
                 prevthresh = thresh;
                 if (cp.fixed_quality) {
@@ -1195,7 +1200,10 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
                     if (achieved < distotarget) { upper = thresh; continue; }
                     lower = thresh;
                 } else {
-                    if (!simulate_tile(cp, te, layno + 1, maxlen, rp)) { lower = thresh; continue; }
+                    const double f1 = g_rt.on ? t2_ms() : 0;
+                    const bool fits = simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    if (g_rt.on) g_rt.sim += t2_ms() - f1;
+                    if (!fits) { lower = thresh; continue; }
                     upper = thresh;
                 }
             }
@@ -1332,7 +1340,7 @@ bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
     const double t0 = trace ? t2_ms() : 0;
     const bool ok = cp.rate_algo == 0 ? pcrd_simple(cp, te, len) : pcrd_feasible(cp, te, len);
     if (trace)
-        fprintf(stderr, "[t2] tile %u blocks %zu: rate %.3f ms = hull %.3f + probes %u (form %.3f, sim %.3f; "
+        fprintf(stderr, "[t2] tile %u blocks %zu: rate %.3f ms = setup %.3f + probes %u (form %.3f, sim %.3f; "
                 "%llu block evals, %llu precinct sims)\n", te.tile->index, te.blist.size(), t2_ms() - t0, g_rt.hull,
                 g_rt.probes, g_rt.form, g_rt.sim, (unsigned long long)g_rt.redo, (unsigned long long)g_rt.precs);
     return ok;
