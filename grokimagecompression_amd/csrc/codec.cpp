@@ -1240,7 +1240,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
-                            c->results.as<EncResult>(), s, cp.cblksty));
+                            c->results.as<EncResult>(), s, cp.cblksty, lone_call() ? lone_bpw(nblk) : 0));
     // per-pass distortion only when some layer is rate-controlled
     // (TileProcessor::needs_rate_control, TileProcessor.cpp:260-266)
     bool need_rc = force_dist != 0;
@@ -2134,9 +2134,9 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         if (terr[lt] == 5)
             return set_err(GRKGPU_ECORRUPT, "QCD marker: number of step sizes is less than 3 * (tile decompositions) + 1");
         if (terr[lt] == 4)
-            return set_err(GRKGPU_EUNSUPPORTED, "tile-component coding style not supported (code-block style "
-                                                "differing from the main header's, MCT over components of different "
-                                                "wavelets, or reduce too large)");
+            return set_err(GRKGPU_EUNSUPPORTED, "tile-component coding style not supported (HT code-block style, "
+                                                "code-blocks above 64 x 64, MCT over components of different "
+                                                "wavelets or sizes, or reduce too large)");
     }
     bool any_roi = false;
     for (uint32_t lt = 0; lt < nsh; ++lt)

@@ -754,6 +754,11 @@ struct RateProbe {
     std::vector<double> lo_d, hi_d;    // simple: largest slope compared false, smallest compared true
     std::vector<uint32_t> lo_u, hi_u;  // feasible: the slope it stopped at, smallest slope it passed
     std::vector<uint8_t> valid;        // bounds hold for the current layer records
+    // blocks a probe still has to check: a block whose bounds hold over the
+    // whole remaining bisection interval [lower, upper] never changes again
+    // in this layer's search (each probe lies in that interval, which only
+    // shrinks), so prune() drops it
+    std::vector<uint32_t> active;
     bool fresh = true;                 // no probe of the current layer yet: evaluate every block
     // packets of layers [0, layers) in THRESH_CALC order, grouped per precinct
     uint32_t layers = 0, nprec = 0, npoc = 0;  // npoc: POC groups per component
@@ -783,6 +788,7 @@ void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
     rp.lo_d.assign(nb, 0); rp.hi_d.assign(nb, 0);
     rp.lo_u.assign(nb, 0); rp.hi_u.assign(nb, 0);
     rp.valid.assign(nb, 0);
+    rp.active.clear();
     rp.dirty.assign(rp.nprec, 1);
     rp.layers = 0;
     rp.fresh = true;
@@ -1077,12 +1083,13 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
             }
         redo.resize(nb);
         for (size_t i = 0; i < nb; ++i) redo[i] = (uint32_t)i;
+        rp.active = redo;
     } else {
-        for (size_t i = 0; i < nb; ++i) {
+        for (uint32_t i : rp.active) {
             bool ok = rp.valid[i] != 0;
             if constexpr (FEASIBLE) ok = ok && rp.lo_u[i] <= (uint32_t)thresh && (uint32_t)thresh < rp.hi_u[i];
             else ok = ok && ((double)thresh - rp.hi_d[i] < DBL_EPSILON) && !((double)thresh - rp.lo_d[i] < DBL_EPSILON);
-            if (!ok) redo.push_back((uint32_t)i);
+            if (!ok) redo.push_back(i);
         }
     }
     std::vector<uint8_t> changed(redo.size());
@@ -1113,6 +1120,29 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         rp.fresh = true;
     }
     if (need_sum || final) sum_layer(te, layno, L);
+}
+
+// RateProbe::active after a probe: keep the blocks whose layer record could
+// still change for some threshold of [L, U] (the bisection interval, ends in
+// either order in the search; every later probe of this layer is a midpoint
+// of two points of it, so lies in it).  The bound tests are monotone in the
+// threshold (a rounded difference is monotone), so a block valid at both ends
+// is valid in between.
+void prune_simple(RateProbe &rp, double L, double U) {
+    size_t k = 0;
+    for (uint32_t i : rp.active) {
+        const bool keep = !rp.valid[i] || !(U - rp.hi_d[i] < DBL_EPSILON) || (L - rp.lo_d[i] < DBL_EPSILON);
+        if (keep) rp.active[k++] = i;
+    }
+    rp.active.resize(k);
+}
+void prune_feasible(RateProbe &rp, uint32_t L, uint32_t U) {
+    size_t k = 0;
+    for (uint32_t i : rp.active) {
+        const bool keep = !rp.valid[i] || !(rp.lo_u[i] <= L && U < rp.hi_u[i]);
+        if (keep) rp.active[k++] = i;
+    }
+    rp.active.resize(k);
 }
 
 bool layer_needs_rate_control(const CodingParams &cp, uint32_t layno) {
@@ -1203,8 +1233,9 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
                     const double f1 = g_rt.on ? t2_ms() : 0;
                     const bool fits = simulate_tile(cp, te, layno + 1, maxlen, rp);
                     if (g_rt.on) g_rt.sim += t2_ms() - f1;
-                    if (!fits) { lower = thresh; continue; }
-                    upper = thresh;
+                    if (!fits) lower = thresh;
+                    else upper = thresh;
+                    if (upper != -1) prune_simple(rp, std::min(lower, upper), std::max(lower, upper));
                 }
             }
             const double good = (upper == -1) ? thresh : upper;
@@ -1313,8 +1344,9 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
                         g_rt.form += f1 - f0;
                         g_rt.sim += f2 - f1;
                     }
-                    if (!fits) { lower = thresh; continue; }
-                    upper = thresh;
+                    if (!fits) lower = thresh;
+                    else upper = thresh;
+                    prune_feasible(rp, std::min(lower, upper), std::max(lower, upper));
                 }
             }
             form_layer<true>(cp, te, layno, (uint16_t)upper, true, true, rp);
