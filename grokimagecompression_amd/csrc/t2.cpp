@@ -740,7 +740,7 @@ bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ui
 struct RateTrace {
     bool on = false;
     double hull = 0, form = 0, sim = 0;
-    uint32_t probes = 0;
+    uint32_t probes = 0, skipped = 0;
     uint64_t redo = 0, precs = 0;
 };
 thread_local RateTrace g_rt;
@@ -759,10 +759,23 @@ struct RateProbe {
     // in this layer's search (each probe lies in that interval, which only
     // shrinks), so prune() drops it
     std::vector<uint32_t> active;
+    // code-block bytes of the layer records of layers [0, layno]: in total
+    // and per component (kept up to date by form_layer); without SOP / EPH a
+    // probe whose bytes exceed the budget, or a component cap, cannot fit
+    // (simulate_tile's budget never wraps then), so it needs no simulation
+    std::vector<uint8_t> comp;          // per block: its component
+    uint64_t body_prev = 0;             // layers below layno (fixed during its search)
+    std::vector<uint64_t> comp_prev;
+    int64_t body = 0;                   // layer layno
+    std::vector<int64_t> comp_body;
     bool fresh = true;                 // no probe of the current layer yet: evaluate every block
     // packets of layers [0, layers) in THRESH_CALC order, grouped per precinct
     uint32_t layers = 0, nprec = 0, npoc = 0;  // npoc: POC groups per component
     bool bad = false;
+    // the plan holds every precinct holding code-blocks once per layer (so
+    // the simulated packets carry exactly the layer records' bytes), and
+    // comp_exact: each component's groups hold only that component's packets
+    bool body_exact = false, comp_exact = false;
     std::vector<PacketId> order;
     std::vector<size_t> group_end;     // end index of each (compno, poc) group
     std::vector<uint32_t> head, pos;   // packets of precinct p: order[pos[head[p] .. head[p + 1])]
@@ -773,16 +786,24 @@ struct RateProbe {
 // precinct ids of te.blist (a precinct = one resolution's precinct of a component)
 void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
     rp.prec.clear();
+    rp.comp.clear();
     uint32_t base = 0;
     for (uint32_t k = 0; k < cp.numcomps; ++k) {
         TileComp &tc = te.tile->comps[k];
         for (auto &res : tc.res) {
             for (uint32_t b = 0; b < res.numbands; ++b)
                 for (size_t p = 0; p < res.bands[b].precs.size(); ++p)
-                    for (size_t n = 0; n < res.bands[b].precs[p].cblks.size(); ++n) rp.prec.push_back(base + (uint32_t)p);
+                    for (size_t n = 0; n < res.bands[b].precs[p].cblks.size(); ++n) {
+                        rp.prec.push_back(base + (uint32_t)p);
+                        rp.comp.push_back((uint8_t)k);
+                    }
             base += res.pw * res.ph;
         }
     }
+    rp.body_prev = 0;
+    rp.comp_prev.assign(cp.numcomps, 0);
+    rp.body = 0;
+    rp.comp_body.assign(cp.numcomps, 0);
     rp.nprec = base;
     const size_t nb = rp.prec.size();
     rp.lo_d.assign(nb, 0); rp.hi_d.assign(nb, 0);
@@ -840,6 +861,17 @@ void probe_plan(CodingParams &cp, TileEnc &te, uint32_t max_layers, RateProbe &r
     for (uint32_t p = 0; p < nprec && !rp.bad; ++p)
         for (uint32_t q = rp.head[p] + 1; q < rp.head[p + 1]; ++q)
             if (rp.order[rp.pos[q]].layno <= rp.order[rp.pos[q - 1]].layno) rp.bad = true;
+    {
+        std::vector<uint8_t> has(nprec, 0);
+        for (uint32_t p : rp.prec) has[p] = 1;
+        rp.body_exact = !rp.bad;
+        for (uint32_t p = 0; p < nprec && rp.body_exact; ++p)
+            if (has[p] && rp.head[p + 1] - rp.head[p] != max_layers) rp.body_exact = false;
+        rp.comp_exact = rp.body_exact;
+        for (size_t gi = 0, i = 0; gi < rp.group_end.size() && rp.comp_exact; ++gi)
+            for (; i < rp.group_end[gi]; ++i)
+                if (max_comp > 1 && rp.order[i].compno != gi / rp.npoc) { rp.comp_exact = false; break; }
+    }
     rp.hbytes.assign(rp.order.size(), 0);
     rp.dbytes.assign(rp.order.size(), 0);
     rp.dirty.assign(nprec, 1);
@@ -1062,7 +1094,8 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     const uint32_t L = cp.numlayers;
     const std::vector<EncPass> &P = *te.passes;
     const size_t nb = te.blist.size();
-    auto eval = [&](size_t i) -> bool {  // true if the block's layer record changed
+    // true if the block's layer record changed; *dlen = its change of bytes
+    auto eval = [&](size_t i, int64_t *dlen) -> bool {
         Cblk &c = *te.blist[i];
         EncCblkState &s = (*te.cblk)[c.gidx];
         uint32_t cumul;
@@ -1070,7 +1103,9 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.lo_d[i], &rp.hi_d[i]);
         EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + layno];
         const uint32_t old = ly.numpasses;
+        const int64_t oldlen = old ? (int64_t)ly.len : 0;
         set_layer(te, c.gidx, layno, L, cumul);
+        *dlen = (ly.numpasses ? (int64_t)ly.len : 0) - oldlen;
         return ly.numpasses != old;
     };
     std::vector<uint32_t> redo;
@@ -1093,18 +1128,33 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         }
     }
     std::vector<uint8_t> changed(redo.size());
+    std::vector<int64_t> dlen(redo.size());
     g_rt.redo += redo.size();
     if (redo.size() > 2048) {
         host_parallel_for(redo.size(), 256, [&](size_t a, size_t b) {
-            for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j]);
+            for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j], &dlen[j]);
         });
     } else {
-        for (size_t j = 0; j < redo.size(); ++j) changed[j] = eval(redo[j]);
+        for (size_t j = 0; j < redo.size(); ++j) changed[j] = eval(redo[j], &dlen[j]);
     }
     const bool keep = !final && (FEASIBLE || thresh != 0);
+    if (full) {  // the layer's bytes from scratch (records of earlier probes included)
+        rp.body = 0;
+        std::fill(rp.comp_body.begin(), rp.comp_body.end(), 0);
+        for (size_t i = 0; i < nb; ++i) {
+            const EncLayer &ly = (*te.layers)[(size_t)te.blist[i]->gidx * L + layno];
+            if (!ly.numpasses) continue;
+            rp.body += ly.len;
+            rp.comp_body[rp.comp[i]] += ly.len;
+        }
+    }
     for (size_t j = 0; j < redo.size(); ++j) {
         const uint32_t i = redo[j];
         if (changed[j]) rp.dirty[rp.prec[i]] = 1;
+        if (!full) {
+            rp.body += dlen[j];
+            rp.comp_body[rp.comp[i]] += dlen[j];
+        }
         rp.valid[i] = keep;
     }
     rp.fresh = false;
@@ -1118,8 +1168,26 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         // simulate a different layer count (a new plan)
         std::fill(rp.valid.begin(), rp.valid.end(), 0);
         rp.fresh = true;
+        rp.body_prev += (uint64_t)rp.body;
+        for (size_t k = 0; k < rp.comp_prev.size(); ++k) rp.comp_prev[k] += (uint64_t)rp.comp_body[k];
+        rp.body = 0;
+        std::fill(rp.comp_body.begin(), rp.comp_body.end(), 0);
     }
     if (need_sum || final) sum_layer(te, layno, L);
+}
+
+// The probe's code-block bytes alone exceed the budget or a component cap:
+// simulate_tile would return false (without SOP / EPH its running budget
+// only shrinks by what each packet writes, so it never wraps).
+bool body_over(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len, RateProbe &rp) {
+    if (cp.csty & (CSTY_SOP | CSTY_EPH)) return false;
+    if (rp.layers != max_layers) probe_plan(cp, te, max_layers, rp);
+    if (!rp.body_exact) return false;  // the walk's packets are not the records' bytes once each
+    if (rp.body_prev + (uint64_t)rp.body > max_len) return true;
+    if (cp.max_comp_size && rp.comp_exact)
+        for (size_t k = 0; k < rp.comp_body.size(); ++k)
+            if (rp.comp_prev[k] + (uint64_t)rp.comp_body[k] > cp.max_comp_size) return true;
+    return false;
 }
 
 // RateProbe::active after a probe: keep the blocks whose layer record could
@@ -1231,7 +1299,9 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
                     lower = thresh;
                 } else {
                     const double f1 = g_rt.on ? t2_ms() : 0;
-                    const bool fits = simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    const bool over = body_over(cp, te, layno + 1, maxlen, rp);
+                    g_rt.skipped += over;
+                    const bool fits = !over && simulate_tile(cp, te, layno + 1, maxlen, rp);
                     if (g_rt.on) g_rt.sim += t2_ms() - f1;
                     if (!fits) lower = thresh;
                     else upper = thresh;
@@ -1338,7 +1408,9 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
                     lower = thresh;
                 } else {
                     const double f1 = g_rt.on ? t2_ms() : 0;
-                    const bool fits = simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    const bool over = body_over(cp, te, layno + 1, maxlen, rp);
+                    g_rt.skipped += over;
+                    const bool fits = !over && simulate_tile(cp, te, layno + 1, maxlen, rp);
                     if (g_rt.on) {
                         const double f2 = t2_ms();
                         g_rt.form += f1 - f0;
@@ -1373,8 +1445,9 @@ bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
     const bool ok = cp.rate_algo == 0 ? pcrd_simple(cp, te, len) : pcrd_feasible(cp, te, len);
     if (trace)
         fprintf(stderr, "[t2] tile %u blocks %zu: rate %.3f ms = setup %.3f + probes %u (form %.3f, sim %.3f; "
-                "%llu block evals, %llu precinct sims)\n", te.tile->index, te.blist.size(), t2_ms() - t0, g_rt.hull,
-                g_rt.probes, g_rt.form, g_rt.sim, (unsigned long long)g_rt.redo, (unsigned long long)g_rt.precs);
+                "%llu block evals, %llu precinct sims, %u probes over budget by their code-block bytes)\n", te.tile->index,
+                te.blist.size(), t2_ms() - t0, g_rt.hull, g_rt.probes, g_rt.form, g_rt.sim,
+                (unsigned long long)g_rt.redo, (unsigned long long)g_rt.precs, g_rt.skipped);
     return ok;
 }
 
