@@ -118,7 +118,11 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const uint32_t sh = 3 * r;
         const uint32_t zcx = T.zc[(P >> sh) & 0x1FF];  // read for every kind (LDS, in bounds)
         keep_here(zcx);
-        const uint32_t cx = kind == 0 ? zcx : kind == 1 ? (si & 0x7f) : kind == 2 ? (uint32_t)CX_AGG : (uint32_t)CX_UNI;
+        // context of the symbol kind, as mask arithmetic (a select chain
+        // here compiled to exec-mask branches around each arm)
+        const uint32_t m0 = 0u - (uint32_t)(kind == 0), m1 = 0u - (uint32_t)(kind == 1);
+        const uint32_t cx = (zcx & m0) | ((si & 0x7fu) & m1) |
+                            (((uint32_t)CX_AGG + (uint32_t)(kind > 2)) & ~(m0 | m1));
         const uint32_t bit = d.decode(cxw, T.mq, cx);
         if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
         const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;

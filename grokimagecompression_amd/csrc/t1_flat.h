@@ -163,6 +163,11 @@ struct BitDecT {
     static constexpr bool kLazy = LAZY;
     FlatBits bits;
     uint32_t A, C, consumed, cq, cqn;  // cq: next carry event, cqn: the one after
+    // the stream word after W's bits, read from the ring one refill ahead:
+    // a refill only ORs it in, and the LDS read of the following word has
+    // until the next refill to land (a refill that waits on its own read
+    // stalls the whole wavefront at almost every decision step)
+    uint32_t nextw;
     const uint32_t *cp;
     bool raw;  // the current segment is raw (BYPASS): bits straight from the stream
     // the lane's word ring (FlatBits), set once before the first init
@@ -180,15 +185,18 @@ struct BitDecT {
         const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
         bits.W = (w0 << 32) | w1;
         bits.NB = 64;
+        nextw = fb_word(bits);
         raw = true;
+    }
+    GRK_HD void refill() {
+        bits.W |= (uint64_t)nextw << (32 - bits.NB);
+        bits.NB += 32;
+        nextw = fb_word(bits);
     }
     GRK_HD uint32_t rawbit() {
         const uint32_t b = (uint32_t)(bits.W >> 63);
         bits.W <<= 1;
-        if (--bits.NB < 32) {
-            bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
-            bits.NB += 32;
-        }
+        if (--bits.NB < 32) refill();
         return b;
     }
     GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
@@ -201,6 +209,7 @@ struct BitDecT {
         bits.NB = 33;
         A = 0x8000;
         consumed = 31;
+        nextw = fb_word(bits);
         cq = carries[0];
         cp = carries + 1;
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
@@ -235,10 +244,7 @@ struct BitDecT {
         const uint32_t c1 = consumed + n;
         if (cq < c1) { C += 1u << (16 + c1 - cq); next_carry(); }  // carry event (see Unstuff)
         consumed = c1;
-        if (bits.NB < 32) {
-            bits.W |= (uint64_t)fb_word(bits) << (32 - bits.NB);
-            bits.NB += 32;
-        }
+        if (bits.NB < 32) refill();
         cxw[cx] = keep ? wd : (tw | (nmps << 31));  // unconditional LDS write: no branch
 #ifdef T1_TRACE
         T1_TRACE(cx, mps ^ (uint32_t)lps, A, C >> 16);
