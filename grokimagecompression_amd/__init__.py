@@ -195,7 +195,9 @@ class Stats(ctypes.Structure):
                 ("t1_ms", ctypes.c_float), ("gather_ms", ctypes.c_float), ("d2h_ms", ctypes.c_float),
                 ("host_t2_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("num_cblks", ctypes.c_uint64),
                 ("cs_bytes", ctypes.c_uint64), ("mq_symbols", ctypes.c_uint64), ("rate_ms", ctypes.c_float),
-                ("packet_ms", ctypes.c_float)]
+                ("packet_ms", ctypes.c_float), ("rate_probes", ctypes.c_uint32), ("rate_probes_skipped", ctypes.c_uint32),
+                ("rate_block_evals", ctypes.c_uint64), ("rate_precinct_sims", ctypes.c_uint64),
+                ("rate_form_ms", ctypes.c_float), ("rate_sim_ms", ctypes.c_float)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -1469,6 +1469,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         std::vector<PlanItem> plan;
         std::vector<uint8_t> tlm;
         double rate_ms = 0, packet_ms = 0;
+        RateStats rs;
         bool ok = true;
     };
     std::vector<TileOut> touts(tiles.size());
@@ -1490,7 +1491,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             tenc.distotile = 0;
             for (auto &tc : tile.comps) for_each_cblk(tc, [&](Band &, Cblk &cb) { tenc.distotile += blk_disto[cb.gidx]; });
             const double tr0 = now_ms();
-            if (!rate_allocate(cpt, tenc, tile_bound)) { to.ok = false; continue; }
+            if (!rate_allocate(cpt, tenc, tile_bound, &to.rs)) { to.ok = false; continue; }
             const double tp0 = now_ms();
             to.rate_ms = tp0 - tr0;
             // The tile-parts' packets (T2::encode_packets per tile-part,
@@ -1580,10 +1581,17 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         }
     });
     double t_packets = 0;
+    RateStats rsum;
     for (auto &to : touts) {
         if (!to.ok) return set_err(GRKGPU_EINVAL, "rate allocation failed");
         t_rate += to.rate_ms;
         t_packets += to.packet_ms;
+        rsum.probes += to.rs.probes;
+        rsum.skipped += to.rs.skipped;
+        rsum.evals += to.rs.evals;
+        rsum.sims += to.rs.sims;
+        rsum.form_ms += to.rs.form_ms;
+        rsum.sim_ms += to.rs.sim_ms;
         const uint64_t base = hdr.size();
         hdr.putn(to.hdr.v.data(), to.hdr.size());
         for (PlanItem it : to.plan) {
@@ -1645,6 +1653,12 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     st.mq_symbols = nsym;
     st.rate_ms = (float)t_rate;
     st.packet_ms = (float)t_packets;
+    st.rate_probes = rsum.probes;
+    st.rate_probes_skipped = rsum.skipped;
+    st.rate_block_evals = rsum.evals;
+    st.rate_precinct_sims = rsum.sims;
+    st.rate_form_ms = (float)rsum.form_ms;
+    st.rate_sim_ms = (float)rsum.sim_ms;
     return GRKGPU_OK;
 }
 

@@ -14,8 +14,6 @@
 #include <float.h>
 #include <limits.h>
 #include <math.h>
-#include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -736,9 +734,9 @@ bool simulate_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ui
 //    only the precincts holding a block whose layer record changed since the
 //    last probe are simulated again; the packet order for a layer count is
 //    built once.
-// GRKGPU_T2_TRACE=1: per-tile breakdown of the rate allocation on stderr
+// the current rate allocation's RateStats (one allocation per thread at a time)
 struct RateTrace {
-    bool on = false;
+    bool on = true;
     double hull = 0, form = 0, sim = 0;
     uint32_t probes = 0, skipped = 0;
     uint64_t redo = 0, precs = 0;
@@ -1433,21 +1431,21 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
 
 }  // namespace
 
-bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len) {
+bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st) {
     te.distolayer.assign(cp.numlayers + 1, 0.0);
     te.blist.clear();
     for_each_block(te, [&](Cblk &c) { te.blist.push_back(&c); });
     if (!(cp.disto_alloc || cp.fixed_quality)) return true;
-    static const bool trace = getenv("GRKGPU_T2_TRACE") && atoi(getenv("GRKGPU_T2_TRACE"));
     g_rt = RateTrace{};
-    g_rt.on = trace;
-    const double t0 = trace ? t2_ms() : 0;
     const bool ok = cp.rate_algo == 0 ? pcrd_simple(cp, te, len) : pcrd_feasible(cp, te, len);
-    if (trace)
-        fprintf(stderr, "[t2] tile %u blocks %zu: rate %.3f ms = setup %.3f + probes %u (form %.3f, sim %.3f; "
-                "%llu block evals, %llu precinct sims, %u probes over budget by their code-block bytes)\n", te.tile->index,
-                te.blist.size(), t2_ms() - t0, g_rt.hull, g_rt.probes, g_rt.form, g_rt.sim,
-                (unsigned long long)g_rt.redo, (unsigned long long)g_rt.precs, g_rt.skipped);
+    if (st) {
+        st->probes = g_rt.probes;
+        st->skipped = g_rt.skipped;
+        st->evals = g_rt.redo;
+        st->sims = g_rt.precs;
+        st->form_ms = g_rt.form;
+        st->sim_ms = g_rt.sim;
+    }
     return ok;
 }
 

@@ -98,7 +98,15 @@ bool write_packet(const CodingParams &cp, TileEnc &te, const PacketId &pk, ByteB
 
 // Rate allocation (TileProcessor::rate_allocate_encode, TileProcessor.cpp:
 // 1649-1683): forms every layer of the tile; len = the tile buffer bound.
-bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len);
+// what the bisection did (grkgpu_stats rate_*): probes, probes decided by
+// their code-block bytes alone, block evaluations, precinct simulations and
+// the time forming layers / simulating packets
+struct RateStats {
+    uint32_t probes = 0, skipped = 0;
+    uint64_t evals = 0, sims = 0;
+    double form_ms = 0, sim_ms = 0;
+};
+bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st = nullptr);
 
 // distortion weight of a pass (t1_getwmsedec, t1.cpp:912-930)
 double t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno, uint32_t qmfbid,

@@ -148,6 +148,13 @@ typedef struct {
     uint64_t mq_symbols;  /* MQ symbols coded (encode) */
     float rate_ms;        /* host rate allocation (PCRD) time (summed over tiles) */
     float packet_ms;      /* host packet / tile-part writing time (summed over tiles) */
+    /* the PCRD bisection, summed over tiles: probes (thresholds tried), those
+     * decided by their code-block bytes alone (no packet simulation), block
+     * evaluations, precinct simulations, and the time forming layers /
+     * simulating packets (part of rate_ms) */
+    uint32_t rate_probes, rate_probes_skipped;
+    uint64_t rate_block_evals, rate_precinct_sims;
+    float rate_form_ms, rate_sim_ms;
 } grkgpu_stats;
 
 /* One kernel launch of the last call's forward DWT, timed with HIP events on

@@ -105,7 +105,8 @@ int main(int argc, char **argv) {
         te.distotile = distotile;
         CodingParams cpt = cp;
         const auto t0 = std::chrono::steady_clock::now();
-        if (!rate_allocate(cpt, te, (uint64_t)(budget * 1.2))) { printf("rate_allocate failed\n"); return 1; }
+        RateStats rs;
+        if (!rate_allocate(cpt, te, (uint64_t)(budget * 1.2), &rs)) { printf("rate_allocate failed\n"); return 1; }
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         best = std::min(best, ms);
         digest = 1469598103934665603ull;
@@ -115,7 +116,10 @@ int main(int argc, char **argv) {
             digest = (digest ^ ly.len) * 1099511628211ull;
             tot += ly.len;
         }
-        if (rep == 0) printf("blocks %zu passes %zu bytes %llu ", cst.size(), passes.size(), (unsigned long long)tot);
+        if (rep == 0)
+            printf("blocks %zu passes %zu bytes %llu probes %u (%u by bytes alone) evals %llu sims %llu form_ms %.2f "
+                   "sim_ms %.2f ", cst.size(), passes.size(), (unsigned long long)tot, rs.probes, rs.skipped,
+                   (unsigned long long)rs.evals, (unsigned long long)rs.sims, rs.form_ms, rs.sim_ms);
     }
     printf("digest %016llx best_ms %.3f\n", (unsigned long long)digest, best);
     return 0;
