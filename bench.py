@@ -377,6 +377,10 @@ def main():
                          "enc_msym_per_s": round(se["mq_symbols"] / (se["t1_ms"] * 1e-3) / 1e6, 1),
                          "dec_msym_per_s": round(se["mq_symbols"] / (sd["t1_ms"] * 1e-3) / 1e6, 1)},
           "note": "symbols = MQ decisions of the encoder (the decoder decodes the same ones)"}
+    # the same lone frame's stages (the batch's stage_ms are one call among 16 in flight)
+    keys = ("t1_ms", "host_t2_ms", "rate_ms", "packet_ms", "total_ms")
+    t1["lone_frame"]["stage_ms"] = {"enc": {k: round(se[k], 3) for k in keys},
+                                    "dec": {k: round(sd[k], 3) for k in keys}}
     roof_mpix = HBM_PEAK_GBS * 1e9 / b_e2e(C, BITS) / 1e6
     e2e = {"B_e2e_bytes_per_px": round(b_e2e(C, BITS), 3), "roofline_mpix_per_s": round(roof_mpix, 1),
            "frac": round(value / world / roof_mpix, 5)}
