@@ -209,7 +209,7 @@ class DwtOptions(ctypes.Structure):
                 ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("pair_group", ctypes.c_int32),
                 ("inv01_min_samples", ctypes.c_uint64), ("f64_lift", ctypes.c_int32), ("t1_dec_sort", ctypes.c_int32),
                 ("t1_dec_bpw", ctypes.c_int32), ("mid_th", ctypes.c_int32),
-                ("t1_enc_bpw", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("t1_enc_bpw", ctypes.c_int32), ("t1_enc_sort", ctypes.c_int32)]
 
 
 class LaunchTime(ctypes.Structure):

@@ -89,6 +89,7 @@ struct grkgpu_ctx {
     DevBuf img, work, coef, ll, scratch, mqout, blocks, results, gather, packed, cs, sym, symoff, dwtjobs, ubuf, segs;
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs, h_segs;
     DevBuf dwtjobs53;  // decode: the 5/3 tile-components' job table when 9/7 ones share the call
+    DevBuf t1order;    // encode: the MQ coder's work order (keys, permutation, bucket counters)
     HostBuf h_dwtjobs53;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
@@ -233,7 +234,7 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->t1_dec_bpw = g_dwt_opts.t1_dec_bpw;
     out->mid_th = g_dwt_opts.mid_th;
     out->t1_enc_bpw = g_dwt_opts.t1_enc_bpw;
-    out->pad_ = 0;
+    out->t1_enc_sort = g_dwt_opts.t1_enc_sort;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -254,6 +255,8 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
         return set_err(GRKGPU_EINVAL, "mid_th must be 0, 8, 16 or 24");
     if (o->t1_enc_bpw < 0 || o->t1_enc_bpw > 64 || (o->t1_enc_bpw & (o->t1_enc_bpw - 1)))
         return set_err(GRKGPU_EINVAL, "t1_enc_bpw must be 0 or a power of two <= 64");
+    if (o->t1_enc_sort != 0 && o->t1_enc_sort != 1) return set_err(GRKGPU_EINVAL, "t1_enc_sort must be 0 or 1");
+    g_dwt_opts.t1_enc_sort = o->t1_enc_sort;
     g_dwt_opts.t1_enc_bpw = o->t1_enc_bpw;
     g_dwt_opts.f64_lift = o->f64_lift;
     g_dwt_opts.t1_dec_sort = o->t1_dec_sort;
@@ -1120,6 +1123,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
     HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
+    HIPCHK(c->t1order.ensure((size_t)t1_order_words(nblk) * 4 + 256));
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
     HIPCHK(c->results.ensure((size_t)nblk * sizeof(EncResult) + 256));
@@ -1240,7 +1244,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
-                            c->results.as<EncResult>(), s, cp.cblksty, lone_call() ? lone_bpw(nblk) : 0));
+                            c->results.as<EncResult>(), s, cp.cblksty, lone_call() ? lone_bpw(nblk) : 0,
+                            c->t1order.as<uint32_t>()));
     // per-pass distortion only when some layer is rate-controlled
     // (TileProcessor::needs_rate_control, TileProcessor.cpp:260-266)
     bool need_rc = force_dist != 0;

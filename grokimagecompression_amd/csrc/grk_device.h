@@ -112,10 +112,11 @@ struct DwtOptions {
     uint64_t inv01_min_samples = (uint64_t)1 << 23;  // ... when the larger has this many samples
     int32_t pair_group = 0;  // fused level pairs: workgroups walk groups of this many columns top-down (0: row-major)
     int32_t f64_lift = 0;    // forward 9/7 fused pair: lifting in f64 FMA + floor instead of v_mad_i64_i32
-    int32_t t1_dec_sort = -1;  // T1 decode: blocks in decreasing order of expected work (-1: when lone, see lone_bpw)
+    int32_t t1_dec_sort = 1;   // T1 decode: blocks in decreasing order of expected work (-1: only a lone call)
     int32_t t1_dec_bpw = 0;  // T1 decode: blocks per wavefront (0: by block count)
     int32_t mid_th = 0;      // window rows of a level of 2^21 .. 2^23 samples (0: 8)
     int32_t t1_enc_bpw = 0;  // T1 encode (MQ coder): blocks per wavefront (0: by block count)
+    int32_t t1_enc_sort = 1; // T1 encode: MQ coder lanes take the blocks heaviest first (device counting sort)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -146,7 +147,9 @@ hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t n
 // cblksty: the CBLKSTY_* mode switches of the codestream (t1_lane.h), 0 = none
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t cblksty = 0, uint32_t bpw = 0);
+                            hipStream_t s, uint32_t cblksty = 0, uint32_t bpw = 0, uint32_t *order = nullptr);
+// device words the MQ coder's work order needs (launch_t1_encode `order`)
+uint32_t t1_order_words(uint32_t nblocks);
 // Per-pass distortion sums of the blocks k_t1_model coded (same sym /
 // sym_off layout): nmsedec[pass] of every block, in the pass order of
 // t1_encode_cblk (t1.cpp:1222-1260).

@@ -268,6 +268,51 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     r.nsym = nsym;
 }
 
+// Work order for k_t1_mq (the decoder's host-side order, on the device: the
+// encoder's work per block is only known after k_t1_model).  A counting sort
+// of the blocks by their symbol count, heaviest first, in MQ_ORDER_BUCKETS
+// log-spaced buckets (8 per octave): per block its bucket, a histogram with
+// vector atomics, an exclusive scan in one workgroup, then a scatter.  The
+// order inside a bucket follows the atomics (it varies from run to run);
+// every block's output is its own, so the codestream does not.
+constexpr uint32_t MQ_ORDER_BUCKETS = 256;
+__device__ __forceinline__ uint32_t mq_work_bucket(const T1Scratch &s, uint32_t numbps) {
+    uint32_t w = 0;
+    for (uint32_t q = 0; q < numbps && q < 32; ++q) w += s.cnt[q * 4] + s.cnt[q * 4 + 1] + s.cnt[q * 4 + 2];
+    w += 1;
+    const uint32_t o = 31u - (uint32_t)__builtin_clz(w);            // octave
+    const uint32_t f = o >= 3 ? (w >> (o - 3)) & 7u : (w << (3 - o)) & 7u;  // 3 bits below the top one
+    return (MQ_ORDER_BUCKETS - 1) - min((o << 3) | f, MQ_ORDER_BUCKETS - 1);  // heaviest first
+}
+__global__ __launch_bounds__(256) void k_mq_order_hist(const T1Scratch *__restrict__ scr,
+                                                      const EncResult *__restrict__ res, uint32_t n,
+                                                      uint32_t *__restrict__ key, uint32_t *__restrict__ hist) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = mq_work_bucket(scr[i], res[i].numbps);
+    key[i] = k;
+    atomicAdd(&hist[k], 1u);
+}
+__global__ __launch_bounds__(MQ_ORDER_BUCKETS) void k_mq_order_scan(uint32_t *__restrict__ hist) {
+    __shared__ uint32_t s[MQ_ORDER_BUCKETS];
+    const uint32_t t = threadIdx.x;
+    s[t] = hist[t];
+    __syncthreads();
+    for (uint32_t d = 1; d < MQ_ORDER_BUCKETS; d <<= 1) {  // inclusive Hillis-Steele scan
+        const uint32_t v = t >= d ? s[t - d] : 0u;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    hist[t] = s[t] - hist[t];  // exclusive: the bucket's first slot
+}
+__global__ __launch_bounds__(256) void k_mq_order_scatter(const uint32_t *__restrict__ key, uint32_t n,
+                                                         uint32_t *__restrict__ next, uint32_t *__restrict__ perm) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    perm[atomicAdd(&next[key[i]], 1u)] = i;
+}
+
 // Per-pass distortion sums (the nmsedec of t1_enc_sigpass / refpass /
 // clnpass, t1.cpp:197-338, 443-555, 639-782 with t1_getnmsedec_sig/_ref
 // :155-166): one wavefront per block, lane = column.  A sample contributes
@@ -651,9 +696,11 @@ static uint32_t t1_blocks_per_wave(uint32_t n) {
     return n >= 4096 ? 64 : b;
 }
 
+uint32_t t1_order_words(uint32_t n) { return 2 * n + MQ_ORDER_BUCKETS; }
+
 hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
-                            hipStream_t s, uint32_t cblksty, uint32_t bpw_req) {
+                            hipStream_t s, uint32_t cblksty, uint32_t bpw_req, uint32_t *order) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
     if (maxdepth > 32) maxdepth = 32;
@@ -663,12 +710,22 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     const uint32_t bpw = dwt_options().t1_enc_bpw ? (uint32_t)dwt_options().t1_enc_bpw
                          : bpw_req                ? bpw_req
                                                   : t1_blocks_per_wave(n);
+    const uint32_t *perm = nullptr;
+    if (order && dwt_options().t1_enc_sort && n > 64) {  // order: t1_order_words(n) words
+        uint32_t *key = order, *permw = order + n, *hist = order + 2 * n;
+        const hipError_t e = hipMemsetAsync(hist, 0, MQ_ORDER_BUCKETS * 4, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_mq_order_hist, dim3((n + 255) / 256), dim3(256), 0, s, scratch, res, n, key, hist);
+        hipLaunchKernelGGL(k_mq_order_scan, dim3(1), dim3(MQ_ORDER_BUCKETS), 0, s, hist);
+        hipLaunchKernelGGL(k_mq_order_scatter, dim3((n + 255) / 256), dim3(256), 0, s, key, n, hist, permw);
+        perm = permw;
+    }
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty, bpw);
+                           scratch, sym, sym_off, out, res, perm, cblksty, bpw);
     else
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           scratch, sym, sym_off, out, res, (const uint32_t *)nullptr, cblksty, bpw);
+                           scratch, sym, sym_off, out, res, perm, cblksty, bpw);
     return hipGetLastError();
 }
 

@@ -213,11 +213,11 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    kernel, not the fused DC-shift loads): 0 the
  *                    64-bit integer multiply (v_mad_i64_i32), 1 f64 FMA +
  *                    floor (bit-identical results).
- *   t1_dec_sort      T1 decode: 1 = code-blocks handed to the lanes in
- *                    decreasing order of expected work (passes, bytes), so a
- *                    wavefront's lanes finish close together; 0 = stream
- *                    order; -1 (default) = 1 for a call that is the only one
- *                    in progress in the process, else 0.  Same output.
+ *   t1_dec_sort      T1 decode: 1 (default) = code-blocks handed to the
+ *                    lanes in decreasing order of expected work (passes,
+ *                    bytes), so a wavefront's lanes finish close together;
+ *                    0 = stream order; -1 = only for a call that is the only
+ *                    one in progress in the process.  Same output.
  *   t1_dec_bpw       T1 decode: code-blocks per wavefront (1, 2, 4 .. 64);
  *                    0 (default) = a lone call spreads its blocks to give
  *                    every SIMD 1.5 wavefronts, concurrent calls pack 64 (from
@@ -225,7 +225,11 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *   mid_th           window rows (8, 16, 24) of the per-level DWT kernels for
  *                    a level of 2^21 .. 2^23 samples; 0 (default) = 8.
  *   t1_enc_bpw       T1 encode (MQ coder): code-blocks per wavefront, as
- *                    t1_dec_bpw. */
+ *                    t1_dec_bpw.
+ *   t1_enc_sort      T1 encode: 1 (default) = the MQ coder's lanes take the
+ *                    code-blocks in decreasing order of their symbol count (a
+ *                    counting sort on the device after the modelling kernel);
+ *                    0 = block order.  Same codestream. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -239,7 +243,7 @@ typedef struct {
     int32_t t1_dec_bpw;
     int32_t mid_th;
     int32_t t1_enc_bpw;
-    int32_t pad_;
+    int32_t t1_enc_sort;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */

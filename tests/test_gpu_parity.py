@@ -39,6 +39,24 @@ def test_encode_matches_reference_bytes(codec, name):
     assert b == gold
 
 
+@pytest.mark.parametrize("name", ["rgb12_I", "g8_M4_termall", "rgb8_prec_r20_rpcl", "g16_M5_lazy_termall",
+                                  "rgb12_cinema4k"])
+@pytest.mark.parametrize("opts", [dict(t1_enc_sort=0), dict(t1_enc_sort=1, t1_enc_bpw=16)])
+def test_encode_mq_lane_order_matches_reference(codec, name, opts):
+    """The MQ coder's lanes take the blocks in the device work order
+    (t1_enc_sort, default on) or in block order, packed 64 or 16 to a
+    wavefront: the same codestream as the reference either way."""
+    import grokimagecompression_amd as grk
+    if name not in MAN:
+        pytest.skip("fixture %s absent" % name)
+    m = MAN[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    with grk.dwt_options(**opts):
+        b = codec.compress(img, bits, p, offset=off)
+    assert b == open(f"{GOLD}/{name}.j2k", "rb").read()
+
+
 @pytest.mark.parametrize("name", sorted(MAN))
 def test_decode_matches_reference(codec, name):
     gold = open(f"{GOLD}/{name}.j2k", "rb").read()
