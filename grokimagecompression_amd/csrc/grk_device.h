@@ -116,7 +116,7 @@ struct DwtOptions {
     int32_t t1_dec_bpw = 0;  // T1 decode: blocks per wavefront (0: by block count)
     int32_t mid_th = 0;      // window rows of a level of 2^21 .. 2^23 samples (0: 8)
     int32_t t1_enc_bpw = 0;  // T1 encode (MQ coder): blocks per wavefront (0: by block count)
-    int32_t t1_enc_sort = 1; // T1 encode: MQ coder lanes take the blocks heaviest first (device counting sort)
+    int32_t t1_enc_sort = 0; // T1 encode: MQ coder lanes take the blocks heaviest first (device counting sort)
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose

@@ -226,10 +226,11 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    a level of 2^21 .. 2^23 samples; 0 (default) = 8.
  *   t1_enc_bpw       T1 encode (MQ coder): code-blocks per wavefront, as
  *                    t1_dec_bpw.
- *   t1_enc_sort      T1 encode: 1 (default) = the MQ coder's lanes take the
- *                    code-blocks in decreasing order of their symbol count (a
- *                    counting sort on the device after the modelling kernel);
- *                    0 = block order.  Same codestream. */
+ *   t1_enc_sort      T1 encode: 1 = the MQ coder's lanes take the code-blocks
+ *                    in decreasing order of their symbol count (a counting
+ *                    sort on the device after the modelling kernel); 0
+ *                    (default, measured as fast) = block order.  Same
+ *                    codestream. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
