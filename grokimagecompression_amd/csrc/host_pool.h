@@ -7,6 +7,7 @@
 // works on its own loop too, so concurrent callers (frames in flight on other
 // threads) never wait for an idle worker.
 #pragma once
+#include <sched.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -69,9 +70,14 @@ private:
     };
 
     HostPool() {
-        // GRKGPU_HOST_THREADS caps the pool (default: the machine's cores, at
-        // most 16 -- a GPU box grants 16 host cores per GPU)
+        // GRKGPU_HOST_THREADS caps the pool (default: the cores this process
+        // may run on -- its affinity mask, not the machine's -- at most 16, a
+        // GPU box's share per GPU)
         size_t n = std::thread::hardware_concurrency();
+        {
+            cpu_set_t set;
+            if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = (size_t)CPU_COUNT(&set);
+        }
         if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = (size_t)atoi(e);
         n = std::min<size_t>(n ? n : 1, 16);
         for (size_t i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
