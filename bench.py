@@ -353,8 +353,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes": bdwt, "dwt_us": round(dwt_us, 2),
                 "span_us": round(1e3 * sum(spans) / len(spans), 2), "launches": launches,
-                "measured": "sum of the frame's per-launch device times (HIP event pair around each DWT launch on "
-                            "the codec stream, mean of 5 lone 9/7 encodes after the timed region); traffic = PMC "
+                "measured": "sum of the frame's per-launch device times (HIP events on the codec stream before the "
+                            "first DWT launch and after each one, so consecutive launches share an event; mean of 5 "
+                            "lone 9/7 encodes after the timed region); traffic = PMC "
                             "bytes (FETCH_SIZE x 2 + WRITE_SIZE) of the same launches, profiles/dwt_pmc_latest.json",
                 "inverse": {"kernel": "inverse 9/7 DWT of the frame (decode): " +
                                       " + ".join(x["kernel"] for x in ilaunches),
