@@ -90,6 +90,9 @@ struct grkgpu_ctx {
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs, h_segs;
     DevBuf dwtjobs53;  // decode: the 5/3 tile-components' job table when 9/7 ones share the call
     DevBuf t1order;    // encode: the MQ coder's work order (keys, permutation, bucket counters)
+    // encode: the pass records of the last call, kept so that a frame of the
+    // same size does not zero ~20 MB again before overwriting every record
+    std::vector<EncPass> enc_passes;
     HostBuf h_dwtjobs53;
     hipEvent_t ev[8] = {};
     grkgpu_stats stats = {};
@@ -1297,7 +1300,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     double t_t2 = now_ms();
     const uint32_t L = cp.numlayers;
     std::vector<EncCblkState> cst(nblk);
-    std::vector<EncPass> passes;
+    std::vector<EncPass> &passes = c->enc_passes;  // [0, npass) filled below; the tail is unused
+    uint32_t npass = 0;
     std::vector<EncLayer> layers((size_t)nblk * L, EncLayer{0, 0, 0, 0.0});
     std::vector<double> blk_disto(nblk, 0.0);
     const double *mct_norms = nullptr;
@@ -1314,7 +1318,6 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     // sum), then fill them on the host pool (blocks are independent)
     uint64_t nsym = 0;
     {
-        uint32_t npass = 0;
         for (uint32_t i = 0; i < nblk; ++i) {
             const EncResult &r = res[i];
             if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
@@ -1329,7 +1332,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             st.dev_off = eb[i].out_off;
             npass += np;
         }
-        passes.resize(npass);
+        if (passes.size() < npass) passes.resize(npass);
     }
     host_parallel_for(nblk, 1024, [&](size_t b0, size_t b1) {
         for (size_t i = b0; i < b1; ++i) {
@@ -1366,9 +1369,9 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         if (out_total) HIPCHK(hipMemcpyAsync(c->h_slab.p, c->mqout.p, out_total, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         c->bexp.assign(nblk, grkgpu_block_info{});
-        c->bexp_rate.resize(passes.size() + 1);
-        c->bexp_dist.resize(passes.size() + 1);
-        for (size_t k = 0; k < passes.size(); ++k) {
+        c->bexp_rate.resize((size_t)npass + 1);
+        c->bexp_dist.resize((size_t)npass + 1);
+        for (size_t k = 0; k < npass; ++k) {
             c->bexp_rate[k] = passes[k].rate;
             c->bexp_dist[k] = passes[k].dd;
         }
