@@ -197,7 +197,8 @@ class Stats(ctypes.Structure):
                 ("cs_bytes", ctypes.c_uint64), ("mq_symbols", ctypes.c_uint64), ("rate_ms", ctypes.c_float),
                 ("packet_ms", ctypes.c_float), ("rate_probes", ctypes.c_uint32), ("rate_probes_skipped", ctypes.c_uint32),
                 ("rate_block_evals", ctypes.c_uint64), ("rate_precinct_sims", ctypes.c_uint64),
-                ("rate_form_ms", ctypes.c_float), ("rate_sim_ms", ctypes.c_float)]
+                ("rate_form_ms", ctypes.c_float), ("rate_sim_ms", ctypes.c_float), ("passrec_ms", ctypes.c_float),
+                ("pad_", ctypes.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -1340,6 +1340,10 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             const uint32_t np = r.numpasses;
             EncPass *out = passes.data() + cst[i].pass0;
             double cum = 0.0;
+            const BlkInfo &bi = binfo[i];
+            const double wfac = need_rc ? t1_wmsedec_factor(bi.compno, bi.level, bi.orient, cp.irrev ? 0 : 1,
+                                                            (double)bi.stepsize, mct_norms, mct_numcomps)
+                                        : 0.0;
             for (uint32_t k = 0; k < np; ++k) {
                 EncPass ps;
                 ps.rate = r.rate[k];
@@ -1353,9 +1357,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 ps.slope = 0;
                 if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
                     const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
-                    const BlkInfo &bi = binfo[i];
-                    cum += t1_wmsedec(r.nmsedec[k], bi.compno, bi.level, bi.orient, bpno, cp.irrev ? 0 : 1,
-                                      (double)bi.stepsize, mct_norms, mct_numcomps);
+                    cum += t1_wmsedec_at(wfac, r.nmsedec[k], bpno);
                 }
                 ps.dd = cum;
                 out[k] = ps;
@@ -1363,6 +1365,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             blk_disto[i] = cum;
         }
     });
+    const double t_passrec = now_ms() - t_t2;
     if (export_blocks) {
         // the MQ slab to pinned host memory, then one record per block
         HIPCHK(c->h_slab.ensure(out_total + 256));
@@ -1696,6 +1699,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     st.rate_precinct_sims = rsum.sims;
     st.rate_form_ms = (float)rsum.form_ms;
     st.rate_sim_ms = (float)rsum.sim_ms;
+    st.passrec_ms = (float)t_passrec;
     return GRKGPU_OK;
 }
 

@@ -1487,14 +1487,17 @@ double getnorm(uint32_t level, uint32_t orient, bool rev) {
 }
 }  // namespace
 
+double t1_wmsedec_factor(uint32_t compno, uint32_t level, uint32_t orient, uint32_t qmfbid, double stepsize,
+                         const double *mct_norms, uint32_t mct_numcomps) {
+    double w1 = 1;
+    if (mct_norms && compno < mct_numcomps) w1 = mct_norms[compno];
+    return w1 * getnorm(level, orient, qmfbid == 1) * stepsize;
+}
+
 double t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno, uint32_t qmfbid,
                   double stepsize, const double *mct_norms, uint32_t mct_numcomps) {
-    double w1 = 1, w2, wmsedec;
-    if (mct_norms && compno < mct_numcomps) w1 = mct_norms[compno];
-    w2 = getnorm(level, orient, qmfbid == 1);
-    wmsedec = w1 * w2 * stepsize * (1 << bpno);
-    wmsedec *= wmsedec * nmsedec / 8192.0;
-    return wmsedec;
+    return t1_wmsedec_at(t1_wmsedec_factor(compno, level, orient, qmfbid, stepsize, mct_norms, mct_numcomps), nmsedec,
+                         bpno);
 }
 
 }  // namespace grkgpu

@@ -111,5 +111,15 @@ bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st = 
 // distortion weight of a pass (t1_getwmsedec, t1.cpp:912-930)
 double t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno, uint32_t qmfbid,
                   double stepsize, const double *mct_norms, uint32_t mct_numcomps);
+// the same in two steps, the block's constant first (w1 * w2 * stepsize,
+// evaluated left to right as t1.cpp:912-930 does), then per pass:
+// t1_wmsedec_at(factor, nmsedec, bpno) == t1_wmsedec(...) bit for bit
+double t1_wmsedec_factor(uint32_t compno, uint32_t level, uint32_t orient, uint32_t qmfbid, double stepsize,
+                         const double *mct_norms, uint32_t mct_numcomps);
+inline double t1_wmsedec_at(double factor, int32_t nmsedec, int32_t bpno) {
+    double wmsedec = factor * (1 << bpno);
+    wmsedec *= wmsedec * nmsedec / 8192.0;
+    return wmsedec;
+}
 
 }  // namespace grkgpu

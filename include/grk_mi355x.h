@@ -155,6 +155,8 @@ typedef struct {
     uint32_t rate_probes, rate_probes_skipped;
     uint64_t rate_block_evals, rate_precinct_sims;
     float rate_form_ms, rate_sim_ms;
+    float passrec_ms;     /* host: per-pass rate / distortion records from the T1 results (part of host_t2_ms) */
+    uint32_t pad_;
 } grkgpu_stats;
 
 /* One kernel launch of the last call's forward DWT, timed with HIP events on
