@@ -2273,14 +2273,25 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         // blocks grouped by style (a launch each), and -- t1_dec_sort -- since
         // lanes of a wavefront run until its slowest block is done, blocks of
         // similar work (pass count, then coded bytes) together, heaviest first
-        std::vector<uint32_t> ord(nblk);
+        // (an LSD radix sort of one 48-bit key per block -- style, then
+        // passes and bytes descending -- is the comparison sort's stable
+        // order at a fraction of its cost: 26 K blocks, ~0.2 vs ~3 ms)
+        std::vector<uint64_t> key(nblk);
+        for (uint32_t i = 0; i < nblk; ++i) {
+            key[i] = (uint64_t)dsty[i] << 40;
+            if (sort_work)
+                key[i] |= (uint64_t)(255u - std::min<uint32_t>(db[i].numpasses, 255u)) << 32 | (0xFFFFFFFFu - db[i].len);
+        }
+        std::vector<uint32_t> ord(nblk), tmp(nblk);
         for (uint32_t i = 0; i < nblk; ++i) ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
-            if (dsty[a] != dsty[b]) return dsty[a] < dsty[b];
-            if (!sort_work) return false;
-            const DecBlock &x = db[a], &y = db[b];
-            return x.numpasses != y.numpasses ? x.numpasses > y.numpasses : x.len > y.len;
-        });
+        for (int sh = 0; sh < 48; sh += 8) {
+            uint32_t cnt[257] = {0};
+            for (uint32_t i : ord) ++cnt[((key[i] >> sh) & 255u) + 1];
+            if (*std::max_element(cnt + 1, cnt + 257) == nblk) continue;  // one digit value: order unchanged
+            for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+            for (uint32_t i : ord) tmp[cnt[(key[i] >> sh) & 255u]++] = i;
+            ord.swap(tmp);
+        }
         std::vector<DecBlock> db2(nblk);
         std::vector<DecSeg> segs2;
         segs2.reserve(dsegs.size());
