@@ -1128,8 +1128,8 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     std::vector<uint8_t> changed(redo.size());
     std::vector<int64_t> dlen(redo.size());
     g_rt.redo += redo.size();
-    if (redo.size() > 2048) {
-        host_parallel_for(redo.size(), 256, [&](size_t a, size_t b) {
+    if (redo.size() > 512) {  // a probe's re-evaluations (~0.2 us each) on the pool from 512
+        host_parallel_for(redo.size(), 128, [&](size_t a, size_t b) {
             for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j], &dlen[j]);
         });
     } else {
