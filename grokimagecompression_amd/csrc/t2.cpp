@@ -766,6 +766,15 @@ struct RateProbe {
     std::vector<uint64_t> comp_prev;
     int64_t body = 0;                   // layer layno
     std::vector<int64_t> comp_body;
+    // the first layer's packet headers, bounded from above: per block the
+    // bits its records cost (tag-tree bits taken as the whole path, the rest
+    // exact), summed per precinct; a packet of B bits is at most B / 7 + 2
+    // bytes (bit stuffing leaves >= 7 bits in every byte, the flush adds <= 2)
+    std::vector<uint8_t> lev;           // per block: its tag trees' path length
+    std::vector<uint8_t> bnumbps;       // per block: its band's bit-planes
+    std::vector<uint32_t> ub;           // per block: header bits bound of its layer-0 record
+    std::vector<int64_t> prec_bits;     // per precinct: sum of its blocks' ub
+    std::vector<uint8_t> prec_comp;     // per precinct: its component
     bool fresh = true;                 // no probe of the current layer yet: evaluate every block
     // packets of layers [0, layers) in THRESH_CALC order, grouped per precinct
     uint32_t layers = 0, nprec = 0, npoc = 0;  // npoc: POC groups per component
@@ -785,19 +794,32 @@ struct RateProbe {
 void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
     rp.prec.clear();
     rp.comp.clear();
+    rp.lev.clear();
+    rp.bnumbps.clear();
+    rp.prec_comp.clear();
     uint32_t base = 0;
     for (uint32_t k = 0; k < cp.numcomps; ++k) {
         TileComp &tc = te.tile->comps[k];
         for (auto &res : tc.res) {
             for (uint32_t b = 0; b < res.numbands; ++b)
-                for (size_t p = 0; p < res.bands[b].precs.size(); ++p)
-                    for (size_t n = 0; n < res.bands[b].precs[p].cblks.size(); ++n) {
+                for (size_t p = 0; p < res.bands[b].precs.size(); ++p) {
+                    Precinct &pr = res.bands[b].precs[p];
+                    uint32_t depth = 0;  // nodes on a leaf's path to the root
+                    if (!pr.incl.nodes.empty())
+                        for (int32_t nd = 0; nd >= 0; nd = pr.incl.nodes[nd].parent) ++depth;
+                    for (size_t n = 0; n < pr.cblks.size(); ++n) {
                         rp.prec.push_back(base + (uint32_t)p);
                         rp.comp.push_back((uint8_t)k);
+                        rp.lev.push_back((uint8_t)std::min<uint32_t>(depth, 255));
+                        rp.bnumbps.push_back((uint8_t)std::min<uint32_t>(res.bands[b].numbps, 255));
                     }
+                }
+            for (uint32_t p = 0; p < res.pw * res.ph; ++p) rp.prec_comp.push_back((uint8_t)k);
             base += res.pw * res.ph;
         }
     }
+    rp.ub.assign(rp.prec.size(), 0);
+    rp.prec_bits.assign(base, 0);
     rp.body_prev = 0;
     rp.comp_prev.assign(cp.numcomps, 0);
     rp.body = 0;
@@ -1081,6 +1103,42 @@ uint32_t feasible_cumul(const EncCblkState &s, const EncPass *P, uint32_t thresh
     return cumul;
 }
 
+// Upper bound on the packet-header bits block i's layer-0 record costs
+// (packet_header with incl_cur = 0, numlenbits = 3): the inclusion tag tree
+// at threshold 1 emits at most one bit per node of the leaf's path, the
+// missing-MSB tree at most its value plus one per node, the rest exactly.
+// UB_NONE: no bound (a block above its band's bit-planes).
+constexpr uint32_t UB_NONE = 1u << 24;
+uint32_t header_bits_ub(const RateProbe &rp, size_t i, const EncCblkState &s, const EncLayer &ly, const EncPass *P) {
+    uint32_t bits = rp.lev[i];
+    if (!ly.numpasses) return bits;
+    if (rp.bnumbps[i] < s.numbps) return UB_NONE;
+    bits += (rp.bnumbps[i] - s.numbps) + rp.lev[i];
+    const uint32_t n = ly.numpasses;
+    bits += n == 1 ? 1 : n == 2 ? 2 : n <= 5 ? 4 : n <= 36 ? 9 : 16;
+    int32_t increment = 0;
+    uint32_t nump = 0, len = 0;
+    for (uint32_t pn = 0; pn < n; ++pn) {
+        ++nump;
+        len += P[pn].len;
+        if (P[pn].term || pn == n - 1) {
+            increment = std::max<int32_t>(increment, floorlog2((int32_t)len) + 1 - (3 + floorlog2((int32_t)nump)));
+            len = 0;
+            nump = 0;
+        }
+    }
+    bits += (uint32_t)increment + 1;  // comma code
+    const uint32_t numlenbits = 3 + (uint32_t)increment;
+    for (uint32_t pn = 0; pn < n; ++pn) {
+        ++nump;
+        if (P[pn].term || pn == n - 1) {
+            bits += numlenbits + (uint32_t)floorlog2((int32_t)nump);
+            nump = 0;
+        }
+    }
+    return bits;
+}
+
 // One probe or the final formation of layer `layno` at a threshold
 // (make_layer_simple, TileProcessor.cpp:675-780, or makelayer_feasible,
 // :281-364).  A probe re-evaluates only the blocks whose bounds exclude the
@@ -1104,6 +1162,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         const int64_t oldlen = old ? (int64_t)ly.len : 0;
         set_layer(te, c.gidx, layno, L, cumul);
         *dlen = (ly.numpasses ? (int64_t)ly.len : 0) - oldlen;
+        if (layno == 0) rp.ub[i] = header_bits_ub(rp, i, s, ly, P.data() + s.pass0);
         return ly.numpasses != old;
     };
     std::vector<uint32_t> redo;
@@ -1127,6 +1186,11 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     }
     std::vector<uint8_t> changed(redo.size());
     std::vector<int64_t> dlen(redo.size());
+    std::vector<uint32_t> ub_old;  // the layer-0 header bounds before this probe's re-evaluations
+    if (layno == 0 && !full) {
+        ub_old.resize(redo.size());
+        for (size_t j = 0; j < redo.size(); ++j) ub_old[j] = rp.ub[redo[j]];
+    }
     g_rt.redo += redo.size();
     if (redo.size() > 512) {  // a probe's re-evaluations (~0.2 us each) on the pool from 512
         host_parallel_for(redo.size(), 128, [&](size_t a, size_t b) {
@@ -1136,10 +1200,12 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         for (size_t j = 0; j < redo.size(); ++j) changed[j] = eval(redo[j], &dlen[j]);
     }
     const bool keep = !final && (FEASIBLE || thresh != 0);
-    if (full) {  // the layer's bytes from scratch (records of earlier probes included)
+    if (full) {  // the layer's bytes (and first-layer header bounds) from scratch
         rp.body = 0;
         std::fill(rp.comp_body.begin(), rp.comp_body.end(), 0);
+        std::fill(rp.prec_bits.begin(), rp.prec_bits.end(), 0);
         for (size_t i = 0; i < nb; ++i) {
+            if (layno == 0) rp.prec_bits[rp.prec[i]] += rp.ub[i];
             const EncLayer &ly = (*te.layers)[(size_t)te.blist[i]->gidx * L + layno];
             if (!ly.numpasses) continue;
             rp.body += ly.len;
@@ -1152,6 +1218,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         if (!full) {
             rp.body += dlen[j];
             rp.comp_body[rp.comp[i]] += dlen[j];
+            if (layno == 0) rp.prec_bits[rp.prec[i]] += (int64_t)rp.ub[i] - (int64_t)ub_old[j];
         }
         rp.valid[i] = keep;
     }
@@ -1186,6 +1253,34 @@ bool body_over(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_
         for (size_t k = 0; k < rp.comp_body.size(); ++k)
             if (rp.comp_prev[k] + (uint64_t)rp.comp_body[k] > cp.max_comp_size) return true;
     return false;
+}
+
+// The probe certainly fits: a single-layer search (the first layer's
+// header bounds apply), no SOP / EPH, the plan's packets exactly the
+// records, and code-block bytes plus every packet's header bound within the
+// budget and each component cap -- simulate_tile's running budget then
+// covers every packet, so it would return true.
+bool body_fits(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_len, RateProbe &rp) {
+    if (max_layers != 1 || (cp.csty & (CSTY_SOP | CSTY_EPH))) return false;
+    if (rp.layers != max_layers) probe_plan(cp, te, max_layers, rp);
+    if (!rp.body_exact) return false;
+    uint64_t hb = 0;
+    std::vector<uint64_t> chb(cp.numcomps, 0);
+    for (uint32_t p = 0; p < rp.nprec; ++p) {
+        const uint32_t npk = rp.head[p + 1] - rp.head[p];
+        if (!npk) continue;
+        if (rp.prec_bits[p] >= (int64_t)UB_NONE) return false;
+        const uint64_t b = (uint64_t)npk * ((uint64_t)(1 + rp.prec_bits[p]) / 7 + 2);
+        hb += b;
+        chb[rp.prec_comp[p]] += b;
+    }
+    if ((uint64_t)rp.body + hb > max_len) return false;
+    if (cp.max_comp_size) {
+        if (!rp.comp_exact) return false;
+        for (uint32_t k = 0; k < cp.numcomps; ++k)
+            if ((uint64_t)rp.comp_body[k] + chb[k] > cp.max_comp_size) return false;
+    }
+    return true;
 }
 
 // RateProbe::active after a probe: keep the blocks whose layer record could
@@ -1298,8 +1393,9 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
                 } else {
                     const double f1 = g_rt.on ? t2_ms() : 0;
                     const bool over = body_over(cp, te, layno + 1, maxlen, rp);
-                    g_rt.skipped += over;
-                    const bool fits = !over && simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    const bool sure = !over && body_fits(cp, te, layno + 1, maxlen, rp);
+                    g_rt.skipped += over || sure;
+                    const bool fits = sure || (!over && simulate_tile(cp, te, layno + 1, maxlen, rp));
                     if (g_rt.on) g_rt.sim += t2_ms() - f1;
                     if (!fits) lower = thresh;
                     else upper = thresh;
@@ -1407,8 +1503,9 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
                 } else {
                     const double f1 = g_rt.on ? t2_ms() : 0;
                     const bool over = body_over(cp, te, layno + 1, maxlen, rp);
-                    g_rt.skipped += over;
-                    const bool fits = !over && simulate_tile(cp, te, layno + 1, maxlen, rp);
+                    const bool sure = !over && body_fits(cp, te, layno + 1, maxlen, rp);
+                    g_rt.skipped += over || sure;
+                    const bool fits = sure || (!over && simulate_tile(cp, te, layno + 1, maxlen, rp));
                     if (g_rt.on) {
                         const double f2 = t2_ms();
                         g_rt.form += f1 - f0;
