@@ -1166,13 +1166,16 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         return ly.numpasses != old;
     };
     std::vector<uint32_t> redo;
-    const bool full = final || rp.fresh || (!FEASIBLE && thresh == 0);
+    // the final formation re-evaluates only the blocks whose bounds exclude
+    // the threshold, as a probe does: every block was evaluated by the
+    // layer's first probe and its record is exact wherever its bounds hold
+    const bool full = rp.fresh || (!FEASIBLE && thresh == 0);
+    if (layno == 0 && (full || final))
+        for (Cblk *c : te.blist) {
+            EncCblkState &s = (*te.cblk)[c->gidx];
+            s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0;
+        }
     if (full) {
-        if (layno == 0)
-            for (Cblk *c : te.blist) {
-                EncCblkState &s = (*te.cblk)[c->gidx];
-                s.incl_prev = 0; s.incl_cur = 0; s.numlenbits = 0;
-            }
         redo.resize(nb);
         for (size_t i = 0; i < nb; ++i) redo[i] = (uint32_t)i;
         rp.active = redo;

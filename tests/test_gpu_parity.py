@@ -59,17 +59,19 @@ def test_encode_mq_lane_order_matches_reference(codec, name, opts):
 
 def test_rate_control_stats(codec):
     """grkgpu_stats after a rate-controlled encode (the cinema golden): the
-    PCRD bisection's probes, block evaluations (at least the two full
-    passes) and packet simulations are reported; a lossless single-layer
-    encode runs no bisection."""
+    PCRD bisection's probes, block evaluations (at least the first probe's
+    full pass), probes decided without a packet simulation and precinct
+    simulations are reported; a lossless single-layer encode runs no
+    bisection."""
     import grokimagecompression_amd as grk
     m = MAN["rgb12_cinema4k"]
     img, bits = _img(m)
     p, off = grk.CParams.from_cli(m["args"])
     codec.compress(img, bits, p, offset=off)
     st = codec.stats()
-    assert st["rate_probes"] > 0 and st["rate_block_evals"] >= 2 * st["num_cblks"]
-    assert st["rate_precinct_sims"] > 0 and st["rate_probes_skipped"] <= st["rate_probes"]
+    assert st["rate_probes"] > 0 and st["rate_block_evals"] >= st["num_cblks"]
+    assert st["rate_probes_skipped"] <= st["rate_probes"]
+    assert st["rate_precinct_sims"] > 0 or st["rate_probes_skipped"] == st["rate_probes"]
     assert 0 <= st["rate_form_ms"] + st["rate_sim_ms"] <= st["rate_ms"] + 1e-3
     m = MAN["g8_64"]
     img, bits = _img(m)
