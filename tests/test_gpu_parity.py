@@ -71,7 +71,8 @@ def test_rate_control_stats(codec):
     st = codec.stats()
     assert st["rate_probes"] > 0 and st["rate_block_evals"] >= st["num_cblks"]
     assert st["rate_probes_skipped"] <= st["rate_probes"]
-    assert st["rate_precinct_sims"] > 0 or st["rate_probes_skipped"] == st["rate_probes"]
+    # (the simple search's last probe ends it on the 0.001 tolerance before any simulation)
+    assert st["rate_precinct_sims"] > 0 or st["rate_probes_skipped"] >= st["rate_probes"] - 1
     assert 0 <= st["rate_form_ms"] + st["rate_sim_ms"] <= st["rate_ms"] + 1e-3
     m = MAN["g8_64"]
     img, bits = _img(m)
