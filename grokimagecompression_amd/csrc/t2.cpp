@@ -749,8 +749,14 @@ double t2_ms() {
 struct RateProbe {
     // per block, in te.blist order
     std::vector<uint32_t> prec;        // precinct id
-    std::vector<double> lo_d, hi_d;    // simple: largest slope compared false, smallest compared true
-    std::vector<uint32_t> lo_u, hi_u;  // feasible: the slope it stopped at, smallest slope it passed
+    struct BoundD { double lo, hi; };  // simple: largest slope compared false, smallest compared true
+    struct BoundU { uint32_t lo, hi; };  // feasible: the slope it stopped at, smallest slope it passed
+    std::vector<BoundD> bd;            // (a block's two bounds on one cache line)
+    std::vector<BoundU> bu;
+    std::vector<uint32_t> redo;        // per probe: scratch kept across probes
+    std::vector<uint8_t> changed;
+    std::vector<int64_t> dlen;
+    std::vector<uint32_t> ub_old;
     std::vector<uint8_t> valid;        // bounds hold for the current layer records
     // blocks a probe still has to check: a block whose bounds hold over the
     // whole remaining bisection interval [lower, upper] never changes again
@@ -826,8 +832,8 @@ void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
     rp.comp_body.assign(cp.numcomps, 0);
     rp.nprec = base;
     const size_t nb = rp.prec.size();
-    rp.lo_d.assign(nb, 0); rp.hi_d.assign(nb, 0);
-    rp.lo_u.assign(nb, 0); rp.hi_u.assign(nb, 0);
+    rp.bd.assign(nb, RateProbe::BoundD{0, 0});
+    rp.bu.assign(nb, RateProbe::BoundU{0, 0});
     rp.valid.assign(nb, 0);
     rp.active.clear();
     rp.dirty.assign(rp.nprec, 1);
@@ -1155,8 +1161,8 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         Cblk &c = *te.blist[i];
         EncCblkState &s = (*te.cblk)[c.gidx];
         uint32_t cumul;
-        if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.lo_u[i], &rp.hi_u[i]);
-        else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.lo_d[i], &rp.hi_d[i]);
+        if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.bu[i].lo, &rp.bu[i].hi);
+        else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
         EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + layno];
         const uint32_t old = ly.numpasses;
         const int64_t oldlen = old ? (int64_t)ly.len : 0;
@@ -1165,7 +1171,8 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         if (layno == 0) rp.ub[i] = header_bits_ub(rp, i, s, ly, P.data() + s.pass0);
         return ly.numpasses != old;
     };
-    std::vector<uint32_t> redo;
+    std::vector<uint32_t> &redo = rp.redo;
+    redo.clear();
     // the final formation re-evaluates only the blocks whose bounds exclude
     // the threshold, as a probe does: every block was evaluated by the
     // layer's first probe and its record is exact wherever its bounds hold
@@ -1182,14 +1189,16 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     } else {
         for (uint32_t i : rp.active) {
             bool ok = rp.valid[i] != 0;
-            if constexpr (FEASIBLE) ok = ok && rp.lo_u[i] <= (uint32_t)thresh && (uint32_t)thresh < rp.hi_u[i];
-            else ok = ok && ((double)thresh - rp.hi_d[i] < DBL_EPSILON) && !((double)thresh - rp.lo_d[i] < DBL_EPSILON);
+            if constexpr (FEASIBLE) ok = ok && rp.bu[i].lo <= (uint32_t)thresh && (uint32_t)thresh < rp.bu[i].hi;
+            else ok = ok && ((double)thresh - rp.bd[i].hi < DBL_EPSILON) && !((double)thresh - rp.bd[i].lo < DBL_EPSILON);
             if (!ok) redo.push_back(i);
         }
     }
-    std::vector<uint8_t> changed(redo.size());
-    std::vector<int64_t> dlen(redo.size());
-    std::vector<uint32_t> ub_old;  // the layer-0 header bounds before this probe's re-evaluations
+    std::vector<uint8_t> &changed = rp.changed;
+    std::vector<int64_t> &dlen = rp.dlen;
+    std::vector<uint32_t> &ub_old = rp.ub_old;  // the layer-0 header bounds before this probe's re-evaluations
+    changed.resize(redo.size());
+    dlen.resize(redo.size());
     if (layno == 0 && !full) {
         ub_old.resize(redo.size());
         for (size_t j = 0; j < redo.size(); ++j) ub_old[j] = rp.ub[redo[j]];
@@ -1295,7 +1304,7 @@ bool body_fits(CodingParams &cp, TileEnc &te, uint32_t max_layers, uint64_t max_
 void prune_simple(RateProbe &rp, double L, double U) {
     size_t k = 0;
     for (uint32_t i : rp.active) {
-        const bool keep = !rp.valid[i] || !(U - rp.hi_d[i] < DBL_EPSILON) || (L - rp.lo_d[i] < DBL_EPSILON);
+        const bool keep = !rp.valid[i] || !(U - rp.bd[i].hi < DBL_EPSILON) || (L - rp.bd[i].lo < DBL_EPSILON);
         if (keep) rp.active[k++] = i;
     }
     rp.active.resize(k);
@@ -1303,7 +1312,7 @@ void prune_simple(RateProbe &rp, double L, double U) {
 void prune_feasible(RateProbe &rp, uint32_t L, uint32_t U) {
     size_t k = 0;
     for (uint32_t i : rp.active) {
-        const bool keep = !rp.valid[i] || !(rp.lo_u[i] <= L && U < rp.hi_u[i]);
+        const bool keep = !rp.valid[i] || !(rp.bu[i].lo <= L && U < rp.bu[i].hi);
         if (keep) rp.active[k++] = i;
     }
     rp.active.resize(k);
