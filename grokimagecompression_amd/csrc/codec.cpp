@@ -9,6 +9,7 @@
 // Decode (TileProcessor::decode_tile, TileProcessor.cpp:1069-1179):
 //   host header + Tier-2 parse -> H2D codestream -> ONE T1 decode launch ->
 //   per tile/component inverse DWT levels -> inverse MCT + DC shift.
+#include <float.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -1362,6 +1363,22 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 ps.dd = cum;
                 out[k] = ps;
             }
+            // the simple PCRD's slope range over this block's passes, from
+            // the records just written (pcrd_simple's own loop, TileEnc::slopes)
+            double mn = DBL_MAX, mx = -1;
+            for (uint32_t k = 0; k < np; ++k) {
+                const EncPass &ps = out[k];
+                int32_t dr;
+                double dd;
+                if (k == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
+                else { dr = (int32_t)(ps.rate - out[k - 1].rate); dd = ps.dd - out[k - 1].dd; }
+                if (dr == 0) continue;
+                const double r = dd / dr;
+                if (r < mn) mn = r;
+                if (r > mx) mx = r;
+            }
+            cst[i].smin = mn;
+            cst[i].smax = mx;
             blk_disto[i] = cum;
         }
     });
@@ -1523,6 +1540,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             tenc.cblk = &cst;
             tenc.passes = &passes;
             tenc.layers = &layers;
+            tenc.slopes = true;  // the pass-record fill above computed every block's slope range
             init_enc_pocs(cp, tenc);
             CodingParams cpt = cp;
             uint32_t ntp = 0;

@@ -803,6 +803,11 @@ void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
     rp.lev.clear();
     rp.bnumbps.clear();
     rp.prec_comp.clear();
+    const size_t nbl = te.blist.size();
+    rp.prec.reserve(nbl);
+    rp.comp.reserve(nbl);
+    rp.lev.reserve(nbl);
+    rp.bnumbps.reserve(nbl);
     uint32_t base = 0;
     for (uint32_t k = 0; k < cp.numcomps; ++k) {
         TileComp &tc = te.tile->comps[k];
@@ -1361,6 +1366,11 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
             double mn = DBL_MAX, mx = -1;
             for (size_t i = b0; i < b1; ++i) {
                 const EncCblkState &s = (*te.cblk)[te.blist[i]->gidx];
+                if (te.slopes) {  // the per-block extremes, from the pass records' producer
+                    if (s.smin < mn) mn = s.smin;
+                    if (s.smax > mx) mx = s.smax;
+                    continue;
+                }
                 for (uint32_t pn = 0; pn < s.numpasses; ++pn) {
                     const EncPass &ps = P[s.pass0 + pn];
                     int32_t dr;
@@ -1378,7 +1388,7 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
             if (mx > max_slope) max_slope = mx;
         });
     }
-    const double maxSE = tile_max_se(cp, te);
+    const double maxSE = cp.fixed_quality ? tile_max_se(cp, te) : 0.0;  // only the PSNR targets read it
     RateProbe rp;
     probe_init(cp, te, rp);
     if (g_rt.on) g_rt.hull += t2_ms() - h0;
@@ -1491,7 +1501,7 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
         makelayer_final(cp, te, 0);
         return true;
     }
-    const double maxSE = tile_max_se(cp, te);
+    const double maxSE = cp.fixed_quality ? tile_max_se(cp, te) : 0.0;  // only the PSNR targets read it
     RateProbe rp;
     probe_init(cp, te, rp);
     uint32_t upper = USHRT_MAX;

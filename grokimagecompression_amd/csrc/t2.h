@@ -46,6 +46,10 @@ struct EncCblkState {
     uint32_t incl_cur = 0;   // num_passes_included_in_current_layer (packet writer)
     uint32_t numlenbits = 0;
     uint64_t dev_off = 0;    // byte offset of the block's MQ output in the device slab
+    // smallest / largest pass slope dd / dr over passes with dr != 0 (the
+    // simple PCRD's search range, TileProcessor.cpp:528-560), when the pass
+    // records' producer filled them (TileEnc::slopes)
+    double smin = 0, smax = 0;
 };
 
 // Per-POC encoder state (the reference's tcp->pocs[] entries: user range +
@@ -68,6 +72,7 @@ struct TileEnc {
     double distotile = 0;
     std::vector<double> distolayer;
     std::vector<Cblk *> blist;                  // the tile's code-blocks in for_each_block order (rate control)
+    bool slopes = false;                        // EncCblkState::smin / smax hold every block's pass slopes
 };
 
 // number of POC entries of a tile (tcp->numpocs + 1)
