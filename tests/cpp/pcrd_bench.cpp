@@ -7,7 +7,8 @@
 // (e.g. before / after a change) can be compared on the same inputs.
 //
 //   g++ -O2 -std=c++17 -I<csrc> pcrd_bench.cpp <csrc>/t2.cpp <csrc>/codestream.cpp -lpthread
-//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps]
+//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps] [slopes 0|1]
+#include <float.h>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -24,6 +25,7 @@ int main(int argc, char **argv) {
     const uint32_t seed = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
     const uint32_t L = argc > 4 ? (uint32_t)atoi(argv[4]) : 1;
     const int reps = argc > 5 ? atoi(argv[5]) : 3;
+    const bool slopes = argc > 6 && atoi(argv[6]) != 0;  // per-block slope extremes precomputed
     CodingParams cp;
     cp.numcomps = 3;
     cp.image = {0, 0, 4096, 2160};
@@ -85,6 +87,18 @@ int main(int argc, char **argv) {
                             p.term = k + 1 == s.numpasses;
                             passes.push_back(p);
                         }
+                        // the slope range codec.cpp's pass-record fill stores (TileEnc::slopes)
+                        double mn = DBL_MAX, mx = -1;
+                        for (uint32_t k = 0; k < s.numpasses; ++k) {
+                            const EncPass &ps = passes[s.pass0 + k];
+                            const int32_t dr = k ? (int32_t)(ps.rate - passes[s.pass0 + k - 1].rate) : (int32_t)ps.rate;
+                            const double d = k ? ps.dd - passes[s.pass0 + k - 1].dd : ps.dd;
+                            if (dr == 0) continue;
+                            mn = std::min(mn, d / dr);
+                            mx = std::max(mx, d / dr);
+                        }
+                        s.smin = mn;
+                        s.smax = mx;
                         distotile += dd;
                         cst.push_back(s);
                     }
@@ -101,6 +115,7 @@ int main(int argc, char **argv) {
         te.cblk = &cs;
         te.passes = &ps;
         te.layers = &layers;
+        te.slopes = slopes;
         init_enc_pocs(cp, te);
         te.distotile = distotile;
         CodingParams cpt = cp;
