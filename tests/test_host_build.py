@@ -80,6 +80,8 @@ def test_pcrd_incremental_probes_match_full_evaluation(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-I" + c, "-o", str(exe), os.path.join(ROOT, "tests/cpp/pcrd_bench.cpp"),
                     os.path.join(c, "t2.cpp"), os.path.join(c, "codestream.cpp"), "-lpthread"], check=True)
     for (algo, budget, seed, layers), digest in PCRD_DIGESTS:
-        r = subprocess.run([str(exe), str(algo), budget, str(seed), str(layers), "1"], capture_output=True, text=True,
-                           check=True)
-        assert "digest %s" % digest in r.stdout, (algo, budget, seed, layers, r.stdout)
+        # slopes 1: the per-block slope extremes precomputed as codec.cpp's pass-record fill does
+        for slopes in ("0", "1"):
+            r = subprocess.run([str(exe), str(algo), budget, str(seed), str(layers), "1", slopes], capture_output=True,
+                               text=True, check=True)
+            assert "digest %s" % digest in r.stdout, (algo, budget, seed, layers, slopes, r.stdout)
