@@ -210,7 +210,8 @@ class DwtOptions(ctypes.Structure):
                 ("f01_small_min_samples", ctypes.c_uint64), ("inv01", ctypes.c_int32), ("pair_group", ctypes.c_int32),
                 ("inv01_min_samples", ctypes.c_uint64), ("f64_lift", ctypes.c_int32), ("t1_dec_sort", ctypes.c_int32),
                 ("t1_dec_bpw", ctypes.c_int32), ("mid_th", ctypes.c_int32),
-                ("t1_enc_bpw", ctypes.c_int32), ("t1_enc_sort", ctypes.c_int32)]
+                ("t1_enc_bpw", ctypes.c_int32), ("t1_enc_sort", ctypes.c_int32), ("pair_kernel", ctypes.c_int32),
+                ("pair_rows", ctypes.c_int32), ("pair_waves", ctypes.c_int32), ("pair_min_samples", ctypes.c_uint64)]
 
 
 class LaunchTime(ctypes.Structure):
@@ -276,6 +277,7 @@ def lib():
         L.grkgpu_compress_tile_rows.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, U32, U32, U32, U32,
                                                 U32, P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
         L.grkgpu_decompress_tiles.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, P(VP), ctypes.c_int]
+        L.grkgpu_walk_tiles.argtypes = [VP, ctypes.c_size_t, P(ctypes.c_uint8), U32, P(U32)]
         L.grkgpu_decompress_reduced.argtypes = [VP, VP, ctypes.c_size_t, U32, P(ImageDesc), P(VP), ctypes.c_int]
         L.grkgpu_decompress_window.argtypes = [VP, VP, ctypes.c_size_t, U32, U32, U32, U32, P(ImageDesc), P(VP),
                                                ctypes.c_int]
@@ -665,6 +667,18 @@ class dwt_options:
     def __exit__(self, *exc):
         _check(lib().grkgpu_set_dwt_options(ctypes.byref(self.old)))
         return False
+
+
+def walk_tiles(cs):
+    """The tile-part walk of a decode of codestream bytes `cs`, host only
+    (grkgpu_walk_tiles): the list of tiles a decode produces; raises
+    GrkGpuError where the decode fails in the walk."""
+    n = ctypes.c_uint32()
+    buf = ctypes.create_string_buffer(bytes(cs), len(cs))
+    _check(lib().grkgpu_walk_tiles(buf, len(cs), None, 0, ctypes.byref(n)))
+    dec = (ctypes.c_uint8 * max(1, n.value))()
+    _check(lib().grkgpu_walk_tiles(buf, len(cs), dec, n.value, ctypes.byref(n)))
+    return [t for t in range(n.value) if dec[t]]
 
 
 # ---- stage entry points on torch device tensors (per-kernel parity tests) ----

@@ -240,6 +240,10 @@ void grkgpu_get_dwt_options(grkgpu_dwt_options *out) {
     out->mid_th = g_dwt_opts.mid_th;
     out->t1_enc_bpw = g_dwt_opts.t1_enc_bpw;
     out->t1_enc_sort = g_dwt_opts.t1_enc_sort;
+    out->pair_kernel = g_dwt_opts.pair_kernel;
+    out->pair_rows = g_dwt_opts.pair_rows;
+    out->pair_waves = g_dwt_opts.pair_waves;
+    out->pair_min_samples = g_dwt_opts.pair_min_samples;
 }
 
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
@@ -261,6 +265,15 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->t1_enc_bpw < 0 || o->t1_enc_bpw > 64 || (o->t1_enc_bpw & (o->t1_enc_bpw - 1)))
         return set_err(GRKGPU_EINVAL, "t1_enc_bpw must be 0 or a power of two <= 64");
     if (o->t1_enc_sort != 0 && o->t1_enc_sort != 1) return set_err(GRKGPU_EINVAL, "t1_enc_sort must be 0 or 1");
+    if (o->pair_kernel != 0 && o->pair_kernel != 1) return set_err(GRKGPU_EINVAL, "pair_kernel must be 0 or 1");
+    if (o->pair_rows < 0 || o->pair_rows > 65536 || (o->pair_rows & 1))
+        return set_err(GRKGPU_EINVAL, "pair_rows must be 0 or an even count <= 65536");
+    if (o->pair_waves != 0 && o->pair_waves != 3 && o->pair_waves != 4)
+        return set_err(GRKGPU_EINVAL, "pair_waves must be 0, 3 or 4");
+    g_dwt_opts.pair_kernel = o->pair_kernel;
+    g_dwt_opts.pair_rows = o->pair_rows;
+    g_dwt_opts.pair_waves = o->pair_waves;
+    g_dwt_opts.pair_min_samples = o->pair_min_samples;
     g_dwt_opts.t1_enc_sort = o->t1_enc_sort;
     g_dwt_opts.t1_enc_bpw = o->t1_enc_bpw;
     g_dwt_opts.f64_lift = o->f64_lift;
@@ -596,7 +609,9 @@ struct DwtPlan {
     int32_t fmt = SMP_I32;  // ... reading image samples of this format
     bool inverse = false;
     std::vector<uint32_t> f01;  // per level: workgroups per job if levels l, l+1 run fused (k_dwt_fwd01), else 0
-    std::vector<uint8_t> f01ny; // ... and its level-0 row windows per workgroup
+    std::vector<uint8_t> f01ny; // ... and its level-0 row windows per workgroup (k_dwt_fwd01)
+    std::vector<uint8_t> pnw;   // ... or, run by k_dwt_fwd_pair: its level-l waves per workgroup (0: k_dwt_fwd01)
+    std::vector<int32_t> ps1;   // ... and its level-(l+1) rows per segment
     uint32_t i01 = 0;           // inverse: workgroups per job if the last two levels run fused (k_dwt_inv01)
     bool restricted = false;    // inverse jobs limited to output regions (window decode)
 };
@@ -686,26 +701,68 @@ static void dwt_plan_tc(DwtPlan &P, const TileComp &tc, int32_t *work, int32_t *
 // MCT one, and the resolutions are big enough (>= 16 samples each way) for
 // the fused windows; f01_rows = 0 keeps one launch per level.  Returns
 // the workgroups per job, 0 = not fused.
-static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny) {
+static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny, int *nw0, int *s1) {
     const DwtOptions &o = dwt_options();
-    if (P.inverse || !irrev || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || !o.f01_rows) return 0;
+    *nw0 = 0;
+    if (P.inverse || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || !o.f01_rows) return 0;
+    if (!irrev && !o.pair_kernel) return 0;
     const auto &l0 = P.levels[li], &l1 = P.levels[li + 1];
     if (l0.empty() || l0.size() != l1.size()) return 0;
-    // only where the pair still fills the chip (f01_min_samples, default
-    // 2^23): the 8K frame's levels 2 + 3 fused with 4 row windows took
+    uint64_t samples = 0;
+    for (auto &j : l0) samples += (uint64_t)j.rw * j.rh;
+    for (size_t i = 0; i < l0.size(); ++i) {
+        const DwtJob &a = l0[i], &b = l1[i];
+        if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
+        if (a.out != b.in) return 0;  // level l + 1 must read level l's LL
+        if (a.reg_x1 > 0 || b.reg_x1 > 0) return 0;
+    }
+    if (o.pair_kernel) {
+        // k_dwt_fwd_pair: strips of CW1 level-(l+1) columns (3 or 4 level-l
+        // waves, whichever wastes fewer columns at the jobs' widths), segments
+        // of S1 rows sized so that the launch is about one resident wave of
+        // workgroups (3 per CU: 30 KB of LDS and 6 wavefronts each)
+        if (samples < o.pair_min_samples) return 0;
+        uint64_t cols[2] = {0, 0};
+        int maxh = 0;
+        for (auto &b : l1) {
+            for (int k = 0; k < 2; ++k) {
+                const int cw1 = dwt_pair_cw1(irrev, 3 + k);
+                cols[k] += (uint64_t)((b.rw + b.casx + cw1 - 1) / cw1) * (3 + k);
+            }
+            maxh = std::max(maxh, b.rh + b.casy);
+        }
+        *nw0 = o.pair_waves ? o.pair_waves : cols[0] < cols[1] ? 3 : 4;
+        uint64_t strips = 0;
+        for (auto &b : l1) {
+            const int cw1 = dwt_pair_cw1(irrev, *nw0);
+            strips += (uint64_t)((b.rw + b.casx + cw1 - 1) / cw1);
+        }
+        int rows = o.pair_rows;
+        if (!rows) {
+            const uint64_t target = 768;
+            const uint64_t nseg = std::max<uint64_t>(1, (target + strips / 2) / std::max<uint64_t>(strips, 1));
+            rows = (int)(((uint64_t)maxh + nseg - 1) / nseg);
+            // whole level-(l+1) chunks of 8 rows: 9/7 streams start 2 rows
+            // above the segment (8k - 2 rows), 5/3 at it (8k)
+            rows = irrev ? std::max(14, (rows + 2 + 7) / 8 * 8 - 2) : std::max(8, (rows + 7) / 8 * 8);
+        }
+        *s1 = rows;
+        uint32_t maxt = 0;
+        for (auto &b : l1)
+            maxt = std::max<uint32_t>(maxt, (uint32_t)dwt_pair_wgs(irrev, *nw0, rows, b.rw, b.rh, b.casx, b.casy));
+        return maxt;
+    }
+    // k_dwt_fwd01: only where the pair still fills the chip (f01_min_samples,
+    // default 2^23): the 8K frame's levels 2 + 3 fused with 4 row windows took
     // 26 us against 14 + 7 apart (378 workgroups), and with 2 row windows
     // (twice the workgroups; f01_small_min_samples, off by default) 26.4 us
     // of kernel time, the frame's DWT span 220 us against 217 apart
-    uint64_t samples = 0;
-    for (auto &j : l0) samples += (uint64_t)j.rw * j.rh;
     if (samples >= o.f01_min_samples) *ny = o.f01_rows;
     else if (samples >= o.f01_small_min_samples) *ny = 2;
     else return 0;
     uint32_t maxt = 0;
     for (size_t i = 0; i < l0.size(); ++i) {
-        const DwtJob &a = l0[i], &b = l1[i];
-        if (a.snx != b.rw || a.sny != b.rh || a.rw < 16 || a.rh < 16 || b.rw < 16 || b.rh < 16) return 0;
-        if (a.out != b.in) return 0;  // level l + 1 must read level l's LL
+        const DwtJob &b = l1[i];
         int tx;
         const int n = dwt01_tiles(irrev, *ny, b.rw, b.rh, b.casx, b.casy, &tx);
         if (n <= 0) return 0;
@@ -764,10 +821,18 @@ static void dwt_finalize(DwtPlan &P, int irrev) {
     // takes the other one -- no launch reads and writes one buffer.
     P.f01.assign(P.levels.size(), 0);
     P.f01ny.assign(P.levels.size(), 0);
+    P.pnw.assign(P.levels.size(), 0);
+    P.ps1.assign(P.levels.size(), 0);
     bool any = false;
     for (size_t l = 0; l + 1 < P.levels.size(); ++l) {
-        int ny = 4;
-        if ((P.f01[l] = dwt_f01_tiles(P, l, irrev, &ny))) { P.f01ny[l] = (uint8_t)ny; any = true; ++l; }
+        int ny = 4, nw0 = 0, s1 = 0;
+        if ((P.f01[l] = dwt_f01_tiles(P, l, irrev, &ny, &nw0, &s1))) {
+            P.f01ny[l] = (uint8_t)ny;
+            P.pnw[l] = (uint8_t)nw0;
+            P.ps1[l] = s1;
+            any = true;
+            ++l;
+        }
     }
     // the re-deal below pairs job i of every level (one tile-component)
     for (auto &l : P.levels) any = any && l.size() == P.levels[0].size();
@@ -885,10 +950,15 @@ static hipError_t dwt_run_levels(const DwtPlan &P, DwtJob *djobs, int irrev, boo
     for (size_t li = 0; li < P.levels.size(); ++li) {
         const auto &l = P.levels[li];
         if (li < P.f01.size() && P.f01[li]) {
-            snprintf(name, sizeof(name), "k_dwt_fwd01<%s>", wl);
+            snprintf(name, sizeof(name), P.pnw[li] ? "k_dwt_fwd_pair<%s>" : "k_dwt_fwd01<%s>", wl);
             if ((e = log_begin(log, s, name, (uint32_t)li, 2, level_bytes(l) + level_bytes(P.levels[li + 1]), li > 0)))
                 return e;
-            e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, P.f01ny[li], s);
+            if (P.pnw[li])
+                e = launch_dwt_fwd_pair(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, P.pnw[li],
+                                        P.ps1[li], s);
+            else
+                e = launch_dwt_fwd01(djobs + k, djobs + k + l.size(), (uint32_t)l.size(), P.f01[li], irrev, P.f01ny[li],
+                                     s);
             if (e != hipSuccess || (e = log_end(log, s))) return e;
             k += l.size() + P.levels[li + 1].size();
             ++li;
@@ -1909,6 +1979,199 @@ static uint32_t rd32(const uint8_t *p) { return (rd16(p) << 16) | rd16(p + 2); }
 
 static uint32_t ceil_pow2(uint32_t v, uint32_t r) { return (uint32_t)(((uint64_t)v + ((1ull << r) - 1)) >> r); }
 
+
+// ---------------------------------------------------------------------------
+// The reference decoder's walk over the tile-parts, restated over a memory
+// stream (j2k_decode_tiles, j2k.cpp:1136-1224; j2k_read_tile_header :627-978
+// with j2k_read_sot :5138-5260 and j2k_read_sod :5399-5480; the marker read
+// after a decoded tile in j2k_decode_tile :979-1120; the look-ahead of
+// j2k_need_nb_tile_parts_correction :534-625; BufferedStream / mem_stream
+// reads and seeks, util/BufferedStream.cpp, util/mem_stream.cpp).  It decides
+// which tiles a decode produces, from which of their tile-parts, and which
+// short or damaged streams fail:
+//   * tiles are decoded as their last tile-part (TNsot) is read; a stream
+//     that ends -- or reaches EOC -- before a tile is complete still decodes
+//     a tile whose data has begun, from the tile-parts read;
+//   * a tile the walk never reaches is not decoded: its samples stay zero
+//     (the multi-tile output image is cleared first, j2k.cpp:1148-1156);
+//   * a stream ending inside a tile-part header, between a tile-part and the
+//     next one of the same tile, or right after an SOD (a tile with no data)
+//     fails, as do headers the reference refuses (tile-part index order,
+//     Psot, markers outside their place, an unknown marker);
+//   * the once-per-decode look-ahead over the following SOT headers fails on
+//     an SOT cut inside its 10 header bytes, wherever the walk itself stops.
+// A tile-part's data length is Psot less its header, clamped to the stream
+// (Psot = 0: up to the last 2 bytes); skipped tiles (outside a decode
+// window) step over their tile-parts, which a memory stream does past its
+// end without failing -- the next read fails instead.
+// ---------------------------------------------------------------------------
+struct TpMarker { uint32_t m; size_t off; uint32_t len; };
+struct TileWalk {
+    std::vector<std::vector<std::pair<size_t, size_t>>> parts;  // per tile: data of the tile-parts read
+    std::vector<std::vector<TpMarker>> marks;                  // per tile: its tile-part header markers
+    std::vector<std::vector<uint32_t>> seq;                    // per tile: codestream index of each tile-part
+    std::vector<uint8_t> decoded;                              // per tile: decoded by the walk
+    uint32_t ntp = 0;
+};
+
+static bool tph_marker(uint32_t m) {  // allowed in a tile-part header (j2k.cpp:87-106, J2K_DEC_STATE_TPH)
+    switch (m) {
+        case 0xFF52: case 0xFF53: case 0xFF5E: case 0xFF5C: case 0xFF5D: case 0xFF5F: case 0xFF58: case 0xFF61:
+        case 0xFF64: case 0xFF74: case 0xFF75: case 0xFF77: return true;
+        default: return false;
+    }
+}
+
+// j2k_need_nb_tile_parts_correction from position q (after tile `tile`'s
+// last tile-part): false = the decode fails; *fix = a later SOT of the same
+// tile has TPsot == TNsot (the non-conformant streams the reference patches)
+static bool tp_lookahead(const uint8_t *cs, size_t len, uint64_t q, uint32_t tile, bool *fix, std::string &err) {
+    *fix = false;
+    for (;;) {
+        if (q > len || len - q < 2) return true;  // no further marker: assumed fine
+        const uint32_t m = rd16(cs + q);
+        q += 2;
+        if (m != 0xFF90) return true;
+        if (len - q < 2) { err = "Stream too short"; return false; }
+        if (rd16(cs + q) != 10) { err = "Inconsistent marker size"; return false; }
+        q += 2;
+        if (len - q < 8) { err = "Stream too short"; return false; }
+        const uint32_t t = rd16(cs + q), tot = rd32(cs + q + 2), part = cs[q + 6], nparts = cs[q + 7];
+        q += 8;
+        if (t == tile) { *fix = part == nparts; return true; }
+        if (tot < 14) return true;  // 0: the last tile-part; < 14: invalid -- assumed fine
+        q += tot - 12;              // a seek past the end succeeds; the next read fails
+    }
+}
+
+// skip[t]: tile t lies outside the decode window (m_skip_data, j2k.cpp:5262-5274)
+static bool walk_tile_parts(const uint8_t *cs, size_t len, size_t sot0, uint32_t ntiles, const std::vector<uint8_t> &skip,
+                            TileWalk &w, std::string &err) {
+    enum : uint32_t { TPHSOT = 0x08, TPH = 0x10, NEOC = 0x40, EOC = 0x100 };
+    w.parts.assign(ntiles, {});
+    w.marks.assign(ntiles, {});
+    w.seq.assign(ntiles, {});
+    w.decoded.assign(ntiles, 0);
+    w.ntp = 0;
+    std::vector<int32_t> cur_tp(ntiles, -1);
+    std::vector<uint32_t> nb_tp(ntiles, 0);
+    std::vector<uint8_t> has_data(ntiles, 0);
+    uint64_t p = sot0 + 2;  // the first SOT's code was read with the main header
+    // bytes left; past the end (after a seek) the stream's unsigned count is huge
+    auto left = [&]() -> uint64_t { return p <= len ? len - p : ~0ull; };
+    auto read = [&](uint64_t n, uint64_t *at) -> bool {  // a short read takes what is left
+        *at = p;
+        if (p <= len && n <= len - p) { p += n; return true; }
+        if (p < len) p = len;
+        return false;
+    };
+    uint32_t state = TPHSOT, tcur = 0, tpl = 0, ndec = 0;
+    bool ready = false, last_tp = false, checked = false, skipping = false;
+    uint64_t at;
+    for (uint32_t nr = 0; nr < ntiles; ++nr) {
+        uint32_t marker = 0xFF90;
+        if (state == EOC) marker = 0xFFD9;
+        else if (state != TPHSOT) { err = "Stream too short"; return false; }
+        while (!ready && marker != 0xFFD9) {
+            while (marker != 0xFF93) {
+                if (left() == 0) { state = NEOC; break; }
+                if (!read(2, &at)) { err = "Stream too short"; return false; }
+                uint32_t ms = rd16(cs + at);
+                if (ms < 2) { err = "Inconsistent marker size"; return false; }
+                if (state & TPH) tpl -= ms + 2;
+                ms -= 2;
+                const bool sot = marker == 0xFF90;
+                if (sot ? !(state & TPHSOT) : (!(state & TPH) || !tph_marker(marker))) {
+                    err = "Marker is not compliant with its position";
+                    return false;
+                }
+                if (!read(ms, &at)) { err = "Stream too short"; return false; }
+                if (sot) {  // j2k_read_sot
+                    if (ms != 8) { err = "Error reading SOT marker"; return false; }
+                    const uint32_t t = rd16(cs + at), psot = rd32(cs + at + 2), part = cs[at + 6], nparts = cs[at + 7];
+                    if (t >= ntiles) { err = "Invalid tile number"; return false; }
+                    tcur = t;
+                    if (cur_tp[t] + 1 != (int32_t)part) { err = "Invalid tile part index"; return false; }
+                    ++cur_tp[t];
+                    if (psot && psot < 14 && psot != 12) { err = "Psot value is not correct"; return false; }
+                    if (!psot) last_tp = true;
+                    if (nb_tp[t] && part >= nb_tp[t]) { err = "Current tile part number greater than the tile-parts"; return false; }
+                    if (nparts) {
+                        if (part >= nparts) { err = "In SOT marker, TPSot is not valid"; return false; }
+                        nb_tp[t] = nparts;
+                    }
+                    if (nb_tp[t] && nb_tp[t] == part + 1) ready = true;
+                    tpl = last_tp ? 0u : psot - 12;
+                    state = TPH;
+                    skipping = skip[t] != 0;
+                    w.seq[t].push_back(w.ntp++);
+                } else if (marker == 0xFF52 || marker == 0xFF5C || marker == 0xFF53 || marker == 0xFF5D ||
+                           marker == 0xFF5E || marker == 0xFF5F || marker == 0xFF61) {
+                    w.marks[tcur].push_back({marker, (size_t)at, ms});
+                }
+                if (skipping) {  // the rest of the tile-part stepped over
+                    p += tpl;
+                    marker = 0xFF93;
+                } else {
+                    if (!read(2, &at)) { err = "Stream too short"; return false; }
+                    marker = rd16(cs + at);
+                }
+            }
+            if (left() == 0 && state == NEOC) break;
+            if (!skipping) {  // j2k_read_sod
+                if (last_tp) tpl = (uint32_t)(left() - 2);
+                else if (tpl >= 2) tpl -= 2;
+                if (tpl && tpl > left()) tpl = (uint32_t)left();
+                if (tpl) {
+                    w.parts[tcur].push_back({(size_t)p, tpl});
+                    has_data[tcur] = 1;
+                    p += tpl;
+                }
+                state = TPHSOT;
+                if (ready && !checked) {
+                    checked = true;
+                    bool fix = false;
+                    if (!tp_lookahead(cs, len, p, tcur, &fix, err)) return false;
+                    if (fix) { err = "non-conformant tile-part count (TPsot == TNsot) not supported"; return false; }
+                }
+                if (!ready) {
+                    if (!read(2, &at)) { err = "Stream too short"; return false; }
+                    marker = rd16(cs + at);
+                }
+            } else {
+                skipping = false;
+                ready = false;
+                state = TPHSOT;
+                if (!read(2, &at)) { err = "Stream too short"; return false; }
+                marker = rd16(cs + at);
+            }
+        }
+        if (marker == 0xFFD9 && state != EOC) { state = EOC; tcur = 0; }
+        if (!ready) {  // the stream ended or reached EOC: the next tile holding data, if any
+            while (tcur < ntiles && !has_data[tcur]) ++tcur;
+            if (tcur == ntiles) break;
+        }
+        // j2k_decode_tile
+        if (!has_data[tcur]) { err = "Failed to decode tile (no tile data)"; return false; }
+        w.decoded[tcur] = 1;
+        has_data[tcur] = 0;
+        ready = false;
+        ++ndec;
+        if (left() == 0 && state == NEOC) break;
+        if (state != EOC && read(2, &at)) {  // the marker after the tile: EOC, SOT, or the end
+            const uint32_t m = rd16(cs + at);
+            if (m == 0xFFD9) { tcur = 0; state = EOC; }
+            else if (m != 0xFF90) {
+                if (left() == 0) state = NEOC;
+                else if (nr + 1 < ntiles) { err = "Stream too short, expected SOT"; return false; }
+            }
+        }
+        if (left() == 0 && state == NEOC) break;
+    }
+    if (!ndec) { err = "No tiles were decoded"; return false; }
+    return true;
+}
+
 // reduce > 0 (whole-image decode only): the image at resolution
 // numres - 1 - reduce (grk_decompress -r, cp_reduce, grok.h:698-702): every
 // packet is still parsed, code-blocks of the dropped resolutions are not
@@ -2002,40 +2265,22 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     Rect cwin[GRKGPU_MAX_COMPS];
     for (uint32_t k = 0; k < nc; ++k) cwin[k] = comp_rect({ix0, iy0, ix1, iy1}, cp.dx[k], cp.dy[k]);
 
-    // tile-parts: SOT/SOD chunks per tile (j2k.cpp j2k_read_sot / j2k_read_sod)
-    // and the coding-parameter markers of their headers (COD / COC / QCD /
-    // QCC / RGN / POC / PPT, j2k.cpp:3829-4990), applied to the tile's own
-    // copy of the parameters below
-    struct TpMarker { uint32_t m; size_t off; uint32_t len; };
-    std::vector<std::vector<std::pair<size_t, size_t>>> tparts(ntiles);
-    std::vector<std::vector<TpMarker>> tmarks(ntiles);
-    std::vector<std::vector<uint32_t>> tpseq(ntiles);  // codestream-order index of each of the tile's tile-parts
-    uint32_t ntp_total = 0;
-    while (pos + 2 <= len) {
-        uint32_t m = rd16(csb + pos);
-        if (m == 0xFFD9) break;
-        if (m != 0xFF90 || pos + 12 > len) return set_err(GRKGPU_ECORRUPT, "expected SOT");
-        uint32_t isot = rd16(csb + pos + 4), psot = rd32(csb + pos + 6);
-        if (isot >= ntiles) return set_err(GRKGPU_ECORRUPT, "bad tile index");
-        size_t sot = pos;
-        size_t end = psot ? sot + psot : len - 2;
-        if (end > len) end = len;
-        pos += 12;
-        while (pos + 4 <= end && rd16(csb + pos) != 0xFF93) {
-            uint32_t mm = rd16(csb + pos);
-            const uint32_t ml = rd16(csb + pos + 2);
-            if (ml < 2 || pos + 2 + ml > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part header marker");
-            if (mm == 0xFF52 || mm == 0xFF5C || mm == 0xFF53 || mm == 0xFF5D || mm == 0xFF5E || mm == 0xFF5F ||
-                mm == 0xFF61)
-                tmarks[isot].push_back({mm, pos + 4, ml - 2});
-            pos += 2 + ml;
-        }
-        pos += 2;
-        if (pos > end) return set_err(GRKGPU_ECORRUPT, "bad tile-part");
-        tparts[isot].push_back({pos, end - pos});
-        tpseq[isot].push_back(ntp_total++);
-        pos = end;
-    }
+    // tile-parts: the reference's walk (walk_tile_parts) -- which tiles are
+    // decoded, from which tile-parts, and where a short stream fails; the
+    // coding-parameter markers of the tile-part headers (COD / COC / QCD / QCC
+    // / RGN / POC / PPT, j2k.cpp:3829-4990) are applied to the tile's own copy
+    // of the parameters below
+    std::vector<uint8_t> wskip(ntiles, 0);
+    if (win)
+        for (uint32_t t = 0; t < ntiles; ++t)
+            wskip[t] = !overlap(comp_rect(tile_rect(cp, t), 1u << reduce, 1u << reduce), {ix0, iy0, ix1, iy1});
+    TileWalk walk;
+    if (!walk_tile_parts(csb, len, pos, ntiles, wskip, walk, err)) return set_err(GRKGPU_ECORRUPT, err);
+    const auto &tparts = walk.parts;
+    const auto &tmarks = walk.marks;
+    const auto &tpseq = walk.seq;
+    bool missing = false;  // tiles the walk did not decode: zero in the output
+    for (uint32_t t = tb; t < te; ++t) missing = missing || (!walk.decoded[t] && !wskip[t]);
     // PPM (j2k_merge_ppm, j2k.cpp:4766-4900): the main header's packed packet
     // headers, Zppm order, as Nppm / Ippm pairs -- the i-th pair holds the
     // headers of the codestream's i-th tile-part
@@ -2092,6 +2337,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             for (uint32_t k = 0; k < 16; ++k) troi[lt][k] = cp.roishift[k];
             if (win && !overlap(comp_rect(tile.r, 1u << reduce, 1u << reduce), {ix0, iy0, ix1, iy1}))
                 continue;  // left without components: skipped below
+            if (!walk.decoded[t]) continue;  // never reached: its samples stay zero
             // the tile's coding parameters: the main header's, then its
             // tile-part headers' markers (precedence tile COC > tile COD >
             // main COC > main COD; QCC / QCD alike); POC entries appended
@@ -2420,6 +2666,21 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     if (opad)
         for (uint32_t k = 0; k < nc; ++k)
             HIPCHK(hipMemsetAsync(dst.p[k], 0, (ooff[k + 1] - ooff[k]) * 4, s));
+    else if (missing)  // tiles the tile-part walk never reached: zero (their regions only -- a shard's
+                       // device planes hold other tiles)
+        for (uint32_t t = tb; t < te; ++t) {
+            if (walk.decoded[t] || wskip[t]) continue;
+            for (uint32_t k = 0; k < nc; ++k) {
+                const Rect cr = comp_rect(tile_rect(cp, t), cp.dx[k], cp.dy[k]);
+                const Rect rr{ceil_pow2(cr.x0, reduce), ceil_pow2(cr.y0, reduce), ceil_pow2(cr.x1, reduce),
+                              ceil_pow2(cr.y1, reduce)};
+                const Rect o = intersect(rr, orect[k]);
+                if (o.empty()) continue;
+                const uint32_t ow = orect[k].w();
+                HIPCHK(hipMemset2DAsync(dst.p[k] + (uint64_t)(o.y0 - orect[k].y0) * ow + (o.x0 - orect[k].x0),
+                                        (size_t)ow * 4, 0, (size_t)o.w() * 4, o.h(), s));
+            }
+        }
     ShiftArr sh{}, mn{}, mx{};
     for (uint32_t k = 0; k < nc; ++k) {
         sh.v[k] = cp.shift[k];
@@ -2520,6 +2781,21 @@ extern "C" int grkgpu_decompress_ex(grkgpu_ctx *c, const uint8_t *csb, size_t le
     if (win && (dp->DA_x1 <= dp->DA_x0 || dp->DA_y1 <= dp->DA_y0)) return set_err(GRKGPU_EINVAL, "empty decode area");
     return decompress_impl(c, csb, len, img, planes, planes_on_device, 0, 0xffffffffu, dp->cp_reduce,
                            win ? &w : nullptr, dp->cp_layer);
+}
+
+extern "C" int grkgpu_walk_tiles(const uint8_t *csb, size_t len, uint8_t *decoded, uint32_t cap, uint32_t *ntiles) {
+    if (!csb || !ntiles) return set_err(GRKGPU_EINVAL, "null argument");
+    CodingParams cp;
+    size_t pos = 0;
+    std::string err;
+    if (!parse_main_header(csb, len, cp, pos, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
+    const uint32_t n = cp.tw * cp.th;
+    *ntiles = n;
+    TileWalk walk;
+    if (!walk_tile_parts(csb, len, pos, n, std::vector<uint8_t>(n, 0), walk, err)) return set_err(GRKGPU_ECORRUPT, err);
+    if (decoded)
+        for (uint32_t t = 0; t < n && t < cap; ++t) decoded[t] = walk.decoded[t];
+    return GRKGPU_OK;
 }
 
 extern "C" int grkgpu_decompress_tiles(grkgpu_ctx *c, const uint8_t *csb, size_t len, uint32_t tile_begin,

@@ -30,6 +30,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
+#include <cstdlib>
 
 #include "grk_device.h"
 
@@ -773,6 +775,374 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
         fwd_vertical<IRREV, RW, T>(lo, hi, rh1, casy1);
         fwd_horizontal_store<IRREV, F::THW, F::W1, T>(J1, lo, hi, ty1 * 4 + w, yw, gx0, lane);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Forward levels l and l + 1 streamed down column strips (k_dwt_fwd_pair;
+// 5/3 and 9/7).  k_dwt_fwd01 lifts independent windows: every window
+// re-reads and re-lifts 2 x 4 halo rows, and every workgroup re-computes the
+// LL halo of its level-(l+1) window -- the 8K frame's pair read 1.49x its
+// input and lifted ~1.8x its samples.  Here a workgroup owns a strip of
+// CW1 level-(l+1) columns x S1 rows and walks it top to bottom:
+//   * NW0 level-l waves, side by side (128 columns each, PW = 60 / 62 LL
+//     columns of core), stream down the strip in chunks of C0 = 16 rows.
+//     The vertical lifting is carried from chunk to chunk: the last P = NS + 2
+//     rows of a chunk, partially lifted, stay in registers and head the next
+//     chunk's array, so no row is loaded or lifted twice (vlift_stream).  The
+//     next chunk's rows are loaded before the current one is lifted.
+//   * A chunk's 16 finished rows are lifted horizontally; their HL / LH / HH
+//     samples go to the Mallat bands in HBM, the LL row into an LDS ring of
+//     RING rows x LW columns.
+//   * NW1 level-(l+1) waves stream the LL rows out of the ring in chunks of
+//     C1 = 8 rows the same way (LL whole-sample symmetric extension applied
+//     to the ring's row / column indices), then store LL_{l+1} and the level's
+//     bands as k_dwt_fwd does.
+//   * One workgroup barrier per level-l chunk; a level-(l+1) chunk runs in
+//     the first iteration after the level-l chunk holding its last LL row.
+// A segment re-reads only the rows above and below it that its two lifting
+// halos need (~2 x 12 rows per segment of 2 S1), and a strip the 2 x 4 LL
+// columns of the level-(l+1) halo plus the level-l halo at its sides.
+// ---------------------------------------------------------------------------
+template <bool IRREV, int NW0_, int C0_ = 16, int PF_ = 1>
+struct PairGeo {
+    static constexpr int NS = IRREV ? 4 : 2;           // lifting steps: halo rows / columns per side
+    static constexpr int P = NS + 2;                   // rows carried from one chunk to the next
+    static constexpr int PW = (DWT_WIN - 2 * NS) / 2;  // LL columns per level-l wave (60 / 62)
+    static constexpr int NW0 = NW0_;                   // level-l waves
+    static constexpr int LW = NW0 * PW;                // LL columns a workgroup computes
+    static constexpr int CW = DWT_WIN - 2 * NS;        // core columns of a level-(l+1) window
+    static constexpr int CW1 = LW - 2 * NS;            // level-(l+1) core columns per workgroup
+    static constexpr int NW1 = (CW1 + CW - 1) / CW;    // level-(l+1) waves
+    static constexpr int WAVES = NW0 + NW1;
+    static constexpr int C0 = C0_, C1 = 8;             // rows per chunk (level l, level l + 1)
+    static constexpr int RING = 32;                    // LL rows held in LDS
+    static constexpr bool PF = PF_ != 0;               // level-l rows of the next chunk loaded before the lifting
+};
+
+// Vertical lifting step S over rows k >= K0 of parity K0 (see vstep).
+template <int OP, int K0, int S, int R, typename T>
+__device__ __forceinline__ void vstep_at(T (&v)[R]) {
+#pragma unroll
+    for (int k = K0; k + 1 + S < R; k += 2) v[k] = liftv<OP>(v[k], v[k - 1], v[k + 1]);
+}
+
+// Streaming vertical lifting of an array of R = P + C rows whose even rows
+// are low pass.  FIRST: fresh rows, the steps start at the array's top (its
+// first NS rows come out inexact).  Otherwise rows [0, P) are the previous
+// array's rows [C, C + P) as it left them: its last two rows raw, the two
+// before with the first one / two steps, the two before those final.  Step S
+// then resumes at row P - 1 - S.  Either way rows [2, 2 + C) come out final
+// and the array's last P rows are left in the state the next chunk expects
+// (every step S stops at k + 1 + S < R).
+template <bool IRREV, bool FIRST, int R, typename T>
+__device__ __forceinline__ void vlift_stream(T (&lo)[R], T (&hi)[R]) {
+    if constexpr (!IRREV) {
+        vstep_at<0, FIRST ? 1 : 3, 0>(lo); vstep_at<0, FIRST ? 1 : 3, 0>(hi);
+        vstep_at<1, 2, 1>(lo); vstep_at<1, 2, 1>(hi);
+    } else {
+        vstep_at<2, FIRST ? 1 : 5, 0>(lo); vstep_at<2, FIRST ? 1 : 5, 0>(hi);
+        vstep_at<3, FIRST ? 2 : 4, 1>(lo); vstep_at<3, FIRST ? 2 : 4, 1>(hi);
+        vstep_at<4, 3, 2>(lo); vstep_at<4, 3, 2>(hi);
+        vstep_at<5, FIRST ? 4 : 2, 3>(lo); vstep_at<5, FIRST ? 4 : 2, 3>(hi);
+    }
+}
+
+// Horizontal lifting of one vertically lifted row (9/7: after the vertical
+// scale, K/2 for a high row, 1/K for a low one).  rw, rh > 1.
+template <bool IRREV, typename T>
+__device__ __forceinline__ void hlift_row(T &L, T &H, bool high) {
+    if constexpr (IRREV) {
+        const int32_t k = high ? 5039 : 6659;
+        L = scalev(L, k); H = scalev(H, k);
+        H = liftv<2>(H, L, from_next(L));
+        L = liftv<3>(L, from_prev(H), H);
+        H = liftv<4>(H, L, from_next(L));
+        L = liftv<5>(L, from_prev(H), H);
+        H = scalev(H, 5039);
+        L = scalev(L, 6659);
+    } else {
+        H = lift<0>(H, L, from_next(L));
+        L = lift<1>(L, from_prev(H), H);
+    }
+}
+
+// Workgroup barrier ordering LDS only: outstanding global loads (the next
+// chunk's rows) stay in flight across it.
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// mirror_idx for n >= 2 without the small-n loop: exact within one
+// reflection, any valid index beyond (rows no kept sample depends on)
+__device__ __forceinline__ int mirror1(int p, int n) {
+    p = p < 0 ? -p : p;
+    p = p >= n ? 2 * (n - 1) - p : p;
+    return p < 0 ? 0 : p;
+}
+
+// byte offsets of rows t .. t + N - 1 of a resolution of rh rows (mirrored
+// at its edges); wave-uniform
+template <int N>
+__device__ __forceinline__ void row_offsets(int t, int rh, int st, int (&so)[N]) {
+    if (t >= 0 && t + N <= rh) {
+#pragma unroll
+        for (int r = 0; r < N; ++r) so[r] = (t + r) * st;
+    } else {
+#pragma unroll
+        for (int r = 0; r < N; ++r) so[r] = mirror1(t + r, rh) * st;
+    }
+}
+
+// strip geometry shared by the kernel and the host
+struct PairStrip {
+    int xs1, ys1, ye1, t1, nC1, e0, t0, nC0, Q0, Q1, P0, P1;
+};
+template <bool IRREV, int NW0, int C0X>
+__device__ __forceinline__ bool pair_strip(const DwtJob &J0, const DwtJob &J1, int S1, int wg, PairStrip &g, int &tx,
+                                           int &ntx) {
+    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    constexpr int NS = G::NS;
+    const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
+    ntx = (rw1 + casx1 + G::CW1 - 1) / G::CW1;
+    const int nty = (rh1 + casy1 + S1 - 1) / S1;
+    if (wg >= ntx * nty) return false;
+    tx = wg % ntx;
+    const int ty = wg / ntx;
+    g.xs1 = tx * G::CW1 - casx1;
+    g.ys1 = ty * S1 - casy1;
+    g.ye1 = min(g.ys1 + S1, rh1);
+    g.t1 = g.ys1 - NS;                                        // level-(l+1) stream: first row
+    g.nC1 = (g.ye1 - g.t1 - 2 + G::C1 - 1) / G::C1;           // chunks until row ye1 - 1 is final
+    const int lo1 = max(0, g.t1), hi1 = min(rh1, g.ye1 + NS);  // LL rows it needs exactly
+    const int casy0 = J0.casy;
+    g.Q0 = ty == 0 ? INT32_MIN : g.ys1;                       // level-l band pair rows owned
+    g.Q1 = ty == nty - 1 ? INT32_MAX : g.ys1 + S1;
+    g.P0 = tx == 0 ? INT32_MIN : g.xs1;                       // ... and pair columns
+    g.P1 = tx == ntx - 1 ? INT32_MAX : g.xs1 + G::CW1;
+    const int first = ty == 0 ? min(lo1, -casy0) : lo1;      // first pair row to compute
+    const int plast = (J0.rh - 1 - casy0) >> 1;
+    const int pmax = ty == nty - 1 ? max(hi1 - 1, plast) : hi1 - 1;
+    g.t0 = 2 * first + casy0 - NS;                           // level-l stream: first row
+    g.e0 = first - (NS - 2) / 2;                             // pair row of its first emitted row
+    g.nC0 = (pmax + 1 - g.e0 + G::C0 / 2 - 1) / (G::C0 / 2);
+    return true;
+}
+
+// level-l waves of k_dwt_fwd_pair (VEC: 8-byte column-pair loads)
+template <bool IRREV, int NW0, int C0X, bool VEC, typename T>
+__device__ __forceinline__ void pair_level0(const DwtJob &J0, const PairStrip &g,
+                                            int32_t (*ll)[PairGeo<IRREV, NW0>::LW + 1], int k, int lane) {
+    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    constexpr int NS = G::NS, P = G::P, C0 = G::C0, RING = G::RING;
+    const int rw0 = J0.rw, rh0 = J0.rh, casx0 = J0.casx, casy0 = J0.casy;
+    const int xw = 2 * (g.xs1 - NS + G::PW * k) + casx0 - NS;  // window column origin
+    const int gx0 = xw + 2 * lane, gx1 = gx0 + 1;
+    const rsrc_t in = mkbuf(J0.in, J0.in_bytes);
+    const int st = (int)J0.in_stride * 4;
+    const int o0 = VEC ? gx0 * 4 : mirror_idx(gx0, rw0) * 4, o1 = mirror_idx(gx1, rw0) * 4;
+    const bool lane_core = lane >= NS / 2 && lane < NS / 2 + G::PW;
+    const int pc = (gx0 - casx0) >> 1;  // this lane's pair column (LL coordinates)
+    const bool own_c = lane_core && pc >= g.P0 && pc < g.P1;
+    const bool okx0 = own_c && gx0 >= 0 && gx0 < rw0, okx1 = own_c && gx1 >= 0 && gx1 < rw0;
+    const int vl = okx0 ? pc * 4 : OOB;
+    const int vh = okx1 ? (J0.snx + pc + casx0) * 4 : OOB;
+    const rsrc_t bandb = mkbuf(J0.bands, J0.bands_bytes);
+    const int bst = (int)J0.bands_stride * 4;
+    // LDS column of this lane's LL sample; the halo lanes write a spare column
+    const int lcol = lane_core ? pc - (g.xs1 - NS) : G::LW;
+    auto ldrows = [&](int t, T *a, T *b, auto n) {
+        constexpr int N = decltype(n)::value;
+        int so[N];
+        row_offsets<N>(t, rh0, st, so);
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            if constexpr (VEC) {
+                const auto p = __builtin_amdgcn_raw_buffer_load_b64(in, o0, so[r], 0);
+                a[r] = (T)(int32_t)p[0]; b[r] = (T)(int32_t)p[1];
+            } else {
+                a[r] = (T)ld32(in, o0, so[r]); b[r] = (T)ld32(in, o1, so[r]);
+            }
+        }
+    };
+    T lo[P + C0], hi[P + C0], nlo[G::PF ? C0 : 1], nhi[G::PF ? C0 : 1];
+    ldrows(g.t0, lo, hi, std::integral_constant<int, P + C0>{});
+    for (int c = 0; c <= g.nC0; ++c) {
+        if (c < g.nC0) {
+            const bool more = c + 1 < g.nC0;  // wave-uniform
+            if (G::PF && more) ldrows(g.t0 + P + (c + 1) * C0, nlo, nhi, std::integral_constant<int, G::PF ? C0 : 1>{});
+            if (c == 0) vlift_stream<IRREV, true>(lo, hi);
+            else vlift_stream<IRREV, false>(lo, hi);
+            const int tb = g.t0 + c * C0;
+            const int pb = (tb + 2 - casy0) >> 1;  // pair row of the chunk's first emitted row
+#pragma unroll
+            for (int i = 2; i < 2 + C0; ++i) {
+                T Lv = lo[i], Hv = hi[i];
+                hlift_row<IRREV>(Lv, Hv, i & 1);
+                const int t = tb + i;
+                const int p = pb + (i - 2) / 2;
+                // rows this workgroup does not own: stores dropped through an
+                // out-of-range lane offset (no branch)
+                const bool rok = p >= g.Q0 && p < g.Q1 && t >= 0 && t < rh0;  // wave-uniform
+                const int rl = rok ? vl : OOB, rh = rok ? vh : OOB;
+                if ((i & 1) == 0) {
+                    ll[(p - g.e0) & (RING - 1)][lcol] = to_i32(Lv);
+                    st32(to_i32(Hv), bandb, rh, p * bst);  // HL
+                } else {
+                    const int so = (J0.sny + p + casy0) * bst;  // LH | HH
+                    st32(to_i32(Lv), bandb, rl, so);
+                    st32(to_i32(Hv), bandb, rh, so);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < P; ++r) { lo[r] = lo[r + C0]; hi[r] = hi[r + C0]; }
+            if (more) {
+                if constexpr (G::PF) {
+#pragma unroll
+                    for (int r = 0; r < C0; ++r) { lo[P + r] = nlo[r]; hi[P + r] = nhi[r]; }
+                } else {  // loaded now, in flight across the barrier
+                    ldrows(g.t0 + P + (c + 1) * C0, lo + P, hi + P, std::integral_constant<int, C0>{});
+                }
+            }
+        }
+        lds_barrier();
+    }
+}
+
+// level-(l+1) waves of k_dwt_fwd_pair
+template <bool IRREV, int NW0, int C0X, typename T>
+__device__ __forceinline__ void pair_level1(const DwtJob &J1, const PairStrip &g,
+                                            int32_t (*ll)[PairGeo<IRREV, NW0>::LW + 1], int a, int lane) {
+    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    constexpr int NS = G::NS, P = G::P, C1 = G::C1, RING = G::RING, LW = G::LW;
+    const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
+    const int base = g.xs1 - NS;  // LL column of LDS column 0
+    const int oa = a == 0 ? 0 : max(0, min(a * G::CW, LW - DWT_WIN));
+    const int gx0 = base + oa + 2 * lane, gx1 = gx0 + 1;
+    const int c0 = min(max(mirror_idx(gx0, rw1) - base, 0), LW - 1);
+    const int c1 = min(max(mirror_idx(gx1, rw1) - base, 0), LW - 1);
+    const bool lane_core = lane >= NS / 2 && lane < NS / 2 + G::CW / 2;
+    const int ox0 = g.xs1 + a * G::CW, ox1 = g.xs1 + min((a + 1) * G::CW, G::CW1);  // columns this wave stores
+    const bool own0 = lane_core && gx0 >= ox0 && gx0 < ox1 && gx0 >= 0 && gx0 < rw1;
+    const bool own1 = lane_core && gx1 >= ox0 && gx1 < ox1 && gx1 >= 0 && gx1 < rw1;
+    const int vl = own0 ? ((gx0 - casx1) >> 1) * 4 : OOB;
+    const int vh = own1 ? (J1.snx + ((gx1 - 1 + casx1) >> 1)) * 4 : OOB;
+    const rsrc_t outb = mkbuf(J1.out, J1.out_bytes), bandb = mkbuf(J1.bands, J1.bands_bytes);
+    const int ost = (int)J1.out_stride * 4, bst = (int)J1.bands_stride * 4;
+    auto ldsrows = [&](int t, T *x, T *y, auto n) {
+        constexpr int N = decltype(n)::value;
+        int rr[N];
+        if (t >= 0 && t + N <= rh1) {
+#pragma unroll
+            for (int r = 0; r < N; ++r) rr[r] = (t + r - g.e0) & (RING - 1);
+        } else {
+#pragma unroll
+            for (int r = 0; r < N; ++r) rr[r] = (mirror1(t + r, rh1) - g.e0) & (RING - 1);
+        }
+#pragma unroll
+        for (int r = 0; r < N; ++r) { x[r] = (T)ll[rr[r]][c0]; y[r] = (T)ll[rr[r]][c1]; }
+    };
+    T lo[P + C1], hi[P + C1];
+    int j = 0;
+    const int hi1 = min(rh1, g.ye1 + NS);
+    for (int c = 0; c <= g.nC0; ++c) {
+        for (; j < g.nC1; ++j) {
+            // ready once the level-l chunk holding its last exact LL row is in the ring
+            const int mj = min(hi1, g.t1 + P + (j + 1) * C1) - 1;
+            if ((mj - g.e0) / (G::C0 / 2) + 1 > c) break;
+            if (j == 0) {
+                ldsrows(g.t1, lo, hi, std::integral_constant<int, P + C1>{});
+                vlift_stream<IRREV, true>(lo, hi);
+            } else {
+                ldsrows(g.t1 + P + j * C1, lo + P, hi + P, std::integral_constant<int, C1>{});
+                vlift_stream<IRREV, false>(lo, hi);
+            }
+            const int tb = g.t1 + j * C1;
+#pragma unroll
+            for (int i = 2; i < 2 + C1; ++i) {
+                T Lv = lo[i], Hv = hi[i];
+                hlift_row<IRREV>(Lv, Hv, i & 1);
+                const int t = tb + i;
+                const bool rok = t >= g.ys1 && t < g.ye1 && t >= 0;  // wave-uniform
+                const int rl = rok ? vl : OOB, rh = rok ? vh : OOB;
+                if ((i & 1) == 0) {  // low row -> LL | HL
+                    const int iy = (t - casy1) >> 1;
+                    st32(to_i32(Lv), outb, rl, iy * ost);
+                    st32(to_i32(Hv), bandb, rh, iy * bst);
+                } else {             // high row -> LH | HH
+                    const int so = (J1.sny + ((t - 1 + casy1) >> 1)) * bst;
+                    st32(to_i32(Lv), bandb, rl, so);
+                    st32(to_i32(Hv), bandb, rh, so);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < P; ++r) { lo[r] = lo[r + C1]; hi[r] = hi[r + C1]; }
+        }
+        lds_barrier();
+    }
+}
+
+template <bool IRREV, int NW0, int C0X, typename T = int32_t>
+__global__ __launch_bounds__((64 * PairGeo<IRREV, NW0>::WAVES)) __attribute__((amdgpu_waves_per_eu((C0X >> 8) ? 1 : 6))) void k_dwt_fwd_pair(const DwtJob *__restrict__ jobs0,
+                                                                                   const DwtJob *__restrict__ jobs1,
+                                                                                   int S1, int lay) {
+    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    __shared__ int32_t ll[G::RING][G::LW + 1];  // + a spare column for the halo lanes' writes
+    const int gx = gridDim.x;
+    int L = blockIdx.y * gx + blockIdx.x;
+    if (lay & 1) L = xcd_remap(L, gx * gridDim.y);
+    const int job = L / gx, wg = L % gx;
+    const DwtJob &J0 = jobs0[job];
+    const DwtJob &J1 = jobs1[job];
+    PairStrip g;
+    int tx, ntx;
+    if (!pair_strip<IRREV, NW0, C0X>(J0, J1, S1, wg, g, tx, ntx)) return;  // uniform over the workgroup
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w < NW0) {
+        const int xw = 2 * (g.xs1 - G::NS + G::PW * w) + J0.casx - G::NS;
+        const bool vec = (J0.casx | (J0.in_stride & 1)) == 0 && xw >= 0 && xw + DWT_WIN <= J0.rw;  // wave-uniform
+        if (vec) pair_level0<IRREV, NW0, C0X, true, T>(J0, g, ll, w, lane);
+        else pair_level0<IRREV, NW0, C0X, false, T>(J0, g, ll, w, lane);
+    } else {
+        pair_level1<IRREV, NW0, C0X, T>(J1, g, ll, w - NW0, lane);
+    }
+}
+
+// Host geometry of k_dwt_fwd_pair: level-(l+1) core columns per workgroup for
+// nw0 level-l waves (3 or 4), and workgroups per job for S1 rows per segment.
+int dwt_pair_cw1(int irrev, int nw0) {
+    if (irrev) return nw0 == 3 ? PairGeo<true, 3>::CW1 : PairGeo<true, 4>::CW1;
+    return nw0 == 3 ? PairGeo<false, 3>::CW1 : PairGeo<false, 4>::CW1;
+}
+int dwt_pair_wgs(int irrev, int nw0, int s1, int rw1, int rh1, int casx1, int casy1) {
+    const int cw1 = dwt_pair_cw1(irrev, nw0);
+    return ((rw1 + casx1 + cw1 - 1) / cw1) * ((rh1 + casy1 + s1 - 1) / s1);
+}
+
+hipError_t launch_dwt_fwd_pair(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_wgs, int irrev,
+                               int nw0, int s1, hipStream_t s) {
+    if (!njobs || !max_wgs || s1 < 2 || (s1 & 1)) return hipErrorInvalidValue;
+    const int lay = 1;  // XCD-contiguous runs: a strip's horizontal neighbours share an L2
+    const dim3 g(max_wgs, njobs);
+#define GRK_PAIR(IR, NW, C)                                                                          \
+    hipLaunchKernelGGL((k_dwt_fwd_pair<IR, NW, C>), g, dim3(64 * PairGeo<IR, NW>::WAVES), 0, s, jobs0, jobs1, s1, lay)
+    static const int chunk = getenv("GRKGPU_PAIR_CHUNK") ? atoi(getenv("GRKGPU_PAIR_CHUNK")) : 16;
+    switch (chunk) {
+        case 8:
+            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 0x108); else GRK_PAIR(true, 4, 0x108); }
+            else { if (nw0 == 3) GRK_PAIR(false, 3, 0x108); else GRK_PAIR(false, 4, 0x108); }
+            break;
+        case 80:  // 8 rows, no prefetch registers
+            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 8); else GRK_PAIR(true, 4, 8); }
+            else { if (nw0 == 3) GRK_PAIR(false, 3, 8); else GRK_PAIR(false, 4, 8); }
+            break;
+        case 160:
+            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 16); else GRK_PAIR(true, 4, 16); }
+            else { if (nw0 == 3) GRK_PAIR(false, 3, 16); else GRK_PAIR(false, 4, 16); }
+            break;
+        default:
+            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 0x110); else GRK_PAIR(true, 4, 0x110); }
+            else { if (nw0 == 3) GRK_PAIR(false, 3, 0x110); else GRK_PAIR(false, 4, 0x110); }
+    }
+#undef GRK_PAIR
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -117,6 +117,11 @@ struct DwtOptions {
     int32_t mid_th = 0;      // window rows of a level of 2^21 .. 2^23 samples (0: 8)
     int32_t t1_enc_bpw = 0;  // T1 encode (MQ coder): blocks per wavefront (0: by block count)
     int32_t t1_enc_sort = 0; // T1 encode: MQ coder lanes take the blocks heaviest first (device counting sort)
+    int32_t pair_kernel = 1;  // fused forward level pairs: 1 = k_dwt_fwd_pair (streamed strips, 5/3 + 9/7),
+                              // 0 = k_dwt_fwd01 (9/7 windows, f01_rows)
+    int32_t pair_rows = 0;    // k_dwt_fwd_pair: level-(l+1) rows per segment (even; 0 = by size)
+    int32_t pair_waves = 0;   // k_dwt_fwd_pair: level-l waves per workgroup (3 / 4; 0 = by width)
+    uint64_t pair_min_samples = (uint64_t)1 << 20;  // k_dwt_fwd_pair: fuse pairs from this many level-l samples
 };
 const DwtOptions &dwt_options();
 // level geometry code (window rows) for a level of that many samples whose
@@ -141,6 +146,13 @@ hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t n
                             int na, hipStream_t s);
 hipError_t launch_dwt_fwd01(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_tiles, int irrev,
                             int ny, hipStream_t s);
+// forward levels l and l + 1 streamed down column strips (k_dwt_fwd_pair, 5/3
+// and 9/7): level-(l+1) core columns per workgroup with nw0 (3 / 4) level-l
+// waves, workgroups per job at s1 level-(l+1) rows per segment
+int dwt_pair_cw1(int irrev, int nw0);
+int dwt_pair_wgs(int irrev, int nw0, int s1, int rw1, int rh1, int casx1, int casy1);
+hipError_t launch_dwt_fwd_pair(const DwtJob *jobs0, const DwtJob *jobs1, uint32_t njobs, uint32_t max_wgs, int irrev,
+                               int nw0, int s1, hipStream_t s);
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.

@@ -232,7 +232,18 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    in decreasing order of their symbol count (a counting
  *                    sort on the device after the modelling kernel); 0
  *                    (default, measured as fast) = block order.  Same
- *                    codestream. */
+ *                    codestream.
+ *   pair_kernel      fused forward level pairs: 1 (default) = k_dwt_fwd_pair
+ *                    (5/3 and 9/7; workgroups stream column strips top to
+ *                    bottom, the vertical lifting carried in registers, the
+ *                    LL rows through an LDS ring), pairs of at least
+ *                    pair_min_samples level-l samples (default 2^20);
+ *                    0 = k_dwt_fwd01 (9/7 only, f01_rows windows).  f01_rows
+ *                    = 0 turns both off.
+ *   pair_rows        k_dwt_fwd_pair: level-(l+1) rows per segment (even); 0
+ *                    (default) = sized for one resident wave of workgroups.
+ *   pair_waves       k_dwt_fwd_pair: level-l wavefronts per workgroup, 3 or 4;
+ *                    0 (default) = whichever wastes fewer columns. */
 typedef struct {
     int32_t fuse_level0;
     int32_t f01_rows;
@@ -247,6 +258,10 @@ typedef struct {
     int32_t mid_th;
     int32_t t1_enc_bpw;
     int32_t t1_enc_sort;
+    int32_t pair_kernel;
+    int32_t pair_rows;
+    int32_t pair_waves;
+    uint64_t pair_min_samples;
 } grkgpu_dwt_options;
 void grkgpu_get_dwt_options(grkgpu_dwt_options *out);  /* current values */
 int grkgpu_set_dwt_options(const grkgpu_dwt_options *opts);  /* NULL: the defaults */
@@ -434,6 +449,14 @@ int grkgpu_decompress_ex(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, const g
  * for the shard's tiles only. */
 int grkgpu_decompress_tiles(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t tile_begin,
                             uint32_t tile_end, int32_t *const *planes, int planes_on_device);
+
+/* The tile-part walk of a decode, host only (no device needed): the
+ * reference decoder's walk over the tile-parts (j2k_decode_tiles,
+ * j2k.cpp:1136-1224) -- GRKGPU_OK and decoded[t] = 1 for every
+ * tile a decode produces (others stay zero in its output), or the error a
+ * short or damaged stream makes the whole decode fail with.  *ntiles = the
+ * tile count; decoded holds cap entries (may be NULL). */
+int grkgpu_walk_tiles(const uint8_t *cs, size_t len, uint8_t *decoded, uint32_t cap, uint32_t *ntiles);
 
 void grkgpu_free(void *p);
 

@@ -460,8 +460,41 @@ def test_dwt_fused01_stage_vs_oracle(oracle, ny, shape_off, numres):
     opts = dict(f01_rows=4, f01_min_samples=1 << 16, f01_small_min_samples=0) if ny == "mix" else \
         dict(f01_rows=4, f01_min_samples=0, pair_group=3) if ny == "g3" else \
         dict(f01_rows=4, f01_min_samples=0, f64_lift=1) if ny == "d" else dict(f01_rows=int(ny), f01_min_samples=0)
-    with grk.dwt_options(**opts):
+    with grk.dwt_options(pair_kernel=0, **opts):
         grk.dwt_fwd(t, x0, y0, numres, True)
+        torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("irrev", [False, True])
+@pytest.mark.parametrize("geo", [(0, 0), (0, 3), (14, 4), (8, 3), (30, 0), (62, 4), (16, 4)])
+@pytest.mark.parametrize("shape_off", [((32, 32), (0, 0)), ((33, 35), (1, 1)), ((77, 100), (3, 5)),
+                                       ((129, 200), (1, 0)), ((513, 257), (0, 3)), ((300, 497), (2, 2)),
+                                       ((37, 260), (1, 1)), ((700, 1030), (1, 1)), ((1100, 45), (0, 1)),
+                                       ((1081, 1921), (0, 1))])
+@pytest.mark.parametrize("numres", [3, 6])
+def test_dwt_pair_stage_vs_oracle(oracle, irrev, geo, shape_off, numres):
+    """Forward level pairs streamed down column strips (k_dwt_fwd_pair, the
+    default for pairs of >= 2^20 samples; here forced onto every qualifying
+    pair: 0+1, 2+3, ...), 5/3 and 9/7, at several segment heights
+    (pair_rows; 0 = by size) and 3 / 4 level-l wavefronts per workgroup
+    (pair_waves; 0 = by width), on odd sizes and offsets: every cas parity,
+    resolution edges inside the first / last chunk, strips and segments cut
+    by the image edge."""
+    import torch
+    import grokimagecompression_amd as grk
+    (h, w), (x0, y0) = shape_off
+    rows, waves = geo
+    if irrev and rows and rows % 8 != 6:
+        rows += 6 - rows % 8 if rows % 8 < 6 else 14 - rows % 8  # the 9/7 stream's whole chunks (8k - 2)
+    rng = np.random.default_rng(h * 31 + w + numres + 7 * irrev)
+    a = rng.integers(-(1 << 20), 1 << 20, size=(h, w)).astype(np.int32) if irrev else \
+        rng.integers(-(1 << 16), 1 << 16, size=(h, w)).astype(np.int32)
+    ref = oracle.dwt_fwd(a, x0, y0, numres, irrev)
+    t = torch.from_numpy(a).cuda()
+    with grk.dwt_options(pair_kernel=1, f01_rows=4, pair_min_samples=0, pair_rows=rows, pair_waves=waves,
+                         fuse_level0=0):
+        grk.dwt_fwd(t, x0, y0, numres, irrev)
         torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), ref)
 
