@@ -265,7 +265,7 @@ int grkgpu_set_dwt_options(const grkgpu_dwt_options *o) {
     if (o->t1_enc_bpw < 0 || o->t1_enc_bpw > 64 || (o->t1_enc_bpw & (o->t1_enc_bpw - 1)))
         return set_err(GRKGPU_EINVAL, "t1_enc_bpw must be 0 or a power of two <= 64");
     if (o->t1_enc_sort != 0 && o->t1_enc_sort != 1) return set_err(GRKGPU_EINVAL, "t1_enc_sort must be 0 or 1");
-    if (o->pair_kernel != 0 && o->pair_kernel != 1) return set_err(GRKGPU_EINVAL, "pair_kernel must be 0 or 1");
+    if (o->pair_kernel < 0 || o->pair_kernel > 2) return set_err(GRKGPU_EINVAL, "pair_kernel must be 0, 1 or 2");
     if (o->pair_rows < 0 || o->pair_rows > 65536 || (o->pair_rows & 1))
         return set_err(GRKGPU_EINVAL, "pair_rows must be 0 or an even count <= 65536");
     if (o->pair_waves != 0 && o->pair_waves != 3 && o->pair_waves != 4)
@@ -705,7 +705,13 @@ static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny, i
     const DwtOptions &o = dwt_options();
     *nw0 = 0;
     if (P.inverse || (li == 0 && P.fused0) || li + 1 >= P.levels.size() || !o.f01_rows) return 0;
-    if (!irrev && !o.pair_kernel) return 0;
+    // k_dwt_fwd_pair for 5/3 (pair_kernel 1, the default) or for both (2);
+    // 9/7 keeps k_dwt_fwd01's windows by default: the streamed pair moves
+    // less (435 vs 593 MB read per 8K frame) but its barrier-coupled
+    // strips leave the 64-bit fixed-point lifting latency-bound -- 198 us
+    // against 185 (profiles/r05/dwt_pair_ab.txt)
+    const bool stream = o.pair_kernel == 2 || (o.pair_kernel == 1 && !irrev);
+    if (!irrev && !stream) return 0;
     const auto &l0 = P.levels[li], &l1 = P.levels[li + 1];
     if (l0.empty() || l0.size() != l1.size()) return 0;
     uint64_t samples = 0;
@@ -716,7 +722,7 @@ static uint32_t dwt_f01_tiles(const DwtPlan &P, size_t li, int irrev, int *ny, i
         if (a.out != b.in) return 0;  // level l + 1 must read level l's LL
         if (a.reg_x1 > 0 || b.reg_x1 > 0) return 0;
     }
-    if (o.pair_kernel) {
+    if (stream) {
         // k_dwt_fwd_pair: strips of CW1 level-(l+1) columns (3 or 4 level-l
         // waves, whichever wastes fewer columns at the jobs' widths), segments
         // of S1 rows sized so that the launch is about one resident wave of
@@ -1122,19 +1128,20 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         subs = subs || cp.dx[k] != 1 || cp.dy[k] != 1;
         mixed = mixed || cp.dx[k] != cp.dx[0] || cp.dy[k] != cp.dy[0];
     }
-    if (subs && (row0 || col0 || nrows != ih || ncols != iw))
-        return set_err(GRKGPU_EUNSUPPORTED, "row / column shards of subsampled images are not supported");
-    // the rectangle each caller plane covers (component grid), its stride,
-    // and its offset in the staging buffer (samples)
+    // the rectangle each caller plane covers (the rows / columns held, on the
+    // component's grid: ceil(x / dx), TileComponent.cpp:150-196 -- a tile's
+    // plane holds its tile-component, as grk_write_tile's data does,
+    // TileProcessor.cpp:1923-1972), its stride, and its offset in the staging
+    // buffer (samples)
     Rect prect[GRKGPU_MAX_COMPS];
     uint64_t poff[GRKGPU_MAX_COMPS + 1];
     poff[0] = 0;
+    const Rect held{cp.image.x0 + col0, cp.image.y0 + row0, cp.image.x0 + col0 + ncols, cp.image.y0 + row0 + nrows};
     for (uint32_t k = 0; k < nc; ++k) {
-        prect[k] = subs ? comp_rect(cp.image, cp.dx[k], cp.dy[k])
-                        : Rect{cp.image.x0 + col0, cp.image.y0 + row0, cp.image.x0 + col0 + ncols,
-                               cp.image.y0 + row0 + nrows};
+        prect[k] = comp_rect(held, cp.dx[k], cp.dy[k]);
         poff[k + 1] = poff[k] + (uint64_t)prect[k].w() * prect[k].h();
     }
+    (void)subs;
     // element offset of tile-component tc's first sample in plane k
     auto plane_org = [&](uint32_t k, const TileComp &tc) {
         return (uint64_t)(tc.r.y0 - prect[k].y0) * prect[k].w() + (tc.r.x0 - prect[k].x0);
@@ -2191,10 +2198,14 @@ static bool walk_tile_parts(const uint8_t *cs, size_t len, size_t sot0, uint32_t
 // and their passes still count toward the block's pass total
 // (T2::skip_packet_data, T2.cpp:758-819), so T1 runs those passes over the
 // 0xFF fill past the decoded bytes, exactly as the reference does.
+// host_only: stop after the host Tier-2 (tile-part walk, packet headers, the
+// code-block table) -- no device call; *decoded_out (when given) receives the
+// tiles decoded (grkgpu_walk_tiles)
 static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu_image_desc *img,
                            int32_t *const *planes, int planes_on_device, uint32_t tb, uint32_t te,
-                           uint32_t reduce = 0, const Rect *win = nullptr, uint32_t max_layers = 0) {
-    if (!c || !csb || !planes) return set_err(GRKGPU_EINVAL, "null argument");
+                           uint32_t reduce = 0, const Rect *win = nullptr, uint32_t max_layers = 0,
+                           bool host_only = false, std::vector<uint8_t> *decoded_out = nullptr) {
+    if ((!c && !host_only) || !csb || (!planes && !host_only)) return set_err(GRKGPU_EINVAL, "null argument");
     ActiveCall active;
     double t_start = now_ms();
     CodingParams cp;
@@ -2229,8 +2240,6 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         img->x0 = ix0; img->y0 = iy0;
         img->x1 = ox1; img->y1 = oy1;
     }
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
     const uint32_t nc = cp.numcomps, ntiles = cp.tw * cp.th;
     const uint32_t iw = ox1 - ix0;
     if (te > ntiles) te = ntiles;
@@ -2436,7 +2445,11 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             uint32_t packno = 0;
             PackedHdr packed{tpacked[lt].data(), tpacked[lt].size(), 0};
             for (const auto &pk : order) {
-                if (off >= tlen) break;  // the data ends before the packets do (truncated stream)
+                // the data ends before the packets do (a truncated stream):
+                // the remaining packets are empty (a zero-length header reads
+                // as "no data", T2.cpp:393-400) -- unless the headers are packed
+                // (PPM / PPT), which keep coming; their bodies are then empty
+                if (off >= tlen && !tpacked_on[lt]) break;
                 const bool skip = max_layers && pk.layno >= max_layers;
                 int64_t used = decode_packet(tile.comps[pk.compno], pk.resno, pk.precno, pk.layno, td + off, tlen - off,
                                              base + off, tcp.csty, &packno, skip, tcp.comp[pk.compno].cblksty,
@@ -2527,6 +2540,10 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
         }
     }
     if (too_deep) return set_err(GRKGPU_ECORRUPT, "unsupported bpno_plus_one >= 31 (code-block bit-planes + ROI shift)");
+    if (decoded_out) *decoded_out = walk.decoded;
+    if (host_only) return GRKGPU_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
     const uint32_t nblk = (uint32_t)db.size();
     seg_first.push_back((uint32_t)dsegs.size());
     bool mixed_sty = false;  // tile-components of different code-block styles: one decode launch per style
@@ -2785,16 +2802,15 @@ extern "C" int grkgpu_decompress_ex(grkgpu_ctx *c, const uint8_t *csb, size_t le
 
 extern "C" int grkgpu_walk_tiles(const uint8_t *csb, size_t len, uint8_t *decoded, uint32_t cap, uint32_t *ntiles) {
     if (!csb || !ntiles) return set_err(GRKGPU_EINVAL, "null argument");
-    CodingParams cp;
-    size_t pos = 0;
-    std::string err;
-    if (!parse_main_header(csb, len, cp, pos, err)) return set_err(GRKGPU_EUNSUPPORTED, err);
-    const uint32_t n = cp.tw * cp.th;
-    *ntiles = n;
-    TileWalk walk;
-    if (!walk_tile_parts(csb, len, pos, n, std::vector<uint8_t>(n, 0), walk, err)) return set_err(GRKGPU_ECORRUPT, err);
+    grkgpu_image_desc d{};
+    int rc = grkgpu_read_header(csb, len, &d);
+    if (rc) return rc;
+    std::vector<uint8_t> dec;
+    rc = decompress_impl(nullptr, csb, len, nullptr, nullptr, 0, 0, 0xffffffffu, 0, nullptr, 0, true, &dec);
+    if (rc) return rc;
+    *ntiles = (uint32_t)dec.size();
     if (decoded)
-        for (uint32_t t = 0; t < n && t < cap; ++t) decoded[t] = walk.decoded[t];
+        for (uint32_t t = 0; t < dec.size() && t < cap; ++t) decoded[t] = dec[t];
     return GRKGPU_OK;
 }
 

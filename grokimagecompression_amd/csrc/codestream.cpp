@@ -387,16 +387,20 @@ struct BitReader {
     const uint8_t *p;
     size_t n, off = 0;
     uint32_t buf = 0, ct = 0;
-    bool err = false;
+    uint32_t fails = 0;  // reads that ran out of bytes (BitIO::bytein returning false, BitIO.cpp:95-104)
     BitReader(const uint8_t *pp, size_t nn) : p(pp), n(nn) {}
-    void bytein() {
+    // past the end the reader keeps its state (ct stays 0): every later read
+    // fails too, and a failed read leaves the bits it got at the top of the
+    // value, zeros below (BitIO::read, BitIO.cpp:143-160)
+    bool bytein() {
+        if (off >= n) { ++fails; return false; }
         ct = (buf == 0xff) ? 7 : 8;
-        if (off >= n) { err = true; buf = 0; return; }
         buf = p[off++];
+        return true;
     }
-    uint32_t bit() { if (ct == 0) bytein(); ct--; return (buf >> ct) & 1; }
+    uint32_t bit() { if (ct == 0 && !bytein()) return 0; ct--; return (buf >> ct) & 1; }
     uint32_t read(uint32_t k) { uint32_t v = 0; for (uint32_t i = 0; i < k; ++i) v = (v << 1) | bit(); return v; }
-    void align() { if (buf == 0xff) bytein(); ct = 0; }
+    bool align() { if (buf == 0xff && !bytein()) return false; ct = 0; return true; }  // BitIO::inalign
     uint32_t numpasses() {
         if (!read(1)) return 1;
         if (!read(1)) return 2;
@@ -406,7 +410,7 @@ struct BitReader {
         if (v != 31) return v + 6;
         return read(7) + 37;
     }
-    uint32_t comma() { uint32_t k = 0; while (bit() && !err) ++k; return k; }
+    uint32_t comma() { uint32_t k = 0, f = fails; while (bit() && fails == f) ++k; return k; }
     // TagTree::decodeValue (TagTree.cpp:295-321)
     int64_t tagtree(TagTree &t, uint32_t leaf, int64_t threshold) {
         int32_t stk[64], sp = 0, node = (int32_t)leaf;
@@ -416,8 +420,10 @@ struct BitReader {
             TagTree::Node &nd = t.nodes[node];
             if (low > nd.low) nd.low = low; else low = nd.low;
             while (low < threshold && low < nd.value) {
-                if (bit()) nd.value = low; else ++low;
-                if (err) return INT64_MAX;
+                const uint32_t f = fails;
+                const uint32_t b = bit();
+                if (fails != f) return INT64_MAX;
+                if (b) nd.value = low; else ++low;
             }
             nd.low = low;
             if (sp == 0) break;
@@ -484,12 +490,16 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
             if (pr.cblks.empty()) continue;
             for (uint32_t cb = 0; cb < pr.cblks.size(); ++cb) {
                 Cblk &c = pr.cblks[cb];
+                // a read past the header's bytes fails the packet -- except a
+                // segment length's, which T2.cpp:595-598 only warns about
+                // (the bits read so far, zeros below, are its value)
+                const uint32_t f0 = r.fails;
                 uint32_t inc = c.included ? r.read(1) : (r.tagtree(pr.incl, cb, layno + 1) <= (int64_t)layno);
-                if (r.err) return -1;
+                if (r.fails != f0) return -1;
                 if (!inc) continue;
                 if (!c.included) {
                     int64_t k = r.tagtree(pr.imsb, cb, INT64_MAX);
-                    if (r.err || k < 0) return -1;
+                    if (r.fails != f0 || k < 0) return -1;
                     // more missing bit-planes than the band has: the reference
                     // warns and takes the band's count (T2.cpp:516-521)
                     c.numbps = k > (int64_t)b.numbps ? b.numbps : (uint32_t)((int64_t)b.numbps - k);
@@ -498,7 +508,9 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                     c.included = true;
                 }
                 uint32_t np = r.numpasses();
+                if (r.fails != f0) return -1;
                 c.numlenbits += r.comma();
+                if (r.fails != f0) return -1;
                 if (single && np > 109) np = 109;  // single segment: truncated (T2.cpp:566-577)
                 // the packet's passes fill the open segment, then new ones
                 // (T2::read_packet_header, T2.cpp:560-605)
@@ -515,7 +527,6 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
                     const uint32_t bits = c.numlenbits + (uint32_t)floorlog2((int32_t)take);
                     if (bits > 32) return -1;  // "too many bits in segment length", T2.cpp:590-593
                     const uint32_t L = r.read(bits);
-                    if (r.err) return -1;
                     parts.push_back({&c, si, take, L});
                     c.segs[si].numpasses += take;
                     left -= take;
@@ -525,8 +536,7 @@ int64_t decode_packet(TileComp &tc, uint32_t resno, uint32_t precno, uint32_t la
             }
         }
     }
-    r.align();
-    if (r.err) return -1;
+    if (!r.align()) return -1;
     // EPH (T2.cpp:405-418 / 640-652): skipped when present -- it ends the
     // header, wherever the header is
     size_t hoff = r.off;

@@ -31,7 +31,6 @@
 
 #include <algorithm>
 #include <type_traits>
-#include <cstdlib>
 
 #include "grk_device.h"
 
@@ -781,16 +780,16 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
 // Forward levels l and l + 1 streamed down column strips (k_dwt_fwd_pair;
 // 5/3 and 9/7).  k_dwt_fwd01 lifts independent windows: every window
 // re-reads and re-lifts 2 x 4 halo rows, and every workgroup re-computes the
-// LL halo of its level-(l+1) window -- the 8K frame's pair read 1.49x its
-// input and lifted ~1.8x its samples.  Here a workgroup owns a strip of
-// CW1 level-(l+1) columns x S1 rows and walks it top to bottom:
+// LL halo of its level-(l+1) window -- the 8K frame's pair reads 1.49x its
+// input.  Here a workgroup owns a strip of CW1 level-(l+1) columns x S1 rows
+// and walks it top to bottom:
 //   * NW0 level-l waves, side by side (128 columns each, PW = 60 / 62 LL
-//     columns of core), stream down the strip in chunks of C0 = 16 rows.
+//     columns of core), stream down the strip in chunks of C0 = 8 rows.
 //     The vertical lifting is carried from chunk to chunk: the last P = NS + 2
 //     rows of a chunk, partially lifted, stay in registers and head the next
 //     chunk's array, so no row is loaded or lifted twice (vlift_stream).  The
-//     next chunk's rows are loaded before the current one is lifted.
-//   * A chunk's 16 finished rows are lifted horizontally; their HL / LH / HH
+//     next chunk's rows are loaded before the barrier that ends a chunk.
+//   * A chunk's finished rows are lifted horizontally; their HL / LH / HH
 //     samples go to the Mallat bands in HBM, the LL row into an LDS ring of
 //     RING rows x LW columns.
 //   * NW1 level-(l+1) waves stream the LL rows out of the ring in chunks of
@@ -801,9 +800,16 @@ __global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_fwd01(const DwtJob *__re
 //     the first iteration after the level-l chunk holding its last LL row.
 // A segment re-reads only the rows above and below it that its two lifting
 // halos need (~2 x 12 rows per segment of 2 S1), and a strip the 2 x 4 LL
-// columns of the level-(l+1) halo plus the level-l halo at its sides.
+// columns of the level-(l+1) halo plus the level-l halo at its sides: the 8K
+// frame's 9/7 pair reads 435 MB for 398 MB of input (k_dwt_fwd01: 593 MB).
+// Measured (profiles/r05/dwt_pair_ab.txt): the 5/3 pairs beat one launch per
+// level (8K: levels 1 + 2 in 54 us against 47 + 16, 3 + 4 in 11 against
+// 9 + 7), so they are the 5/3 default; the 9/7 pair (198 us) does not beat
+// k_dwt_fwd01 (185 us) -- its 64-bit fixed-point lifting chains stay
+// latency-bound at the ~3 resident waves per SIMD the strips leave -- and
+// runs only on request (grkgpu_dwt_options.pair_kernel = 2).
 // ---------------------------------------------------------------------------
-template <bool IRREV, int NW0_, int C0_ = 16, int PF_ = 1>
+template <bool IRREV, int NW0_, int C0_ = 8, int C1_ = 8>
 struct PairGeo {
     static constexpr int NS = IRREV ? 4 : 2;           // lifting steps: halo rows / columns per side
     static constexpr int P = NS + 2;                   // rows carried from one chunk to the next
@@ -814,9 +820,8 @@ struct PairGeo {
     static constexpr int CW1 = LW - 2 * NS;            // level-(l+1) core columns per workgroup
     static constexpr int NW1 = (CW1 + CW - 1) / CW;    // level-(l+1) waves
     static constexpr int WAVES = NW0 + NW1;
-    static constexpr int C0 = C0_, C1 = 8;             // rows per chunk (level l, level l + 1)
+    static constexpr int C0 = C0_, C1 = C1_;           // rows per chunk (level l, level l + 1)
     static constexpr int RING = 32;                    // LL rows held in LDS
-    static constexpr bool PF = PF_ != 0;               // level-l rows of the next chunk loaded before the lifting
 };
 
 // Vertical lifting step S over rows k >= K0 of parity K0 (see vstep).
@@ -898,7 +903,7 @@ struct PairStrip {
 template <bool IRREV, int NW0, int C0X>
 __device__ __forceinline__ bool pair_strip(const DwtJob &J0, const DwtJob &J1, int S1, int wg, PairStrip &g, int &tx,
                                            int &ntx) {
-    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    using G = PairGeo<IRREV, NW0, (C0X & 255), ((C0X >> 12) & 15)>;
     constexpr int NS = G::NS;
     const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
     ntx = (rw1 + casx1 + G::CW1 - 1) / G::CW1;
@@ -930,7 +935,7 @@ __device__ __forceinline__ bool pair_strip(const DwtJob &J0, const DwtJob &J1, i
 template <bool IRREV, int NW0, int C0X, bool VEC, typename T>
 __device__ __forceinline__ void pair_level0(const DwtJob &J0, const PairStrip &g,
                                             int32_t (*ll)[PairGeo<IRREV, NW0>::LW + 1], int k, int lane) {
-    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    using G = PairGeo<IRREV, NW0, (C0X & 255), ((C0X >> 12) & 15)>;
     constexpr int NS = G::NS, P = G::P, C0 = G::C0, RING = G::RING;
     const int rw0 = J0.rw, rh0 = J0.rh, casx0 = J0.casx, casy0 = J0.casy;
     const int xw = 2 * (g.xs1 - NS + G::PW * k) + casx0 - NS;  // window column origin
@@ -962,12 +967,11 @@ __device__ __forceinline__ void pair_level0(const DwtJob &J0, const PairStrip &g
             }
         }
     };
-    T lo[P + C0], hi[P + C0], nlo[G::PF ? C0 : 1], nhi[G::PF ? C0 : 1];
+    T lo[P + C0], hi[P + C0];
     ldrows(g.t0, lo, hi, std::integral_constant<int, P + C0>{});
     for (int c = 0; c <= g.nC0; ++c) {
         if (c < g.nC0) {
             const bool more = c + 1 < g.nC0;  // wave-uniform
-            if (G::PF && more) ldrows(g.t0 + P + (c + 1) * C0, nlo, nhi, std::integral_constant<int, G::PF ? C0 : 1>{});
             if (c == 0) vlift_stream<IRREV, true>(lo, hi);
             else vlift_stream<IRREV, false>(lo, hi);
             const int tb = g.t0 + c * C0;
@@ -993,14 +997,8 @@ __device__ __forceinline__ void pair_level0(const DwtJob &J0, const PairStrip &g
             }
 #pragma unroll
             for (int r = 0; r < P; ++r) { lo[r] = lo[r + C0]; hi[r] = hi[r + C0]; }
-            if (more) {
-                if constexpr (G::PF) {
-#pragma unroll
-                    for (int r = 0; r < C0; ++r) { lo[P + r] = nlo[r]; hi[P + r] = nhi[r]; }
-                } else {  // loaded now, in flight across the barrier
-                    ldrows(g.t0 + P + (c + 1) * C0, lo + P, hi + P, std::integral_constant<int, C0>{});
-                }
-            }
+            // the next chunk's rows, in flight across the barrier
+            if (more) ldrows(g.t0 + P + (c + 1) * C0, lo + P, hi + P, std::integral_constant<int, C0>{});
         }
         lds_barrier();
     }
@@ -1010,7 +1008,7 @@ __device__ __forceinline__ void pair_level0(const DwtJob &J0, const PairStrip &g
 template <bool IRREV, int NW0, int C0X, typename T>
 __device__ __forceinline__ void pair_level1(const DwtJob &J1, const PairStrip &g,
                                             int32_t (*ll)[PairGeo<IRREV, NW0>::LW + 1], int a, int lane) {
-    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    using G = PairGeo<IRREV, NW0, (C0X & 255), ((C0X >> 12) & 15)>;
     constexpr int NS = G::NS, P = G::P, C1 = G::C1, RING = G::RING, LW = G::LW;
     const int rw1 = J1.rw, rh1 = J1.rh, casx1 = J1.casx, casy1 = J1.casy;
     const int base = g.xs1 - NS;  // LL column of LDS column 0
@@ -1080,10 +1078,10 @@ __device__ __forceinline__ void pair_level1(const DwtJob &J1, const PairStrip &g
 }
 
 template <bool IRREV, int NW0, int C0X, typename T = int32_t>
-__global__ __launch_bounds__((64 * PairGeo<IRREV, NW0>::WAVES)) __attribute__((amdgpu_waves_per_eu((C0X >> 8) ? 1 : 6))) void k_dwt_fwd_pair(const DwtJob *__restrict__ jobs0,
+__global__ __launch_bounds__((64 * PairGeo<IRREV, NW0>::WAVES)) __attribute__((amdgpu_waves_per_eu((C0X >> 16) & 15))) void k_dwt_fwd_pair(const DwtJob *__restrict__ jobs0,
                                                                                    const DwtJob *__restrict__ jobs1,
                                                                                    int S1, int lay) {
-    using G = PairGeo<IRREV, NW0, (C0X & 255), (C0X >> 8)>;
+    using G = PairGeo<IRREV, NW0, (C0X & 255), ((C0X >> 12) & 15)>;
     __shared__ int32_t ll[G::RING][G::LW + 1];  // + a spare column for the halo lanes' writes
     const int gx = gridDim.x;
     int L = blockIdx.y * gx + blockIdx.x;
@@ -1123,24 +1121,12 @@ hipError_t launch_dwt_fwd_pair(const DwtJob *jobs0, const DwtJob *jobs1, uint32_
     const dim3 g(max_wgs, njobs);
 #define GRK_PAIR(IR, NW, C)                                                                          \
     hipLaunchKernelGGL((k_dwt_fwd_pair<IR, NW, C>), g, dim3(64 * PairGeo<IR, NW>::WAVES), 0, s, jobs0, jobs1, s1, lay)
-    static const int chunk = getenv("GRKGPU_PAIR_CHUNK") ? atoi(getenv("GRKGPU_PAIR_CHUNK")) : 16;
-    switch (chunk) {
-        case 8:
-            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 0x108); else GRK_PAIR(true, 4, 0x108); }
-            else { if (nw0 == 3) GRK_PAIR(false, 3, 0x108); else GRK_PAIR(false, 4, 0x108); }
-            break;
-        case 80:  // 8 rows, no prefetch registers
-            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 8); else GRK_PAIR(true, 4, 8); }
-            else { if (nw0 == 3) GRK_PAIR(false, 3, 8); else GRK_PAIR(false, 4, 8); }
-            break;
-        case 160:
-            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 16); else GRK_PAIR(true, 4, 16); }
-            else { if (nw0 == 3) GRK_PAIR(false, 3, 16); else GRK_PAIR(false, 4, 16); }
-            break;
-        default:
-            if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 0x110); else GRK_PAIR(true, 4, 0x110); }
-            else { if (nw0 == 3) GRK_PAIR(false, 3, 0x110); else GRK_PAIR(false, 4, 0x110); }
-    }
+    // chunk geometry C0 | C1 << 12 | waves per SIMD << 16: 8-row chunks at
+    // both levels, 6 wavefronts per SIMD (75 VGPRs) -- measured best against
+    // 16-row chunks (4 or 3 per SIMD), 4-row chunks (8 per SIMD) and the next
+    // chunk's rows held in registers during the lifting (profiles/r05/dwt_pair_ab.txt)
+    if (irrev) { if (nw0 == 3) GRK_PAIR(true, 3, 0x68008); else GRK_PAIR(true, 4, 0x68008); }
+    else { if (nw0 == 3) GRK_PAIR(false, 3, 0x68008); else GRK_PAIR(false, 4, 0x68008); }
 #undef GRK_PAIR
     return hipGetLastError();
 }

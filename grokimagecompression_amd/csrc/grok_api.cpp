@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -235,6 +236,12 @@ TileRect tile_rect(uint32_t t, uint32_t tw, uint32_t tx0, uint32_t ty0, uint32_t
             (uint32_t)std::min<uint64_t>(d.y1, (uint64_t)ty0 + (uint64_t)(q + 1) * tdy)};
 }
 
+// The matrix size of each grk_set_MCT allocation (the ABI's mct_data is a
+// bare pointer): map_cparams refuses an image whose component count differs,
+// instead of reading past the allocation.
+static std::mutex g_mct_mu;
+static std::unordered_map<const void *, uint32_t> g_mct_n;
+
 // grk_cparameters -> grkgpu_cparams (j2k_setup_encoder's reading of them,
 // codestream/j2k.cpp:1609-2050); false for options outside grk_mi355x.h
 bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p) {
@@ -243,6 +250,14 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
     if (g->isHT) { GRK_ERROR("HTJ2K is not supported"); return false; }
     if (g->mct_data) {  // grk_set_MCT: numcomps x numcomps matrix, then numcomps DC shifts (j2k.cpp:1899-1956)
         if (numcomps > GRKGPU_MAX_COMPS) return false;
+        {
+            std::lock_guard<std::mutex> lk(g_mct_mu);
+            const auto it = g_mct_n.find(g->mct_data);
+            if (it == g_mct_n.end() || it->second != numcomps) {
+                GRK_ERROR("custom MCT matrix (grk_set_MCT) of %u components for an image of %u", it == g_mct_n.end() ? 0u : it->second, numcomps);
+                return false;
+            }
+        }
         p->mct_ncomp = numcomps;
         memcpy(p->mct_matrix, g->mct_data, sizeof(float) * numcomps * numcomps);
         memcpy(p->mct_dc_shift, (const uint8_t *)g->mct_data + sizeof(float) * numcomps * numcomps,
@@ -657,9 +672,35 @@ GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image
     grkgpu_ctx *ctx = lease.ctx;
     if (!ctx) return false;
     std::vector<int32_t *> planes(image->numcomps);
+    // The planes take the extent the decode writes under the current settings
+    // (cp_reduce and the decode area may have changed since grk_read_header /
+    // grk_set_decode_area filled the image in): grk_image_comp_header_update
+    // (image.cpp:124-155) without an area, update_image_dimensions
+    // (image.cpp:207-246) with one -- the decoder's own output geometry, so
+    // a stale w / h can never make it write past a plane.
+    const uint32_t r = c->dparams.cp_reduce;
+    if (r >= c->hinfo.numresolutions) {
+        GRK_ERROR("Error decoding component: the number of resolutions to remove is higher than the number of "
+                  "resolutions of this component");
+        return false;
+    }
+    const grkgpu_image_desc &d = c->desc;
     for (uint32_t k = 0; k < image->numcomps; ++k) {
-        if (!grk_image_single_component_data_alloc(&image->comps[k])) return false;
-        planes[k] = image->comps[k].data;
+        grk_image_comp &cp = image->comps[k];
+        cp.dx = d.dx[k];
+        cp.dy = d.dy[k];
+        if (c->window) {
+            comp_geom(cp, c->win[0], c->win[1], c->win[2], c->win[3], r);
+            cp.x0 = cdiv(c->win[0], cp.dx);
+            cp.y0 = cdiv(c->win[1], cp.dy);
+        } else {
+            cp.x0 = cdiv(d.x0, cp.dx);
+            cp.y0 = cdiv(d.y0, cp.dy);
+            cp.w = cdivpow2(cdiv(d.x1, cp.dx) - cp.x0, r);
+            cp.h = cdivpow2(cdiv(d.y1, cp.dy) - cp.y0, r);
+        }
+        if (!grk_image_single_component_data_alloc(&cp)) return false;
+        planes[k] = cp.data;
     }
     grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
     if (c->window) { dp.DA_x0 = c->win[0]; dp.DA_y0 = c->win[1]; dp.DA_x1 = c->win[2]; dp.DA_y1 = c->win[3]; }
@@ -729,10 +770,21 @@ static TileRect tile_decoded_rect(const Codec *c, uint32_t t, bool clip) {
     return o;
 }
 
+// rectangle o (reference grid, decoded resolution) on component k's grid:
+// ceil(x / dx) (the nested ceilings of a reduced decode commute)
+static TileRect comp_tile_rect(const Codec *c, const TileRect &o, uint32_t k) {
+    const uint32_t dx = c->desc.dx[k] ? c->desc.dx[k] : 1, dy = c->desc.dy[k] ? c->desc.dy[k] : 1;
+    return {cdiv(o.x0, dx), cdiv(o.y0, dy), cdiv(o.x1, dx), cdiv(o.y1, dy)};
+}
+
+// get_tile_size(true) (TileProcessor.cpp:1435-1447): every component's
+// tile-component at the decoded resolution, at its sample width
 static uint64_t tile_data_bytes(const Codec *c, const TileRect &o) {
     uint64_t n = 0;
-    for (uint32_t k = 0; k < c->desc.numcomps; ++k)
-        n += (uint64_t)((c->desc.prec[k] + 7) >> 3) * (o.x1 - o.x0) * (o.y1 - o.y0);
+    for (uint32_t k = 0; k < c->desc.numcomps; ++k) {
+        const TileRect r = comp_tile_rect(c, o, k);
+        n += (uint64_t)((c->desc.prec[k] + 7) >> 3) * (r.x1 - r.x0) * (r.y1 - r.y0);
+    }
     return n;
 }
 
@@ -745,11 +797,6 @@ GRK_EXPORT bool grk_read_tile_header(grk_codec *codec, uint16_t *tile_index, uin
                                      uint32_t *y0, uint32_t *x1, uint32_t *y1, uint32_t *nb_comps, bool *go_on) {
     Codec *c = (Codec *)codec;
     if (!c || !c->decompressor || !c->have_header || !tile_index || !data_size) return false;
-    for (uint32_t k = 0; k < c->desc.numcomps; ++k)
-        if (c->desc.dx[k] != 1 || c->desc.dy[k] != 1) {
-            GRK_ERROR("tile-by-tile decode of subsampled components is not supported (grk_decode decodes them)");
-            return false;
-        }
     const grkgpu_header_info &h = c->hinfo;
     if (!c->tile_order_ready) {
         for (uint32_t t : stream_tile_order(c->cs, h.tw * h.th)) {
@@ -795,36 +842,54 @@ GRK_EXPORT bool grk_decode_tile_data(grk_codec *codec, uint16_t tile_index, uint
     const TileRect o = tile_decoded_rect(c, tile_index, false);
     const uint64_t need = tile_data_bytes(c, o);
     if (need > data_size) return false;
-    const uint32_t w = o.x1 - o.x0, h = o.y1 - o.y0, nc = c->desc.numcomps;
+    const uint32_t nc = c->desc.numcomps;
+    // per component: its samples of the tile (tile-component rectangle ct[k])
+    // read from a plane whose first row / column is (px0[k], py0[k]), stride pst[k]
+    TileRect ct[GRKGPU_MAX_COMPS];
+    for (uint32_t k = 0; k < nc; ++k) ct[k] = comp_tile_rect(c, o, k);
     std::vector<int32_t> buf;
-    const int32_t *src;
-    uint32_t sstride, sx0 = 0, sy0 = 0;
-    uint64_t splane;
+    const int32_t *pl[GRKGPU_MAX_COMPS];
+    uint32_t pst[GRKGPU_MAX_COMPS], px0[GRKGPU_MAX_COMPS], py0[GRKGPU_MAX_COMPS];
     {
         Lease lease(0);
         if (!lease.ctx) return false;
-        if (c->dparams.cp_reduce == 0) {
-            buf.resize((size_t)w * h * nc);
+        if (c->dparams.cp_reduce == 0) {  // the tile as a decode window: plane k = its tile-component
+            uint64_t tot = 0;
+            for (uint32_t k = 0; k < nc; ++k) tot += (uint64_t)(ct[k].x1 - ct[k].x0) * (ct[k].y1 - ct[k].y0);
+            buf.resize(tot);
             std::vector<int32_t *> planes(nc);
-            for (uint32_t k = 0; k < nc; ++k) planes[k] = buf.data() + (size_t)k * w * h;
+            uint64_t off = 0;
+            for (uint32_t k = 0; k < nc; ++k) {
+                planes[k] = buf.data() + off;
+                pl[k] = planes[k];
+                pst[k] = ct[k].x1 - ct[k].x0;
+                px0[k] = ct[k].x0;
+                py0[k] = ct[k].y0;
+                off += (uint64_t)pst[k] * (ct[k].y1 - ct[k].y0);
+            }
             grkgpu_dparams dp{0, c->dparams.cp_layer, o.x0, o.y0, o.x1, o.y1};
             if (grkgpu_decompress_ex(lease.ctx, c->cs.data(), c->cs.size(), &dp, nullptr, planes.data(), 0)) {
                 GRK_ERROR("%s", grkgpu_last_error());
                 return false;
             }
-            src = buf.data();
-            sstride = w;
-            splane = (uint64_t)w * h;
-        } else {
+        } else {  // the whole reduced image once, then each tile cut out of it
+            const uint32_t r = c->dparams.cp_reduce;
+            const grkgpu_image_desc &dd = c->desc;
+            uint64_t roff[GRKGPU_MAX_COMPS + 1];
+            roff[0] = 0;
+            uint32_t rw[GRKGPU_MAX_COMPS];
+            for (uint32_t k = 0; k < nc; ++k) {  // grk_image_comp_header_update's plane sizes
+                const uint32_t dx = dd.dx[k] ? dd.dx[k] : 1, dy = dd.dy[k] ? dd.dy[k] : 1;
+                rw[k] = cdivpow2(cdiv(dd.x1, dx) - cdiv(dd.x0, dx), r);
+                const uint32_t rh = cdivpow2(cdiv(dd.y1, dy) - cdiv(dd.y0, dy), r);
+                roff[k + 1] = roff[k] + (uint64_t)rw[k] * rh;
+            }
             if (c->reduced.empty()) {
                 grkgpu_image_desc d{};
-                grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
-                const uint32_t r = c->dparams.cp_reduce;
-                const uint32_t rw = cdivpow2(c->desc.x1 - c->desc.x0, r);  // the core's plane size
-                const uint32_t rh = cdivpow2(c->desc.y1 - c->desc.y0, r);
-                c->reduced.resize((size_t)rw * rh * nc);
+                grkgpu_dparams dp{r, c->dparams.cp_layer, 0, 0, 0, 0};
+                c->reduced.resize(roff[nc]);
                 std::vector<int32_t *> planes(nc);
-                for (uint32_t k = 0; k < nc; ++k) planes[k] = c->reduced.data() + (size_t)k * rw * rh;
+                for (uint32_t k = 0; k < nc; ++k) planes[k] = c->reduced.data() + roff[k];
                 if (grkgpu_decompress_ex(lease.ctx, c->cs.data(), c->cs.size(), &dp, &d, planes.data(), 0)) {
                     GRK_ERROR("%s", grkgpu_last_error());
                     c->reduced.clear();
@@ -832,20 +897,23 @@ GRK_EXPORT bool grk_decode_tile_data(grk_codec *codec, uint16_t tile_index, uint
                 }
                 c->reduced_desc = d;
             }
-            const grkgpu_image_desc &d = c->reduced_desc;
-            src = c->reduced.data();
-            sstride = d.x1 - d.x0;
-            splane = (uint64_t)sstride * (d.y1 - d.y0);
-            sx0 = o.x0 - d.x0;
-            sy0 = o.y0 - d.y0;
+            const grkgpu_image_desc &d = c->reduced_desc;  // the reduced image (reference grid)
+            for (uint32_t k = 0; k < nc; ++k) {
+                const TileRect org = comp_tile_rect(c, {d.x0, d.y0, d.x1, d.y1}, k);
+                pl[k] = c->reduced.data() + roff[k];
+                pst[k] = rw[k];
+                px0[k] = org.x0;
+                py0[k] = org.y0;
+            }
         }
     }
     uint8_t *dst = data;
     for (uint32_t k = 0; k < nc; ++k) {
         const uint32_t sz = (c->desc.prec[k] + 7) >> 3;
         const bool sg = c->desc.sgnd[k] != 0;
-        const int32_t *p = src + splane * k + (uint64_t)sy0 * sstride + sx0;
-        for (uint32_t y = 0; y < h; ++y, p += sstride)
+        const uint32_t w = ct[k].x1 - ct[k].x0, h = ct[k].y1 - ct[k].y0;
+        const int32_t *p = pl[k] + (uint64_t)(ct[k].y0 - py0[k]) * pst[k] + (ct[k].x0 - px0[k]);
+        for (uint32_t y = 0; y < h; ++y, p += pst[k])
             for (uint32_t x = 0; x < w; ++x) {
                 const int32_t v = p[x];
                 if (sz == 1) *dst++ = (uint8_t)(sg ? (int8_t)v : (int8_t)(v & 0xff));
@@ -957,9 +1025,10 @@ GRK_EXPORT bool grk_write_tile(grk_codec *codec, uint16_t tile_index, uint8_t *d
     d.x0 = img->x0; d.y0 = img->y0; d.x1 = img->x1; d.y1 = img->y1;
     d.numcomps = img->numcomps;
     for (uint32_t k = 0; k < img->numcomps; ++k) {
-        if (img->comps[k].dx != 1 || img->comps[k].dy != 1) { GRK_ERROR("subsampling is not supported"); return false; }
         d.prec[k] = img->comps[k].prec;
         d.sgnd[k] = (int32_t)img->comps[k].sgnd;
+        d.dx[k] = img->comps[k].dx ? img->comps[k].dx : 1;
+        d.dy[k] = img->comps[k].dy ? img->comps[k].dy : 1;
     }
     grkgpu_cparams p;
     if (!map_cparams(&c->cparams, d.numcomps, &p)) return false;
@@ -980,13 +1049,21 @@ GRK_EXPORT bool grk_write_tile(grk_codec *codec, uint16_t tile_index, uint8_t *d
     const uint32_t tdx = p.tile_size_on ? p.cp_tdx : d.x1 - p.cp_tx0, tdy = p.tile_size_on ? p.cp_tdy : d.y1 - p.cp_ty0;
     const uint32_t tw = (uint32_t)(((uint64_t)d.x1 - p.cp_tx0 + tdx - 1) / tdx);
     const TileRect tr = tile_rect(tile_index, tw, p.cp_tx0, p.cp_ty0, tdx, tdy, d);
-    const uint64_t area = (uint64_t)(tr.x1 - tr.x0) * (tr.y1 - tr.y0);
-    if (area * sz * d.numcomps != data_size) {
+    // the tile's data: each component's tile-component (the tile on its grid,
+    // ceil(x / dx)), one after the other (TileProcessor::copy_image_data_to_tile,
+    // TileProcessor.cpp:1923-1972; get_tile_size(false))
+    uint64_t off[GRKGPU_MAX_COMPS + 1];
+    off[0] = 0;
+    for (uint32_t k = 0; k < d.numcomps; ++k) {
+        const uint64_t w = cdiv(tr.x1, d.dx[k]) - cdiv(tr.x0, d.dx[k]), h = cdiv(tr.y1, d.dy[k]) - cdiv(tr.y0, d.dy[k]);
+        off[k + 1] = off[k] + w * h * sz;
+    }
+    if (off[d.numcomps] != data_size) {
         GRK_ERROR("Size mismatch between tile data and sent data.");
         return false;
     }
     grkgpu_planes pl{};
-    for (uint32_t k = 0; k < d.numcomps; ++k) pl.planes[k] = data + area * sz * k;
+    for (uint32_t k = 0; k < d.numcomps; ++k) pl.planes[k] = data + off[k];
     pl.sample_fmt = sz == 1 ? (d.sgnd[0] ? GRKGPU_SAMPLE_I8 : GRKGPU_SAMPLE_U8)
                             : (d.sgnd[0] ? GRKGPU_SAMPLE_I16 : GRKGPU_SAMPLE_U16);
     pl.on_device = 0;
@@ -1037,6 +1114,10 @@ GRK_EXPORT bool grk_set_MCT(grk_cparameters *parameters, float *matrix, int32_t 
     parameters->tcp_mct = 2;
     parameters->mct_data = malloc(msize + ssize);
     if (!parameters->mct_data) return false;
+    {
+        std::lock_guard<std::mutex> lk(g_mct_mu);
+        g_mct_n[parameters->mct_data] = n;
+    }
     memcpy(parameters->mct_data, matrix, msize);
     memcpy((uint8_t *)parameters->mct_data + msize, dc_shift, ssize);
     return true;

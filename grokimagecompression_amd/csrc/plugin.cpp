@@ -431,12 +431,20 @@ int32_t encode_file(grkgpu_ctx *ctx, grkp_cparameters *params, const char *path,
 // ---- batch route (grk_compress / grk_decompress with -ImgDir / -OutDir,
 // grk_compress.cpp:2224-2243, grk_decompress.cpp:1237-1262) ----
 // The plugin walks the input directory itself: frames in flight on worker
-// threads, each with its own GPU context -- FRAMES_PER_DEVICE per device,
+// threads, each with its own GPU context -- frames_per_device() per device,
 // over every device for deviceId -1 (grok.h:1816-1821) -- so one frame's host
 // work (rate control, Tier-2, file output in the host's callback) overlaps
 // the others' GPU work.  The host polls plugin_is_batch_complete and ends the
 // batch with plugin_stop_batch_encode / _decode.
-constexpr int FRAMES_PER_DEVICE = 4;
+// Frames in flight per device: GRKGPU_PLUGIN_FRAMES (1 .. 64; the plugin ABI
+// has no parameter for it), default 16 -- the concurrency the bench measured
+// best for the 8K and the cinema frames (profiles/r03_concurrency_sweep.txt,
+// profiles/r04z/c5_concurrency_sweep.txt).
+static int frames_per_device() {
+    const char *e = getenv("GRKGPU_PLUGIN_FRAMES");
+    const int v = e ? atoi(e) : 16;
+    return v < 1 ? 1 : v > 64 ? 64 : v;
+}
 
 struct Batch {
     bool decode = false;
@@ -521,7 +529,8 @@ bool batch_start(Batch *b) {
         for (int d = 0; d < grkgpu_device_count(); ++d) devs.push_back(d);
     else
         devs.push_back(g_device);
-    for (int f = 0; f < FRAMES_PER_DEVICE; ++f)
+    const int fpd = frames_per_device();
+    for (int f = 0; f < fpd; ++f)
         for (int d : devs) {
             grkgpu_ctx *c = nullptr;
             if (grkgpu_create(d, &c) != GRKGPU_OK) continue;

@@ -233,13 +233,14 @@ int grkgpu_set_launch_timing(grkgpu_ctx *ctx, int on);
  *                    sort on the device after the modelling kernel); 0
  *                    (default, measured as fast) = block order.  Same
  *                    codestream.
- *   pair_kernel      fused forward level pairs: 1 (default) = k_dwt_fwd_pair
- *                    (5/3 and 9/7; workgroups stream column strips top to
- *                    bottom, the vertical lifting carried in registers, the
- *                    LL rows through an LDS ring), pairs of at least
- *                    pair_min_samples level-l samples (default 2^20);
- *                    0 = k_dwt_fwd01 (9/7 only, f01_rows windows).  f01_rows
- *                    = 0 turns both off.
+ *   pair_kernel      fused forward level pairs: k_dwt_fwd_pair (workgroups
+ *                    stream column strips top to bottom, the vertical lifting
+ *                    carried in registers, the LL rows through an LDS ring)
+ *                    for pairs of at least pair_min_samples level-l samples
+ *                    (default 2^20) -- 1 (default): 5/3 pairs, 9/7 pairs by
+ *                    k_dwt_fwd01's windows (f01_rows); 2: both wavelets
+ *                    streamed; 0: no 5/3 pairs, 9/7 by k_dwt_fwd01.
+ *                    f01_rows = 0 turns every fused pair off.
  *   pair_rows        k_dwt_fwd_pair: level-(l+1) rows per segment (even); 0
  *                    (default) = sized for one resident wave of workgroups.
  *   pair_waves       k_dwt_fwd_pair: level-l wavefronts per workgroup, 3 or 4;

@@ -42,6 +42,11 @@ CASES = [
     ("tte3", [1, 2048, 2048, 1024, 1024, 8, 1]),
     ("tte4", [1, 256, 256, 128, 128, 8, 0]),
     ("tte5", [1, 512, 512, 256, 256, 8, 0]),
+    # subsampled components through grk_write_tile / grk_read_tile_header /
+    # grk_decode_tile_data (not a ctest case: the test_tile_encoder program
+    # with its components on 2 x 2 / 2 x 1 grids)
+    ("tte420", [3, 512, 512, 256, 256, 8, 1, "OUT", 420]),
+    ("tte422_I", [3, 768, 512, 256, 256, 8, 0, "OUT", 422]),
 ]
 AREA = [0, 0, 1024, 1024]  # ttd1 (tests/CMakeLists.txt:106)
 
@@ -76,7 +81,7 @@ def generate(outdir):
     with tempfile.TemporaryDirectory() as tmp:
         for name, args in CASES:
             j2k = os.path.join(outdir, "tiles", name + ".j2k")
-            run("enc", *args, j2k)
+            run("enc", *[j2k if a == "OUT" else a for a in args] + ([] if "OUT" in args else [j2k]))
             full, area, rta = (os.path.join(tmp, name + s) for s in (".full", ".area", ".rta"))
             run("dec", 0, 0, 0, 0, j2k, full)
             run("dec", *AREA, j2k, area)

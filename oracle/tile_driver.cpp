@@ -13,6 +13,10 @@
 //       grk_start_compress, then grk_write_tile for every tile in order with
 //       the byte ramp data[i] = (uint8_t)i (test_tile_encoder.cpp:158),
 //       grk_end_compress, into a file stream.
+//       Optional SUB after IRREV: 420 / 422 -- components 1.. on a 2 x 2 /
+//       2 x 1 grid (SIZ XRsiz / YRsiz); each tile's data is then every
+//       component's tile-component, one after the other
+//       (TileProcessor::copy_image_data_to_tile).
 //   tile_driver dec X0 Y0 X1 Y1 IN.j2k OUT.bin
 //       what tests/test_tile_decoder.cpp does (ttd0..2): grk_read_header,
 //       grk_set_decode_area, then grk_read_tile_header / grk_decode_tile_data
@@ -40,6 +44,9 @@ static int enc_mode(int argc, char **argv) {
     const uint32_t nc = (uint32_t)atoi(argv[2]), w = (uint32_t)atoi(argv[3]), h = (uint32_t)atoi(argv[4]);
     const uint32_t tw = (uint32_t)atoi(argv[5]), th = (uint32_t)atoi(argv[6]), prec = (uint32_t)atoi(argv[7]);
     const bool irrev = atoi(argv[8]) != 0;
+    const int sub = argc > 10 ? atoi(argv[10]) : 0;
+    const char *outp = argc > 10 ? argv[9] : argv[9];
+    const uint32_t sdx = sub == 420 || sub == 422 ? 2 : 1, sdy = sub == 420 ? 2 : 1;
     grk_initialize(nullptr, 0);
     grk_cparameters p;
     grk_set_default_encoder_parameters(&p);
@@ -56,12 +63,13 @@ static int enc_mode(int argc, char **argv) {
     std::vector<grk_image_cmptparm> cm(nc);
     memset(cm.data(), 0, nc * sizeof(grk_image_cmptparm));
     for (uint32_t k = 0; k < nc; ++k) {
-        cm[k].dx = cm[k].dy = 1;
-        cm[k].w = w;
-        cm[k].h = h;
+        cm[k].dx = k ? sdx : 1;
+        cm[k].dy = k ? sdy : 1;
+        cm[k].w = (w + cm[k].dx - 1) / cm[k].dx;
+        cm[k].h = (h + cm[k].dy - 1) / cm[k].dy;
         cm[k].prec = prec;
     }
-    grk_stream *st = grk_stream_create_file_stream(argv[9], 1024 * 1024, false);
+    grk_stream *st = grk_stream_create_file_stream(outp, 1024 * 1024, false);
     grk_codec *codec = st ? grk_create_compress(GRK_CODEC_J2K, st) : nullptr;
     grk_set_error_handler(err_cb, nullptr);
     grk_image *img = grk_image_create(nc, cm.data(), GRK_CLRSPC_SRGB);
@@ -74,7 +82,9 @@ static int enc_mode(int argc, char **argv) {
     int rc = 0;
     if (!codec || !img || !grk_setup_encoder(codec, &p, img) || !grk_start_compress(codec, img)) rc = 1;
     // every tile carries the same ramp (the reference test sizes it for a full tile)
-    const uint64_t tile_bytes = (uint64_t)tw * th * nc * (prec / 8);
+    uint64_t tile_bytes = 0;
+    for (uint32_t k = 0; k < nc; ++k)
+        tile_bytes += (uint64_t)((tw + cm[k].dx - 1) / cm[k].dx) * ((th + cm[k].dy - 1) / cm[k].dy) * (prec / 8);
     std::vector<uint8_t> data(tile_bytes);
     for (uint64_t i = 0; i < tile_bytes; ++i) data[i] = (uint8_t)i;
     const uint32_t ntiles = (w / tw) * (h / th);

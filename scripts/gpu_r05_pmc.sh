@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 i=0
 for SPEC in "$@"; do
   i=$((i+1))
-  for G in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD" "FETCH_SIZE" "WRITE_SIZE"; do
+  for G in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY" "FETCH_SIZE" "WRITE_SIZE"; do
     n=$(echo $G | cut -c1-5)
     ENVS=$(echo "$SPEC" | tr ' ' '\n' | grep '=' | grep -v '^[a-z]' | tr '\n' ' ')
     ARGS=$(echo "$SPEC" | tr ' ' '\n' | grep -v '^[A-Z_]*=' | grep -v '^-$' | tr '\n' ' ')

@@ -25,10 +25,10 @@ for d in sys.argv[1:]:
         w = per("SQ_WAVES") or 1
         line = "%-48s" % k[:48]
         if "SQ_WAVES" in v:
-            line += " waves %6d valu/w %7.0f salu/w %6.0f vmem/w %5.0f cyc/w %8.0f busy %.0f waitinst %.2f valu_act %.2f" % (
-                w, per("SQ_INSTS_VALU") / w, per("SQ_INSTS_SALU") / w, per("SQ_INSTS_VMEM_RD") / w,
-                per("SQ_WAVE_CYCLES") / w, per("SQ_BUSY_CYCLES"), per("SQ_WAIT_INST_ANY") / max(per("SQ_WAVE_CYCLES"), 1),
-                per("SQ_ACTIVE_INST_VALU") / max(per("SQ_WAVE_CYCLES"), 1))
+            cyc = max(per("SQ_WAVE_CYCLES"), 1)
+            line += " waves %6d valu/w %7.0f salu/w %6.0f cyc/w %8.0f wait %.2f waitinst %.2f valu_act %.2f any_act %.2f" % (
+                w, per("SQ_INSTS_VALU") / w, per("SQ_INSTS_SALU") / w, cyc / w, per("SQ_WAIT_ANY") / cyc,
+                per("SQ_WAIT_INST_ANY") / cyc, per("SQ_ACTIVE_INST_VALU") / cyc, per("SQ_ACTIVE_INST_ANY") / cyc)
         if "FETCH_SIZE" in v:
             line += " read %.1f MB" % (2 * per("FETCH_SIZE") * 1024 / 1e6)
         if "WRITE_SIZE" in v:

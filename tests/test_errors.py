@@ -233,31 +233,33 @@ def _cut_manifest():
 
 
 def test_tile_walk_matches_reference():
-    """The decoder's tile-part walk (grkgpu_walk_tiles, host only) on streams
-    cut at ~1,400 positions (oracle/make_golden_cut.py: tile-part header
-    edges, right after SOD, inside tile data, the tail), against the
-    reference's own decodes of the same prefixes: where the reference returns
-    an image, the walk accepts the stream and decodes exactly the tiles that
-    image holds (the others are zero); where the reference fails, the walk
-    fails or leaves it to the packet headers (checked on the GPU,
-    test_cut_stream_matches_reference)."""
+    """The decoder's host side (grkgpu_walk_tiles: the tile-part walk, the
+    packet headers and the code-block table, no device) on streams cut at
+    ~1,400 positions (oracle/make_golden_cut.py: tile-part header edges,
+    right after SOD, inside tile data, the tail), against the reference's own
+    decodes of the same prefixes: it fails exactly where the reference fails
+    (a stream ending inside a tile-part header, between a tile's tile-parts,
+    inside a packet header -- but not inside a segment length, which the
+    reference only warns about), and otherwise decodes exactly the tiles the
+    reference's image holds (the others are zero)."""
     grk = _grk()
     man = _cut_manifest()
-    refused = 0
+    ncuts = 0
     for name, rec in man.items():
         cs = _cs(name)
         for n, want in rec["cuts"].items():
+            ncuts += 1
             try:
                 got = grk.walk_tiles(cs[:int(n)])
             except grk.GrkGpuError:
                 got = None
             if want == "error":
-                refused += got is None
+                assert got is None, (name, n, got)
                 continue
             assert got is not None, (name, n)
             if want["tiles"] is not None:
                 assert got == want["tiles"], (name, n, got, want["tiles"])
-    assert refused > 500
+    assert ncuts > 1000
 
 
 @pytest.mark.gpu
@@ -288,21 +290,6 @@ def test_cut_stream_matches_reference(codec):
             sha = hashlib.sha256(np.ascontiguousarray(out, dtype=np.int32).tobytes()).hexdigest()
             assert sha == want["sha"], (name, n)
     assert np.array_equal(codec.decompress(_cs("g8_tiles64")), np.load("%s/g8_tiles64.dec.npy" % GOLD))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", ["rgb12_I", "g8_256", "g16_128", "rgb8_128x96"])
-def test_cut_stream_matches_oracle(codec, oracle, name):
-    """A stream cut inside its last packets (lost tail of a transfer): both the
-    GPU path and the oracle truncate the overlong segments the way
-    T2::read_packet_data does (T2.cpp:686-698) and decode the rest; the GPU
-    output equals the oracle's bit for bit (9/7 included).  No reference
-    fixture holds a cut stream, so the oracle side is parity unpinned."""
-    cs = _cs(name)
-    for k in (40, 300, 1000):
-        cut = cs[:-k]
-        ref = oracle.decode(cut)
-        assert np.array_equal(codec.decompress(cut), ref), k
 
 
 @pytest.mark.gpu

@@ -492,7 +492,7 @@ def test_dwt_pair_stage_vs_oracle(oracle, irrev, geo, shape_off, numres):
         rng.integers(-(1 << 16), 1 << 16, size=(h, w)).astype(np.int32)
     ref = oracle.dwt_fwd(a, x0, y0, numres, irrev)
     t = torch.from_numpy(a).cuda()
-    with grk.dwt_options(pair_kernel=1, f01_rows=4, pair_min_samples=0, pair_rows=rows, pair_waves=waves,
+    with grk.dwt_options(pair_kernel=2, f01_rows=4, pair_min_samples=0, pair_rows=rows, pair_waves=waves,
                          fuse_level0=0):
         grk.dwt_fwd(t, x0, y0, numres, irrev)
         torch.cuda.synchronize()

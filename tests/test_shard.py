@@ -176,3 +176,59 @@ def test_gloo_subgroup_sharded():
     expect = b"H" + b"".join(b"T%d;" % t for t in range(ntiles)) + b"E"
     assert res[1][0] == expect and res[2][0] is None and res[0] == (None, [])
     assert sorted(res[1][1] + res[2][1]) == list(range(ntiles))
+
+
+def _zero_tlm(cs):
+    """The golden with its TLM records zeroed (what rank 0's header holds)."""
+    pos = 2
+    while True:
+        m, L = struct.unpack(">HH", cs[pos:pos + 4])
+        if m == 0xFF55:
+            return cs[:pos + 6] + bytes(L - 4) + cs[pos + 2 + L:]
+        pos += 2 + L
+
+
+class SliceCoder:
+    """Stand-in coder over a golden codestream: rank payloads are its main
+    header (TLM records zeroed, as the encoder writes them before the
+    tile-parts exist) and a share of its tile-parts."""
+
+    def __init__(self, cs):
+        self.head, self.parts, self.eoc = split_codestream(_zero_tlm(cs))
+
+    def compress_tiles(self, img, prec, params, b, e, parts, offset=(0, 0), sgnd=False, row0=None, height=None):
+        return (self.head if parts & 1 else b"") + b"".join(self.parts[b:e]) + (self.eoc if parts & 2 else b"")
+
+
+def _tlm_worker(rank, world, port, name, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    cs = open(os.path.join(GOLD, name + ".j2k"), "rb").read()
+    coder = SliceCoder(cs)
+    out = shard.compress_sharded(coder, None, 12, None, len(coder.parts), dist=dist)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["rgb12_cinema2k", "rgb12_cinema4k"])
+def test_gloo_world2_sharded_tlm(name):
+    """A sharded encode of a TLM-bearing stream (the cinema profiles, one
+    tile-part per component): rank 0's main header carries TLM records it
+    cannot know, the gather patches them from the gathered tile-parts
+    (shard.patch_tlm, j2k_write_updated_tlm) -- the assembled codestream is
+    the reference's byte for byte."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + (os.getpid() % 1000) + len(name) % 7
+    procs = [ctx.Process(target=_tlm_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    cs = open(os.path.join(GOLD, name + ".j2k"), "rb").read()
+    assert _zero_tlm(cs) != cs
+    assert res[0] == cs and res[1] is None
+    assert shard.patch_tlm(b"H" + b"T0;") == b"H" + b"T0;"
