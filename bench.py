@@ -26,7 +26,8 @@ flight per GPU, each on its own codec context, HIP stream and host thread.
   e2e_frac         value / (8e12 / B_e2e), B_e2e = C (ceil(prec/8) + 4 * 4/3 + 4).
   roofline         the forward 9/7 DWT (dominant HBM kernel): B_DWT over the
                    sum of its launches' device times; roofline.inverse the
-                   same for the decode's inverse 9/7 DWT.
+                   same for the decode's inverse 9/7 DWT; roofline.r53 the
+                   forward and inverse 5/3 DWT (8K workload).
   cpu_baseline     the REFERENCE (Grok 5.1.0 libgrok compiled from source,
                    oracle/_ref) on every host core of the process's affinity
                    mask, one frame pair.
@@ -310,59 +311,88 @@ def main():
         out = []
         for i, l in enumerate(runs[0]):
             ms = sum(r[i]["ms"] for r in runs) / len(runs)
-            out.append({"kernel": l["kernel"], "levels": list(range(l["level0"], l["level0"] + l["levels"])),
-                        "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"],
+            lv = list(range(l["level0"], l["level0"] + l["levels"]))
+            # B_DWT of a launch = 8 B x (its first level's samples) x (1 + 1/4 per further level)
+            first = l["bytes"] * 4 // (4 + 1) if len(lv) == 2 else l["bytes"]
+            out.append({"kernel": l["kernel"], "levels": lv,
+                        "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"], "first_level_bytes": first,
                         "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
                         "frac": round(l["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         assert sum(x["algorithmic_bytes"] for x in out) == bdwt, "per-launch bytes must add up to B_DWT"
         return out
 
-    spans, fruns, iruns, ispans = [], [], [], []
-    with torch.cuda.stream(streams[0]):
-        for _ in range(6):
-            codecs[0].compress(frame, BITS, p97, view=True)
-            spans.append(codecs[0].stats()["dwt_ms"])
-        cs97 = bytes(codecs[0].compress(frame, BITS, p97, view=True))
-        for _ in range(6):
-            codecs[0].decompress(cs97, out=outs[0][0])
-            ispans.append(codecs[0].stats()["dwt_ms"])
-        codecs[0].set_launch_timing(True)
-        for _ in range(6):
-            codecs[0].compress(frame, BITS, p97, view=True)
-            fruns.append(codecs[0].launch_times())
-        for _ in range(6):
-            codecs[0].decompress(cs97, out=outs[0][0])
-            iruns.append(codecs[0].launch_times())
-        codecs[0].set_launch_timing(False)
-    # the first of each pays one-time setup
-    spans, ispans, fruns, iruns = spans[1:], ispans[1:], fruns[1:], iruns[1:]
-    launches, ilaunches = launch_table(fruns), launch_table(iruns)
+    def measure(params):
+        """Per-launch forward / inverse DWT times of the frame under params:
+        (forward launches, inverse launches, forward span us, inverse span us)."""
+        spans, fruns, iruns, ispans = [], [], [], []
+        with torch.cuda.stream(streams[0]):
+            for _ in range(6):
+                codecs[0].compress(frame, BITS, params, view=True)
+                spans.append(codecs[0].stats()["dwt_ms"])
+            cs = bytes(codecs[0].compress(frame, BITS, params, view=True))
+            for _ in range(6):
+                codecs[0].decompress(cs, out=outs[0][0])
+                ispans.append(codecs[0].stats()["dwt_ms"])
+            codecs[0].set_launch_timing(True)
+            for _ in range(6):
+                codecs[0].compress(frame, BITS, params, view=True)
+                fruns.append(codecs[0].launch_times())
+            for _ in range(6):
+                codecs[0].decompress(cs, out=outs[0][0])
+                iruns.append(codecs[0].launch_times())
+            codecs[0].set_launch_timing(False)
+        # the first of each pays one-time setup
+        spans, ispans, fruns, iruns = spans[1:], ispans[1:], fruns[1:], iruns[1:]
+        return (launch_table(fruns), launch_table(iruns), 1e3 * sum(spans) / len(spans),
+                1e3 * sum(ispans) / len(ispans))
+
+    launches, ilaunches, span_us, ispan_us = measure(p97)
     dwt_us = sum(x["us"] for x in launches)
     idwt_us = sum(x["us"] for x in ilaunches)
     achieved = bdwt / (dwt_us * 1e-6) / 1e9
-    traffic = None
+    traffic = traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     # the PMC passes (scripts/pmc_bench.sh) profile the default 8K workload only
     if args.workload == "8k" and os.path.exists(pmc):
         d = json.load(open(pmc))
         tot = sum(e["bytes"] for k, v in d["kernels"].items()
                   if ("k_dwt_fwd<true" in k or "k_dwt_fwd01<true" in k) for e in v)
-        traffic = round(tot)
+        traffic, traffic_src = round(tot), d["source"]
+    floor = sum(x["first_level_bytes"] for x in launches)
     roofline = {"bound": "hbm", "kernel": "forward 9/7 DWT of the frame: " + " + ".join(x["kernel"] for x in launches),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_fused_floor": floor,
+                "traffic_vs_floor": round(traffic / floor, 4) if traffic else None,
                 "algorithmic_bytes": bdwt, "dwt_us": round(dwt_us, 2),
-                "span_us": round(1e3 * sum(spans) / len(spans), 2), "launches": launches,
+                "span_us": round(span_us, 2), "launches": launches,
                 "measured": "sum of the frame's per-launch device times (HIP events on the codec stream before the "
                             "first DWT launch and after each one, so consecutive launches share an event; mean of 5 "
-                            "lone 9/7 encodes after the timed region); traffic = PMC "
-                            "bytes (FETCH_SIZE x 2 + WRITE_SIZE) of the same launches, profiles/dwt_pmc_latest.json",
+                            "lone 9/7 encodes after the timed region); traffic = PMC bytes (FETCH_SIZE x 2 + "
+                            "WRITE_SIZE) of the same launches (profiles/dwt_pmc_latest.json, source %s); "
+                            "traffic_fused_floor = 8 B per sample of each launch's first level (its input read and "
+                            "its outputs written once)" % traffic_src,
                 "inverse": {"kernel": "inverse 9/7 DWT of the frame (decode): " +
                                       " + ".join(x["kernel"] for x in ilaunches),
                             "achieved": round(bdwt / (idwt_us * 1e-6) / 1e9, 1), "unit": "GB/s",
                             "frac": round(bdwt / (idwt_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                             "algorithmic_bytes": bdwt, "dwt_us": round(idwt_us, 2),
-                            "span_us": round(1e3 * sum(ispans) / len(ispans), 2), "launches": ilaunches}}
+                            "span_us": round(ispan_us, 2), "launches": ilaunches}}
+    if args.workload == "8k":
+        # the other half of every step: the 5/3 transform of the same frame
+        # (forward: DC shift + RCT fused into level 0, then streamed level pairs)
+        l53, il53, s53, is53 = measure(pb)
+        f53, i53 = sum(x["us"] for x in l53), sum(x["us"] for x in il53)
+        roofline["r53"] = {
+            "forward": {"kernel": " + ".join(x["kernel"] for x in l53), "dwt_us": round(f53, 2),
+                        "achieved": round(bdwt / (f53 * 1e-6) / 1e9, 1), "unit": "GB/s",
+                        "frac": round(bdwt / (f53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(s53, 2),
+                        "launches": l53},
+            "inverse": {"kernel": " + ".join(x["kernel"] for x in il53), "dwt_us": round(i53, 2),
+                        "achieved": round(bdwt / (i53 * 1e-6) / 1e9, 1), "unit": "GB/s",
+                        "frac": round(bdwt / (i53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(is53, 2),
+                        "launches": il53},
+            "algorithmic_bytes": bdwt}
 
     # T1 figures: batch throughput + a lone frame's encode / decode T1 kernels
     with torch.cuda.stream(streams[0]):

@@ -2328,6 +2328,7 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
     std::vector<std::vector<uint8_t>> tbufs(nsh);  // tiles of several tile-parts: their data concatenated
     std::vector<std::vector<uint8_t>> tpacked(nsh);  // packed packet headers (PPM / PPT) of each tile
     std::vector<uint8_t> tpacked_on(nsh, 0);
+    std::vector<size_t> ppm_from(nsh, 0);  // PPM: where each tile's packet headers start in ppm_buf
     std::vector<uint8_t> contig(nsh, 1);
     // 1: bad POC marker, 2: corrupt packet header, 3: bad tile-part COD / COC
     // / QCD / QCC / RGN / PPT, 4: tile-component parameters this decoder does
@@ -2407,11 +2408,15 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
                 std::vector<uint8_t> &ph = tpacked[lt];
                 ph.clear();
                 if (!ppm_chunk.empty()) {
-                    for (uint32_t q : tpseq[t]) {
-                        if (q >= ppm_chunk.size()) { ok = false; break; }
-                        ph.insert(ph.end(), ppm_buf.begin() + ppm_chunk[q].first,
-                                  ppm_buf.begin() + ppm_chunk[q].first + ppm_chunk[q].second);
-                    }
+                    // the reference reads PPM headers through one running
+                    // pointer over the merged Nppm chunks (T2.cpp:366-375): a
+                    // tile's headers start at its first tile-part's chunk and
+                    // run on past its own chunks when the stream ended before
+                    // its later tile-parts (the tile is decoded from the
+                    // tile-parts read, its later packets' headers still parsed)
+                    for (uint32_t q : tpseq[t])
+                        if (q >= ppm_chunk.size()) ok = false;
+                    if (ok && !tpseq[t].empty()) ppm_from[lt] = ppm_chunk[tpseq[t][0]].first;
                     tpacked_on[lt] = 1;
                 } else if (!ppt.empty()) {
                     for (auto &q : ppt) ph.insert(ph.end(), csb + q.off, csb + q.off + q.len);
@@ -2443,7 +2448,8 @@ static int decompress_impl(grkgpu_ctx *c, const uint8_t *csb, size_t len, grkgpu
             decode_packet_order(tcp, tile, order);
             size_t off = 0;
             uint32_t packno = 0;
-            PackedHdr packed{tpacked[lt].data(), tpacked[lt].size(), 0};
+            PackedHdr packed = ppm_chunk.empty() ? PackedHdr{tpacked[lt].data(), tpacked[lt].size(), 0}
+                                                 : PackedHdr{ppm_buf.data() + ppm_from[lt], ppm_buf.size() - ppm_from[lt], 0};
             for (const auto &pk : order) {
                 // the data ends before the packets do (a truncated stream):
                 // the remaining packets are empty (a zero-length header reads
