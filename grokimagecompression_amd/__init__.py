@@ -336,7 +336,11 @@ class _CtxView:
     (grkgpu_give_output; freed instead if the Codec was closed) -- numpy
     arrays made from __array_interface__ keep this object as their base, and
     every view of them keeps that base.  A caller that drops its view before
-    the next compress (the bench) gets the same buffer back every time."""
+    the next compress (the bench) gets the same buffer back every time.  A
+    caller that keeps views alive across compresses holds one pinned buffer
+    (the codestream's size plus ~1/8) per live view; buffers given back while
+    the context already has one are kept as spares (at most 4, the largest)
+    and reused by later compresses instead of pinning new ones."""
 
     def __init__(self, codec, ptr, n):
         self.codec = codec

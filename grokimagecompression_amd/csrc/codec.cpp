@@ -110,9 +110,14 @@ struct grkgpu_ctx {
     std::vector<hipEvent_t> lev;
     std::vector<grkgpu_launch_time> ltimes;
     std::vector<std::pair<uint32_t, uint32_t>> lidx;  // per logged launch: its start / end event in lev
-    // guards h_out against grkgpu_give_output from another thread
+    // guards h_out and out_spare against grkgpu_give_output from another thread
     std::mutex out_mu;
+    // output buffers given back while h_out held a newer one (a caller keeping
+    // several views alive): the next compress whose h_out was taken reuses one
+    // instead of pinning a fresh buffer; at most OUT_SPARE, the largest kept
+    std::vector<std::pair<void *, size_t>> out_spare;
 };
+static constexpr size_t OUT_SPARE = 4;
 
 // Device check, cached per device index (hipGetDeviceProperties is slow and
 // the stage entry points run it per call).  device < 0: the calling thread's
@@ -193,6 +198,7 @@ void grkgpu_destroy(grkgpu_ctx *c) {
     for (auto &e : c->ev) if (e) hipEventDestroy(e);
     for (auto &e : c->lev) if (e) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    for (auto &b : c->out_spare) hipHostFree(b.first);
     delete c;
 }
 
@@ -308,7 +314,15 @@ int grkgpu_give_output(grkgpu_ctx *c, void *buf, size_t cap) {
     }
     std::lock_guard<std::mutex> lk(c->out_mu);
     if (cap > c->h_out.cap) std::swap(buf, c->h_out.p), std::swap(cap, c->h_out.cap);
-    if (buf) hipHostFree(buf);
+    if (!buf) return GRKGPU_OK;
+    if (c->out_spare.size() < OUT_SPARE) {
+        c->out_spare.push_back({buf, cap});
+        return GRKGPU_OK;
+    }
+    auto small = std::min_element(c->out_spare.begin(), c->out_spare.end(),
+                                  [](const auto &a, const auto &b) { return a.second < b.second; });
+    if (cap > small->second) std::swap(buf, small->first), std::swap(cap, small->second);
+    hipHostFree(buf);
     return GRKGPU_OK;
 }
 
@@ -339,12 +353,14 @@ int grkgpu_get_stats(grkgpu_ctx *c, grkgpu_stats *out) {
 
 void grkgpu_free(void *p) { free(p); }
 
-// Per-block scratch of the T1 stage entry points: the block state, then either
-// 32 symbol-stream slots (encode) or the unstuffed-stream region of a segment
-// of up to GRKGPU_T1_MAX_SEG bytes (decode).
+// Per-block scratch of the T1 stage entry points (per record; the records are
+// the block count rounded up to 64): encode -- the encoder's interleaved rows
+// for 32 planes, then 32 symbol-stream slots; decode -- the block state, then
+// the unstuffed-stream region of a segment of up to GRKGPU_T1_MAX_SEG bytes.
 static uint32_t t1_stage_dec_words() { return t1_unstuff_region_words(GRKGPU_T1_MAX_SEG); }
 size_t grkgpu_t1_scratch_bytes(void) {
-    return sizeof(T1Scratch) + std::max<size_t>(32 * (size_t)sym_slot_bytes(64, 64), (size_t)t1_stage_dec_words() * 4);
+    return std::max<size_t>(t1e_scratch_bytes(64, 32) / 64 + 32 * (size_t)sym_slot_bytes(64, 64),
+                            sizeof(T1Scratch) + (size_t)t1_stage_dec_words() * 4);
 }
 
 }  // extern "C"
@@ -1231,7 +1247,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->work.ensure(arena * 4 + 256));
     HIPCHK(c->coef.ensure(arena * 4 + 256));
     HIPCHK(c->ll.ensure(llarena * 4 + 256));
-    HIPCHK(c->scratch.ensure((size_t)nblk * sizeof(T1Scratch) + 256));
+    HIPCHK(c->scratch.ensure((size_t)t1e_scratch_bytes(nblk, maxdepth) + 256));
     HIPCHK(c->t1order.ensure((size_t)t1_order_words(nblk) * 4 + 256));
     HIPCHK(c->mqout.ensure(out_total + 256));
     HIPCHK(c->blocks.ensure((size_t)nblk * sizeof(EncBlock) + 256));
@@ -1352,7 +1368,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(hipMemcpyAsync(c->blocks.p, c->h_blocks.p, (size_t)nblk * sizeof(EncBlock), hipMemcpyHostToDevice, s));
     memcpy(c->h_symoff.p, symoff.data(), symoff.size() * 8);
     HIPCHK(hipMemcpyAsync(c->symoff.p, c->h_symoff.p, symoff.size() * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
+    HIPCHK(launch_t1_encode(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.p,
                             c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), maxdepth, c->mqout.as<uint8_t>(),
                             c->results.as<EncResult>(), s, cp.cblksty, lone_call() ? lone_bpw(nblk) : 0,
                             c->t1order.as<uint32_t>()));
@@ -1362,8 +1378,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     for (uint32_t l = 0; l < cp.numlayers; ++l)
         need_rc = need_rc || (cp.disto_alloc && cp.rates[l] > 0.0) || (cp.fixed_quality && cp.distoratio[l] > 0.0f);
     if (need_rc)
-        HIPCHK(launch_t1_dist(c->blocks.as<EncBlock>(), nblk, c->coef.as<int32_t>(), c->scratch.as<T1Scratch>(),
-                              c->sym.as<uint8_t>(), c->symoff.as<uint64_t>(), c->results.as<EncResult>(), s));
+        HIPCHK(launch_t1_dist(c->blocks.as<EncBlock>(), nblk, maxdepth, c->coef.as<int32_t>(), c->scratch.p,
+                              c->results.as<EncResult>(), s));
     HIPCHK(hipEventRecord(c->ev[4], s));
     if (nblk)
         HIPCHK(hipMemcpy2DAsync(c->h_results.p, sizeof(EncResult), c->results.p, sizeof(EncResult),
@@ -1755,6 +1771,13 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     HIPCHK(c->h_gather.ensure(gi.size() * sizeof(GatherItem) + hdr.size() + 512));
     HIPCHK(c->packed.ensure(total + 256));
     std::unique_lock<std::mutex> out_lk(c->out_mu);
+    if (!c->h_out.p && !c->out_spare.empty()) {  // taken by a view: reuse a given-back buffer
+        auto big = std::max_element(c->out_spare.begin(), c->out_spare.end(),
+                                    [](const auto &a, const auto &b) { return a.second < b.second; });
+        c->h_out.p = big->first;
+        c->h_out.cap = big->second;
+        c->out_spare.erase(big);
+    }
     HIPCHK(c->h_out.ensure(total + 256));
     const size_t gbytes = gi.size() * sizeof(GatherItem);
     const size_t hoff = (gbytes + 255) & ~(size_t)255;
@@ -2931,13 +2954,14 @@ extern "C" int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t 
     if (!blocks || !coef || !scratch || !out || !results) return set_err(GRKGPU_EINVAL, "null argument");
     int rc = check_device(-1);
     if (rc) return rc;
-    // scratch layout: nblocks T1Scratch records, then 32 fixed symbol slots per block
-    uint8_t *sym = (uint8_t *)scratch + (size_t)nblocks * sizeof(T1Scratch);
-    HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, (T1Scratch *)scratch, sym, nullptr, 32, out,
+    // scratch layout: the encoder's rows for nblocks (rounded up to 64) blocks
+    // of 32 planes, then 32 fixed symbol slots per block
+    uint8_t *sym = (uint8_t *)scratch + t1e_scratch_bytes(nblocks, 32);
+    HIPCHK(launch_t1_encode((const EncBlock *)blocks, nblocks, coef, scratch, sym, nullptr, 32, out,
                             (EncResult *)results, (hipStream_t)stream));
     if (with_distortion)
-        HIPCHK(launch_t1_dist((const EncBlock *)blocks, nblocks, coef, (const T1Scratch *)scratch, sym, nullptr,
-                              (EncResult *)results, (hipStream_t)stream));
+        HIPCHK(launch_t1_dist((const EncBlock *)blocks, nblocks, 32, coef, scratch, (EncResult *)results,
+                              (hipStream_t)stream));
     return GRKGPU_OK;
 }
 

@@ -156,17 +156,19 @@ hipError_t launch_dwt_fwd_pair(const DwtJob *jobs0, const DwtJob *jobs1, uint32_
 // sym: symbol-stream arena; sym_off[i] = block i's byte offset (n+1 entries,
 // capacity = (sym_off[i+1]-sym_off[i]) / sym_slot_bytes(w,h) planes), or null
 // for the fixed layout of 32 planes x sym_slot_bytes(64,64) per block.
-// cblksty: the CBLKSTY_* mode switches of the codestream (t1_lane.h), 0 = none
-hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
+// cblksty: the CBLKSTY_* mode switches of the codestream (t1_lane.h), 0 = none.
+// scratch: t1e_scratch_bytes(n, maxdepth) bytes (t1_lane.h EncScratch), with
+// maxdepth >= every block's plane capacity (<= 32)
+hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, void *scratch,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
                             hipStream_t s, uint32_t cblksty = 0, uint32_t bpw = 0, uint32_t *order = nullptr);
 // device words the MQ coder's work order needs (launch_t1_encode `order`)
 uint32_t t1_order_words(uint32_t nblocks);
-// Per-pass distortion sums of the blocks k_t1_model coded (same sym /
-// sym_off layout): nmsedec[pass] of every block, in the pass order of
+// Per-pass distortion sums of the blocks k_t1_model coded (same scratch and
+// maxdepth): nmsedec[pass] of every block, in the pass order of
 // t1_encode_cblk (t1.cpp:1222-1260).
-hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coef, const T1Scratch *scratch,
-                          const uint8_t *sym, const uint64_t *sym_off, EncResult *res, hipStream_t s);
+hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, uint32_t maxdepth, const int32_t *coef,
+                          const void *scratch, EncResult *res, hipStream_t s);
 // ubuf: unstuffed-stream arena; block i's region at ubuf + i * fixed_words
 // words, or (fixed_words == 0) at blocks[i].pad * 16 bytes
 // (t1_unstuff_region_words words each).

@@ -133,6 +133,34 @@ __global__ void k_mct_inv_dcshift(PlanePtrs src, uint32_t sstride, uint32_t tw, 
 // Decode = lane decoder (one lane per block, write-only bit-plane rows) +
 // rebuild (workgroup per block: values + post-decode scaling, coalesced).
 // ---------------------------------------------------------------------------
+// Lane-interleaved rows (t1_lane.h) through buffer instructions: the group's
+// region is one buffer resource (wave-uniform, SGPRs) and a row access is a
+// 32-bit lane offset, so the decoder keeps one offset VGPR per row index
+// instead of a 64-bit pointer per state array.
+struct LRef {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t so, vo;
+    __device__ operator uint64_t() const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
+        return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+    }
+    __device__ const LRef &operator=(uint64_t v) const {
+        const __attribute__((ext_vector_type(2))) uint32_t p = {(uint32_t)v, (uint32_t)(v >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(p, r, vo, so, 0);
+        return *this;
+    }
+};
+// so: the field's byte offset (scalar); vo: the lane's byte offset + rows
+struct LRow {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t so, vo;
+    __device__ LRef operator[](uint32_t y) const { return LRef{r, so, vo + y * 512u}; }
+    __device__ LRow operator+(uint32_t n) const { return LRow{r, so, vo + n * 512u}; }
+};
+// the buffer resource of one 64-block group of lane-interleaved rows
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+}
 template <int LANES>
 __device__ __forceinline__ void t1_tables_init(uint8_t *zc, uint8_t *sc, uint32_t *mq) {
     for (uint32_t k = threadIdx.x; k < 2048; k += LANES) zc[k] = zc_lut_entry(k >> 9, k & 511);
@@ -141,9 +169,17 @@ __device__ __forceinline__ void t1_tables_init(uint8_t *zc, uint8_t *sc, uint32_
     __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blocks, const int32_t *__restrict__ coef,
-                                                T1Scratch *__restrict__ scr, EncResult *__restrict__ res) {
-    const uint32_t i = blockIdx.x, x = threadIdx.x;
+// One wavefront per block, lane = row.  Workgroup b runs on XCD b % 8 (the
+// dispatcher deals workgroups round-robin), so the 64 blocks of group g are
+// given to workgroups of one XCD, back to back: their row words, 8 bytes per
+// lane at a 512-byte stride (the group layout, t1_lane.h EncScratch), meet as
+// whole lines in that XCD's L2.
+__global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth,
+                                                const int32_t *__restrict__ coef, uint8_t *__restrict__ scr,
+                                                EncResult *__restrict__ res) {
+    const uint32_t wg = blockIdx.x, k = wg >> 3;
+    const uint32_t i = (((k >> 6) << 3) | (wg & 7)) * 64 + (k & 63), x = threadIdx.x;
+    if (i >= n) return;
     const EncBlock b = blocks[i];
     const int32_t *src = coef + b.coef_off;
     uint32_t m[64];
@@ -165,12 +201,15 @@ __global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blo
         uint32_t t = 32u - (uint32_t)__clz(orv);
         numbps = t <= 6 ? 0 : t - 6;
     }
-    T1Scratch &S = scr[i];
-    S.st.neg[x + 1] = x < b.h ? negrow : 0;
-    if (x == 0) S.st.neg[0] = 0;
-    if (x == 63) S.st.neg[65] = 0;
+    const EncScratch E = enc_scratch(scr, n, maxdepth);
+    uint64_t *G = E.group(i >> 6) + (i & 63);  // row R of this block: G[R * 64]
+    G[(T1E_NEG + x + 1) * 64] = x < b.h ? negrow : 0;
+    if (x == 0) G[T1E_NEG * 64] = 0;
+    if (x == 63) G[(T1E_NEG + 65) * 64] = 0;
+    const uint32_t nd = numbps < maxdepth ? numbps : maxdepth;  // numbps > maxdepth: refused (res.pad)
     uint64_t acc = 0;  // significance before plane p = OR of the planes above
-    for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
+    for (uint32_t d = 0; d < nd; ++d) {
+        const uint32_t p = numbps - 1 - d;
         uint64_t mine = 0;
 #pragma unroll
         for (int y = 0; y < 64; ++y) {
@@ -178,8 +217,8 @@ __global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blo
             if (x == (uint32_t)y) mine = bal;
         }
         if (x < b.h) {
-            S.pa[p * 64 + x] = mine;
-            S.pb[p * 64 + x] = acc;
+            G[(t1e_depth_row(d) + T1E_BITS + x) * 64] = mine;
+            G[(t1e_depth_row(d) + T1E_ABOVE + x) * 64] = acc;
         }
         acc |= mine;
     }
@@ -190,8 +229,14 @@ __global__ __launch_bounds__(64) void k_t1_prep(const EncBlock *__restrict__ blo
 }
 
 // Context modelling, one lane per (block, bit-plane): lanes are laid out
-// depth-major (depth = numbps-1-p) so a wavefront holds the same depth of 64
-// neighbouring blocks -- similar statistics, little divergence.
+// depth-major (depth = numbps-1-p) so a wavefront holds the same depth of the
+// 64 blocks of a group -- similar statistics, little divergence -- and, with
+// the group-interleaved rows of t1_lane.h EncScratch, every row access of the
+// wavefront is one 512-byte run.  Per-block rows (round 4) had each lane read
+// its own 8-byte rows from 64 different lines, evicted between stripes: 3.3-3.7
+// GB read per 8K 9/7 frame; interleaved 1.2-1.3 GB (profiles/r05/
+// t1_model_interleave.txt), the post-SPP / visited rows moved from the symbol
+// slots into the group rows with them.
 __device__ __forceinline__ uint64_t sym_block_off(const uint64_t *sym_off, uint32_t i, uint32_t *cap) {
     if (!sym_off) {
         *cap = 32;
@@ -200,17 +245,17 @@ __device__ __forceinline__ uint64_t sym_block_off(const uint64_t *sym_off, uint3
     return sym_off[i];
 }
 
-__global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth,
-                                                 T1Scratch *__restrict__ scr, uint8_t *__restrict__ sym,
-                                                 const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res,
-                                                 uint32_t cblksty) {
+__global__ __launch_bounds__(64) void k_t1_model(
+    const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth, uint8_t *__restrict__ scr,
+    uint8_t *__restrict__ sym, const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res, uint32_t cblksty) {
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_ring[32 * 64];  // SymOut: 32 words per lane, word j at (j % 32) * 64 + lane
     for (uint32_t k = threadIdx.x; k < 256; k += 64) s_sc[k] = sc_lut_entry(k);
     __syncthreads();
-    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= n * maxdepth) return;
-    const uint32_t i = t % n, d = t / n;
+    // wavefront = (group, depth): lane = the group's block
+    const uint32_t n64 = t1_scratch_records(n), w0 = blockIdx.x * 64;
+    const uint32_t g0 = w0 % n64, d = w0 / n64, i = g0 + threadIdx.x;
+    if (d >= maxdepth || i >= n) return;
     const uint32_t numbps = res[i].numbps;
     if (d >= numbps) return;
     const EncBlock b = blocks[i];
@@ -223,11 +268,16 @@ __global__ __launch_bounds__(64) void k_t1_model(const EncBlock *__restrict__ bl
         return;
     }
     const uint32_t p = numbps - 1 - d;
-    T1Scratch &S = scr[i];
+    const EncScratch E = enc_scratch(scr, n, maxdepth);
+    const __amdgpu_buffer_rsrc_t gr = group_rsrc(E.group(g0 >> 6), 64 * E.rec_rows * 8);
+    const uint32_t lo = threadIdx.x * 8, dr = t1e_depth_row(d);
+    const LRow bits{gr, (dr + T1E_BITS) * 512, lo}, above{gr, (dr + T1E_ABOVE) * 512, lo};
+    const LRow ref{gr, (d ? dr - T1E_DEPTH_ROWS + T1E_ABOVE : 0) * 512, lo}, negr{gr, T1E_NEG * 512, lo};
+    const LRow tmp{gr, (dr + T1E_POST) * 512, lo};
     uint8_t *base = sym + off + (uint64_t)p * slot;
-    t1_model_plane(b.w, b.h, b.orient, S.pa + p * 64, S.pb + p * 64, p + 1 < numbps ? S.pb + (p + 1) * 64 : nullptr,
-                   S.st.neg, (uint64_t *)(base + sym_stream_bytes(b.w, b.h)), s_sc, (uint32_t *)base, S.cnt + p * 4,
-                   cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps), s_ring + threadIdx.x);
+    t1_model_plane(b.w, b.h, b.orient, bits, above, ref, d > 0, negr, tmp, s_sc, (uint32_t *)base,
+                   E.cnt + (size_t)i * 128 + p * 4, cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps),
+                   s_ring + threadIdx.x);
 }
 
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
@@ -235,7 +285,7 @@ constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder'
 // MQ coding, one lane per block (lane j codes block perm[j], or j).
 template <int LANES, int MINW = 1, bool LAZY = false>
 __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
-                                                 const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
+                                                 const uint32_t *__restrict__ cnt, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
                                                  EncResult *__restrict__ res, const uint32_t *__restrict__ perm,
                                                  uint32_t cblksty, uint32_t bpw) {
@@ -258,12 +308,12 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     uint32_t cap;
     const uint64_t off = sym_block_off(sym_off, i, &cap);
     uint32_t len;
-    uint32_t np = t1_mq_block<LAZY>(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, scr[i].cnt, s_mq,
+    uint32_t np = t1_mq_block<LAZY>(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, cnt + (size_t)i * 128, s_mq,
                               s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len, cblksty);
     r.numpasses = np;
     r.len = len;
     uint32_t nsym = 0;
-    const uint32_t *c = scr[i].cnt;
+    const uint32_t *c = cnt + (size_t)i * 128;
     for (uint32_t q = 0; q < r.numbps && q < 32; ++q) nsym += c[q * 4] + c[q * 4 + 1] + c[q * 4 + 2];
     r.nsym = nsym;
 }
@@ -276,20 +326,20 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
 // order inside a bucket follows the atomics (it varies from run to run);
 // every block's output is its own, so the codestream does not.
 constexpr uint32_t MQ_ORDER_BUCKETS = 256;
-__device__ __forceinline__ uint32_t mq_work_bucket(const T1Scratch &s, uint32_t numbps) {
+__device__ __forceinline__ uint32_t mq_work_bucket(const uint32_t *c, uint32_t numbps) {
     uint32_t w = 0;
-    for (uint32_t q = 0; q < numbps && q < 32; ++q) w += s.cnt[q * 4] + s.cnt[q * 4 + 1] + s.cnt[q * 4 + 2];
+    for (uint32_t q = 0; q < numbps && q < 32; ++q) w += c[q * 4] + c[q * 4 + 1] + c[q * 4 + 2];
     w += 1;
     const uint32_t o = 31u - (uint32_t)__builtin_clz(w);            // octave
     const uint32_t f = o >= 3 ? (w >> (o - 3)) & 7u : (w << (3 - o)) & 7u;  // 3 bits below the top one
     return (MQ_ORDER_BUCKETS - 1) - min((o << 3) | f, MQ_ORDER_BUCKETS - 1);  // heaviest first
 }
-__global__ __launch_bounds__(256) void k_mq_order_hist(const T1Scratch *__restrict__ scr,
+__global__ __launch_bounds__(256) void k_mq_order_hist(const uint32_t *__restrict__ cnt,
                                                       const EncResult *__restrict__ res, uint32_t n,
                                                       uint32_t *__restrict__ key, uint32_t *__restrict__ hist) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint32_t k = mq_work_bucket(scr[i], res[i].numbps);
+    const uint32_t k = mq_work_bucket(cnt + (size_t)i * 128, res[i].numbps);
     key[i] = k;
     atomicAdd(&hist[k], 1u);
 }
@@ -321,10 +371,9 @@ __global__ __launch_bounds__(256) void k_mq_order_scatter(const uint32_t *__rest
 // to the cleanup pass) and to every lower plane's refinement pass.  The
 // SPP membership comes from the post-SPP significance rows k_t1_model left
 // behind each plane's symbol stream.
-__global__ __launch_bounds__(64) void k_t1_dist(const EncBlock *__restrict__ blocks, const int32_t *__restrict__ coef,
-                                                const T1Scratch *__restrict__ scr, const uint8_t *__restrict__ sym,
-                                                const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res,
-                                                NmseLut lutv) {
+__global__ __launch_bounds__(64) void k_t1_dist(const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth,
+                                                const int32_t *__restrict__ coef, const uint8_t *__restrict__ scr,
+                                                EncResult *__restrict__ res, NmseLut lutv) {
     __shared__ NmseLut lut;
     {
         const int16_t *src = &lutv.sig[0];
@@ -344,20 +393,19 @@ __global__ __launch_bounds__(64) void k_t1_dist(const EncBlock *__restrict__ blo
         uint32_t ng;
         m[y] = ((uint32_t)y < b.h && x < b.w) ? quant_mag(src[(size_t)y * b.stride + x], b.qmfbid, b.inv_step, &ng) : 0;
     }
-    uint32_t cap;
-    const uint64_t off = sym_block_off(sym_off, i, &cap);
-    const uint32_t slot = sym_slot_bytes(b.w, b.h);
+    const EncScratch E = enc_scratch(const_cast<uint8_t *>(scr), n, maxdepth);
+    const uint64_t *G = E.group(i >> 6) + (i & 63);
     for (int32_t p = (int32_t)numbps - 1; p >= 0; --p) {
-        const uint64_t *post = (const uint64_t *)(sym + off + (uint64_t)p * slot + sym_stream_bytes(b.w, b.h));
+        // the block's post-SPP significance rows of plane p (row y at post[y * 64])
+        const uint64_t *post = G + (size_t)(t1e_depth_row(numbps - 1 - (uint32_t)p) + T1E_POST) * 64;
         int32_t a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll
         for (int y = 0; y < 64; ++y) {
-            if ((uint32_t)y >= b.h) break;
-            const uint32_t mag = m[y];
+            const uint32_t mag = (uint32_t)y < b.h ? m[y] : 0u;  // no break: m stays in registers
             const uint32_t win = p > 0 ? (mag >> p) & 127u : mag & 127u;
             if ((mag >> (p + 6)) == 1u) {
                 const int32_t v = p > 0 ? lut.sig[win] : lut.sig0[win];
-                if ((post[y] >> x) & 1u) a0 += v; else a2 += v;
+                if ((post[(size_t)y * 64] >> x) & 1u) a0 += v; else a2 += v;
             } else if (mag >> (p + 7)) {
                 a1 += p > 0 ? lut.ref[win] : lut.ref0[win];
             }
@@ -444,36 +492,24 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     unstuff_segment(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words));
 }
 
-// Lane-interleaved rows (t1_lane.h) through buffer instructions: the group's
-// region is one buffer resource (wave-uniform, SGPRs) and a row access is a
-// 32-bit lane offset, so the decoder keeps one offset VGPR per row index
-// instead of a 64-bit pointer per state array.
-struct LRef {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t so, vo;
-    __device__ operator uint64_t() const {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
-        return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-    }
-    __device__ const LRef &operator=(uint64_t v) const {
-        const __attribute__((ext_vector_type(2))) uint32_t p = {(uint32_t)v, (uint32_t)(v >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b64(p, r, vo, so, 0);
-        return *this;
-    }
-};
-// so: the field's byte offset (scalar); vo: the lane's byte offset + rows
-struct LRow {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t so, vo;
-    __device__ LRef operator[](uint32_t y) const { return LRef{r, so, vo + y * 512u}; }
-    __device__ LRow operator+(uint32_t n) const { return LRow{r, so, vo + n * 512u}; }
-};
 struct LState {
     LRow sig, neg, vis, ref;
 };
 
-template <int LANES, bool LAZY = false>
-__global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
+// Decoder workgroups: DEC_WAVES wavefronts share one copy of the LUTs in LDS,
+// and the kernel is held to 128 VGPRs (a few spills at pass boundaries), so 4
+// wavefronts fit per SIMD by both registers and LDS (38 KB per workgroup: the
+// LUTs, 19 context words per lane -- odd, so the lanes spread over the banks --
+// and the bit readers' word rings).  Against one wavefront per workgroup at 144
+// VGPRs (3 per SIMD): 8K batch 3264-3280 -> 3507-3508 Mpixels/s, lone decode
+// T1 31.7-31.9 -> 30.9-31.3 ms (profiles/r05/t1_dec_wg_ab.txt).  (Round 3's
+// 128-VGPR build with single-wavefront workgroups had measured no gain: LDS
+// then still held it near 3 per SIMD.)
+constexpr int DEC_WAVES = 4;
+constexpr uint32_t DEC_CX_STRIDE = 19;
+
+template <int LANES, bool LAZY, int WAVES, int WPE>
+__global__ __launch_bounds__(LANES * WAVES) __attribute__((amdgpu_waves_per_eu(WPE))) void k_t1_decode_ub(const DecBlock *__restrict__ blocks, uint32_t n,
                                                         const uint32_t *__restrict__ ubuf, uint32_t fixed_words,
                                                         T1Scratch *__restrict__ scr, const DecSeg *__restrict__ segs,
                                                         const uint32_t *__restrict__ seg_first, uint32_t sty,
@@ -481,15 +517,17 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_mq[48];
-    __shared__ uint32_t s_cx[LANES * 21];
-    __shared__ uint32_t s_ring[LANES * FB_RING];  // bit readers' word rings (t1_flat.h FlatBits), slot stride 64
+    __shared__ uint32_t s_cx[WAVES * LANES * DEC_CX_STRIDE];
+    __shared__ uint32_t s_ring[WAVES * LANES * FB_RING];  // bit readers' word rings (t1_flat.h FlatBits), slot stride 64
     static_assert(LANES == 64, "the word rings interleave 64 lanes");
-    for (uint32_t k = threadIdx.x; k < 2048; k += LANES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
-    for (uint32_t k = threadIdx.x; k < 256; k += LANES) s_sc[k] = sc_win_entry(k);
-    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
+    for (uint32_t k = threadIdx.x; k < 2048; k += LANES * WAVES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
+    for (uint32_t k = threadIdx.x; k < 256; k += LANES * WAVES) s_sc[k] = sc_win_entry(k);
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES * WAVES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
-    if (threadIdx.x >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
-    const uint32_t i = blockIdx.x * bpw + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
+    const uint32_t gw = blockIdx.x * WAVES + wv;  // the wavefront's index in the grid
+    const uint32_t i = gw * bpw + lane;
     if (i >= n) return;
     const DecBlock b = blocks[i];
     if (b.len == 0 || b.numpasses == 0 || b.numbps == 0 || b.numbps > T1_MAX_DEC_BPS) return;
@@ -497,14 +535,15 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     // lane-interleaved state and bit-plane rows of this block (t1_lane.h T1Group)
     // bpw is a power of two <= 64, so the wavefront's blocks share one group:
     // the group (and the buffer resource) stays wave-uniform, in SGPRs
-    const uint32_t grp = __builtin_amdgcn_readfirstlane((blockIdx.x * bpw) >> 6);
+    const uint32_t grp = __builtin_amdgcn_readfirstlane((gw * bpw) >> 6);
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         t1_group_base(scr, grp, sizeof(T1Scratch)), 0, (int)(64 * sizeof(T1Scratch)), 0x00020000);
     const uint32_t lo = (i & 63) * 8;
     LState st{LRow{gr, T1R_SIG * 512, lo}, LRow{gr, T1R_NEG * 512, lo}, LRow{gr, T1R_VIS * 512, lo},
               LRow{gr, T1R_REF * 512, lo}};
     const LRow pa{gr, T1R_PA * 512, lo}, pb{gr, T1R_PB * 512, lo};
-    uint32_t *cxw = s_cx + threadIdx.x * 21;
+    uint32_t *const ring = s_ring + wv * (LANES * FB_RING) + lane;
+    uint32_t *cxw = s_cx + threadIdx.x * DEC_CX_STRIDE;
     if (segs) {
         const uint32_t q0 = seg_first[i], nseg = seg_first[i + 1] - q0;
         const DecSeg s0 = segs[q0];
@@ -512,7 +551,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
         for (uint32_t y = 0; y < b.h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
         mq_reset_words(cxw, T.mq);
         BitDecT<LAZY> d;
-        d.set_ring(s_ring + threadIdx.x, 6);
+        d.set_ring(ring, 6);
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));
         SegCursor cur{segs + q0, ubuf, nseg, 0, s0.npasses};
         t1_decode_passes(d, b.numpasses, b.numbps, b.w, b.h, st, T, cxw, pa, pb, sty, cur, roi ? roi[i] : 0u);
@@ -520,7 +559,7 @@ __global__ __launch_bounds__(LANES) void k_t1_decode_ub(const DecBlock *__restri
     }
     const uint32_t *region = ubuf + ub_region(b, i, fixed_words);
     t1_decode_v5(region + 4, region[0], region + 4 + unstuff_word_cap(b.len), b.numpasses, b.numbps, b.w, b.h, st, T,
-                 cxw, pa, pb, s_ring + threadIdx.x, 6);
+                 cxw, pa, pb, ring, 6);
 }
 
 // Rebuild of the decoded values from the lane-interleaved bit-plane rows:
@@ -698,34 +737,38 @@ static uint32_t t1_blocks_per_wave(uint32_t n) {
 
 uint32_t t1_order_words(uint32_t n) { return 2 * n + MQ_ORDER_BUCKETS; }
 
-hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, T1Scratch *scratch,
+hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *coef, void *scratch_v,
                             uint8_t *sym, const uint64_t *sym_off, uint32_t maxdepth, uint8_t *out, EncResult *res,
                             hipStream_t s, uint32_t cblksty, uint32_t bpw_req, uint32_t *order) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_prep, dim3(n), dim3(64), 0, s, blocks, coef, scratch, res);
+    uint8_t *scratch = (uint8_t *)scratch_v;
     if (maxdepth > 32) maxdepth = 32;
-    uint64_t threads = (uint64_t)n * maxdepth;
-    hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s, blocks, n, maxdepth,
-                       scratch, sym, sym_off, res, cblksty);
+    if (maxdepth < 1) maxdepth = 1;
+    const uint32_t groups8 = (t1_scratch_records(n) / 64 + 7) & ~7u;  // k_t1_prep's XCD deal: whole rounds of 8 groups
+    hipLaunchKernelGGL(k_t1_prep, dim3(groups8 * 64), dim3(64), 0, s, blocks, n, maxdepth, coef, scratch, res);
+    const uint64_t threads = (uint64_t)t1_scratch_records(n) * maxdepth;
+    hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)(threads / 64)), dim3(64), 0, s, blocks, n, maxdepth, scratch, sym,
+                       sym_off, res, cblksty);
     const uint32_t bpw = dwt_options().t1_enc_bpw ? (uint32_t)dwt_options().t1_enc_bpw
                          : bpw_req                ? bpw_req
                                                   : t1_blocks_per_wave(n);
     const uint32_t *perm = nullptr;
+    const uint32_t *cnt = enc_scratch(scratch, n, maxdepth).cnt;
     if (order && dwt_options().t1_enc_sort && n > 64) {  // order: t1_order_words(n) words
         uint32_t *key = order, *permw = order + n, *hist = order + 2 * n;
         const hipError_t e = hipMemsetAsync(hist, 0, MQ_ORDER_BUCKETS * 4, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_mq_order_hist, dim3((n + 255) / 256), dim3(256), 0, s, scratch, res, n, key, hist);
+        hipLaunchKernelGGL(k_mq_order_hist, dim3((n + 255) / 256), dim3(256), 0, s, cnt, res, n, key, hist);
         hipLaunchKernelGGL(k_mq_order_scan, dim3(1), dim3(MQ_ORDER_BUCKETS), 0, s, hist);
         hipLaunchKernelGGL(k_mq_order_scatter, dim3((n + 255) / 256), dim3(256), 0, s, key, n, hist, permw);
         perm = permw;
     }
     if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           scratch, sym, sym_off, out, res, perm, cblksty, bpw);
+                           cnt, sym, sym_off, out, res, perm, cblksty, bpw);
     else
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           scratch, sym, sym_off, out, res, perm, cblksty, bpw);
+                           cnt, sym, sym_off, out, res, perm, cblksty, bpw);
     return hipGetLastError();
 }
 
@@ -750,10 +793,13 @@ const NmseLut &nmse_lut() {
     return L;
 }
 
-hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, const int32_t *coef, const T1Scratch *scratch,
-                          const uint8_t *sym, const uint64_t *sym_off, EncResult *res, hipStream_t s) {
+hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, uint32_t maxdepth, const int32_t *coef,
+                          const void *scratch, EncResult *res, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_dist, dim3(n), dim3(64), 0, s, blocks, coef, scratch, sym, sym_off, res, nmse_lut());
+    if (maxdepth > 32) maxdepth = 32;
+    if (maxdepth < 1) maxdepth = 1;
+    hipLaunchKernelGGL(k_t1_dist, dim3(n), dim3(64), 0, s, blocks, n, maxdepth, coef, (const uint8_t *)scratch, res,
+                       nmse_lut());
     return hipGetLastError();
 }
 
@@ -766,13 +812,17 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     const uint32_t bpw = dwt_options().t1_dec_bpw ? (uint32_t)dwt_options().t1_dec_bpw
                          : bpw_req                ? bpw_req
                                                   : t1_blocks_per_wave(n);
+    // DEC_WAVES wavefronts per workgroup share the LUTs (roi only for BYPASS:
+    // the ROI shift only moves BYPASS pass boundaries)
+    const uint32_t nw = (n + bpw - 1) / bpw, nwg = (nw + DEC_WAVES - 1) / DEC_WAVES;
     if (cblksty & CBLKSTY_LAZY)
-        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
-                           n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi, bpw);
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true, DEC_WAVES, DEC_WAVES>), dim3(nwg), dim3(DEC_LANES * DEC_WAVES),
+                           0, s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi,
+                           bpw);
     else
-        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false>), dim3((n + bpw - 1) / bpw), dim3(DEC_LANES), 0, s, blocks,
-                           n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty,
-                           nullptr, bpw);  // the ROI shift only moves BYPASS pass boundaries
+        hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false, DEC_WAVES, DEC_WAVES>), dim3(nwg),
+                           dim3(DEC_LANES * DEC_WAVES), 0, s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch,
+                           segs, seg_first, cblksty, nullptr, bpw);
     hipLaunchKernelGGL(k_t1_rebuild, dim3((n + 63) / 64, 64 / RB_ROWS), dim3(256), 0, s, blocks, n, scratch, tiles,
                        roi);
     return hipGetLastError();

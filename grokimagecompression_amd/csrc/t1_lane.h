@@ -372,7 +372,7 @@ GRK_HD uint32_t sym_stream_bytes(uint32_t w, uint32_t h) {
     // stripe column, 4 segmentation symbols (SEGSYM)
     return (w * h * 2 + ((h + 3) / 4) * w * 2 + 4 + 15) & ~15u;
 }
-GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h) + 2 * 64 * 8; }
+GRK_HD uint32_t sym_slot_bytes(uint32_t w, uint32_t h) { return sym_stream_bytes(w, h); }
 
 // A lane's symbol stream, 4 symbols per word.  On the GPU the 64 lanes of a
 // wavefront write 64 different streams, and a word stored straight to HBM is
@@ -524,11 +524,17 @@ GRK_HD uint32_t sc_symbol(const uint8_t *sc, uint64_t sW, uint64_t nW, uint64_t 
     return (si & 0x7f) | ((((uint32_t)(neg >> x) & 1u) ^ (raw ? 0u : (si >> 7))) << 5);
 }
 
-GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0 && (uint32_t)y < h) ? a[y] : 0; }
+// a: a row array (host: a pointer; device: the lane-interleaved rows of
+// kernels.hip LRow)
+template <class A>
+GRK_HD uint64_t ldrow(const A &a, int32_t y, uint32_t h) {
+    return (y >= 0 && (uint32_t)y < h) ? (uint64_t)a[y] : 0;
+}
 
 // Model bit-plane p of one block.  above = significance before plane p,
-// ref = significance before plane p+1 (refined-before flags), negr = sign
-// rows (index y+1), tmp = 128 rows of scratch.  Writes the plane's stream and
+// ref = significance before plane p+1 (refined-before flags; has_ref false
+// for the top plane), negr = sign rows (index y+1), tmp = 128 rows of scratch
+// (post-SPP significance, then the SPP's visited rows).  Writes the plane's stream and
 // cnt[0..2] = symbols of its SPP / MRP / CUP (SPP and MRP are empty for the
 // top plane).  Semantics: t1.cpp:197-338 (SPP), 443-555 (MRP), 639-782 (CUP).
 //
@@ -537,13 +543,13 @@ GRK_HD uint64_t ldrow(const uint64_t *a, int32_t y, uint32_t h) { return (y >= 0
 // stripe's first row, t1.cpp:168-190), i.e. row k+4 reads as insignificant
 // for row k+3; SEGSYM -- the cleanup pass ends with the segmentation symbols
 // 1 0 1 0 in the uniform context (mqc_segmark_enc, t1.cpp:1244-1245).
-GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64_t *bitp, const uint64_t *above,
-                           const uint64_t *ref, const uint64_t *negr, uint64_t *tmp, const uint8_t *sc,
-                           uint32_t *out, uint32_t *cnt, uint32_t cblksty = 0, bool raw_spp = false,
-                           uint32_t *ring = nullptr) {
+template <class R, class T>
+GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bitp, const R &above, const R &ref,
+                           bool has_ref, const R &negr, const T &tmp, const uint8_t *sc, uint32_t *out, uint32_t *cnt,
+                           uint32_t cblksty = 0, bool raw_spp = false, uint32_t *ring = nullptr) {
     const uint64_t wm = w >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << w) - 1);
     const bool vsc = (cblksty & CBLKSTY_VSC) != 0;
-    uint64_t *postS = tmp, *visS = tmp + 64;
+    const T postS = tmp, visS = tmp + 64;
     SymOut so{out, 0, 0, ring, 0};
     // ---- significance propagation ----
     uint64_t U = 0;  // post-SPP significance of row k-1
@@ -629,7 +635,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const uint64
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             m[r] = ldrow(above, (int32_t)(k + r), h);
-            o1[r] = ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
+            o1[r] = has_ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
             bit[r] = ldrow(bitp, (int32_t)(k + r), h);
             const uint64_t nb = dil(sS[r]) | dil(sS[r + 2]) | (sS[r + 1] << 1) | (sS[r + 1] >> 1);
             o0[r] = nb & ~o1[r];
@@ -937,6 +943,35 @@ struct T1Scratch {
     uint64_t pb[32 * 64];
     uint32_t cnt[32 * 4];  // encoder: symbols per (plane, pass type)
 };
+
+// ---- lane-interleaved scratch (encoder) ----
+// The encoder's modelling kernel runs one lane per (block, bit-plane) with the
+// 64 lanes of a wavefront at the same depth (numbps - 1 - plane) of the 64
+// blocks of a group, so its rows are kept like the decoder's: the 64 blocks of
+// a group share a region in which row R of block l is word R * 64 + l, and the
+// bit-plane rows are indexed by depth, so every row access of a wavefront is
+// one 512-byte run.  Per block: the sign rows (66), then per depth 256 rows:
+// the plane's magnitude bits, the significance before it, and the modelling
+// kernel's post-SPP significance and SPP-visited rows.  The symbol counts per
+// (plane, pass) sit ahead of the groups, 128 words per block.
+constexpr uint32_t T1E_NEG = 0, T1E_PL = 66, T1E_DEPTH_ROWS = 256;
+constexpr uint32_t T1E_BITS = 0, T1E_ABOVE = 64, T1E_POST = 128, T1E_VIS = 192;  // inside a depth
+GRK_HD constexpr uint32_t t1e_rec_rows(uint32_t maxdepth) { return T1E_PL + maxdepth * T1E_DEPTH_ROWS; }
+GRK_HD constexpr uint32_t t1e_depth_row(uint32_t d) { return T1E_PL + d * T1E_DEPTH_ROWS; }
+// bytes of the encoder scratch for n blocks of at most maxdepth planes
+GRK_HD constexpr uint64_t t1e_scratch_bytes(uint32_t n, uint32_t maxdepth) {
+    return (uint64_t)((n + 63) & ~63u) * (128 * 4 + (uint64_t)t1e_rec_rows(maxdepth) * 8);
+}
+struct EncScratch {
+    uint32_t *cnt;    // 128 words per block
+    uint64_t *rows;   // the groups
+    uint32_t rec_rows;
+    GRK_HD uint64_t *group(uint32_t g) const { return rows + (uint64_t)g * 64 * rec_rows; }
+};
+GRK_HD EncScratch enc_scratch(void *base, uint32_t n, uint32_t maxdepth) {
+    const uint32_t n64 = (n + 63) & ~63u;
+    return EncScratch{(uint32_t *)base, (uint64_t *)((uint8_t *)base + (uint64_t)n64 * 128 * 4), t1e_rec_rows(maxdepth)};
+}
 
 // ---- lane-interleaved scratch (decoder) ----
 // The 64 blocks of a decoder wavefront (a "group") share one region of

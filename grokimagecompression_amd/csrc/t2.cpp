@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 
@@ -909,6 +910,12 @@ void probe_plan(CodingParams &cp, TileEnc &te, uint32_t max_layers, RateProbe &r
     rp.layers = max_layers;
 }
 
+// UB_NONE: no header bound (a block above its band's bit-planes; header_bits_ub).
+constexpr uint32_t UB_NONE = 1u << 24;
+#ifdef GRKGPU_CHECK_HEADER_UB
+std::atomic<uint64_t> g_ub_checks{0}, g_ub_viol{0};
+#endif
+
 // the packets of one precinct, in layer order: header and body bytes
 void probe_precinct(CodingParams &cp, TileEnc &te, RateProbe &rp, uint32_t p) {
     const uint32_t L = cp.numlayers;
@@ -930,6 +937,13 @@ void probe_precinct(CodingParams &cp, TileEnc &te, RateProbe &rp, uint32_t p) {
         }
         rp.hbytes[rp.pos[q]] = w.bytes;
         rp.dbytes[rp.pos[q]] = d;
+#ifdef GRKGPU_CHECK_HEADER_UB
+        // the bound body_fits takes for this packet (header_bits_ub summed per precinct)
+        if (rp.layers == 1 && rp.body_exact && !(cp.csty & (CSTY_SOP | CSTY_EPH)) && rp.prec_bits[p] < (int64_t)UB_NONE) {
+            ++g_ub_checks;
+            if ((uint64_t)w.bytes > (uint64_t)(1 + rp.prec_bits[p]) / 7 + 2) ++g_ub_viol;
+        }
+#endif
     }
 }
 
@@ -1118,8 +1132,6 @@ uint32_t feasible_cumul(const EncCblkState &s, const EncPass *P, uint32_t thresh
 // (packet_header with incl_cur = 0, numlenbits = 3): the inclusion tag tree
 // at threshold 1 emits at most one bit per node of the leaf's path, the
 // missing-MSB tree at most its value plus one per node, the rest exactly.
-// UB_NONE: no bound (a block above its band's bit-planes).
-constexpr uint32_t UB_NONE = 1u << 24;
 uint32_t header_bits_ub(const RateProbe &rp, size_t i, const EncCblkState &s, const EncLayer &ly, const EncPass *P) {
     uint32_t bits = rp.lev[i];
     if (!ly.numpasses) return bits;
@@ -1549,6 +1561,10 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
 }
 
 }  // namespace
+#ifdef GRKGPU_CHECK_HEADER_UB
+uint64_t header_ub_checks() { return g_ub_checks.load(); }
+uint64_t header_ub_violations() { return g_ub_viol.load(); }
+#endif
 
 bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st) {
     te.distolayer.assign(cp.numlayers + 1, 0.0);

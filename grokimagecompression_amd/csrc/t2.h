@@ -112,6 +112,13 @@ struct RateStats {
     double form_ms = 0, sim_ms = 0;
 };
 bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st = nullptr);
+#ifdef GRKGPU_CHECK_HEADER_UB
+// checked builds (tests/cpp/pcrd_bench.cpp): every simulated first-layer
+// packet of a single-layer search is compared with the header bound the
+// body_fits shortcut relies on; checks made / packets above their bound
+uint64_t header_ub_checks();
+uint64_t header_ub_violations();
+#endif
 
 // distortion weight of a pass (t1_getwmsedec, t1.cpp:912-930)
 double t1_wmsedec(int32_t nmsedec, uint32_t compno, uint32_t level, uint32_t orient, int32_t bpno, uint32_t qmfbid,

@@ -505,11 +505,11 @@ typedef struct {
     uint32_t pad;
 } grkgpu_dec_block;
 
-/* scratch: >= nblocks * grkgpu_t1_scratch_bytes() device bytes for encode;
- * decode: >= (nblocks rounded up to a multiple of 64) *
- * grkgpu_t1_scratch_bytes() (the decoder keeps the state of 64 blocks
- * interleaved), and every segment at most GRKGPU_T1_MAX_SEG bytes (w*h*4 + 64
- * for a 64x64 block, the encoder's slab bound). */
+/* scratch: >= (nblocks rounded up to a multiple of 64) *
+ * grkgpu_t1_scratch_bytes() device bytes, encode and decode (both keep the
+ * rows of 64 blocks interleaved); decode: every segment at most
+ * GRKGPU_T1_MAX_SEG bytes (w*h*4 + 64 for a 64x64 block, the encoder's slab
+ * bound). */
 #define GRKGPU_T1_MAX_SEG (64 * 64 * 4 + 64)
 size_t grkgpu_t1_scratch_bytes(void);
 int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,

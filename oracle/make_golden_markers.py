@@ -220,6 +220,30 @@ def case_tp_cod_copy(tmp):
     return write(main, tps), None
 
 
+def case_tp_cod_conflict(tmp):
+    """Coding parameters that change in a later tile-part (the standard allows
+    COD / QCD only in a tile's first tile-part; the reference reads them from
+    any tile-part header, warns about a second COD and lets the last one win,
+    j2k.cpp:3816-3825, since a tile's packets are parsed only after all its
+    tile-parts, j2k.cpp:1136-1224).  Tile 0's second tile-part repeats the COD
+    with the MCT switched off; tile 1's last tile-part repeats the QCD with
+    other step-size mantissas (same exponents, so the packets parse alike)."""
+    img = synth(96, 160, 3, 12, 306)
+    main, tps = parse(enc(img, 12, ["-I", "-t", "96,96", "-u", "R", "-n", "3", "-r", "10"], tmp))
+    cod = bytearray(find(main, COD)[0])
+    assert cod[4] == 1
+    cod[4] = 0
+    qcd = bytearray(find(main, QCD)[0])
+    for o in range(1, len(qcd) - 1, 2):  # SPqcd: expn << 11 | mant
+        qcd[o + 1] ^= 0x55
+    t0 = [tp for tp in tps if tp["isot"] == 0]
+    t1 = [tp for tp in tps if tp["isot"] == 1]
+    assert len(t0) >= 2 and len(t1) >= 2
+    t0[1]["hdr"] = [(COD, bytes(cod))] + t0[1]["hdr"]
+    t1[-1]["hdr"] = [(QCD, bytes(qcd))] + t1[-1]["hdr"]
+    return write(main, tps), None
+
+
 def case_tile_rgn(tmp):
     """ROI shift carried by tile 1's header only (main RGN removed): tile 0
     decodes without the shift it was coded with, as the reference does."""
@@ -358,7 +382,7 @@ def case_mixed_cblksty(tmp):
 
 
 CASES = [("tile_cod", case_tile_cod), ("main_coc", case_main_coc), ("tile_coc", case_tile_coc),
-         ("tp_cod_copy", case_tp_cod_copy), ("tile_rgn", case_tile_rgn), ("ppt", case_ppt), ("ppm", case_ppm), ("ppt_tparts", case_ppt_tparts),
+         ("tp_cod_copy", case_tp_cod_copy), ("tp_cod_conflict", case_tp_cod_conflict), ("tile_rgn", case_tile_rgn), ("ppt", case_ppt), ("ppm", case_ppm), ("ppt_tparts", case_ppt_tparts),
          ("ppm_1tile", case_ppm_1tile), ("mixed_wavelet", case_mixed_wavelet), ("siqnt", case_siqnt),
          ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod), ("mixed_cblksty", case_mixed_cblksty)]
 

@@ -7,7 +7,12 @@
 // (e.g. before / after a change) can be compared on the same inputs.
 //
 //   g++ -O2 -std=c++17 -I<csrc> pcrd_bench.cpp <csrc>/t2.cpp <csrc>/codestream.cpp -lpthread
-//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps] [slopes 0|1]
+//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps] [slopes 0|1] [terms 0|1|2]
+// terms: codeword segment ends -- 0 the last pass only, 1 every pass (TERMALL),
+// 2 the BYPASS pattern (passes 10, then the raw MRP and the cleanup of every
+// later plane).  Built with -DGRKGPU_CHECK_HEADER_UB it also prints how many
+// simulated first-layer packets were checked against the header bound of
+// t2.cpp's body_fits shortcut, and how many exceeded it (must be 0).
 #include <float.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -26,6 +31,7 @@ int main(int argc, char **argv) {
     const uint32_t L = argc > 4 ? (uint32_t)atoi(argv[4]) : 1;
     const int reps = argc > 5 ? atoi(argv[5]) : 3;
     const bool slopes = argc > 6 && atoi(argv[6]) != 0;  // per-block slope extremes precomputed
+    const int terms = argc > 7 ? atoi(argv[7]) : 0;
     CodingParams cp;
     cp.numcomps = 3;
     cp.image = {0, 0, 4096, 2160};
@@ -84,7 +90,8 @@ int main(int argc, char **argv) {
                             p.rate = rate;
                             dd += std::ldexp(U(rng) + 0.05, 2 * (int)(s.numbps - plane)) * (1 + r);
                             p.dd = dd;
-                            p.term = k + 1 == s.numpasses;
+                            p.term = k + 1 == s.numpasses || terms == 1 ||
+                                     (terms == 2 && (k == 9 || (k > 9 && (k - 10) % 3 != 0)));
                             passes.push_back(p);
                         }
                         // the slope range codec.cpp's pass-record fill stores (TileEnc::slopes)
@@ -137,5 +144,9 @@ int main(int argc, char **argv) {
                    (unsigned long long)rs.evals, (unsigned long long)rs.sims, rs.form_ms, rs.sim_ms);
     }
     printf("digest %016llx best_ms %.3f\n", (unsigned long long)digest, best);
+#ifdef GRKGPU_CHECK_HEADER_UB
+    printf("header_ub checks %llu violations %llu\n", (unsigned long long)header_ub_checks(),
+           (unsigned long long)header_ub_violations());
+#endif
     return 0;
 }

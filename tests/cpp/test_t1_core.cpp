@@ -53,12 +53,14 @@ int main(int argc, char **argv) {
             uint32_t lnb = t1_prep_serial(coef.data(), w, w, h, qmfbid, inv_step, scr.st, scr.pa);
             uint32_t cx[32];
             t1_prep_above(h, lnb, scr.pa, scr.pb);
-            const uint32_t slot = sym_slot_bytes(w, h), sb = sym_stream_bytes(w, h);
+            const uint32_t slot = sym_slot_bytes(w, h);
             std::vector<uint32_t> sym((size_t)(lnb ? lnb : 1) * slot / 4 + 16, 0);
+            uint64_t tmp[128];
             for (uint32_t p = 0; p < lnb; ++p) {
                 uint32_t *base = sym.data() + (size_t)p * slot / 4;
-                t1_model_plane(w, h, orient, scr.pa + p * 64, scr.pb + p * 64, p + 1 < lnb ? scr.pb + (p + 1) * 64 : nullptr,
-                               scr.st.neg, (uint64_t *)(base + sb / 4), sc, base, scr.cnt + p * 4);
+                const uint64_t *ref = p + 1 < lnb ? scr.pb + (p + 1) * 64 : scr.pb;
+                t1_model_plane<const uint64_t *, uint64_t *>(w, h, orient, scr.pa + p * 64, scr.pb + p * 64, ref,
+                                                             p + 1 < lnb, scr.st.neg, tmp, sc, base, scr.cnt + p * 4);
             }
             std::vector<uint32_t> sout(w * h * 2 + 64, 0);
             uint32_t srate[100], slen = 0;

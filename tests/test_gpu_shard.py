@@ -208,3 +208,28 @@ def test_view_outlives_later_compress():
     assert v3.tobytes() == ref_big
     del v3, sl
     gc.collect()
+
+
+def test_views_held_across_compresses_reuse_spares():
+    """A caller keeping a rolling window of live views: every buffer given back
+    while the context already has one becomes a spare that a later compress
+    reuses (no fresh pinned buffer per call) -- every view keeps its
+    own bytes throughout."""
+    import gc
+    import grokimagecompression_amd as grk
+    codec = grk.Codec(0)
+    imgs = [synth.synth_image(64 + 40 * k, 80 + 30 * k, 3, 12, 10 + k) for k in range(3)]
+    refs = [codec.compress(im, 12) for im in imgs]
+    live = []
+    for it in range(12):
+        k = it % 3
+        live.append((k, codec.compress(imgs[k], 12, view=True)))
+        if len(live) > 3:
+            live.pop(0)
+            gc.collect()
+        for kk, v in live:
+            assert v.tobytes() == refs[kk], (it, kk)
+    del live
+    gc.collect()
+    assert codec.compress(imgs[2], 12, view=True).tobytes() == refs[2]
+    codec.close()

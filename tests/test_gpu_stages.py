@@ -74,7 +74,7 @@ def _gpu_encode(cases, with_distortion):
     t_blocks = torch.from_numpy(eb.view(np.uint8)).to(dev)
     t_out = torch.zeros(16 + n * (MAX_SEG + 16), dtype=torch.uint8, device=dev)
     t_res = torch.zeros(n * ENC_RESULT.itemsize, dtype=torch.uint8, device=dev)
-    t_scr = torch.empty(n * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
+    t_scr = torch.empty((n + 63) // 64 * 64 * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream(0).cuda_stream)
     grk._check(L.grkgpu_t1_encode_blocks(t_blocks.data_ptr(), n, t_coef.data_ptr(), t_scr.data_ptr(),
                                          t_out.data_ptr(), t_res.data_ptr(), with_distortion, s))

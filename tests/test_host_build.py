@@ -85,3 +85,25 @@ def test_pcrd_incremental_probes_match_full_evaluation(tmp_path):
             r = subprocess.run([str(exe), str(algo), budget, str(seed), str(layers), "1", slopes], capture_output=True,
                                text=True, check=True)
             assert "digest %s" % digest in r.stdout, (algo, budget, seed, layers, slopes, r.stdout)
+
+
+def test_pcrd_header_bound_holds(tmp_path):
+    """The body_fits shortcut of the rate allocator (t2.cpp) skips a probe's
+    packet simulation when the code-block bytes plus a bound on every packet
+    header fit the budget; a checked build compares every simulated
+    first-layer packet of a single-layer search with that bound:
+    none may exceed it -- with one codeword segment per block, with TERMALL
+    (a length per pass) and with BYPASS's segment pattern."""
+    exe = tmp_path / "pcrd_bench_checked"
+    c = os.path.join(ROOT, "grokimagecompression_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-DGRKGPU_CHECK_HEADER_UB", "-I" + c, "-o", str(exe),
+                    os.path.join(ROOT, "tests/cpp/pcrd_bench.cpp"), os.path.join(c, "t2.cpp"),
+                    os.path.join(c, "codestream.cpp"), "-lpthread"], check=True)
+    for algo in ("0", "1"):
+        for budget in ("1.29e6", "4e5", "3e6"):
+            for terms in ("0", "1", "2"):
+                r = subprocess.run([str(exe), algo, budget, "1", "1", "1", "1", terms], capture_output=True, text=True,
+                                   check=True)
+                m = re.search(r"header_ub checks (\d+) violations (\d+)", r.stdout)
+                assert m, r.stdout
+                assert int(m.group(1)) > 0 and int(m.group(2)) == 0, (algo, budget, terms, r.stdout)
