@@ -295,14 +295,16 @@ def main():
                         "inside the timed region"}
 
     # roofline: the 9/7 DWT of the frame, measured alone after the timed
-    # region on one context, forward (encode) and inverse (decode).  Each
-    # launch's device time comes from an event pair around it on the codec
-    # stream (grkgpu_set_launch_timing), mean of 5 encodes / decodes after one
-    # warm-up; its algorithmic bytes are 8 B per sample of every level it
-    # computes (B_DWT split per launch).  frac = B_DWT over the
-    # SUM of the frame's per-launch means (the figure a rocprofv3 kernel
-    # summary of the same launches reproduces: profiles/r04*_kernel_stats*),
-    # peak 8 TB/s; span_us = events around the whole level sequence.
+    # region on one context, forward (encode) and inverse (decode).  frac =
+    # B_DWT (8 B per sample of every level) over span_us, the
+    # device time of the frame's whole level sequence: HIP events on the codec
+    # stream right before its first launch and after its last, nothing else
+    # between them (mean of 5 encodes / decodes after one warm-up), peak 8
+    # TB/s.  The per-launch breakdown comes from 5 more runs with an event
+    # after every launch (grkgpu_set_launch_timing; consecutive launches share
+    # an event); those events add ~1-5 us per launch, so their sum (dwt_us)
+    # stands above both span_us and a rocprofv3 kernel summary of the same
+    # launches (scripts/roofline_check.py, profiles/r05*/roofline_check.txt).
     bdwt = dwt_bytes(H, W, C)
     torch.cuda.synchronize()
     p97 = grk.CParams.make(irreversible=True)
@@ -349,7 +351,7 @@ def main():
     launches, ilaunches, span_us, ispan_us = measure(p97)
     dwt_us = sum(x["us"] for x in launches)
     idwt_us = sum(x["us"] for x in ilaunches)
-    achieved = bdwt / (dwt_us * 1e-6) / 1e9
+    achieved = bdwt / (span_us * 1e-6) / 1e9
     traffic = traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "dwt_pmc_latest.json")
     # the PMC passes (scripts/pmc_bench.sh) profile the default 8K workload only
@@ -366,16 +368,17 @@ def main():
                 "traffic_vs_floor": round(traffic / floor, 4) if traffic else None,
                 "algorithmic_bytes": bdwt, "dwt_us": round(dwt_us, 2),
                 "span_us": round(span_us, 2), "launches": launches,
-                "measured": "sum of the frame's per-launch device times (HIP events on the codec stream before the "
-                            "first DWT launch and after each one, so consecutive launches share an event; mean of 5 "
-                            "lone 9/7 encodes after the timed region); traffic = PMC bytes (FETCH_SIZE x 2 + "
+                "measured": "span_us = device time of the frame's forward level sequence (HIP events on the codec "
+                            "stream before its first launch and after its last; mean of 5 lone 9/7 encodes after the "
+                            "timed region); launches[].us from 5 more encodes with an event after every launch "
+                            "(their sum dwt_us carries the extra events' overhead); traffic = PMC bytes (FETCH_SIZE x 2 + "
                             "WRITE_SIZE) of the same launches (profiles/dwt_pmc_latest.json, source %s); "
                             "traffic_fused_floor = 8 B per sample of each launch's first level (its input read and "
                             "its outputs written once)" % traffic_src,
                 "inverse": {"kernel": "inverse 9/7 DWT of the frame (decode): " +
                                       " + ".join(x["kernel"] for x in ilaunches),
-                            "achieved": round(bdwt / (idwt_us * 1e-6) / 1e9, 1), "unit": "GB/s",
-                            "frac": round(bdwt / (idwt_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                            "achieved": round(bdwt / (ispan_us * 1e-6) / 1e9, 1), "unit": "GB/s",
+                            "frac": round(bdwt / (ispan_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                             "algorithmic_bytes": bdwt, "dwt_us": round(idwt_us, 2),
                             "span_us": round(ispan_us, 2), "launches": ilaunches}}
     if args.workload == "8k":
@@ -385,12 +388,12 @@ def main():
         f53, i53 = sum(x["us"] for x in l53), sum(x["us"] for x in il53)
         roofline["r53"] = {
             "forward": {"kernel": " + ".join(x["kernel"] for x in l53), "dwt_us": round(f53, 2),
-                        "achieved": round(bdwt / (f53 * 1e-6) / 1e9, 1), "unit": "GB/s",
-                        "frac": round(bdwt / (f53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(s53, 2),
+                        "achieved": round(bdwt / (s53 * 1e-6) / 1e9, 1), "unit": "GB/s",
+                        "frac": round(bdwt / (s53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(s53, 2),
                         "launches": l53},
             "inverse": {"kernel": " + ".join(x["kernel"] for x in il53), "dwt_us": round(i53, 2),
-                        "achieved": round(bdwt / (i53 * 1e-6) / 1e9, 1), "unit": "GB/s",
-                        "frac": round(bdwt / (i53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(is53, 2),
+                        "achieved": round(bdwt / (is53 * 1e-6) / 1e9, 1), "unit": "GB/s",
+                        "frac": round(bdwt / (is53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(is53, 2),
                         "launches": il53},
             "algorithmic_bytes": bdwt}
 

@@ -33,8 +33,9 @@ def test_bench_line_keeps_the_contract():
         assert k in rf, k
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
-    # frac = B_DWT over the sum of the frame's per-launch device times
-    assert abs(rf["algorithmic_bytes"] / (rf["dwt_us"] * 1e-6) / 1e9 - rf["achieved"]) < 0.5
+    # frac = B_DWT over the device time of the frame's level sequence (span_us);
+    # the per-launch breakdown sums to dwt_us
+    assert abs(rf["algorithmic_bytes"] / (rf["span_us"] * 1e-6) / 1e9 - rf["achieved"]) < 0.5
     assert abs(sum(x["us"] for x in rf["launches"]) - rf["dwt_us"]) < 0.05
     inv = rf["inverse"]
     assert 0 < inv["frac"] < 1 and inv["launches"] and sum(x["algorithmic_bytes"] for x in inv["launches"]) == \
