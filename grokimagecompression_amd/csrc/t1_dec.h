@@ -180,9 +180,16 @@ GRK_HD uint32_t nib4(const uint64_t *r4, uint32_t sh) {
            spread8((uint32_t)(r4[2] >> sh) & 0xFFu) << 2 | spread8((uint32_t)(r4[3] >> sh) & 0xFFu) << 3;
 }
 
-template <class D>
+template <bool REG, class D>
 GRK_HD void d3_mrp_stripe(D &d, uint32_t *cxw, const DecTables &T, const uint64_t *e, const uint64_t *nb,
                           const uint64_t *ref, uint64_t *bit, uint64_t mem) {
+    // REG: the pass's three contexts (t1.cpp dec_refpass: 14 + (refined before
+    // ? 2 : a significant neighbour)) live in registers for the stripe -- no
+    // LDS round trip on the decision chain: lone 8K 9/7 decode T1 30.4 / 31.3
+    // -> 29.4 / 29.2 ms, the 16-frame batch unchanged (3438 / 3514 vs 3452 /
+    // 3486 Mpixels/s alternating, profiles/r05/t1_mrp_reg_ab.txt)
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+    if constexpr (REG) { w0 = cxw[CX_MAG]; w1 = cxw[CX_MAG + 1]; w2 = cxw[CX_MAG + 2]; }
     for (uint32_t g = 0; g < 8; ++g) {
         const uint32_t sh = 8 * g;
         if (!((mem >> sh) & 0xFFu)) continue;
@@ -193,14 +200,23 @@ GRK_HD void d3_mrp_stripe(D &d, uint32_t *cxw, const DecTables &T, const uint64_
         while (E) {
             const uint32_t pos = (uint32_t)__builtin_ctz(E);
             E &= E - 1;
-            const uint32_t cx = CX_MAG + (((R >> pos) & 1) ? 2u : (N >> pos) & 1);  // t1.cpp dec_refpass contexts
-            res |= d.decode(cxw, T.mq, cx) << pos;
+            const uint32_t k = ((R >> pos) & 1) ? 2u : (N >> pos) & 1;
+            if constexpr (REG) {
+                uint32_t wd = k == 2 ? w2 : k == 1 ? w1 : w0;
+                res |= d.decode_reg(wd, T.mq, CX_MAG + k) << pos;
+                w0 = k == 0 ? wd : w0;
+                w1 = k == 1 ? wd : w1;
+                w2 = k == 2 ? wd : w2;
+            } else {
+                res |= d.decode(cxw, T.mq, CX_MAG + k) << pos;
+            }
         }
         if (res) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) bit[i] |= (uint64_t)unspread8(res >> i) << sh;
         }
     }
+    if constexpr (REG) { cxw[CX_MAG] = w0; cxw[CX_MAG + 1] = w1; cxw[CX_MAG + 2] = w2; }
 }
 
 // Codeword segments of a block: a single one (NoSegs) or a cursor that
@@ -219,7 +235,7 @@ struct NoSegs {
 // ST / RP: the block state and the bit-plane row pointers -- plain arrays
 // (BlockState, uint64_t *: host tests) or the GPU decoder's lane-interleaved
 // rows (kernels.hip LState / LRow, t1_lane.h).
-template <class D, class S = NoSegs, class ST = BlockState, class RP = uint64_t *>
+template <class D, class S = NoSegs, class ST = BlockState, class RP = uint64_t *, bool MRPREG = true>
 GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t w, uint32_t h, ST &st,
                              const DecTables &T, uint32_t *cxw, RP sigafter, RP refbit,
                              uint32_t sty = 0, S segs = S(), uint32_t roishift = 0) {
@@ -263,7 +279,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
                     nb[i] = dil(s.sig[i]) | dil(s.sig[i + 2]) | (sg << 1) | (sg >> 1);
                     mem |= e[i];
                 }
-                if (mem) d3_mrp_stripe(d, cxw, T, e, nb, s.ref, s.bit, mem);
+                if (mem) d3_mrp_stripe<MRPREG>(d, cxw, T, e, nb, s.ref, s.bit, mem);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     st.ref[k + 1 + i] = s.ref[i] | e[i];  // every refined sample is now "refined once"

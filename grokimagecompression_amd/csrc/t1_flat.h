@@ -225,7 +225,31 @@ struct BitDecT {
         if constexpr (LAZY) {
             if (raw) return rawbit();
         }
-        const uint32_t wd = cxw[cx];
+        uint32_t wd = cxw[cx];
+        const uint32_t bit = step(wd, tab);
+        cxw[cx] = wd;  // unconditional LDS write: no branch
+#ifdef T1_TRACE
+        T1_TRACE(cx, bit, A, C >> 16);
+#endif
+        return bit;
+    }
+    // the same decision with the context word in a register (the magnitude
+    // refinement keeps its three contexts in registers for a stripe: no LDS
+    // round trip on its decision chain)
+    GRK_HD uint32_t decode_reg(uint32_t &wd, const uint32_t *tab, uint32_t cx) {
+        if constexpr (LAZY) {
+            if (raw) return rawbit();
+        }
+        const uint32_t bit = step(wd, tab);
+#ifdef T1_TRACE
+        T1_TRACE(cx, bit, A, C >> 16);
+#else
+        (void)cx;
+#endif
+        return bit;
+    }
+    // one MQ decision with context word wd (updated in place)
+    GRK_HD uint32_t step(uint32_t &wd, const uint32_t *tab) {
         const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
         uint32_t a = A - qe;
         const bool lo = (C >> 16) < qe;
@@ -245,10 +269,7 @@ struct BitDecT {
         if (cq < c1) { C += 1u << (16 + c1 - cq); next_carry(); }  // carry event (see Unstuff)
         consumed = c1;
         if (bits.NB < 32) refill();
-        cxw[cx] = keep ? wd : (tw | (nmps << 31));  // unconditional LDS write: no branch
-#ifdef T1_TRACE
-        T1_TRACE(cx, mps ^ (uint32_t)lps, A, C >> 16);
-#endif
+        wd = keep ? wd : (tw | (nmps << 31));
         return mps ^ (uint32_t)lps;
     }
 };
@@ -282,7 +303,7 @@ struct SegCursor {
 // v5: the nested pass / stripe / column walk (lanes of a wavefront stay
 // converged on the pass structure) fed by the unstuffed bit stream.
 // ring / rsh: the lane's word ring (FlatBits).
-template <class ST = BlockState, class RP = uint64_t *>
+template <class ST = BlockState, class RP = uint64_t *, bool MRPREG = true>
 GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t *carries, uint32_t numpasses,
                          uint32_t numbps, uint32_t w, uint32_t h, ST &st, const DecTables &T, uint32_t *cxw,
                          RP sa, RP rb, uint32_t *ring, uint32_t rsh) {
@@ -291,7 +312,7 @@ GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t 
     BitDec d;
     d.set_ring(ring, rsh);
     d.init(words, nwords, carries);
-    t1_decode_passes(d, numpasses, numbps, w, h, st, T, cxw, sa, rb);
+    t1_decode_passes<BitDec, NoSegs, ST, RP, MRPREG>(d, numpasses, numbps, w, h, st, T, cxw, sa, rb);
 }
 
 }  // namespace grkgpu

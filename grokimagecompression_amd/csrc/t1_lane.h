@@ -555,18 +555,23 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
     uint64_t U = 0;  // post-SPP significance of row k-1
     for (uint32_t k = 0; k < h; k += 4) {
         const uint32_t nr = h - k < 4 ? h - k : 4;
-        uint64_t pre[4], bit[4], C[4], post[4], ng[6];
+        // Rows are read only where the stripe needs them (the lanes that skip
+        // a read fetch nothing): the plane's bits where a sample can become
+        // significant -- a candidate, and a significant sample in or next to
+        // the stripe to start the propagation -- and the sign rows where one
+        // did.
+        uint64_t pre[4], bit[4] = {0, 0, 0, 0}, C[4], post[4], ng[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             pre[r] = ldrow(above, (int32_t)(k + r), h);
-            bit[r] = ldrow(bitp, (int32_t)(k + r), h);
             C[r] = (uint32_t)r < nr ? ~pre[r] & wm : 0;
             post[r] = pre[r];
         }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
-        if (vsc) ng[5] = 0;
         const uint64_t D = vsc ? 0 : ldrow(above, (int32_t)(k + 4), h);
+        if ((C[0] | C[1] | C[2] | C[3]) && (pre[0] | pre[1] | pre[2] | pre[3] | U | D)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+        }
         // fixed point of the causal significance recurrence; the W->E chain
         // inside a row is resolved with one carry-propagating add
         for (int it = 0; it < 300; ++it) {
@@ -584,6 +589,11 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
                 post[r] = np;
             }
             if (!changed) break;
+        }
+        if ((post[0] ^ pre[0]) | (post[1] ^ pre[1]) | (post[2] ^ pre[2]) | (post[3] ^ pre[3])) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
+            if (vsc) ng[5] = 0;
         }
         uint64_t coded[4];
         Ctx4 cz[4];
@@ -630,17 +640,19 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
     for (uint32_t k = 0; k < h; k += 4) {
         uint64_t m[4], o0[4], o1[4], bit[4], sS[6];
 #pragma unroll
+        for (int r = 0; r < 4; ++r) m[r] = ldrow(above, (int32_t)(k + r), h);
+        uint64_t cols = m[0] | m[1] | m[2] | m[3];
+        if (!cols) continue;  // no member: nothing else of the stripe is read
+#pragma unroll
         for (int i = 0; i < 6; ++i) sS[i] = ldrow(postS, (int32_t)(k + i) - 1, h);
         if (vsc) sS[5] = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            m[r] = ldrow(above, (int32_t)(k + r), h);
             o1[r] = has_ref ? ldrow(ref, (int32_t)(k + r), h) : 0;
             bit[r] = ldrow(bitp, (int32_t)(k + r), h);
             const uint64_t nb = dil(sS[r]) | dil(sS[r + 2]) | (sS[r + 1] << 1) | (sS[r + 1] >> 1);
             o0[r] = nb & ~o1[r];
         }
-        uint64_t cols = m[0] | m[1] | m[2] | m[3];
         while (cols) {
             const uint32_t x = ctz64(cols);
             cols &= cols - 1;
@@ -662,17 +674,23 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
     U = 0;  // post-CUP significance of row k-1
     for (uint32_t k = 0; k < h; k += 4) {
         const uint32_t nr = h - k < 4 ? h - k : 4;
-        uint64_t sS[4], cand[4], bit[4], pc[4], ng[6];
+        uint64_t sS[4], cand[4], bit[4] = {0, 0, 0, 0}, pc[4], ng[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             sS[r] = ldrow(postS, (int32_t)(k + r), h);
-            bit[r] = ldrow(bitp, (int32_t)(k + r), h);
             cand[r] = (uint32_t)r < nr ? ~(sS[r] | ldrow(visS, (int32_t)(k + r), h)) & wm : 0;
-            pc[r] = sS[r] | (cand[r] & bit[r]);
+        }
+        if (cand[0] | cand[1] | cand[2] | cand[3]) {  // the bits of candidates, the signs of new significance
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bit[r] = ldrow(bitp, (int32_t)(k + r), h);
+            if ((cand[0] & bit[0]) | (cand[1] & bit[1]) | (cand[2] & bit[2]) | (cand[3] & bit[3])) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
+                if (vsc) ng[5] = 0;
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
-        if (vsc) ng[5] = 0;
+        for (int r = 0; r < 4; ++r) pc[r] = sS[r] | (cand[r] & bit[r]);
         const uint64_t D = vsc ? 0 : ldrow(postS, (int32_t)(k + 4), h);
         uint64_t agg = 0;
         if (nr == 4) {

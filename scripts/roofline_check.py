@@ -5,6 +5,9 @@ the run end with: 6 span-timed encodes (events around the level sequence
 only; the first is a warm-up), the encode whose stream the decode timing
 uses, 6 launch-timed encodes (an event after every launch; the first a
 warm-up), then the lone-frame T1 figure's encode.
+The inverse launches (k_dwt_inv per level, then k_dwt_inv01 for the last two)
+end with 6 span-timed decodes, 6 launch-timed decodes, then the lone-frame
+T1 figure's decode.
   python scripts/roofline_check.py PROF_DIR BENCH_JSON"""
 import glob
 import json
@@ -41,6 +44,16 @@ def main(d, bench):
     b = rl["algorithmic_bytes"]
     print("bench roofline frac %.4f (span); by rocprof kernel sum %.4f, by rocprof span %.4f"
           % (rl["frac"], b / (mean(sk) * 1e-6) / 8e12, b / (mean(ss) * 1e-6) / 8e12))
+    inv = rl["inverse"]
+    m = len(inv["launches"])
+    ifw = [(n_, s, e) for n_, s, e in rows if "k_dwt_inv<true" in n_ or "k_dwt_inv01<true" in n_]
+    n = m
+    ik, iss = enc(ifw[-12 * m:-7 * m])  # span-timed decodes 2..6
+    lk2, _ = enc(ifw[-6 * m:-m])         # launch-timed decodes 2..6
+    print("inverse 9/7 DWT of the frame (%d launches): bench span_us %.2f, rocprof kernel sum %.2f (first start to "
+          "last end %.2f); launch-timed: bench dwt_us %.2f, rocprof kernel sum %.2f"
+          % (m, inv["span_us"], mean(ik), mean(iss), inv["dwt_us"], mean(lk2)))
+    print("bench inverse frac %.4f (span); by rocprof kernel sum %.4f" % (inv["frac"], b / (mean(ik) * 1e-6) / 8e12))
 
 
 if __name__ == "__main__":
