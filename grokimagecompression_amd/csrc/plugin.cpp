@@ -437,12 +437,17 @@ int32_t encode_file(grkgpu_ctx *ctx, grkp_cparameters *params, const char *path,
 // the others' GPU work.  The host polls plugin_is_batch_complete and ends the
 // batch with plugin_stop_batch_encode / _decode.
 // Frames in flight per device: GRKGPU_PLUGIN_FRAMES (1 .. 64; the plugin ABI
-// has no parameter for it), default 16 -- the concurrency the bench measured
-// best for the 8K and the cinema frames (profiles/r03_concurrency_sweep.txt,
-// profiles/r04z/c5_concurrency_sweep.txt).
+// has no parameter for it), default 8 -- measured on this route itself
+// (scripts/plugin_batch_sweep.py, 24 DCI 4K cinema frames through
+// grk_compress's directory mode, two rounds: 4 -> 72 / 70, 8 -> 67 / 82, 16 ->
+// 58 / 61 Mpixels/s; profiles/r05/plugin_batch_sweep.txt): the host's own
+// per-frame work (PPM read, its rate control and Tier-2, the file write)
+// bounds the route, and more frames in flight only contend for its cores.
+// (The library's own frame batch runs best at 16: profiles/r03_concurrency_
+// sweep.txt, profiles/r04z/c5_concurrency_sweep.txt.)
 static int frames_per_device() {
     const char *e = getenv("GRKGPU_PLUGIN_FRAMES");
-    const int v = e ? atoi(e) : 16;
+    const int v = e ? atoi(e) : 8;
     return v < 1 ? 1 : v > 64 ? 64 : v;
 }
 
