@@ -1169,8 +1169,8 @@ int dwt_inv01_tiles(int irrev, int rw_b, int rh_b, int casx_b, int casy_b) {
     return ((rw_b + casx_b + cx - 1) / cx) * ((rh_b + casy_b + cy - 1) / cy);
 }
 
-template <bool IRREV, int NA>
-__global__ __launch_bounds__(64 * DWT_WAVES) void k_dwt_inv01(const DwtJob *__restrict__ jobsA,
+template <bool IRREV, int NA, int WPE = 1>
+__global__ __launch_bounds__(64 * DWT_WAVES) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dwt_inv01(const DwtJob *__restrict__ jobsA,
                                                              const DwtJob *__restrict__ jobsB, int lay) {
     using G = I01Geo<IRREV, NA>;
     constexpr int H = G::H, CW = G::CW;
@@ -1291,7 +1291,12 @@ hipError_t launch_dwt_inv01(const DwtJob *jobsA, const DwtJob *jobsB, uint32_t n
         if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 4>), g, b, 0, s, jobsA, jobsB, lay);
         else hipLaunchKernelGGL((k_dwt_inv01<false, 4>), g, b, 0, s, jobsA, jobsB, lay);
     } else {
-        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 2>), g, b, 0, s, jobsA, jobsB, lay);
+        // 9/7 held to 80 VGPRs: 6 wavefronts per SIMD instead of 5 (36 B of
+        // spills): 183.6-184.7 -> 179.5-182.3 us on the 8K frame, three
+        // alternating rounds (profiles/r05/dwt_occupancy_ab.txt); the 5/3 pair
+        // at 128 VGPRs (4 instead of 3) and the 5/3 DC shift + RCT level 0 at 5
+        // per SIMD (96 VGPRs, spilled) gained nothing / lost 45 %
+        if (irrev) hipLaunchKernelGGL((k_dwt_inv01<true, 2, 6>), g, b, 0, s, jobsA, jobsB, lay);
         else hipLaunchKernelGGL((k_dwt_inv01<false, 2>), g, b, 0, s, jobsA, jobsB, lay);
     }
     return hipGetLastError();
