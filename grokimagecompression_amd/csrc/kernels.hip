@@ -492,6 +492,119 @@ __global__ __launch_bounds__(64) void k_t1_unstuff(const DecBlock *__restrict__ 
     unstuff_segment(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words));
 }
 
+// The same pre-pass with one wavefront per code-block segment: 64 bytes per
+// step, one per lane.  A byte's bit count (7 after a 0xFF, else 8) and its
+// bit position in the output stream come from a wave prefix sum, its bits are
+// ORed into the step's words in LDS (a byte may straddle two words), the
+// completed words leave as one coalesced store, the partial last one stays
+// for the next step; a marker (0xFF then > 0x8F) ends the stream at the first
+// lane holding one, and carry events are compacted by ballot in stream
+// order.  Output identical to unstuff_segment's.  The lane-per-block pass runs
+// 64 blocks' serial byte loops per wavefront -- ~390 wavefronts for a whole
+// 8K frame, a long dependent chain per lane: the shorter chain for a call
+// alone on the GPU, the fewer instructions for a batch (launch_t1_decode).
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t *tot) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+    }
+    *tot = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ void unstuff_segment_wave(const uint8_t *__restrict__ data, uint64_t data_off, uint32_t len,
+                                     uint32_t *__restrict__ region, uint32_t *wbuf, uint32_t lane) {
+    uint32_t *words = region + 4, *carries = words + unstuff_word_cap(len);
+    uint32_t bitpos = 0, nc = 0;  // bits emitted, carry events written
+    bool pff_in = false;          // the byte before this step's first one is 0xFF
+    if (lane < 20) wbuf[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t base = 0; base < len; base += 64) {
+        const uint32_t j = base + lane;
+        const bool inb = j < len;
+        const uint32_t b = inb ? (uint32_t)data[data_off + j] : 0u;
+        const uint32_t prev = __shfl_up(b, 1, 64);
+        const bool pff = lane ? prev == 0xffu : pff_in;
+        const uint64_t mk = __ballot(inb && pff && b > 0x8fu);  // markers: the stream ends at the first
+        const uint32_t first = mk ? (uint32_t)__builtin_ctzll(mk) : 64u;
+        const bool valid = inb && lane < first;
+        const uint32_t nb = valid ? (pff ? 7u : 8u) : 0u;
+        uint32_t tot;
+        const uint32_t o = bitpos + wave_excl_scan(nb, lane, &tot);
+        // carry event: a stuffed byte's top bit (see Unstuff)
+        const bool ev = valid && pff && (b & 0x80u);
+        const uint64_t em = __ballot(ev);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+        if (ev) carries[nc + rank] = o - 1 + 17;
+        nc += (uint32_t)__builtin_popcountll(em);
+        // the byte's bits at stream bits [o, o + nb), MSB first; word index relative to this step's first
+        if (nb) {
+            const uint32_t v = b & (pff ? 0x7fu : 0xffu);
+            const uint32_t k = (o >> 5) - (bitpos >> 5), p = o & 31u, e = p + nb;
+            if (e <= 32) {
+                atomicOr(&wbuf[k], v << (32 - e));
+            } else {
+                atomicOr(&wbuf[k], v >> (e - 32));
+                atomicOr(&wbuf[k + 1], v << (64 - e));
+            }
+        }
+        // one wavefront's LDS operations complete in order; the fence keeps the
+        // compiler from moving the reads above the ORs (no workgroup barrier:
+        // the other wavefronts of the workgroup work on other blocks)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t end = bitpos + tot, done = (end >> 5) - (bitpos >> 5);  // completed words
+        uint32_t w = lane < 20 ? wbuf[lane] : 0u;
+        if (lane < done) words[(bitpos >> 5) + lane] = w;
+        // the partial word moves to slot 0, the rest is cleared
+        const uint32_t carry_w = __shfl(w, (int)done, 64);
+        if (lane < 20) wbuf[lane] = lane == 0 ? carry_w : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        bitpos = end;
+        pff_in = __shfl(b, 63, 64) == 0xffu;
+        if (mk) break;
+    }
+    // tail (Unstuff::tail): the pending bits, then 1-bits; a word of 1-bits
+    // when none is pending; then 1-bit words to a multiple of 4 and 8 more
+    const uint32_t nw0 = bitpos >> 5, pend = bitpos & 31u;
+    const uint32_t w0 = __shfl(lane < 20 ? wbuf[lane] : 0u, 0, 64);
+    const uint32_t tailw = pend ? (w0 | ((1u << (32 - pend)) - 1u)) : 0xffffffffu;
+    uint32_t nw = nw0 + 1;
+    nw += (4 - (nw & 3)) & 3;
+    if ((nw - nw0 - 1) == 0) nw += 4;  // the serial pass writes at least one 1-bit word after the tail
+    nw += 8;
+    for (uint32_t q = lane; nw0 + q < nw; q += 64) words[nw0 + q] = q == 0 ? tailw : 0xffffffffu;
+    if (lane == 0) {
+        carries[nc] = 0xffffffffu;
+        region[0] = nw;
+        region[1] = nc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_t1_unstuff_w(const DecBlock *__restrict__ blocks, uint32_t n,
+                                                     const uint8_t *__restrict__ data, uint32_t *__restrict__ ubuf,
+                                                     uint32_t fixed_words, const DecSeg *__restrict__ segs,
+                                                     const uint32_t *__restrict__ seg_first) {
+    __shared__ uint32_t s_w[4][20];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 4 + wv;
+    if (i >= n) return;
+    const DecBlock b = blocks[i];
+    if (b.len == 0 || b.numpasses == 0 || b.numbps == 0 || b.numbps > T1_MAX_DEC_BPS) return;
+    if (segs) {
+        for (uint32_t q = seg_first[i]; q < seg_first[i + 1]; ++q) {
+            const DecSeg sg = segs[q];
+            unstuff_segment_wave(data, sg.data_off, sg.len, ubuf + (size_t)sg.ub_off * 4, s_w[wv], lane);
+        }
+        return;
+    }
+    unstuff_segment_wave(data, b.data_off, b.len, ubuf + ub_region(b, i, fixed_words), s_w[wv], lane);
+}
+
 struct LState {
     LRow sig, neg, vis, ref;
 };
@@ -807,8 +920,18 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
                             int32_t *tiles, hipStream_t s, uint32_t *ubuf, uint32_t fixed_words, const DecSeg *segs,
                             const uint32_t *seg_first, uint32_t cblksty, const uint8_t *roi, uint32_t bpw_req) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
-                       seg_first);
+    // a call alone on the GPU (bpw_req: the lone packing) or a small one
+    // unstuffs a segment per wavefront: 1.37 ms -> 0.27 ms per 8K frame, lone
+    // decode T1 29.0 / 29.8 -> 28.1 / 27.5 ms; under 16 frames in flight the
+    // lane-per-block pass does the same work in fewer instructions, and the
+    // batch is issue-bound: 3529 / 3473 vs 3473 / 3415 Mpixels/s with the
+    // wavefront pass (profiles/r05/t1_unstuff_wave_ab.txt)
+    if (bpw_req || n <= 4096)
+        hipLaunchKernelGGL(k_t1_unstuff_w, dim3((n + 3) / 4), dim3(256), 0, s, blocks, n, data, ubuf, fixed_words, segs,
+                           seg_first);
+    else
+        hipLaunchKernelGGL(k_t1_unstuff, dim3((n + 63) / 64), dim3(64), 0, s, blocks, n, data, ubuf, fixed_words, segs,
+                           seg_first);
     const uint32_t bpw = dwt_options().t1_dec_bpw ? (uint32_t)dwt_options().t1_dec_bpw
                          : bpw_req                ? bpw_req
                                                   : t1_blocks_per_wave(n);
