@@ -282,9 +282,11 @@ __global__ __launch_bounds__(64) void k_t1_model(
 
 constexpr uint32_t MQ_CX_STRIDE = 21;  // LDS words per lane for the MQ encoder's context words
 
-// MQ coding, one lane per block (lane j codes block perm[j], or j).
-template <int LANES, int MINW = 1, bool LAZY = false>
-__global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
+// MQ coding, one lane per block (lane j codes block perm[j], or j).  WAVES
+// wavefronts per workgroup share the state table and the read-ahead slack
+// (CXS: context words per lane).
+template <int LANES, int MINW = 1, bool LAZY = false, int WAVES = 1, uint32_t CXS = MQ_CX_STRIDE>
+__global__ __launch_bounds__(LANES * WAVES, MINW) void k_t1_mq(const EncBlock *__restrict__ blocks, uint32_t n,
                                                  const uint32_t *__restrict__ cnt, const uint8_t *__restrict__ sym,
                                                  const uint64_t *__restrict__ sym_off, uint8_t *__restrict__ out,
                                                  EncResult *__restrict__ res, const uint32_t *__restrict__ perm,
@@ -292,14 +294,14 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     __shared__ uint32_t s_mq[48];
     // 19 context words per lane at an odd stride (no bank conflicts).  The
     // read-ahead of the symbol after a pass's last one may index up to 31
-    // (its value is never used): a lane's slots plus the tail slack keep it
-    // inside the array.  21 words per lane (not 32) keeps LDS from limiting
-    // the occupancy: 5.6 KB per 64-lane workgroup -> 7 wavefronts per SIMD.
-    __shared__ uint32_t s_cx[LANES * MQ_CX_STRIDE + 32];
-    for (uint32_t k = threadIdx.x; k < 47; k += LANES) s_mq[k] = c_mq_tab[k];
+    // (its value is never used): the next lane's slots, or for the last lane
+    // the tail slack, keep it inside the array.
+    __shared__ uint32_t s_cx[WAVES * LANES * CXS + 32];
+    for (uint32_t k = threadIdx.x; k < 47; k += LANES * WAVES) s_mq[k] = c_mq_tab[k];
     __syncthreads();
-    if (threadIdx.x >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
-    const uint32_t j = blockIdx.x * bpw + threadIdx.x;
+    const uint32_t lane = threadIdx.x % LANES;
+    if (lane >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
+    const uint32_t j = (blockIdx.x * WAVES + threadIdx.x / LANES) * bpw + lane;
     if (j >= n) return;
     const uint32_t i = perm ? perm[j] : j;
     const EncBlock b = blocks[i];
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(LANES, MINW) void k_t1_mq(const EncBlock *__restric
     const uint64_t off = sym_block_off(sym_off, i, &cap);
     uint32_t len;
     uint32_t np = t1_mq_block<LAZY>(r.numbps, (const uint32_t *)(sym + off), sym_slot_bytes(b.w, b.h) / 4, cnt + (size_t)i * 128, s_mq,
-                              s_cx + threadIdx.x * MQ_CX_STRIDE, (uint32_t *)(out + b.out_off), r.rate, &len, cblksty);
+                              s_cx + threadIdx.x * CXS, (uint32_t *)(out + b.out_off), r.rate, &len, cblksty);
     r.numpasses = np;
     r.len = len;
     uint32_t nsym = 0;
@@ -825,6 +827,7 @@ hipError_t launch_mct_inv_dcshift(const PlanePtrs &src, uint32_t sstride, uint32
 // per block, so throughput = resident blocks / block time: 64 lanes per
 // wavefront keep 4x more blocks resident per wave slot than 16.
 constexpr int MQ_LANES = 64;
+constexpr int MQ_WAVES = 4;  // wavefronts per MQ-coder workgroup
 // T1 decoder: 64 blocks (lanes) per wavefront, same reasoning (8K frame batch,
 // 12 frames in flight: 2.0-2.2 vs 1.25 Gpix/s with 16; a lone frame decodes
 // ~10% faster with 16).
@@ -876,12 +879,17 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
         hipLaunchKernelGGL(k_mq_order_scatter, dim3((n + 255) / 256), dim3(256), 0, s, key, n, hist, permw);
         perm = permw;
     }
+    // MQ_WAVES wavefronts per workgroup, 19 context words per lane: LDS no
+    // longer holds the coder at 7 wavefronts per SIMD (5.7 KB per single-
+    // wavefront workgroup); 8 per SIMD by registers and LDS: 8K batch 3519 /
+    // 3476 -> 3664 / 3577 Mpixels/s alternating (profiles/r05/t1_mq_wg_ab.txt)
+    const uint32_t nwv = (n + bpw - 1) / bpw, nwg = (nwv + MQ_WAVES - 1) / MQ_WAVES;
     if (cblksty & CBLKSTY_LAZY)
-        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           cnt, sym, sym_off, out, res, perm, cblksty, bpw);
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true, MQ_WAVES, 19>), dim3(nwg), dim3(MQ_LANES * MQ_WAVES), 0, s,
+                           blocks, n, cnt, sym, sym_off, out, res, perm, cblksty, bpw);
     else
-        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3((n + bpw - 1) / bpw), dim3(MQ_LANES), 0, s, blocks, n,
-                           cnt, sym, sym_off, out, res, perm, cblksty, bpw);
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false, MQ_WAVES, 19>), dim3(nwg), dim3(MQ_LANES * MQ_WAVES), 0, s,
+                           blocks, n, cnt, sym, sym_off, out, res, perm, cblksty, bpw);
     return hipGetLastError();
 }
 
