@@ -565,6 +565,44 @@ def test_large_config_hashes(codec, name):
     assert synth.image_sha256(d) == m["dec_sha256"]
 
 
+@pytest.mark.parametrize("name", ["C3_8k_rgb12_I", "C3_8k_rgb12"])
+def test_large_config_concurrent_calls(name):
+    """The same full-size configs through calls that overlap on the GPU (two
+    contexts on two threads): a call that is not alone takes the batch code
+    paths -- 64 blocks per coder wavefront, the lane-per-block unstuff pass --
+    and must give the reference's codestream and decoded image as well."""
+    import threading
+    import grokimagecompression_amd as grk
+    import torch
+    m = LARGE[name]
+    img, bits = _img(m)
+    p, off = grk.CParams.from_cli(m["args"])
+    t = torch.from_numpy(img).cuda()
+    codecs = [grk.Codec(0), grk.Codec(0)]
+    go = threading.Barrier(2)
+    errs = []
+
+    def run(c):
+        try:
+            go.wait()
+            for _ in range(2):
+                b = c.compress(t, bits, p, offset=off)
+                assert hashlib.sha256(b).hexdigest() == m["j2k_sha256"]
+                d = c.decompress(b)
+                assert synth.image_sha256(d) == m["dec_sha256"]
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(c,)) for c in codecs]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for c in codecs:
+        c.close()
+    assert not errs, errs
+
+
 def test_large_tiled_16k(codec):
     """C4: 16384^2 16-bit, 1024^2 tiles, 7 resolutions (256 tiles)."""
     import grokimagecompression_amd as grk
