@@ -245,6 +245,7 @@ __device__ __forceinline__ uint64_t sym_block_off(const uint64_t *sym_off, uint3
     return sym_off[i];
 }
 
+template <bool COND>
 __global__ __launch_bounds__(64) void k_t1_model(
     const EncBlock *__restrict__ blocks, uint32_t n, uint32_t maxdepth, uint8_t *__restrict__ scr,
     uint8_t *__restrict__ sym, const uint64_t *__restrict__ sym_off, EncResult *__restrict__ res, uint32_t cblksty) {
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(64) void k_t1_model(
     const LRow ref{gr, (d ? dr - T1E_DEPTH_ROWS + T1E_ABOVE : 0) * 512, lo}, negr{gr, T1E_NEG * 512, lo};
     const LRow tmp{gr, (dr + T1E_POST) * 512, lo};
     uint8_t *base = sym + off + (uint64_t)p * slot;
-    t1_model_plane(b.w, b.h, b.orient, bits, above, ref, d > 0, negr, tmp, s_sc, (uint32_t *)base,
+    t1_model_plane<LRow, LRow, COND>(b.w, b.h, b.orient, bits, above, ref, d > 0, negr, tmp, s_sc, (uint32_t *)base,
                    E.cnt + (size_t)i * 128 + p * 4, cblksty, t1_pass_raw(cblksty, (int32_t)p, 0, numbps),
                    s_ring + threadIdx.x);
 }
@@ -863,8 +864,8 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
     const uint32_t groups8 = (t1_scratch_records(n) / 64 + 7) & ~7u;  // k_t1_prep's XCD deal: whole rounds of 8 groups
     hipLaunchKernelGGL(k_t1_prep, dim3(groups8 * 64), dim3(64), 0, s, blocks, n, maxdepth, coef, scratch, res);
     const uint64_t threads = (uint64_t)t1_scratch_records(n) * maxdepth;
-    hipLaunchKernelGGL(k_t1_model, dim3((uint32_t)(threads / 64)), dim3(64), 0, s, blocks, n, maxdepth, scratch, sym,
-                       sym_off, res, cblksty);
+    hipLaunchKernelGGL(k_t1_model<true>, dim3((uint32_t)(threads / 64)), dim3(64), 0, s, blocks, n, maxdepth, scratch,
+                       sym, sym_off, res, cblksty);
     const uint32_t bpw = dwt_options().t1_enc_bpw ? (uint32_t)dwt_options().t1_enc_bpw
                          : bpw_req                ? bpw_req
                                                   : t1_blocks_per_wave(n);
@@ -946,7 +947,20 @@ hipError_t launch_t1_decode(const DecBlock *blocks, uint32_t n, const uint8_t *d
     // DEC_WAVES wavefronts per workgroup share the LUTs (roi only for BYPASS:
     // the ROI shift only moves BYPASS pass boundaries)
     const uint32_t nw = (n + bpw - 1) / bpw, nwg = (nw + DEC_WAVES - 1) / DEC_WAVES;
-    if (cblksty & CBLKSTY_LAZY)
+    // A launch of few blocks does not fill the GPU, so occupancy buys nothing
+    // and the 128-VGPR cap's spills sit on each lane's chain: single-wavefront
+    // workgroups at the uncapped 144 VGPRs -- the 512^2 image (70 blocks)
+    // decodes in 9.1-9.4 ms of T1 against 16.8-18.4 (profiles/r05/
+    // t1_lone_variants.txt); the 4K frame (6,321 blocks, more than 4,096)
+    // and the lone 8K frame were the same either way
+    if (n <= 4096) {
+        if (cblksty & CBLKSTY_LAZY)
+            hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true, 1, 1>), dim3(nw), dim3(DEC_LANES), 0, s, blocks, n,
+                               (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi, bpw);
+        else
+            hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, false, 1, 1>), dim3(nw), dim3(DEC_LANES), 0, s, blocks, n,
+                               (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, nullptr, bpw);
+    } else if (cblksty & CBLKSTY_LAZY)
         hipLaunchKernelGGL((k_t1_decode_ub<DEC_LANES, true, DEC_WAVES, DEC_WAVES>), dim3(nwg), dim3(DEC_LANES * DEC_WAVES),
                            0, s, blocks, n, (const uint32_t *)ubuf, fixed_words, scratch, segs, seg_first, cblksty, roi,
                            bpw);

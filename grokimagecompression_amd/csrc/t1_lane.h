@@ -543,7 +543,7 @@ GRK_HD uint64_t ldrow(const A &a, int32_t y, uint32_t h) {
 // stripe's first row, t1.cpp:168-190), i.e. row k+4 reads as insignificant
 // for row k+3; SEGSYM -- the cleanup pass ends with the segmentation symbols
 // 1 0 1 0 in the uniform context (mqc_segmark_enc, t1.cpp:1244-1245).
-template <class R, class T>
+template <class R, class T, bool COND = true>
 GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bitp, const R &above, const R &ref,
                            bool has_ref, const R &negr, const T &tmp, const uint8_t *sc, uint32_t *out, uint32_t *cnt,
                            uint32_t cblksty = 0, bool raw_spp = false, uint32_t *ring = nullptr) {
@@ -568,7 +568,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
             post[r] = pre[r];
         }
         const uint64_t D = vsc ? 0 : ldrow(above, (int32_t)(k + 4), h);
-        if ((C[0] | C[1] | C[2] | C[3]) && (pre[0] | pre[1] | pre[2] | pre[3] | U | D)) {
+        if (!COND || ((C[0] | C[1] | C[2] | C[3]) && (pre[0] | pre[1] | pre[2] | pre[3] | U | D))) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bit[r] = ldrow(bitp, (int32_t)(k + r), h);
         }
@@ -590,7 +590,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
             }
             if (!changed) break;
         }
-        if ((post[0] ^ pre[0]) | (post[1] ^ pre[1]) | (post[2] ^ pre[2]) | (post[3] ^ pre[3])) {
+        if (!COND || ((post[0] ^ pre[0]) | (post[1] ^ pre[1]) | (post[2] ^ pre[2]) | (post[3] ^ pre[3]))) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
             if (vsc) ng[5] = 0;
@@ -642,7 +642,7 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
 #pragma unroll
         for (int r = 0; r < 4; ++r) m[r] = ldrow(above, (int32_t)(k + r), h);
         uint64_t cols = m[0] | m[1] | m[2] | m[3];
-        if (!cols) continue;  // no member: nothing else of the stripe is read
+        if (COND && !cols) continue;  // no member: nothing else of the stripe is read
 #pragma unroll
         for (int i = 0; i < 6; ++i) sS[i] = ldrow(postS, (int32_t)(k + i) - 1, h);
         if (vsc) sS[5] = 0;
@@ -680,10 +680,10 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
             sS[r] = ldrow(postS, (int32_t)(k + r), h);
             cand[r] = (uint32_t)r < nr ? ~(sS[r] | ldrow(visS, (int32_t)(k + r), h)) & wm : 0;
         }
-        if (cand[0] | cand[1] | cand[2] | cand[3]) {  // the bits of candidates, the signs of new significance
+        if (!COND || (cand[0] | cand[1] | cand[2] | cand[3])) {  // the bits of candidates, the signs of new significance
 #pragma unroll
             for (int r = 0; r < 4; ++r) bit[r] = ldrow(bitp, (int32_t)(k + r), h);
-            if ((cand[0] & bit[0]) | (cand[1] & bit[1]) | (cand[2] & bit[2]) | (cand[3] & bit[3])) {
+            if (!COND || ((cand[0] & bit[0]) | (cand[1] & bit[1]) | (cand[2] & bit[2]) | (cand[3] & bit[3]))) {
 #pragma unroll
                 for (int i = 0; i < 6; ++i) ng[i] = negr[k + i];
                 if (vsc) ng[5] = 0;
