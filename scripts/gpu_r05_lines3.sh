@@ -1,0 +1,16 @@
+# C5 (x2) and C4 lines on the final build
+set -o pipefail
+T=${1:-r05w}
+mkdir -p gpurun_out/$T
+export TMPDIR=/tmp
+for r in 1 2; do
+timeout -k 10 400 python3 -u bench.py --workload c5 --steps 10 --warmup 2 > gpurun_out/$T/c5_$r.json 2> gpurun_out/$T/c5_$r.err || { tail -30 gpurun_out/$T/c5_$r.err; exit 1; }
+python3 - gpurun_out/$T/c5_$r.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+e, dd = d["stage_ms"]["enccin"], d["stage_ms"]["deccin"]
+print(sys.argv[1], "value", d["value"], "cpu", d["cpu_baseline"]["value"], "enc t1 %.2f host_t2 %.2f rate %.2f | dec t1 %.2f host_t2 %.2f" % (e["t1_ms"], e["host_t2_ms"], e["rate_ms"], dd["t1_ms"], dd["host_t2_ms"]))
+PY
+done
+timeout -k 10 400 python3 -u bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/$T/c4.json 2> gpurun_out/$T/c4.err || { tail -30 gpurun_out/$T/c4.err; exit 1; }
+python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('c4', d['value'], d.get('cpu_baseline'))" gpurun_out/$T/c4.json
