@@ -14,3 +14,5 @@ PY
 done
 timeout -k 10 400 python3 -u bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/$T/c4.json 2> gpurun_out/$T/c4.err || { tail -30 gpurun_out/$T/c4.err; exit 1; }
 python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('c4', d['value'], d.get('cpu_baseline'))" gpurun_out/$T/c4.json
+timeout -k 10 400 python3 -u bench.py > gpurun_out/$T/bench_default.json 2> gpurun_out/$T/bench_default.err || { tail -20 gpurun_out/$T/bench_default.err; exit 1; }
+python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('bench default', d['steps'], d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['inverse']['frac'], d['pcie_inclusive']['value'])" gpurun_out/$T/bench_default.json
