@@ -880,17 +880,29 @@ hipError_t launch_t1_encode(const EncBlock *blocks, uint32_t n, const int32_t *c
         hipLaunchKernelGGL(k_mq_order_scatter, dim3((n + 255) / 256), dim3(256), 0, s, key, n, hist, permw);
         perm = permw;
     }
-    // MQ_WAVES wavefronts per workgroup, 19 context words per lane: LDS no
-    // longer holds the coder at 7 wavefronts per SIMD (5.7 KB per single-
-    // wavefront workgroup); 8 per SIMD by registers and LDS: 8K batch 3519 /
-    // 3476 -> 3664 / 3577 Mpixels/s alternating (profiles/r05/t1_mq_wg_ab.txt)
+    // Concurrent calls: MQ_WAVES wavefronts per workgroup, 19 context words
+    // per lane -- LDS no longer holds the coder at 7 wavefronts per SIMD (5.7
+    // KB per single-wavefront workgroup); 8 per SIMD by registers and LDS: 8K
+    // batch 3519 / 3476 -> 3664 / 3577 Mpixels/s alternating (profiles/r05/
+    // t1_mq_wg_ab.txt).  A call alone on the GPU or a small launch keeps one
+    // wavefront per workgroup: its lanes' chains run on separate CUs instead of
+    // four wavefronts sharing one CU's LDS -- the 512^2 image's coder took
+    // 6.8 ms in 4-wavefront workgroups against 4.1 (profiles/r05/
+    // rocprof_512_r4_r5.txt)
     const uint32_t nwv = (n + bpw - 1) / bpw, nwg = (nwv + MQ_WAVES - 1) / MQ_WAVES;
-    if (cblksty & CBLKSTY_LAZY)
+    const bool wide = !bpw_req && n > 4096;
+    if (wide && (cblksty & CBLKSTY_LAZY))
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true, MQ_WAVES, 19>), dim3(nwg), dim3(MQ_LANES * MQ_WAVES), 0, s,
                            blocks, n, cnt, sym, sym_off, out, res, perm, cblksty, bpw);
-    else
+    else if (wide)
         hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false, MQ_WAVES, 19>), dim3(nwg), dim3(MQ_LANES * MQ_WAVES), 0, s,
                            blocks, n, cnt, sym, sym_off, out, res, perm, cblksty, bpw);
+    else if (cblksty & CBLKSTY_LAZY)
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, true>), dim3(nwv), dim3(MQ_LANES), 0, s, blocks, n, cnt, sym, sym_off,
+                           out, res, perm, cblksty, bpw);
+    else
+        hipLaunchKernelGGL((k_t1_mq<MQ_LANES, 1, false>), dim3(nwv), dim3(MQ_LANES), 0, s, blocks, n, cnt, sym, sym_off,
+                           out, res, perm, cblksty, bpw);
     return hipGetLastError();
 }
 
