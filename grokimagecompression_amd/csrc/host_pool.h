@@ -8,7 +8,9 @@
 // threads) never wait for an idle worker.
 #pragma once
 #include <sched.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <atomic>
@@ -70,17 +72,39 @@ private:
     };
 
     HostPool() {
-        // GRKGPU_HOST_THREADS caps the pool (default: the cores this process
-        // may run on -- its affinity mask, not the machine's -- at most 16, a
-        // GPU box's share per GPU)
+        // GRKGPU_HOST_THREADS sets the pool size (the caller counts as one).
+        // Default: half the CPUs this process may use -- its affinity mask,
+        // or the cgroup's CPU quota when that is smaller (a GPU box: 16 of
+        // 256), at most 16 -- since the frames in flight run their own host
+        // work on their own threads beside the pool, and threads beyond the
+        // quota get the whole process throttled.  Measured on one box, pool
+        // of 16 / 8 (profiles/r05/host_pool_ab.txt): DCI 4K cinema batch
+        // 2029-2228 -> 2464-2533 Mpixels/s, the 8K batch 3526 / 3555 ->
+        // 3546 / 3622, the C4 tile shard 2278 / 2273 -> 2215 / 2260.
         size_t n = std::thread::hardware_concurrency();
         {
             cpu_set_t set;
             if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = (size_t)CPU_COUNT(&set);
         }
-        if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = (size_t)atoi(e);
-        n = std::min<size_t>(n ? n : 1, 16);
+        const size_t quota = cgroup_cpus();
+        if (quota && quota < n) n = quota;
+        n = std::max<size_t>(std::min<size_t>(n, 16) / 2, 1);
+        if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = std::min<size_t>(std::max(atoi(e), 1), 16);
         for (size_t i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    }
+    // CPUs of the cgroup v2 quota ("quota period" in cpu.max), 0 if none
+    static size_t cgroup_cpus() {
+        FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+        if (!f) return 0;
+        char q[32] = {0};
+        unsigned long long period = 0;
+        size_t n = 0;
+        if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period) {
+            const unsigned long long quota = strtoull(q, nullptr, 10);
+            n = (size_t)((quota + period - 1) / period);
+        }
+        fclose(f);
+        return n;
     }
     ~HostPool() {
         {
