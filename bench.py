@@ -188,6 +188,12 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
+    # N ranks on one node share its CPU quota: each rank's host pool (the
+    # library's default is half the process's share, host_pool.h) gets half of
+    # its 1/N slice, so the ranks' frame threads and pools stay within it
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    if lw > 1 and "GRKGPU_HOST_THREADS" not in os.environ:
+        os.environ["GRKGPU_HOST_THREADS"] = str(max(1, min(16, host_threads() // lw) // 2))
 
     import grokimagecompression_amd as grk
     import synth

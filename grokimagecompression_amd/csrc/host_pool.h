@@ -92,19 +92,35 @@ private:
         if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = std::min<size_t>(std::max(atoi(e), 1), 16);
         for (size_t i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
     }
-    // CPUs of the cgroup v2 quota ("quota period" in cpu.max), 0 if none
+    // CPUs of the cgroup's quota (v2 cpu.max "quota period", or v1
+    // cfs_quota_us / cfs_period_us), 0 if none
     static size_t cgroup_cpus() {
-        FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
-        if (!f) return 0;
-        char q[32] = {0};
-        unsigned long long period = 0;
-        size_t n = 0;
-        if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period) {
-            const unsigned long long quota = strtoull(q, nullptr, 10);
-            n = (size_t)((quota + period - 1) / period);
+        unsigned long long quota = 0, period = 0;
+        bool have = false;
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0) {
+                quota = strtoull(q, nullptr, 10);
+                have = true;
+            }
+            fclose(f);
+        } else if (FILE *f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+            long long q = -1;
+            if (fscanf(f, "%lld", &q) == 1 && q > 0) {
+                quota = (unsigned long long)q;
+                have = true;
+            }
+            fclose(f);
+            if (have) {
+                have = false;
+                if (FILE *g = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+                    have = fscanf(g, "%llu", &period) == 1;
+                    fclose(g);
+                }
+            }
         }
-        fclose(f);
-        return n;
+        if (!have || !period) return 0;
+        return (size_t)((quota + period - 1) / period);
     }
     ~HostPool() {
         {
