@@ -749,6 +749,7 @@ double t2_ms() {
 
 struct RateProbe {
     // per block, in te.blist order
+    std::vector<uint32_t> gidx;        // its record index (te.blist[i]->gidx, without the pointer chase)
     std::vector<uint32_t> prec;        // precinct id
     struct BoundD { double lo, hi; };  // simple: largest slope compared false, smallest compared true
     struct BoundU { uint32_t lo, hi; };  // feasible: the slope it stopped at, smallest slope it passed
@@ -830,6 +831,8 @@ void probe_init(const CodingParams &cp, TileEnc &te, RateProbe &rp) {
             base += res.pw * res.ph;
         }
     }
+    rp.gidx.resize(te.blist.size());
+    for (size_t i = 0; i < te.blist.size(); ++i) rp.gidx[i] = te.blist[i]->gidx;
     rp.ub.assign(rp.prec.size(), 0);
     rp.prec_bits.assign(base, 0);
     rp.body_prev = 0;
@@ -1175,15 +1178,15 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     const size_t nb = te.blist.size();
     // true if the block's layer record changed; *dlen = its change of bytes
     auto eval = [&](size_t i, int64_t *dlen) -> bool {
-        Cblk &c = *te.blist[i];
-        EncCblkState &s = (*te.cblk)[c.gidx];
+        const uint32_t gidx = rp.gidx[i];
+        EncCblkState &s = (*te.cblk)[gidx];
         uint32_t cumul;
         if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.bu[i].lo, &rp.bu[i].hi);
         else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
-        EncLayer &ly = (*te.layers)[(size_t)c.gidx * L + layno];
+        EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
         const uint32_t old = ly.numpasses;
         const int64_t oldlen = old ? (int64_t)ly.len : 0;
-        set_layer(te, c.gidx, layno, L, cumul);
+        set_layer(te, gidx, layno, L, cumul);
         *dlen = (ly.numpasses ? (int64_t)ly.len : 0) - oldlen;
         if (layno == 0) rp.ub[i] = header_bits_ub(rp, i, s, ly, P.data() + s.pass0);
         return ly.numpasses != old;
@@ -1221,12 +1224,27 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         for (size_t j = 0; j < redo.size(); ++j) ub_old[j] = rp.ub[redo[j]];
     }
     g_rt.redo += redo.size();
+    // A re-evaluation walks its block's pass records, ~0.5 KB away from the
+    // previous block's: fetched PF blocks ahead, its wait is off the chain
+    // (the real C5 frame's evaluations: 35 -> 19 M cycles of pass walking,
+    // tests/cpp/pcrd_bench.cpp on its dumped pass records).
+    constexpr size_t PF = 6;
+    auto prefetch = [&](size_t j) {
+        const EncCblkState &sp = (*te.cblk)[rp.gidx[redo[j]]];
+        const char *pp = (const char *)(P.data() + sp.pass0);
+        for (size_t o = 0; o < (size_t)sp.numpasses * sizeof(EncPass); o += 64) __builtin_prefetch(pp + o);
+    };
+    auto eval_range = [&](size_t a, size_t b) {
+        for (size_t j = a; j < std::min(b, a + PF); ++j) prefetch(j);
+        for (size_t j = a; j < b; ++j) {
+            if (j + PF < b) prefetch(j + PF);
+            changed[j] = eval(redo[j], &dlen[j]);
+        }
+    };
     if (redo.size() > 512) {  // a probe's re-evaluations (~0.2 us each) on the pool from 512
-        host_parallel_for(redo.size(), 128, [&](size_t a, size_t b) {
-            for (size_t j = a; j < b; ++j) changed[j] = eval(redo[j], &dlen[j]);
-        });
+        host_parallel_for(redo.size(), 128, eval_range);
     } else {
-        for (size_t j = 0; j < redo.size(); ++j) changed[j] = eval(redo[j], &dlen[j]);
+        eval_range(0, redo.size());
     }
     const bool keep = !final && (FEASIBLE || thresh != 0);
     if (full) {  // the layer's bytes (and first-layer header bounds) from scratch
@@ -1235,7 +1253,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         std::fill(rp.prec_bits.begin(), rp.prec_bits.end(), 0);
         for (size_t i = 0; i < nb; ++i) {
             if (layno == 0) rp.prec_bits[rp.prec[i]] += rp.ub[i];
-            const EncLayer &ly = (*te.layers)[(size_t)te.blist[i]->gidx * L + layno];
+            const EncLayer &ly = (*te.layers)[(size_t)rp.gidx[i] * L + layno];
             if (!ly.numpasses) continue;
             rp.body += ly.len;
             rp.comp_body[rp.comp[i]] += ly.len;

@@ -7,10 +7,11 @@
 // (e.g. before / after a change) can be compared on the same inputs.
 //
 //   g++ -O2 -std=c++17 -I<csrc> pcrd_bench.cpp <csrc>/t2.cpp <csrc>/codestream.cpp -lpthread
-//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps] [slopes 0|1] [terms 0|1|2]
+//   ./a.out [algo 0|1] [budget_bytes] [seed] [layers] [reps] [slopes 0|1] [terms 0|1|2] [dump]
 // terms: codeword segment ends -- 0 the last pass only, 1 every pass (TERMALL),
 // 2 the BYPASS pattern (passes 10, then the raw MRP and the cleanup of every
-// later plane).  Built with -DGRKGPU_CHECK_HEADER_UB it also prints how many
+// later plane).  dump: real pass records of a cinema frame instead of the
+// synthetic ones (the tile, its rate target, cap and byte bound as dumped).  Built with -DGRKGPU_CHECK_HEADER_UB it also prints how many
 // simulated first-layer packets were checked against the header bound of
 // t2.cpp's body_fits shortcut, and how many exceeded it (must be 0).
 #include <float.h>
@@ -32,6 +33,13 @@ int main(int argc, char **argv) {
     const int reps = argc > 5 ? atoi(argv[5]) : 3;
     const bool slopes = argc > 6 && atoi(argv[6]) != 0;  // per-block slope extremes precomputed
     const int terms = argc > 7 ? atoi(argv[7]) : 0;
+    FILE *dump = argc > 8 ? fopen(argv[8], "rb") : nullptr;
+    double dump_disto = 0;
+    uint64_t dump_bound = 0;
+    if (dump) {
+        uint32_t nl = 0;
+        if (fread(&dump_disto, 8, 1, dump) != 1 || fread(&dump_bound, 8, 1, dump) != 1 || fread(&nl, 4, 1, dump) != 1) return 2;
+    }
     CodingParams cp;
     cp.numcomps = 3;
     cp.image = {0, 0, 4096, 2160};
@@ -45,6 +53,12 @@ int main(int argc, char **argv) {
     cp.prog = PROG_CPRL;
     cp.csty = CSTY_PRT;
     for (int r = 0; r < 7; ++r) cp.prcw[r] = cp.prch[r] = 8;
+    if (dump) {  // -cinema4K 24 as codec.cpp sets it: 6 resolutions, 256^2 precincts above the lowest
+        cp.numres = 6;
+        cp.prcw[0] = cp.prch[0] = 15;
+        cp.pocs[0] = {0, 0, 1, 5, 3, PROG_CPRL};
+        cp.pocs[1] = {5, 0, 1, 6, 3, PROG_CPRL};
+    }
     cp.numpocs = 2;
     cp.pocs[0] = {0, 0, 1, 6, 3, PROG_CPRL};
     cp.pocs[1] = {6, 0, 1, 7, 3, PROG_CPRL};
@@ -55,6 +69,10 @@ int main(int argc, char **argv) {
     cp.rate_algo = algo;
     for (uint32_t l = 0; l < L; ++l) cp.rates[l] = budget * (l + 1) / L;
     cp.max_comp_size = 1041666;
+    if (dump) {  // the dumped tile's rate targets (a single layer)
+        if (fread(&cp.rates[0], sizeof(cp.rates[0]), 1, dump) != 1 ||
+            fread(&cp.max_comp_size, sizeof(cp.max_comp_size), 1, dump) != 1) return 2;
+    }
     generate_qcd(cp);
 
     Tile tile;
@@ -74,6 +92,15 @@ int main(int argc, char **argv) {
                     for (auto &c : pr.cblks) {
                         c.gidx = (uint32_t)cst.size();
                         EncCblkState s;
+                        if (dump) {
+                            if (fread(&s.numbps, 4, 1, dump) != 1 || fread(&s.numpasses, 4, 1, dump) != 1 ||
+                                fread(&s.smin, 8, 1, dump) != 1 || fread(&s.smax, 8, 1, dump) != 1) return 3;
+                            s.pass0 = (uint32_t)passes.size();
+                            passes.resize(passes.size() + s.numpasses);
+                            if (s.numpasses && fread(passes.data() + s.pass0, sizeof(EncPass), s.numpasses, dump) != s.numpasses) return 3;
+                            cst.push_back(s);
+                            continue;
+                        }
                         const uint32_t drop = (uint32_t)(U(rng) * 4);
                         s.numbps = band.numbps > drop + 1 ? band.numbps - drop : 1;
                         s.numpasses = 3 * s.numbps - 2;
@@ -110,6 +137,10 @@ int main(int argc, char **argv) {
                         cst.push_back(s);
                     }
             }
+    if (dump) {
+        distotile = dump_disto;
+        fclose(dump);
+    }
     std::vector<EncLayer> layers((size_t)cst.size() * L);
     double best = 1e30;
     uint64_t digest = 1469598103934665603ull;
@@ -128,7 +159,7 @@ int main(int argc, char **argv) {
         CodingParams cpt = cp;
         const auto t0 = std::chrono::steady_clock::now();
         RateStats rs;
-        if (!rate_allocate(cpt, te, (uint64_t)(budget * 1.2), &rs)) { printf("rate_allocate failed\n"); return 1; }
+        if (!rate_allocate(cpt, te, dump ? dump_bound : (uint64_t)(budget * 1.2), &rs)) { printf("rate_allocate failed\n"); return 1; }
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         best = std::min(best, ms);
         digest = 1469598103934665603ull;
