@@ -11,7 +11,12 @@
 // terms: codeword segment ends -- 0 the last pass only, 1 every pass (TERMALL),
 // 2 the BYPASS pattern (passes 10, then the raw MRP and the cleanup of every
 // later plane).  dump: real pass records of a cinema frame instead of the
-// synthetic ones (the tile, its rate target, cap and byte bound as dumped).  Built with -DGRKGPU_CHECK_HEADER_UB it also prints how many
+// synthetic ones, as a one-off hook in codec.cpp wrote them before its
+// rate_allocate call (round 5; the file is not kept): f64 distotile, u64
+// tile byte bound, u32 layers (1), f64 rate, u64 component cap, then per
+// block in for_each_cblk order u32 numbps, u32 numpasses, f64 smin, f64 smax
+// and its EncPass records.  On the -cinema4K 24 frame of bench.py it
+// reproduces the codec's probes / evaluations / simulations exactly.  Built with -DGRKGPU_CHECK_HEADER_UB it also prints how many
 // simulated first-layer packets were checked against the header bound of
 // t2.cpp's body_fits shortcut, and how many exceeded it (must be 0).
 #include <float.h>
