@@ -1,4 +1,4 @@
-# final build (host pool at half the CPU share): three C5 lines, the default 8K line, C4, the GPU suite
+# final build (host pool at half the CPU share; PCRD pass records prefetched): three C5 lines, the default 8K line, C4, the GPU suite, smoke
 set -o pipefail
 T=${1:-r05f5}
 mkdir -p gpurun_out/$T
