@@ -1458,20 +1458,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             }
             // the simple PCRD's slope range over this block's passes, from
             // the records just written (pcrd_simple's own loop, TileEnc::slopes)
-            double mn = DBL_MAX, mx = -1;
-            for (uint32_t k = 0; k < np; ++k) {
-                const EncPass &ps = out[k];
-                int32_t dr;
-                double dd;
-                if (k == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
-                else { dr = (int32_t)(ps.rate - out[k - 1].rate); dd = ps.dd - out[k - 1].dd; }
-                if (dr == 0) continue;
-                const double r = dd / dr;
-                if (r < mn) mn = r;
-                if (r > mx) mx = r;
-            }
-            cst[i].smin = mn;
-            cst[i].smax = mx;
+            block_slopes(cst[i], out);
             blk_disto[i] = cum;
         }
     });

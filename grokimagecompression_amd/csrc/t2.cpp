@@ -1083,10 +1083,18 @@ void makelayer_final(CodingParams &cp, TileEnc &te, uint32_t layno) {
 // threshold; *lo / *hi = the largest slope that failed / smallest that passed
 // (the comparisons `thresh - slope < DBL_EPSILON` keep their outcomes for
 // every threshold t with !(t - *lo < DBL_EPSILON) and t - *hi < DBL_EPSILON)
-uint32_t simple_cumul(const EncCblkState &s, const EncPass *P, double thresh, double *lo, double *hi) {
+uint32_t simple_cumul(const EncCblkState &s, const EncPass *P, bool slopes, double thresh, double *lo, double *hi) {
     uint32_t cumul = s.incl_prev;
     double l = -HUGE_VAL, h = HUGE_VAL;
     if (thresh == 0) return s.numpasses;
+    if (slopes && cumul == 0 && !s.z0 && !(thresh - s.s0max < DBL_EPSILON)) {
+        // no pass taken yet, so every slope is dd / rate from zero; the
+        // largest fails, so every one does (fl(thresh - x) is monotone in x):
+        // none taken, lo = their std::max fold, hi untouched
+        *lo = s.s0max;
+        *hi = h;
+        return 0;
+    }
     for (uint32_t pn = s.incl_prev; pn < s.numpasses; ++pn) {
         const EncPass &ps = P[pn];
         uint32_t dr;
@@ -1182,7 +1190,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
         EncCblkState &s = (*te.cblk)[gidx];
         uint32_t cumul;
         if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.bu[i].lo, &rp.bu[i].hi);
-        else cumul = simple_cumul(s, P.data() + s.pass0, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
+        else cumul = simple_cumul(s, P.data() + s.pass0, te.slopes, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
         EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
         const uint32_t old = ly.numpasses;
         const int64_t oldlen = old ? (int64_t)ly.len : 0;
@@ -1583,6 +1591,28 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
 uint64_t header_ub_checks() { return g_ub_checks.load(); }
 uint64_t header_ub_violations() { return g_ub_viol.load(); }
 #endif
+
+void block_slopes(EncCblkState &s, const EncPass *P) {
+    double mn = DBL_MAX, mx = -1, m0 = -HUGE_VAL;
+    bool z0 = false;
+    for (uint32_t k = 0; k < s.numpasses; ++k) {
+        const EncPass &ps = P[k];
+        if (ps.rate) m0 = std::max(m0, ps.dd / ps.rate);
+        else if (ps.dd != 0) z0 = true;
+        int32_t dr;
+        double dd;
+        if (k == 0) { dr = (int32_t)ps.rate; dd = ps.dd; }
+        else { dr = (int32_t)(ps.rate - P[k - 1].rate); dd = ps.dd - P[k - 1].dd; }
+        if (dr == 0) continue;
+        const double r = dd / dr;
+        if (r < mn) mn = r;
+        if (r > mx) mx = r;
+    }
+    s.smin = mn;
+    s.smax = mx;
+    s.s0max = m0;
+    s.z0 = z0;
+}
 
 bool rate_allocate(CodingParams &cp, TileEnc &te, uint64_t len, RateStats *st) {
     te.distolayer.assign(cp.numlayers + 1, 0.0);

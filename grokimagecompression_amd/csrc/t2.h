@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <math.h>
 #include <vector>
 
 #include "codestream.h"
@@ -50,6 +51,12 @@ struct EncCblkState {
     // simple PCRD's search range, TileProcessor.cpp:528-560), when the pass
     // records' producer filled them (TileEnc::slopes)
     double smin = 0, smax = 0;
+    // with them: the largest dd / rate over passes with rate != 0 (each pass
+    // against none taken, folded with std::max in pass order from -HUGE_VAL),
+    // and whether a pass has rate == 0 with dd != 0 -- a threshold this
+    // slope fails takes none of the block's passes (simple_cumul)
+    double s0max = -HUGE_VAL;
+    bool z0 = false;
 };
 
 // Per-POC encoder state (the reference's tcp->pocs[] entries: user range +
@@ -74,6 +81,10 @@ struct TileEnc {
     std::vector<Cblk *> blist;                  // the tile's code-blocks in for_each_block order (rate control)
     bool slopes = false;                        // EncCblkState::smin / smax hold every block's pass slopes
 };
+
+// The slope fields of s (smin / smax / s0max / z0) from its pass records P
+// (codec.cpp's pass-record fill; TileEnc::slopes).
+void block_slopes(EncCblkState &s, const EncPass *P);
 
 // number of POC entries of a tile (tcp->numpocs + 1)
 inline uint32_t num_poc_entries(const CodingParams &cp) { return cp.numpocs ? cp.numpocs : 1; }

@@ -103,6 +103,7 @@ int main(int argc, char **argv) {
                             s.pass0 = (uint32_t)passes.size();
                             passes.resize(passes.size() + s.numpasses);
                             if (s.numpasses && fread(passes.data() + s.pass0, sizeof(EncPass), s.numpasses, dump) != s.numpasses) return 3;
+                            block_slopes(s, passes.data() + s.pass0);  // the dump's smin / smax recomputed, plus the rest
                             cst.push_back(s);
                             continue;
                         }
@@ -126,18 +127,8 @@ int main(int argc, char **argv) {
                                      (terms == 2 && (k == 9 || (k > 9 && (k - 10) % 3 != 0)));
                             passes.push_back(p);
                         }
-                        // the slope range codec.cpp's pass-record fill stores (TileEnc::slopes)
-                        double mn = DBL_MAX, mx = -1;
-                        for (uint32_t k = 0; k < s.numpasses; ++k) {
-                            const EncPass &ps = passes[s.pass0 + k];
-                            const int32_t dr = k ? (int32_t)(ps.rate - passes[s.pass0 + k - 1].rate) : (int32_t)ps.rate;
-                            const double d = k ? ps.dd - passes[s.pass0 + k - 1].dd : ps.dd;
-                            if (dr == 0) continue;
-                            mn = std::min(mn, d / dr);
-                            mx = std::max(mx, d / dr);
-                        }
-                        s.smin = mn;
-                        s.smax = mx;
+                        // the slope fields codec.cpp's pass-record fill stores (TileEnc::slopes)
+                        block_slopes(s, passes.data() + s.pass0);
                         distotile += dd;
                         cst.push_back(s);
                     }
