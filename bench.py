@@ -171,6 +171,9 @@ def main():
     ap.add_argument("--concurrency", type=int, default=16, help="frames in flight per GPU: 1, or an even number (half 9/7, half 5/3)")
     ap.add_argument("--workload", default="8k", choices=["8k", "c5", "c4"])
     ap.add_argument("--opt", default="", help="plan options k=v[,k=v] (grkgpu_dwt_options) for the whole run")
+    ap.add_argument("--data", default="smooth", choices=["smooth", "uniform", "const"],
+                    help="synthetic input distribution (SURVEY 8(d)): smooth field + 2%% noise (default), uniform "
+                         "full-range noise (the T1 worst case: most MQ symbols), constant mid-grey (empty blocks)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,7 +209,7 @@ def main():
 
     if args.workload == "c5":
         H, W, C, BITS = 2160, 4096, 3, 12
-        img = synth.synth_image(H, W, C, BITS, 5 + rank)
+        img = synth.synth_image(H, W, C, BITS, 5 + rank, args.data)
         pa, _ = grk.CParams.from_cli(["-cinema4K", "24"])
         pb = pa
         tags = ("cin", "cin")
@@ -214,7 +217,7 @@ def main():
               "tile-part per component, PCRD to 1,302,083 B), enc+dec")
     else:
         H, W, C, BITS = 4320, 7680, 3, 12
-        img = synth.synth_image(H, W, C, BITS, 3 + rank)
+        img = synth.synth_image(H, W, C, BITS, 3 + rank, args.data)
         pa = grk.CParams.make(irreversible=True)
         pb = grk.CParams.make(irreversible=False)
         tags = ("97", "53")
@@ -325,13 +328,19 @@ def main():
     torch.cuda.synchronize()
     p97 = grk.CParams.make(irreversible=True)
 
+    def level_bytes(lvl):
+        rh, rw = H, W
+        for _ in range(lvl):
+            rh, rw = (rh + 1) // 2, (rw + 1) // 2
+        return 8 * rh * rw * C
+
     def launch_table(runs):
         out = []
         for i, l in enumerate(runs[0]):
             ms = sum(r[i]["ms"] for r in runs) / len(runs)
             lv = list(range(l["level0"], l["level0"] + l["levels"]))
-            # B_DWT of a launch = 8 B x (its first level's samples) x (1 + 1/4 per further level)
-            first = l["bytes"] * 4 // (4 + 1) if len(lv) == 2 else l["bytes"]
+            # a launch's floor: its first level's input read and outputs written once
+            first = level_bytes(l["level0"])
             out.append({"kernel": l["kernel"], "levels": lv,
                         "us": round(1e3 * ms, 2), "algorithmic_bytes": l["bytes"], "first_level_bytes": first,
                         "GB_s": round(l["bytes"] / (ms * 1e-3) / 1e9, 1),
@@ -379,12 +388,15 @@ def main():
     floor = sum(x["first_level_bytes"] for x in launches)
     roofline = {"bound": "hbm", "kernel": "forward 9/7 DWT of the frame: " + " + ".join(x["kernel"] for x in launches),
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_launch_sum": round(bdwt / (dwt_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_fused_floor": floor,
                 "traffic_vs_floor": round(traffic / floor, 4) if traffic else None,
                 "algorithmic_bytes": bdwt, "dwt_us": round(dwt_us, 2),
                 "span_us": round(span_us, 2), "launches": launches,
-                "measured": "span_us = device time of the frame's forward level sequence (HIP events on the codec "
+                "measured": "frac = B_DWT / span_us (the basis since round 5); frac_launch_sum = B_DWT / dwt_us, the "
+                            "sum of the per-launch times (round 4's basis, carrying the extra events' overhead); "
+                            "span_us = device time of the frame's forward level sequence (HIP events on the codec "
                             "stream before its first launch and after its last; mean of 5 lone 9/7 encodes after the "
                             "timed region); launches[].us from 5 more encodes with an event after every launch "
                             "(their sum dwt_us carries the extra events' overhead); traffic = PMC bytes (FETCH_SIZE x 2 + "
@@ -395,6 +407,7 @@ def main():
                                       " + ".join(x["kernel"] for x in ilaunches),
                             "achieved": round(bdwt / (ispan_us * 1e-6) / 1e9, 1), "unit": "GB/s",
                             "frac": round(bdwt / (ispan_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                            "frac_launch_sum": round(bdwt / (idwt_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                             "algorithmic_bytes": bdwt, "dwt_us": round(idwt_us, 2),
                             "span_us": round(ispan_us, 2), "launches": ilaunches}}
     if args.workload == "8k":
@@ -406,10 +419,12 @@ def main():
             "forward": {"kernel": " + ".join(x["kernel"] for x in l53), "dwt_us": round(f53, 2),
                         "achieved": round(bdwt / (s53 * 1e-6) / 1e9, 1), "unit": "GB/s",
                         "frac": round(bdwt / (s53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(s53, 2),
+                        "frac_launch_sum": round(bdwt / (f53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                         "launches": l53},
             "inverse": {"kernel": " + ".join(x["kernel"] for x in il53), "dwt_us": round(i53, 2),
                         "achieved": round(bdwt / (is53 * 1e-6) / 1e9, 1), "unit": "GB/s",
                         "frac": round(bdwt / (is53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "span_us": round(is53, 2),
+                        "frac_launch_sum": round(bdwt / (i53 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                         "launches": il53},
             "algorithmic_bytes": bdwt}
 
@@ -485,8 +500,10 @@ def main():
             "value": round(value, 2), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32/f32 (integer encode, f32 9/7 decode)",
-            "data": "synthetic (tests/golden/synth.py smooth+2%% noise, seed %d+rank)" % (5 if args.workload == "c5" else 3),
-            "config": {"workload": wl, "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
+            "data": "synthetic (tests/golden/synth.py %s, seed %d+rank)" % (
+                {"smooth": "smooth+2% noise", "uniform": "uniform full-range noise", "const": "constant mid-grey"}[args.data],
+                5 if args.workload == "c5" else 3),
+            "config": {"workload": wl, "input": args.data, "frames_per_step_per_gpu": 2 * npairs, "frames_in_flight": ncodec,
                        "parallelism": "frame-batch x%d (no collectives)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,

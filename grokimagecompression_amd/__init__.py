@@ -214,6 +214,12 @@ class DwtOptions(ctypes.Structure):
                 ("pair_rows", ctypes.c_int32), ("pair_waves", ctypes.c_int32), ("pair_min_samples", ctypes.c_uint64)]
 
 
+class DeviceSet(ctypes.Structure):
+    """grkgpu_device_set (include/grk_mi355x.h): the device workers of a
+    multi-device call (a device may repeat)."""
+    _fields_ = [("n", ctypes.c_uint32), ("dev", ctypes.c_int32 * 64)]
+
+
 class LaunchTime(ctypes.Structure):
     """grkgpu_launch_time (include/grk_mi355x.h)."""
     _fields_ = [("kernel", ctypes.c_char * 48), ("level0", ctypes.c_uint32), ("levels", ctypes.c_uint32),
@@ -256,6 +262,13 @@ def lib():
         L.grkgpu_get_dwt_options.restype = None
         L.grkgpu_set_dwt_options.argtypes = [P(DwtOptions)]
         L.grkgpu_get_launch_times.argtypes = [VP, P(LaunchTime), U32, P(U32)]
+        L.grkgpu_device_set_for.argtypes = [ctypes.c_int, P(DeviceSet)]
+        L.grkgpu_compress_multi.argtypes = [P(DeviceSet), P(ImageDesc), P(CParams), P(Planes), P(P(ctypes.c_uint8)),
+                                            P(ctypes.c_size_t)]
+        L.grkgpu_decompress_multi.argtypes = [P(DeviceSet), VP, ctypes.c_size_t, P(ImageDesc), P(VP)]
+        L.grkgpu_patch_tlm.argtypes = [VP, ctypes.c_size_t]
+        L.grkgpu_multi_release.argtypes = []
+        L.grkgpu_multi_release.restype = None
         L.grkgpu_default_cparams.argtypes = [P(CParams)]
         L.grkgpu_set_mct.argtypes = [P(CParams), VP, VP, U32]
         L.grkgpu_compress.argtypes = [VP, P(ImageDesc), P(CParams), P(VP), ctypes.c_int, P(P(ctypes.c_uint8)),
@@ -647,6 +660,80 @@ class Codec:
         else:
             _check(lib().grkgpu_decompress(self._ctx, bp, bn, None, ptrs, 1 if on_dev else 0))
         return out
+
+
+def device_set(device=-1):
+    """The device workers grkgpu_device_set_for picks: [device] for device >= 0;
+    for -1 ("all devices", grk_cparameters.deviceId) the GRKGPU_DEVICES list
+    ("0,1" / "0,0" / "all"), else every visible device."""
+    ds = DeviceSet()
+    _check(lib().grkgpu_device_set_for(device, ctypes.byref(ds)))
+    return list(ds.dev[:ds.n])
+
+
+def _devset(devices):
+    ds = DeviceSet()
+    if devices is None:
+        _check(lib().grkgpu_device_set_for(-1, ctypes.byref(ds)))
+        return ds
+    devices = list(devices)
+    if not 0 < len(devices) <= 64:
+        raise GrkGpuError("1 .. 64 device workers")
+    ds.n = len(devices)
+    for k, v in enumerate(devices):
+        ds.dev[k] = v
+    return ds
+
+
+def compress_multi(img, prec, params=None, devices=None, offset=(0, 0), sgnd=False):
+    """One encode over several device workers (grkgpu_compress_multi: the
+    tiles sharded in contiguous ranges, each worker uploading only its tiles'
+    rows; the pieces concatenated in tile order, TLM patched).  img: (c,h,w)
+    host numpy array (int32 or the file's 8 / 16-bit samples).  devices: the
+    workers' devices (a device may repeat), default device_set(-1).  Returns
+    the codestream bytes -- the same bytes as Codec.compress."""
+    c, h, w = img.shape
+    d = ImageDesc()
+    d.x0, d.y0 = offset
+    d.x1, d.y1 = offset[0] + w, offset[1] + h
+    d.numcomps = c
+    for k in range(c):
+        d.prec[k] = prec
+        d.sgnd[k] = 1 if sgnd else 0
+    if img.dtype not in _NP_FMT or not _fmt_fits(_NP_FMT[img.dtype], prec, sgnd):
+        img = img.astype(np.int32)
+    img = np.ascontiguousarray(img)
+    pl = Planes()
+    for k in range(c):
+        pl.planes[k] = img[k].ctypes.data
+    pl.sample_fmt = _NP_FMT[img.dtype]
+    pl.on_device = 0
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    ds = _devset(devices)
+    _check(lib().grkgpu_compress_multi(ctypes.byref(ds), ctypes.byref(d), ctypes.byref(params or CParams.make()),
+                                       ctypes.byref(pl), ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib().grkgpu_free(out)
+
+
+def decompress_multi(buf, devices=None, out=None):
+    """Whole-image decode over several device workers (grkgpu_decompress_multi:
+    each decodes its tile range) into a (c,h,w) int32 host array."""
+    d = read_header(buf)
+    c = d.numcomps
+    shape = (c, d.y1 - d.y0, d.x1 - d.x0)
+    if out is None:
+        out = np.empty(shape, dtype=np.int32)
+    elif _check_out(out, shape, 0):
+        raise GrkGpuError("decompress_multi writes host planes")
+    ptrs = (ctypes.c_void_p * c)(*[out[k].ctypes.data for k in range(c)])
+    bp, bn, keep = _buf_ptr(buf)
+    ds = _devset(devices)
+    _check(lib().grkgpu_decompress_multi(ctypes.byref(ds), bp, bn, None, ptrs))
+    return out
 
 
 class dwt_options:

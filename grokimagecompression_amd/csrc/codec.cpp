@@ -35,6 +35,9 @@ using namespace grkgpu;
 
 static thread_local std::string g_err;
 static int set_err(int code, const std::string &msg) { g_err = msg; return code; }
+namespace grkgpu {
+int set_error(int code, const std::string &msg) { return set_err(code, msg); }  // multi.cpp
+}
 
 #define HIPCHK(expr)                                                                          \
     do {                                                                                      \
@@ -2041,7 +2044,8 @@ static bool tph_marker(uint32_t m) {  // allowed in a tile-part header (j2k.cpp:
 
 // j2k_need_nb_tile_parts_correction from position q (after tile `tile`'s
 // last tile-part): false = the decode fails; *fix = a later SOT of the same
-// tile has TPsot == TNsot (the non-conformant streams the reference patches)
+// tile has TPsot == TNsot (the non-conformant streams the reference patches:
+// walk_tile_parts then raises every tile-part count by one, as j2k.cpp:809-835)
 static bool tp_lookahead(const uint8_t *cs, size_t len, uint64_t q, uint32_t tile, bool *fix, std::string &err) {
     *fix = false;
     for (;;) {
@@ -2083,6 +2087,7 @@ static bool walk_tile_parts(const uint8_t *cs, size_t len, size_t sot0, uint32_t
         return false;
     };
     uint32_t state = TPHSOT, tcur = 0, tpl = 0, ndec = 0;
+    uint32_t corr = 0;  // m_nb_tile_parts_correction: 1 once a TPsot == TNsot stream was detected
     bool ready = false, last_tp = false, checked = false, skipping = false;
     uint64_t at;
     for (uint32_t nr = 0; nr < ntiles; ++nr) {
@@ -2113,9 +2118,10 @@ static bool walk_tile_parts(const uint8_t *cs, size_t len, size_t sot0, uint32_t
                     if (psot && psot < 14 && psot != 12) { err = "Psot value is not correct"; return false; }
                     if (!psot) last_tp = true;
                     if (nb_tp[t] && part >= nb_tp[t]) { err = "Current tile part number greater than the tile-parts"; return false; }
-                    if (nparts) {
-                        if (part >= nparts) { err = "In SOT marker, TPSot is not valid"; return false; }
-                        nb_tp[t] = nparts;
+                    if (nparts) {  // j2k.cpp:5210-5236: TNsot + the correction, as a byte
+                        const uint32_t np = (nparts + corr) & 0xFF;
+                        if (part >= np) { err = "In SOT marker, TPSot is not valid"; return false; }
+                        nb_tp[t] = np;
                     }
                     if (nb_tp[t] && nb_tp[t] == part + 1) ready = true;
                     tpl = last_tp ? 0u : psot - 12;
@@ -2149,7 +2155,12 @@ static bool walk_tile_parts(const uint8_t *cs, size_t len, size_t sot0, uint32_t
                     checked = true;
                     bool fix = false;
                     if (!tp_lookahead(cs, len, p, tcur, &fix, err)) return false;
-                    if (fix) { err = "non-conformant tile-part count (TPsot == TNsot) not supported"; return false; }
+                    if (fix) {  // Issue 254 (j2k.cpp:809-835): every known tile-part count + 1, later TNsot + 1
+                        ready = false;
+                        corr = 1;
+                        for (auto &n : nb_tp)
+                            if (n) n = (n + 1) & 0xFF;
+                    }
                 }
                 if (!ready) {
                     if (!read(2, &at)) { err = "Stream too short"; return false; }

@@ -356,7 +356,24 @@ GRK_EXPORT void grk_deinitialize(void) {
     }
     g_all.clear();
     g_free.clear();
+    grkgpu_multi_release();  // the multi-device calls' pooled contexts
 }
+
+// The device workers of a call: grk_cparameters.deviceId for an encode
+// (-1 = all devices, grok.h:565, grk_compress.cpp:423-426); a decode's
+// grk_dparameters carry no device (grok.h:693-738; grk_decompress -G reaches
+// only a plugin, grk_decompress.cpp:1227-1230), so it runs on device 0
+// unless GRKGPU_DEVICES lists its workers.  Several workers shard the tiles
+// (grkgpu_compress_multi / grkgpu_decompress_multi).
+static bool device_set(int device, grkgpu_device_set *ds) {
+    if (device < -1) device = 0;
+    if (grkgpu_device_set_for(device, ds) != GRKGPU_OK) {
+        GRK_ERROR("%s", grkgpu_last_error());
+        return false;
+    }
+    return true;
+}
+static int decode_device() { return getenv("GRKGPU_DEVICES") ? -1 : 0; }
 
 // ---------------------------------------------------------------------------
 // images (image.cpp grk_image_create / grok.cpp:760-797)
@@ -667,10 +684,8 @@ GRK_EXPORT bool grk_set_decode_area(grk_codec *codec, grk_image *image, uint32_t
 GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image) {
     Codec *c = (Codec *)codec;
     if (!c || !c->decompressor || !c->have_header || !image || image->numcomps != c->desc.numcomps) return false;
-    // grk_dparameters carries no device (grok.h:693-738): device 0
-    Lease lease(0);
-    grkgpu_ctx *ctx = lease.ctx;
-    if (!ctx) return false;
+    grkgpu_device_set ds;
+    if (!device_set(decode_device(), &ds)) return false;
     std::vector<int32_t *> planes(image->numcomps);
     // The planes take the extent the decode writes under the current settings
     // (cp_reduce and the decode area may have changed since grk_read_header /
@@ -704,9 +719,18 @@ GRK_EXPORT bool grk_decode(grk_codec *codec, grk_plugin_tile *, grk_image *image
     }
     grkgpu_dparams dp{c->dparams.cp_reduce, c->dparams.cp_layer, 0, 0, 0, 0};
     if (c->window) { dp.DA_x0 = c->win[0]; dp.DA_y0 = c->win[1]; dp.DA_x1 = c->win[2]; dp.DA_y1 = c->win[3]; }
-    if (grkgpu_decompress_ex(ctx, c->cs.data(), c->cs.size(), &dp, nullptr, planes.data(), 0)) {
-        GRK_ERROR("%s", grkgpu_last_error());
-        return false;
+    if (ds.n > 1 && !c->window && !dp.cp_reduce && !dp.cp_layer) {  // tile shards over the device workers
+        if (grkgpu_decompress_multi(&ds, c->cs.data(), c->cs.size(), nullptr, planes.data())) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
+    } else {
+        Lease lease(ds.dev[0]);
+        if (!lease.ctx) return false;
+        if (grkgpu_decompress_ex(lease.ctx, c->cs.data(), c->cs.size(), &dp, nullptr, planes.data(), 0)) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
     }
     for (uint32_t k = 0; k < image->numcomps; ++k)
         image->comps[k].resno_decoded = c->hinfo.numresolutions - 1 - c->dparams.cp_reduce;
@@ -978,11 +1002,28 @@ GRK_EXPORT bool grk_encode_with_plugin(grk_codec *codec, grk_plugin_tile *tile) 
     grkgpu_image_desc d;
     grkgpu_cparams p;
     if (!image_desc(c->image, &d) || !map_cparams(&c->cparams, d.numcomps, &p)) return false;
-    Lease lease(c->cparams.deviceId);  // held until the codestream is written out of the context's buffer
-    grkgpu_ctx *ctx = lease.ctx;
-    if (!ctx) return false;
+    grkgpu_device_set ds;
+    if (!device_set(c->cparams.deviceId, &ds)) return false;
     std::vector<const int32_t *> planes(d.numcomps);
     for (uint32_t k = 0; k < d.numcomps; ++k) planes[k] = c->image->comps[k].data;
+    if (ds.n > 1) {  // deviceId -1: the tiles sharded over the device workers
+        grkgpu_planes pl{};
+        for (uint32_t k = 0; k < d.numcomps; ++k) pl.planes[k] = planes[k];
+        pl.sample_fmt = GRKGPU_SAMPLE_I32;
+        uint8_t *mo = nullptr;
+        size_t ml = 0;
+        if (grkgpu_compress_multi(&ds, &d, &p, &pl, &mo, &ml)) {
+            GRK_ERROR("%s", grkgpu_last_error());
+            return false;
+        }
+        const bool ok = c->stream->write_all(mo, ml);
+        grkgpu_free(mo);
+        if (!ok) { GRK_ERROR("stream write failed"); return false; }
+        return true;
+    }
+    Lease lease(ds.dev[0]);  // held until the codestream is written out of the context's buffer
+    grkgpu_ctx *ctx = lease.ctx;
+    if (!ctx) return false;
     const uint8_t *out = nullptr;
     size_t len = 0;
     if (grkgpu_compress_view(ctx, &d, &p, planes.data(), 0, &out, &len)) {

@@ -13,8 +13,6 @@ Decode: every rank holds the codestream and decodes its own tile range.
 The encoder/decoder object only needs compress_tiles / decompress_tiles
 (grokimagecompression_amd.Codec).
 """
-import struct
-
 from . import PART_EOC, PART_HEADER, PART_TILES
 
 _DATA_GROUPS = {}
@@ -53,42 +51,22 @@ def tile_rows(begin, end, image_h, tdy, ty0=0, y0=0, tw=1):
 
 
 def patch_tlm(cs):
-    """j2k_write_updated_tlm (j2k.cpp:2555-2577) over an assembled codestream:
-    the main header's TLM records (tile index Ttlm, tile-part length Ptlm, one
-    per tile-part in codestream order, widths from Stlm, j2k.cpp:5027-5063)
-    filled in from the tile-parts' own SOT headers.  Each rank of a sharded
-    encode wrote only its own tile-parts, so rank 0's header could not.  A
-    stream without TLM, or whose TLM does not have one record per tile-part,
-    is returned as it is."""
+    """j2k_write_updated_tlm (j2k.cpp:2555-2577) over an assembled codestream
+    (grkgpu_patch_tlm, host code of libgrk_mi355x): the main header's TLM
+    records (tile index Ttlm, tile-part length Ptlm, one per tile-part in
+    codestream order, filled across all of its TLM markers in order; widths
+    from Stlm, j2k.cpp:5027-5063) from the tile-parts' own SOT headers.  Each
+    rank of a sharded encode wrote only its own tile-parts, so rank 0's
+    header could not.  A stream without TLM (or no codestream at all) comes
+    back as it is; TLM records that do not match the tile-parts one to one
+    raise GrkGpuError -- never a silently stale TLM."""
+    import ctypes
+    from . import lib, _check
     if cs[:2] != b"\xff\x4f":
         return cs
-    pos, tlm = 2, None
-    while pos + 4 <= len(cs):
-        m, L = struct.unpack(">HH", cs[pos:pos + 4])
-        if m == 0xFF90:
-            break
-        if m == 0xFF55:
-            tlm = (pos, L)
-        pos += 2 + L
-    if tlm is None:
-        return cs
-    tpos, L = tlm
-    stlm = cs[tpos + 5]
-    st, sp = (stlm >> 4) & 3, 4 if (stlm >> 6) & 1 else 2
-    if st == 3:
-        return cs
-    n = (L - 4) // (st + sp)
-    recs = []
-    while pos + 12 <= len(cs) and cs[pos:pos + 2] == b"\xff\x90":
-        isot, psot = struct.unpack(">HI", cs[pos + 4:pos + 10])
-        recs.append((isot, psot))
-        if not psot:
-            break
-        pos += psot
-    if len(recs) != n:
-        return cs
-    body = b"".join((isot.to_bytes(st, "big") if st else b"") + psot.to_bytes(sp, "big") for isot, psot in recs)
-    return cs[:tpos + 6] + body + cs[tpos + 6 + len(body):]
+    buf = ctypes.create_string_buffer(bytes(cs), len(cs))
+    _check(lib().grkgpu_patch_tlm(buf, len(cs)))
+    return buf.raw[:len(cs)]
 
 
 def assemble(parts):

@@ -313,6 +313,42 @@ int grkgpu_compress_tiles(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const g
                           const int32_t *const *planes, int planes_on_device, uint32_t tile_begin,
                           uint32_t tile_end, uint32_t parts, uint8_t **out, size_t *outlen);
 
+/* Multi-device calls: one call shards the tiles over several devices
+ *  -- what the reference's callers ask for with
+ * deviceId = -1 (grk_cparameters.deviceId, grok.h:565; grk_compress -G "A
+ * value of -1 will specify all devices", grk_compress.cpp:423-426; the
+ * decompress parameters and the plugin init info carry the same field,
+ * grok.h:789, 1817).  A device set lists the workers: one host thread and
+ * one context (pooled per device across calls) each; a device may appear
+ * more than once.
+ *   grkgpu_device_set_for: device >= 0 -> {device}; device = -1 -> the
+ *     environment's GRKGPU_DEVICES ("0,1,2,3", "0,0", or "all"), else every
+ *     visible device.
+ *   grkgpu_compress_multi: the whole codestream.  Worker k encodes the k-th
+ *     contiguous tile range from just the image rows of its tiles (host
+ *     planes; worker 0 also writes the main header, the last one the EOC);
+ *     the pieces are concatenated in tile order and the TLM records filled in
+ *     from the tile-parts (j2k_write_updated_tlm, j2k.cpp:2555-2577).  Bytes
+ *     identical to grkgpu_compress.  One worker does it all when the image
+ *     has one tile, the planes are on a device, hold a window of the image,
+ *     or a component is subsampled.  *out: free with grkgpu_free.
+ *   grkgpu_decompress_multi: whole-image decode into host planes, each worker
+ *     decoding its tile range (grkgpu_decompress_tiles).
+ *   grkgpu_multi_release: destroy the pooled contexts. */
+#define GRKGPU_MAX_DEVICES 64
+typedef struct {
+    uint32_t n;
+    int32_t dev[GRKGPU_MAX_DEVICES];
+} grkgpu_device_set;
+int grkgpu_device_set_for(int device, grkgpu_device_set *out);
+void grkgpu_multi_release(void);
+/* Host only: fill in the TLM records of a codestream concatenated from tile
+ * shards (j2k_write_updated_tlm, j2k.cpp:2555-2577) from its tile-parts' SOT
+ * headers, in place -- records across all of the main header's TLM markers,
+ * in order.  GRKGPU_EINVAL when the records do not match the tile-parts one
+ * to one (or a tile-part has Psot = 0); a stream without TLM is unchanged. */
+int grkgpu_patch_tlm(uint8_t *cs, size_t len);
+
 /* Same, with planes holding only image rows [row0, row0 + nrows) (relative to
  * img->y0): a rank of a tile-row shard loads just the rows of its tiles.
  * Every tile of [tile_begin, tile_end) must lie inside those rows. */
@@ -352,6 +388,9 @@ typedef struct {
 int grkgpu_compress_ex(grkgpu_ctx *ctx, const grkgpu_image_desc *img, const grkgpu_cparams *p,
                        const grkgpu_planes *planes, uint32_t tile_begin, uint32_t tile_end, uint32_t parts,
                        const uint8_t **out, size_t *outlen);
+/* (multi-device encode: see grkgpu_device_set above) */
+int grkgpu_compress_multi(const grkgpu_device_set *devs, const grkgpu_image_desc *img, const grkgpu_cparams *p,
+                          const grkgpu_planes *planes, uint8_t **out, size_t *outlen);
 
 /* Tier-1 only (the tile hot path of TileProcessor::encode_tile up to and
  * including t1_encode, TileProcessor.cpp:994-1012; SURVEY 8(b)
@@ -450,6 +489,9 @@ int grkgpu_decompress_ex(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, const g
  * for the shard's tiles only. */
 int grkgpu_decompress_tiles(grkgpu_ctx *ctx, const uint8_t *cs, size_t len, uint32_t tile_begin,
                             uint32_t tile_end, int32_t *const *planes, int planes_on_device);
+/* (multi-device decode into host planes: see grkgpu_device_set above) */
+int grkgpu_decompress_multi(const grkgpu_device_set *devs, const uint8_t *cs, size_t len, grkgpu_image_desc *img,
+                            int32_t *const *planes);
 
 /* The tile-part walk of a decode, host only (no device needed): the
  * reference decoder's walk over the tile-parts (j2k_decode_tiles,

@@ -196,6 +196,13 @@ LARGE = [
     ("C3_8k_rgb12_I_r20", (4320, 7680, 3, 12), "smooth", 3, ["-I", "-r", "20"]),
     ("C5_dci4k_rgb12_cinema", (2160, 4096, 3, 12), "smooth", 5, ["-cinema4K", "24"]),
     ("C5b_dci2k_rgb12_cinema", (1080, 2048, 3, 12), "smooth", 6, ["-cinema2K", "24"]),
+    # round 6: SURVEY 8(d)'s other input distributions of the C3 frame --
+    # uniform full-range noise (the T1 worst case: every bit-plane coded, the
+    # most MQ symbols) and a constant mid-grey frame (empty code-blocks)
+    ("C3_8k_rgb12_I_uniform", (4320, 7680, 3, 12), "uniform", 3, ["-I"]),
+    ("C3_8k_rgb12_uniform", (4320, 7680, 3, 12), "uniform", 3, []),
+    ("C3_8k_rgb12_I_const", (4320, 7680, 3, 12), "const", 3, ["-I"]),
+    ("C3_8k_rgb12_const", (4320, 7680, 3, 12), "const", 3, []),
 ]
 
 

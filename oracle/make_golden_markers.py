@@ -381,10 +381,48 @@ def case_mixed_cblksty(tmp):
     return write(main, [dict(isot=0, tpsot=0, tnsot=1, hdr=[], body=body)]), None
 
 
+def _tnsot(tmp, short):
+    """Tiles split into tile-parts by resolution (-u R, 3 parts each) whose
+    TNsot is rewritten one short (TPsot == TNsot on the last part) for the
+    tiles in `short` (None: all)."""
+    img = synth(96, 160, 3, 12, 308)
+    main, tps = parse(enc(img, 12, ["-I", "-t", "64,64", "-u", "R", "-n", "3", "-r", "10"], tmp))
+    count = {}
+    for tp in tps:
+        count[tp["isot"]] = count.get(tp["isot"], 0) + 1
+    assert all(n == 3 for n in count.values()) and all(tp["tnsot"] == 3 for tp in tps)
+    for tp in tps:
+        if short is None or tp["isot"] in short:
+            tp["tnsot"] = count[tp["isot"]] - 1
+    return write(main, tps), None
+
+
+def case_tnsot_all(tmp):
+    """Every tile's TNsot one short: the reference's Issue-254 correction
+    (j2k.cpp:809-835: found by looking past the first tile's 'last'
+    tile-part, then every tile-part count + 1) decodes the whole image."""
+    return _tnsot(tmp, None)
+
+
+def case_tnsot_tile0(tmp):
+    """Only tile 0's TNsot short: the correction also adds 1 to the other
+    tiles' (correct) counts, so none of them is complete by count; they are
+    decoded when the stream ends (j2k_decode_tiles), as the reference does."""
+    return _tnsot(tmp, {0})
+
+
+def case_tnsot_last(tmp):
+    """Only the last tile's TNsot short: the one look-ahead (after tile 0)
+    finds nothing to correct, and that tile's third part then exceeds its
+    count -- the reference refuses the stream."""
+    return _tnsot(tmp, {5})
+
+
 CASES = [("tile_cod", case_tile_cod), ("main_coc", case_main_coc), ("tile_coc", case_tile_coc),
          ("tp_cod_copy", case_tp_cod_copy), ("tp_cod_conflict", case_tp_cod_conflict), ("tile_rgn", case_tile_rgn), ("ppt", case_ppt), ("ppm", case_ppm), ("ppt_tparts", case_ppt_tparts),
          ("ppm_1tile", case_ppm_1tile), ("mixed_wavelet", case_mixed_wavelet), ("siqnt", case_siqnt),
-         ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod), ("mixed_cblksty", case_mixed_cblksty)]
+         ("qcd_short", case_qcd_short), ("coc_then_cod", case_coc_then_cod), ("mixed_cblksty", case_mixed_cblksty),
+         ("tnsot_all", case_tnsot_all), ("tnsot_tile0", case_tnsot_tile0), ("tnsot_last", case_tnsot_last)]
 
 
 # reference decodes with grk_decompress options, -> mk_<name>.<tag>.dec.npy

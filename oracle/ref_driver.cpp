@@ -170,6 +170,7 @@ static bool parse_enc_opts(grk_cparameters *p, int argc, char **argv) {
         }
         else if (a == "-M") p->cblk_sty = (uint8_t)(atoi(v) & 0x7f);
         else if (a == "-u") { p->tp_flag = (uint8_t)v[0]; p->tp_on = 1; }
+        else if (a == "-G") p->deviceId = atoi(v);  // grk_compress.cpp:720-721 (-1: all devices)
         else if (a == "-A") p->rateControlAlgorithm = (uint32_t)atoi(v);
         else if (a == "-R") {  // grk_compress.cpp:1470-1476
             if (sscanf(v, "c=%d,U=%u", &p->roi_compno, &p->roi_shift) != 2) return false;

@@ -548,10 +548,14 @@ def test_mct_stage_vs_oracle(oracle, irrev):
 
 
 @pytest.mark.parametrize("name", ["C1_512_gray8", "C2_4k_rgb8", "C3_8k_rgb12_I", "C3_8k_rgb12", "C3_8k_rgb12_I_r20",
-                                  "C5_dci4k_rgb12_cinema", "C5b_dci2k_rgb12_cinema"])
+                                  "C5_dci4k_rgb12_cinema", "C5b_dci2k_rgb12_cinema",
+                                  "C3_8k_rgb12_I_uniform", "C3_8k_rgb12_uniform", "C3_8k_rgb12_I_const",
+                                  "C3_8k_rgb12_const"])
 def test_large_config_hashes(codec, name):
     """BASELINE.json configs at full size: codestream sha256 == reference's,
-    decoded-image sha256 == reference decoder's."""
+    decoded-image sha256 == reference decoder's.  The C3 frame also as
+    SURVEY 8(d)'s other inputs: uniform full-range 12-bit noise (the T1 worst
+    case, every bit-plane of every block coded) and a constant frame."""
     import grokimagecompression_amd as grk
     import torch
     m = LARGE[name]
@@ -565,7 +569,7 @@ def test_large_config_hashes(codec, name):
     assert synth.image_sha256(d) == m["dec_sha256"]
 
 
-@pytest.mark.parametrize("name", ["C3_8k_rgb12_I", "C3_8k_rgb12"])
+@pytest.mark.parametrize("name", ["C3_8k_rgb12_I", "C3_8k_rgb12", "C3_8k_rgb12_I_uniform", "C3_8k_rgb12_uniform"])
 def test_large_config_concurrent_calls(name):
     """The same full-size configs through calls that overlap on the GPU (two
     contexts on two threads): a call that is not alone takes the batch code

@@ -232,3 +232,60 @@ def test_gloo_world2_sharded_tlm(name):
     assert _zero_tlm(cs) != cs
     assert res[0] == cs and res[1] is None
     assert shard.patch_tlm(b"H" + b"T0;") == b"H" + b"T0;"
+
+
+def _split_tlm(cs, first):
+    """The golden with its one TLM marker split in two (the first `first`
+    records, then the rest), records zeroed: a main header with several TLM
+    markers (Ztlm 0, 1), as j2k_read_tlm accepts them."""
+    pos = 2
+    while True:
+        m, L = struct.unpack(">HH", cs[pos:pos + 4])
+        if m == 0xFF55:
+            stlm = cs[pos + 5]
+            rec = ((stlm >> 4) & 3) + (4 if (stlm >> 6) & 1 else 2)
+            n = (L - 4) // rec
+            a = b"\xff\x55" + struct.pack(">H", 4 + first * rec) + bytes([0, stlm]) + bytes(first * rec)
+            b = b"\xff\x55" + struct.pack(">H", 4 + (n - first) * rec) + bytes([1, stlm]) + bytes((n - first) * rec)
+            return cs[:pos] + a + b + cs[pos + 2 + L:], n
+        pos += 2 + L
+
+
+@pytest.mark.parametrize("name", ["rgb12_cinema2k", "rgb12_cinema4k"])
+def test_patch_tlm_several_markers_and_mismatch(name):
+    """grkgpu_patch_tlm: records are filled across every TLM
+    marker of the main header in order; a TLM whose record count does not
+    match the tile-parts raises instead of shipping a stale TLM."""
+    from grokimagecompression_amd import GrkGpuError
+    cs = open(os.path.join(GOLD, name + ".j2k"), "rb").read()
+    split, n = _split_tlm(cs, 1)
+    assert n >= 3  # one tile-part per component (and per POC for 4K)
+    patched = shard.patch_tlm(split)
+    # the same records as the golden's, now in two markers
+    again, _ = _split_tlm(cs, 1)
+    assert patched != again
+    rec = 5
+    pos = 2
+    got = b""
+    while True:
+        m, L = struct.unpack(">HH", patched[pos:pos + 4])
+        if m == 0xFF90:
+            break
+        if m == 0xFF55:
+            got += patched[pos + 6:pos + 2 + L]
+        pos += 2 + L
+    ref = _zero_tlm(cs)
+    p2 = 2
+    while True:
+        m, L = struct.unpack(">HH", cs[p2:p2 + 4])
+        if m == 0xFF55:
+            assert got == cs[p2 + 6:p2 + 2 + L] and len(got) == n * rec
+            break
+        p2 += 2 + L
+    assert ref != cs
+    # one record too few: refused
+    bad = split.replace(b"\xff\x55" + struct.pack(">H", 4 + (n - 1) * rec) + bytes([1, 0x50]) + bytes((n - 1) * rec),
+                        b"\xff\x55" + struct.pack(">H", 4 + (n - 2) * rec) + bytes([1, 0x50]) + bytes((n - 2) * rec))
+    assert bad != split
+    with pytest.raises(GrkGpuError):
+        shard.patch_tlm(bad)
