@@ -632,13 +632,13 @@ __global__ __launch_bounds__(LANES * WAVES) __attribute__((amdgpu_waves_per_eu(W
                                                         const uint8_t *__restrict__ roi, uint32_t bpw) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
-    __shared__ uint32_t s_mq[48];
+    __shared__ uint32_t s_mq[MQ_DEC_WORDS + 2];  // decoder words (t1_lane.h mq_dec_word)
     __shared__ uint32_t s_cx[WAVES * LANES * DEC_CX_STRIDE];
     __shared__ uint32_t s_ring[WAVES * LANES * FB_RING];  // bit readers' word rings (t1_flat.h FlatBits), slot stride 64
     static_assert(LANES == 64, "the word rings interleave 64 lanes");
     for (uint32_t k = threadIdx.x; k < 2048; k += LANES * WAVES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
     for (uint32_t k = threadIdx.x; k < 256; k += LANES * WAVES) s_sc[k] = sc_win_entry(k);
-    for (uint32_t k = threadIdx.x; k < 47; k += LANES * WAVES) s_mq[k] = c_mq_tab[k];
+    for (uint32_t k = threadIdx.x; k < MQ_DEC_WORDS; k += LANES * WAVES) s_mq[k] = mq_dec_word(c_mq_tab, k);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(LANES * WAVES) __attribute__((amdgpu_waves_per_eu(W
         const DecSeg s0 = segs[q0];
         const uint32_t *region = ubuf + (size_t)s0.ub_off * 4;
         for (uint32_t y = 0; y < b.h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-        mq_reset_words(cxw, T.mq);
+        mq_reset_words_dec(cxw, T.mq);
         BitDecT<LAZY> d;
         d.set_ring(ring, 6);
         d.init(region + 4, region[0], region + 4 + unstuff_word_cap(s0.len));

@@ -76,7 +76,7 @@ GRK_HD void keep_here(uint32_t v) {
 struct DecTables {
     const uint8_t *zc;   // 512 entries for this block's orientation
     const uint8_t *sc;   // 256, window order
-    const uint32_t *mq;  // 47
+    const uint32_t *mq;  // MQ_DEC_WORDS decoder words (t1_lane.h mq_dec_word)
 };
 
 // significance propagation (CUP = false) or cleanup (CUP = true) of one
@@ -332,7 +332,7 @@ GRK_HD void t1_decode_passes(D &d, uint32_t numpasses, uint32_t numbps, uint32_t
         }
         if (passtype == 2 && (sty & CBLKSTY_SEGSYM))
             for (int q = 0; q < 4; ++q) d.decode(cxw, T.mq, CX_UNI);
-        if ((sty & CBLKSTY_RESET) && !(D::kLazy && d.raw)) mq_reset_words(cxw, T.mq);  // after MQ passes (t1.cpp:1104-1105)
+        if ((sty & CBLKSTY_RESET) && !(D::kLazy && d.raw)) mq_reset_words_dec(cxw, T.mq);  // after MQ passes (t1.cpp:1104-1105)
         if (++passtype == 3) { passtype = 0; bpno--; }
     }
 }

@@ -82,26 +82,23 @@ GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, u
 }
 
 // ---------------------------------------------------------------------------
-// Bit reader over the unstuffed words: 64-bit MSB-aligned window W holding
-// NB >= 32 valid bits after every refill, fed one word at a time from a
-// per-lane ring of FB_RING words (LDS on the device: word j of a lane at
-// ring[(j % FB_RING) << rsh], so the 64 lanes' words of one slot sit in 64
-// different banks).  The ring is topped up from the stream in HBM at the
-// start of every stripe (fill: one or two 16-byte chunks, loaded together
-// with the stripe's state rows, whose wait the decoder pays anyway); inside
-// the stripe a refill is an LDS read, and only a ring that runs dry (a
-// stripe coding more than ~300 bits) waits on HBM.  Fetching the stream
-// straight from HBM at each 16-byte boundary stalled the whole wavefront on
-// a memory round trip about every second decision step (64 lanes, ~130
-// decisions per chunk each).  Past the end of the stream it returns 1-bits.
+// Bit reader over the unstuffed words: a two-word window (w0, w1) and the
+// bit offset into it, fed one word at a time from a per-lane ring of FB_RING
+// words (LDS on the device: word j of a lane at ring[(j % FB_RING) << rsh],
+// so the 64 lanes' words of one slot sit in 64 different banks).  The ring is
+// topped up from the stream in HBM at the start of every stripe (fill: one
+// or two 16-byte chunks, loaded together with the stripe's state rows, whose
+// wait the decoder pays anyway); inside the stripe the next word comes from
+// the ring, and only a ring that runs dry (a stripe coding more than ~300
+// bits) reaches HBM.  Fetching the stream straight from HBM at each 16-byte
+// boundary stalled the whole wavefront on a memory round trip about every
+// second decision step.  Past the end of the stream it returns 1-bits.
 // ---------------------------------------------------------------------------
 constexpr uint32_t FB_RING = 16;  // words per lane
 struct FlatBits {
-    uint64_t W;
-    uint32_t NB;
     uint32_t *ring;         // this lane's ring (see above)
     uint32_t rsh;           // slot stride = 1 << rsh words
-    uint32_t rp, wp;        // words taken from / put into the ring (wp - rp held)
+    uint32_t rp, wp;        // ring word of `nextw` (BitDecT), words put into the ring
     uint32_t chunk;         // next chunk of the stream to fetch
     uint32_t nchunks;
     const uint4 *base;
@@ -119,8 +116,8 @@ GRK_HD void fb_put(FlatBits &b, const uint4 &c) {
     b.wp += 4;
 }
 
-// top the ring up to at least FB_RING - 4 words (both chunk loads issued
-// before either is stored)
+// top the ring up (both chunk loads issued before either is stored); never
+// past FB_RING words from rp, the slot the reader still re-reads
 GRK_HD void fb_fill(FlatBits &b) {
     const uint32_t held = b.wp - b.rp;
     if (held <= FB_RING - 8) {
@@ -142,19 +139,18 @@ GRK_HD void fb_start(FlatBits &b, const uint32_t *words, uint32_t nwords) {
     fb_fill(b);
 }
 
-GRK_HD uint32_t fb_word(FlatBits &b) {
-    if (b.wp == b.rp) {  // dry: straight from HBM
+// ring word rp (the ring holds it: rp < wp, or a dry ring is refilled from HBM)
+GRK_HD uint32_t fb_at(FlatBits &b) {
+    if (b.rp >= b.wp) {  // dry: straight from HBM
         const uint4 c0 = fb_load(b, b.chunk++);
         fb_put(b, c0);
     }
-    const uint32_t v = b.ring[(b.rp % FB_RING) << b.rsh];
-    ++b.rp;
-    return v;
+    return b.ring[(b.rp % FB_RING) << b.rsh];
 }
 
 // ---------------------------------------------------------------------------
 // MQ decoder over the unstuffed stream (used by the pass walk of t1_dec.h):
-// branch-free renormalisation.
+// branch-free renormalisation and word advance.
 // ---------------------------------------------------------------------------
 // LAZY: the decoder may meet raw (BYPASS) segments; compiled out otherwise,
 // so the common case keeps its per-symbol path branch-free.
@@ -163,11 +159,12 @@ struct BitDecT {
     static constexpr bool kLazy = LAZY;
     FlatBits bits;
     uint32_t A, C, consumed, cq, cqn;  // cq: next carry event, cqn: the one after
-    // the stream word after W's bits, read from the ring one refill ahead:
-    // a refill only ORs it in, and the LDS read of the following word has
-    // until the next refill to land (a refill that waits on its own read
-    // stalls the whole wavefront at almost every decision step)
-    uint32_t nextw;
+    // the stream bits not yet in C: the window {w0, w1} from bit offset 32 - t
+    // of w0 (t in [0, 31]; t = 0: w0 is used up, the bits start with w1), so
+    // alignbit(w0, w1, t) is the next 32 of them.  nextw: the ring word after
+    // w1 (ring slot bits.rp), re-read from the ring at every decision -- the
+    // read needs no branch, and by the next word advance it has landed
+    uint32_t w0, w1, t, nextw;
     const uint32_t *cp;
     bool raw;  // the current segment is raw (BYPASS): bits straight from the stream
     // the lane's word ring (FlatBits), set once before the first init
@@ -177,39 +174,51 @@ struct BitDecT {
     }
     // stripe start (t1_decode_passes): top the word ring up from HBM
     GRK_HD void fill() { fb_fill(bits); }
+    GRK_HD void load_window() {
+        w0 = fb_at(bits);
+        ++bits.rp;
+        w1 = fb_at(bits);
+        ++bits.rp;
+        nextw = fb_at(bits);
+    }
+    // n bits consumed: the window moves by n (n <= 16); a move past w0 takes
+    // the next word (a select, no branch) and reads the one after from the ring
+    GRK_HD void advance(uint32_t n) {
+        const bool cross = t < n;
+        t = (t - n) & 31u;
+        w0 = cross ? w1 : w0;
+        w1 = cross ? nextw : w1;
+        bits.rp += cross ? 1u : 0u;
+        nextw = fb_at(bits);
+    }
     // raw segment (mqc_raw_init_dec / mqc_raw_decode, mqc_dec.cpp:195-200,
     // mqc_dec_inl.h:90-112): the unstuffed stream IS the raw bit sequence --
     // 7 bits from the byte after a 0xFF, 1-bits from a marker on
     GRK_HD void init_raw(const uint32_t *words, uint32_t nwords) {
         fb_start(bits, words, nwords);
-        const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
-        bits.W = (w0 << 32) | w1;
-        bits.NB = 64;
-        nextw = fb_word(bits);
+        // the first bit is the first word's MSB, offset 0 of the window -- which
+        // t cannot express -- so the window starts one word earlier, at its
+        // end: w0 = (none), w1 = word 0, t = 0, nextw = word 1
+        w0 = 0;
+        w1 = fb_at(bits);
+        ++bits.rp;
+        nextw = fb_at(bits);
+        t = 0;
         raw = true;
     }
-    GRK_HD void refill() {
-        bits.W |= (uint64_t)nextw << (32 - bits.NB);
-        bits.NB += 32;
-        nextw = fb_word(bits);
-    }
     GRK_HD uint32_t rawbit() {
-        const uint32_t b = (uint32_t)(bits.W >> 63);
-        bits.W <<= 1;
-        if (--bits.NB < 32) refill();
+        const uint32_t b = alignbit32(w0, w1, t) >> 31;
+        advance(1);
         return b;
     }
     GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
         raw = false;
         fb_start(bits, words, nwords);
-        const uint64_t w0 = fb_word(bits), w1 = fb_word(bits);
-        const uint64_t v = (w0 << 32) | w1;
-        C = (uint32_t)(v >> 33);  // first 31 stream bits (INITDEC: consumed 24, then 7 shifts)
-        bits.W = v << 31;
-        bits.NB = 33;
-        A = 0x8000;
+        load_window();
+        C = w0 >> 1;  // first 31 stream bits (INITDEC: consumed 24, then 7 shifts)
+        t = 1;        // the next bit is w0's last
+        A = 0x80000000u;  // 0x8000 << 16
         consumed = 31;
-        nextw = fb_word(bits);
         cq = carries[0];
         cp = carries + 1;
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
@@ -229,7 +238,7 @@ struct BitDecT {
         const uint32_t bit = step(wd, tab);
         cxw[cx] = wd;  // unconditional LDS write: no branch
 #ifdef T1_TRACE
-        T1_TRACE(cx, bit, A, C >> 16);
+        T1_TRACE(cx, bit, A >> 16, C >> 16);
 #endif
         return bit;
     }
@@ -242,35 +251,39 @@ struct BitDecT {
         }
         const uint32_t bit = step(wd, tab);
 #ifdef T1_TRACE
-        T1_TRACE(cx, bit, A, C >> 16);
+        T1_TRACE(cx, bit, A >> 16, C >> 16);
 #else
         (void)cx;
 #endif
         return bit;
     }
-    // one MQ decision with context word wd (updated in place)
+    // One MQ decision with context word wd (updated in place).  A is held
+    // << 16 and the context word carries Qe << 16 (mq_dec_word), so the
+    // interval and the code register compare against Qe as it is loaded:
+    // C < Qe << 16  <=>  C[31:16] < Qe, and the renormalisation shift is
+    // clz(A) directly.  The next word comes from the (state, MPS) table with
+    // the MPS flip already in it.  The renormalisation shifts the next n
+    // window bits into C (a bit-field extract of the 32 window bits).
     GRK_HD uint32_t step(uint32_t &wd, const uint32_t *tab) {
-        const uint32_t qe = wd & 0xffffu, mps = wd >> 31;
+        const uint32_t qe = wd & 0xffff0000u;
         uint32_t a = A - qe;
-        const bool lo = (C >> 16) < qe;
+        const bool lo = C < qe;
         const bool lps = lo ? (a >= qe) : (a < qe);
-        const bool keep = !lo && (a & 0x8000u);
-        C = lo ? C : C - (qe << 16);
+        const bool keep = !lo && (int32_t)a < 0;  // MPS, no renormalisation
+        C = lo ? C : C - qe;
         a = lo ? qe : a;
-        const uint32_t nidx = (wd >> (lps ? 22 : 16)) & 63u;
-        const uint32_t nmps = mps ^ (lps ? (wd >> 28) & 1u : 0u);
-        const uint32_t tw = tab[nidx];
-        const uint32_t n = clz32(a) - 16;
-        C = (C << n) | (uint32_t)((bits.W >> 1) >> (63 - n));
-        bits.W <<= n;
-        bits.NB -= n;
+        const uint32_t tw = tab[(wd >> (lps ? 7 : 0)) & 127u];
+        const uint32_t n = clz32(a);
+        const uint32_t win = alignbit32(w0, w1, t);
+        C = (C << n) | bfe32(win, 32 - n, n);
         A = a << n;
         const uint32_t c1 = consumed + n;
         if (cq < c1) { C += 1u << (16 + c1 - cq); next_carry(); }  // carry event (see Unstuff)
         consumed = c1;
-        if (bits.NB < 32) refill();
-        wd = keep ? wd : (tw | (nmps << 31));
-        return mps ^ (uint32_t)lps;
+        advance(n);
+        const uint32_t bit = ((wd >> 15) & 1u) ^ (uint32_t)lps;
+        wd = keep ? wd : tw;
+        return bit;
     }
 };
 using BitDec = BitDecT<false>;
@@ -308,7 +321,7 @@ GRK_HD void t1_decode_v5(const uint32_t *words, uint32_t nwords, const uint32_t 
                          uint32_t numbps, uint32_t w, uint32_t h, ST &st, const DecTables &T, uint32_t *cxw,
                          RP sa, RP rb, uint32_t *ring, uint32_t rsh) {
     for (uint32_t y = 0; y < h + 2; ++y) { st.sig[y] = 0; st.neg[y] = 0; st.vis[y] = 0; st.ref[y] = 0; }
-    mq_reset_words(cxw, T.mq);
+    mq_reset_words_dec(cxw, T.mq);
     BitDec d;
     d.set_ring(ring, rsh);
     d.init(words, nwords, carries);

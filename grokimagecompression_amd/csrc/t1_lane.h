@@ -87,6 +87,22 @@ GRK_HD void vm_wait_all() {
 #endif
 }
 GRK_HD uint32_t clz32(uint32_t v) { return (uint32_t)__builtin_clz(v); }
+// v_alignbit_b32: the low 32 bits of {hi, lo} >> (sh & 31)
+GRK_HD uint32_t alignbit32(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31));
+#endif
+}
+// v_bfe_u32: w bits of v from bit (off & 31); w = 0 gives 0 (w < 32 here)
+GRK_HD uint32_t bfe32(uint32_t v, uint32_t off, uint32_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ubfe(v, off, w);
+#else
+    return w ? (v >> (off & 31)) & ((1u << w) - 1) : 0u;
+#endif
+}
 GRK_HD uint32_t ctz64(uint64_t v) { return (uint32_t)__builtin_ctzll(v); }
 GRK_HD uint64_t dil(uint64_t m) { return m | (m << 1) | (m >> 1); }
 
@@ -122,6 +138,28 @@ GRK_HD void mq_reset_words(uint32_t *cxw, const uint32_t *tab) {
     cxw[CX_UNI] = tab[46];
     cxw[CX_AGG] = tab[3];
     cxw[CX_ZC] = tab[4];
+}
+
+// The DECODER's context words (t1_flat.h BitDecT::step): one word per
+// (state, MPS) pair i = 2 state + mps, so an LPS exchange needs no MPS
+// arithmetic -- Qe[31:16] | MPS[15] | next pair on LPS [13:7] | next pair on
+// MPS [6:0] (the LPS successor already carries SWITCH's MPS flip).  Qe sits
+// where the decoder's A and C registers compare against it (A held << 16,
+// C[31:16] = Chigh), so the decision needs no shifts of it.  94 entries
+// generated from the encoder table (ISO 15444-1 Table C.2).
+GRK_HD uint32_t mq_dec_word(const uint32_t *tab47, uint32_t i) {
+    const uint32_t st = i >> 1, m = i & 1, t = tab47[st];
+    const uint32_t qe = t & 0xffffu, nm = (t >> 16) & 63u, nl = (t >> 22) & 63u, sw = (t >> 28) & 1u;
+    return (qe << 16) | (m << 15) | ((2 * nl + (m ^ sw)) << 7) | (2 * nm + m);
+}
+constexpr uint32_t MQ_DEC_WORDS = 94;
+// mqc_resetstates (mqc_dec.cpp:207-215) in decoder words: UNI -> 46, AGG -> 3,
+// ZC0 -> 4, every other context state 0, MPS 0
+GRK_HD void mq_reset_words_dec(uint32_t *cxw, const uint32_t *tab94) {
+    for (int i = 0; i < NUM_CX; ++i) cxw[i] = tab94[0];
+    cxw[CX_UNI] = tab94[2 * 46];
+    cxw[CX_AGG] = tab94[2 * 3];
+    cxw[CX_ZC] = tab94[2 * 4];
 }
 
 // ---------------------------------------------------------------------------

@@ -41,6 +41,8 @@ static uint64_t g_bypass[3];
 
 using namespace grkgpu;
 static const uint32_t kTab[47] = GRK_MQ_TABLE_INIT;
+static uint32_t kDecTab[MQ_DEC_WORDS];
+static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_word(kTab, i); return true; }();
 static T1Scratch scr;
 
 // per block: passes -> stripes -> columns -> decisions
@@ -78,7 +80,7 @@ int main() {
             uint32_t *wp = (uint32_t *)(((uintptr_t)words.data() + 15) & ~(uintptr_t)15);
             uint32_t ncar = 0;
             const uint32_t nw = t1_unstuff(obuf.data() + 1, len, wp, carr.data(), &ncar);
-            const DecTables DT{zc + orient * 512, scw, kTab};
+            const DecTables DT{zc + orient * 512, scw, kDecTab};
             uint32_t cx4[32], ring[FB_RING];
             ev.clear();
             ev.push_back(Ev{9, 0, 0});

@@ -12,6 +12,8 @@
 
 using namespace grkgpu;
 static const uint32_t kTab[47] = GRK_MQ_TABLE_INIT;
+static uint32_t kDecTab[MQ_DEC_WORDS];
+static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_word(kTab, i); return true; }();
 
 static uint64_t rng = 88172645463325252ull;
 static uint32_t rnd() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return (uint32_t)rng; }
@@ -89,7 +91,7 @@ int main(int argc, char **argv) {
             std::vector<uint8_t> pad(len + 160, 0);
             uint8_t *lp = pad.data() + 16 + (it & 7);
             memcpy(lp, obuf.data() + 1, len);
-            const DecTables DT{zc + orient * 512, scw, kTab};
+            const DecTables DT{zc + orient * 512, scw, kDecTab};
             uint32_t cx4[32];
             std::vector<uint32_t> words(unstuff_word_cap(len) + 8, 0), carr(unstuff_carry_cap(len), 0);
             uint32_t *wp = (uint32_t *)(((uintptr_t)words.data() + 15) & ~(uintptr_t)15);
