@@ -302,6 +302,8 @@ def lib():
         L.grkgpu_dwt_scratch_bytes.restype = ctypes.c_size_t
         L.grkgpu_dwt_scratch_bytes.argtypes = [U32, U32, U32, U32, U32]
         L.grkgpu_t1_scratch_bytes.restype = ctypes.c_size_t
+        L.grkgpu_t1_scratch_bytes_n.restype = ctypes.c_size_t
+        L.grkgpu_t1_scratch_bytes_n.argtypes = [U32]
         L.grkgpu_t1_encode_blocks.argtypes = [VP, U32, VP, VP, VP, VP, ctypes.c_int, VP]
         L.grkgpu_t1_decode_blocks.argtypes = [VP, U32, VP, VP, VP, VP]
         _lib = L

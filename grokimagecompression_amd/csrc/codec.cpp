@@ -365,6 +365,9 @@ size_t grkgpu_t1_scratch_bytes(void) {
     return std::max<size_t>(t1e_scratch_bytes(64, 32) / 64 + 32 * (size_t)sym_slot_bytes(64, 64),
                             sizeof(T1Scratch) + (size_t)t1_stage_dec_words() * 4);
 }
+size_t grkgpu_t1_scratch_bytes_n(uint32_t nblocks) {
+    return (((size_t)nblocks + 63) & ~(size_t)63) * grkgpu_t1_scratch_bytes();
+}
 
 }  // extern "C"
 

@@ -191,6 +191,7 @@ struct Codec {
     grk_cparameters cparams{};
     grk_image *image = nullptr;
     bool setup = false;
+    std::vector<uint8_t> mct;  // grk_set_MCT's matrix + DC shifts, taken out of the parameters at setup
     // decompress
     grk_dparameters dparams{};
     std::vector<uint8_t> cs;
@@ -236,9 +237,15 @@ TileRect tile_rect(uint32_t t, uint32_t tw, uint32_t tx0, uint32_t ty0, uint32_t
             (uint32_t)std::min<uint64_t>(d.y1, (uint64_t)ty0 + (uint64_t)(q + 1) * tdy)};
 }
 
-// The matrix size of each grk_set_MCT allocation (the ABI's mct_data is a
-// bare pointer): map_cparams refuses an image whose component count differs,
-// instead of reading past the allocation.
+// The matrix size of each live grk_set_MCT allocation (the ABI's mct_data is
+// a bare pointer): map_cparams refuses an image whose component count differs
+// from the one grk_set_MCT was given, instead of reading past the allocation.
+// grk_setup_encoder takes the matrix out and frees the allocation, as
+// j2k_setup_encoder does (j2k.cpp:1899-1956 copy, :2052-2055 free), and erases
+// the entry, so a reused address never matches a stale size.  A pointer the
+// caller filled in directly (not from grk_set_MCT) is read as numcomps x
+// numcomps floats + numcomps DC shifts, as the reference reads it, and stays
+// the caller's.
 static std::mutex g_mct_mu;
 static std::unordered_map<const void *, uint32_t> g_mct_n;
 
@@ -253,8 +260,8 @@ bool map_cparams(const grk_cparameters *g, uint32_t numcomps, grkgpu_cparams *p)
         {
             std::lock_guard<std::mutex> lk(g_mct_mu);
             const auto it = g_mct_n.find(g->mct_data);
-            if (it == g_mct_n.end() || it->second != numcomps) {
-                GRK_ERROR("custom MCT matrix (grk_set_MCT) of %u components for an image of %u", it == g_mct_n.end() ? 0u : it->second, numcomps);
+            if (it != g_mct_n.end() && it->second != numcomps) {
+                GRK_ERROR("custom MCT matrix (grk_set_MCT) of %u components for an image of %u", it->second, numcomps);
                 return false;
             }
         }
@@ -983,6 +990,16 @@ GRK_EXPORT bool grk_setup_encoder(grk_codec *codec, grk_cparameters *p, grk_imag
     grkgpu_cparams tmp;
     if (!map_cparams(p, image->numcomps, &tmp)) return false;
     c->cparams = *p;
+    if (p->mct_data) {  // the codec's own copy from here on (j2k.cpp:1899-1956, 2052-2055)
+        const size_t n = image->numcomps, bytes = n * n * sizeof(float) + n * sizeof(int32_t);
+        c->mct.assign((const uint8_t *)p->mct_data, (const uint8_t *)p->mct_data + bytes);
+        c->cparams.mct_data = c->mct.data();
+        std::lock_guard<std::mutex> lk(g_mct_mu);
+        if (g_mct_n.erase(p->mct_data)) {
+            free(p->mct_data);
+            p->mct_data = nullptr;
+        }
+    }
     c->image = image;
     c->setup = true;
     return true;
@@ -1279,14 +1296,31 @@ GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *codec) {
     std::vector<std::vector<grk_marker_info>> tm(nt);
     std::vector<std::vector<grk_tp_index>> tp(nt);
     std::vector<uint32_t> nb_tps(nt, 0);
+    // the decoder's tile-part counts (tcp m_nb_tile_parts) and the TPsot ==
+    // TNsot correction (j2k.cpp:809-835, read_sot :5202-5236): checked once,
+    // after the first tile whose last counted tile-part was read; from then on
+    // every known count and every later TNsot is one higher.  A SOT read_sot
+    // refuses ends the walk before it is recorded.
+    std::vector<uint32_t> nbp(nt, 0);
+    uint32_t corr = 0;
+    bool checked = false;
     while (pos + 12 <= len && rd16(pos) == 0xFF90) {
         const uint32_t isot = rd16(pos + 4), psot = rd16(pos + 6) << 16 | rd16(pos + 8);
         const uint32_t tpsot = cs[pos + 10], tnsot = cs[pos + 11];
         if (isot >= nt) break;
+        if (nbp[isot] && tpsot >= nbp[isot]) break;
+        if (tnsot) {
+            const uint32_t np = (tnsot + corr) & 0xFF;
+            if (tpsot >= np) break;
+            nbp[isot] = np;
+            nb_tps[isot] = np;
+            tp[isot].resize(np, grk_tp_index{});  // grk_realloc to the count (j2k.cpp:5281-5310)
+        } else if (tp[isot].size() < tpsot + 1) {
+            tp[isot].resize(tpsot + 1, grk_tp_index{});
+        }
+        const bool ready = nbp[isot] && nbp[isot] == tpsot + 1;
         const size_t sot = pos;
         tm[isot].push_back({0xFF90, (uint64_t)sot, 12});
-        if (tnsot) nb_tps[isot] = tnsot;
-        if (tp[isot].size() < std::max<uint32_t>(nb_tps[isot], tpsot + 1)) tp[isot].resize(std::max<uint32_t>(nb_tps[isot], tpsot + 1), grk_tp_index{});
         tp[isot][tpsot].start_pos = sot;
         pos += 12;
         while (pos + 4 <= len && rd16(pos) != 0xFF93) {
@@ -1300,6 +1334,23 @@ GRK_EXPORT grk_codestream_index *grk_get_cstr_index(grk_codec *codec) {
         tp[isot][tpsot].end_pos = end;
         if (!psot || end <= pos) break;
         pos = end;
+        if (ready && !checked) {  // j2k_need_nb_tile_parts_correction (j2k.cpp:527-625): the tile's next SOT
+            checked = true;
+            size_t q = pos;
+            while (q + 12 <= len && rd16(q) == 0xFF90 && rd16(q + 2) == 10) {
+                const uint32_t t2 = rd16(q + 4), tot = rd16(q + 6) << 16 | rd16(q + 8);
+                if (t2 == isot) {
+                    if (cs[q + 10] == cs[q + 11]) {
+                        corr = 1;
+                        for (auto &n : nbp)
+                            if (n) n = (n + 1) & 0xFF;
+                    }
+                    break;
+                }
+                if (tot < 14) break;
+                q += tot;
+            }
+        }
     }
     for (uint32_t t = 0; t < nt; ++t)
         if (tm[t].empty() || !nb_tps[t]) return nullptr;  // grk_malloc(0) (j2k_dump.cpp:449-465, 481-498)

@@ -18,6 +18,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -92,35 +93,64 @@ private:
         if (const char *e = getenv("GRKGPU_HOST_THREADS")) n = std::min<size_t>(std::max(atoi(e), 1), 16);
         for (size_t i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
     }
-    // CPUs of the cgroup's quota (v2 cpu.max "quota period", or v1
-    // cfs_quota_us / cfs_period_us), 0 if none
+    // CPUs of the cgroup's quota, 0 if none: the process's own cgroup from
+    // /proc/self/cgroup (v2 "0::/path" -> cpu.max "quota period"; v1 the cpu
+    // controller's line -> cfs_quota_us / cfs_period_us), each directory from
+    // it up to the mount root, the smallest quota found (a parent's limit
+    // binds too); a namespaced cgroup whose path is "/" reads the root files.
     static size_t cgroup_cpus() {
-        unsigned long long quota = 0, period = 0;
-        bool have = false;
-        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-            char q[32] = {0};
-            if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0) {
-                quota = strtoull(q, nullptr, 10);
-                have = true;
+        std::string v2, v1;
+        if (FILE *f = fopen("/proc/self/cgroup", "r")) {
+            char line[4096];
+            while (fgets(line, sizeof(line), f)) {
+                std::string l(line);
+                while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+                const size_t c1 = l.find(':'), c2 = c1 == std::string::npos ? c1 : l.find(':', c1 + 1);
+                if (c2 == std::string::npos) continue;
+                const std::string ctl = l.substr(c1 + 1, c2 - c1 - 1), path = l.substr(c2 + 1);
+                if (l.compare(0, c1, "0") == 0 && ctl.empty()) v2 = path;
+                else if (("," + ctl + ",").find(",cpu,") != std::string::npos) v1 = path;
             }
             fclose(f);
-        } else if (FILE *f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
-            long long q = -1;
-            if (fscanf(f, "%lld", &q) == 1 && q > 0) {
-                quota = (unsigned long long)q;
-                have = true;
-            }
-            fclose(f);
-            if (have) {
-                have = false;
-                if (FILE *g = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
-                    have = fscanf(g, "%llu", &period) == 1;
-                    fclose(g);
-                }
-            }
         }
-        if (!have || !period) return 0;
-        return (size_t)((quota + period - 1) / period);
+        size_t best = 0;
+        auto take = [&best](unsigned long long quota, unsigned long long period) {
+            if (!period) return;
+            const size_t n = (size_t)((quota + period - 1) / period);
+            if (n && (!best || n < best)) best = n;
+        };
+        // each directory from `path` up to the root of `mount`
+        auto walk = [](const std::string &mount, std::string path, const auto &fn) {
+            for (;;) {
+                fn(mount + (path == "/" ? std::string() : path));
+                if (path.empty() || path == "/") break;
+                const size_t k = path.rfind('/');
+                path = k == 0 || k == std::string::npos ? "/" : path.substr(0, k);
+            }
+        };
+        walk("/sys/fs/cgroup", v2.empty() ? "/" : v2, [&](const std::string &d) {
+            if (FILE *f = fopen((d + "/cpu.max").c_str(), "r")) {
+                char q[32] = {0};
+                unsigned long long period = 0;
+                if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0)
+                    take(strtoull(q, nullptr, 10), period);
+                fclose(f);
+            }
+        });
+        walk("/sys/fs/cgroup/cpu", v1.empty() ? "/" : v1, [&](const std::string &d) {
+            long long q = -1;
+            unsigned long long period = 0;
+            if (FILE *f = fopen((d + "/cpu.cfs_quota_us").c_str(), "r")) {
+                if (fscanf(f, "%lld", &q) != 1) q = -1;
+                fclose(f);
+            }
+            if (q <= 0) return;
+            if (FILE *g = fopen((d + "/cpu.cfs_period_us").c_str(), "r")) {
+                if (fscanf(g, "%llu", &period) == 1) take((unsigned long long)q, period);
+                fclose(g);
+            }
+        });
+        return best;
     }
     ~HostPool() {
         {

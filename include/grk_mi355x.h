@@ -547,13 +547,15 @@ typedef struct {
     uint32_t pad;
 } grkgpu_dec_block;
 
-/* scratch: >= (nblocks rounded up to a multiple of 64) *
- * grkgpu_t1_scratch_bytes() device bytes, encode and decode (both keep the
- * rows of 64 blocks interleaved); decode: every segment at most
- * GRKGPU_T1_MAX_SEG bytes (w*h*4 + 64 for a 64x64 block, the encoder's slab
- * bound). */
+/* scratch: >= grkgpu_t1_scratch_bytes_n(nblocks) device bytes, encode and
+ * decode -- that is (nblocks rounded up to a multiple of 64) *
+ * grkgpu_t1_scratch_bytes(): both keep the rows of 64 blocks interleaved, so
+ * n * grkgpu_t1_scratch_bytes() is too small when n % 64 != 0; decode: every
+ * segment at most GRKGPU_T1_MAX_SEG bytes (w*h*4 + 64 for a 64x64 block, the
+ * encoder's slab bound). */
 #define GRKGPU_T1_MAX_SEG (64 * 64 * 4 + 64)
 size_t grkgpu_t1_scratch_bytes(void);
+size_t grkgpu_t1_scratch_bytes_n(uint32_t nblocks);
 int grkgpu_t1_encode_blocks(const grkgpu_enc_block *blocks, uint32_t nblocks, const int32_t *coef,
                             void *scratch, uint8_t *out, grkgpu_enc_result *results, int with_distortion,
                             void *stream);

@@ -1,5 +1,5 @@
 """A few 8K encodes under one grkgpu_dwt_options setting, for rocprofv3
-counter passes on the DWT kernels (scripts/gpu_r05_pmc.sh).
+counter passes on the DWT kernels (scripts/gpu_run.sh dwtpmc).
   python scripts/dwt_enc_once.py 97|53 [k=v ...]"""
 import os
 import sys

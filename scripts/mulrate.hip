@@ -31,6 +31,12 @@ __device__ __forceinline__ double lift_f64(double t, double s, double c13) {
     return t - __builtin_floor(__builtin_fma(s, c13, 0.5));
 }
 
+// one 24-bit multiply-add (v_mad_i32_i24): exact while |s| < 2^23 and
+// |s c| + 4096 < 2^31 -- the bounded-magnitude lift
+__device__ __forceinline__ int32_t fm24s(int32_t a, int32_t b) { return (__mul24(a, b) + 4096) >> 13; }
+// a plain 32-bit multiply (v_mul_lo_u32), exact while |s c| + 4096 < 2^31
+__device__ __forceinline__ int32_t fm32(int32_t a, int32_t b) { return (a * b + 4096) >> 13; }
+
 template <int MODE>
 __global__ __launch_bounds__(256) void kd(int32_t *out, int32_t seed, int iters) {
     constexpr double c13 = 12994.0 / 8192.0;
@@ -65,6 +71,8 @@ __global__ __launch_bounds__(256) void k(int32_t *out, int32_t seed, int iters) 
             if constexpr (MODE == 0) x[i] = x[i] - fm64(x[i] + 77, c);
             else if constexpr (MODE == 1) x[i] = x[i] - fm24(x[i] + 77, c);
             else if constexpr (MODE == 3) x[i] = x[i] - fmdot(x[i] + 77, c);
+            else if constexpr (MODE == 5) x[i] = x[i] - fm24s(x[i] + 77, c);
+            else if constexpr (MODE == 6) x[i] = x[i] - fm32(x[i] + 77, c);
             else x[i] = (x[i] + 77) ^ (x[i] >> 3);
         }
     }
@@ -81,16 +89,18 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *names[5] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain", "dot2 fixmul13",
-                            "f64 lift (fma + floor)"};
-    for (int mode = 0; mode < 5; ++mode) {
+    const char *names[7] = {"v_mad_i64_i32 fixmul13", "24-bit fixmul13", "add/xor/shift chain", "dot2 fixmul13",
+                            "f64 lift (fma + floor)", "one mad_i32_i24 (bounded)", "one mul_lo_u32 (bounded)"};
+    for (int mode = 0; mode < 7; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             hipEventRecord(e0, 0);
             if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             else if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
-            else hipLaunchKernelGGL(kd<4>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else if (mode == 4) hipLaunchKernelGGL(kd<4>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else if (mode == 5) hipLaunchKernelGGL(k<5>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
+            else hipLaunchKernelGGL(k<6>, dim3(nb), dim3(256), 0, 0, out, rep, iters);
             hipEventRecord(e1, 0);
             hipEventSynchronize(e1);
             float ms = 0;

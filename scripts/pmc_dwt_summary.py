@@ -1,4 +1,4 @@
-"""Per-kernel counters per dispatch from scripts/gpu_r05_pmc.sh runs:
+"""Per-kernel counters per dispatch from scripts/gpu_run.sh dwtpmc runs:
 python scripts/pmc_dwt_summary.py gpurun_out/TAG/s1 ... (FETCH_SIZE doubled for
 gfx950's half count, KiB -> bytes)."""
 import collections

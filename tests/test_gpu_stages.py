@@ -74,7 +74,7 @@ def _gpu_encode(cases, with_distortion):
     t_blocks = torch.from_numpy(eb.view(np.uint8)).to(dev)
     t_out = torch.zeros(16 + n * (MAX_SEG + 16), dtype=torch.uint8, device=dev)
     t_res = torch.zeros(n * ENC_RESULT.itemsize, dtype=torch.uint8, device=dev)
-    t_scr = torch.empty((n + 63) // 64 * 64 * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
+    t_scr = torch.empty(L.grkgpu_t1_scratch_bytes_n(n) + 256, dtype=torch.uint8, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream(0).cuda_stream)
     grk._check(L.grkgpu_t1_encode_blocks(t_blocks.data_ptr(), n, t_coef.data_ptr(), t_scr.data_ptr(),
                                          t_out.data_ptr(), t_res.data_ptr(), with_distortion, s))
@@ -135,8 +135,8 @@ def _gpu_decode(items):
     t_data = torch.from_numpy(np.frombuffer(bytes(blob) + bytes(64), np.uint8).copy()).to(dev)
     t_blocks = torch.from_numpy(db.view(np.uint8)).to(dev)
     t_dst = torch.full((dst_off + 16,), 0x5A5A5A5A, dtype=torch.int32, device=dev)
-    nrec = (n + 63) // 64 * 64  # decode: whole 64-block groups (grk_mi355x.h)
-    t_scr = torch.empty(nrec * L.grkgpu_t1_scratch_bytes() + 256, dtype=torch.uint8, device=dev)
+    assert L.grkgpu_t1_scratch_bytes_n(n) == (n + 63) // 64 * 64 * L.grkgpu_t1_scratch_bytes()  # whole 64-block groups
+    t_scr = torch.empty(L.grkgpu_t1_scratch_bytes_n(n) + 256, dtype=torch.uint8, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream(0).cuda_stream)
     grk._check(L.grkgpu_t1_decode_blocks(t_blocks.data_ptr(), n, t_data.data_ptr(), t_scr.data_ptr(),
                                          t_dst.data_ptr(), s))

@@ -138,3 +138,19 @@ def test_oracle_nmsedec_tables_match_reference():
         body = re.search(name + r"\[[^\]]*\]\s*=\s*\{([^}]*)\}", txt).group(1)
         vals = [int(v, 0) for v in body.replace("\n", " ").split(",") if v.strip()]
         assert vals == [int(v) for v in got[128 * k:128 * (k + 1)]], name
+
+
+def test_set_mct_size_mismatch_refused_at_setup(tmp_path):
+    """grk_set_MCT's matrix is n x n for the n it was given; grk_setup_encoder
+    of an image with another component count is refused (ours: an error
+    before anything reaches the device, instead of reading past the
+    allocation; grok_api.cpp map_cparams).  CPU only: setup never touches the
+    GPU."""
+    import numpy as np
+    ours = os.path.join(ROOT, "oracle", "_ref", "ref_driver_mi355x")
+    src, out = tmp_path / "in.i32", tmp_path / "out.j2k"
+    np.zeros((3, 16, 16), dtype="<i4").tofile(src)
+    r = subprocess.run([ours, "enc", str(src), str(out), "16", "16", "3", "8", "0", "-I",
+                        "-mct", "1,0,0,1:0,0"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "custom MCT matrix (grk_set_MCT) of 2 components for an image of 3" in r.stderr
