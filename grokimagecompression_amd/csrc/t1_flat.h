@@ -82,23 +82,33 @@ GRK_HD uint32_t t1_unstuff(const uint8_t *data, uint32_t len, uint32_t *words, u
 }
 
 // ---------------------------------------------------------------------------
-// Bit reader over the unstuffed words: a two-word window (w0, w1) and the
-// bit offset into it, fed one word at a time from a per-lane ring of FB_RING
-// words (LDS on the device: word j of a lane at ring[(j % FB_RING) << rsh],
-// so the 64 lanes' words of one slot sit in 64 different banks).  The ring is
-// topped up from the stream in HBM at the start of every stripe (fill: one
-// or two 16-byte chunks, loaded together with the stripe's state rows, whose
-// wait the decoder pays anyway); inside the stripe the next word comes from
-// the ring, and only a ring that runs dry (a stripe coding more than ~300
-// bits) reaches HBM.  Fetching the stream straight from HBM at each 16-byte
-// boundary stalled the whole wavefront on a memory round trip about every
-// second decision step.  Past the end of the stream it returns 1-bits.
+// Bit reader over the unstuffed words: a two-word window (w0, w1) fed one
+// word at a time from a per-lane ring of FB_RING words (LDS on the device:
+// the 64 lanes' words of one slot sit in 64 different banks, slot stride
+// 1 << rsh words).  The ring is topped up from the stream in HBM at the start
+// of every stripe (fill: one or two 16-byte chunks, loaded together with the
+// stripe's state rows, whose wait the decoder pays anyway); inside the stripe
+// the next word comes from the ring, and only a ring that runs dry (a stripe
+// coding more than ~300 bits) reaches HBM.  Fetching the stream straight from
+// HBM at each 16-byte boundary stalled the whole wavefront on a memory round
+// trip about every second decision step.  Past the end of the stream it
+// returns 1-bits.
+//
+// Position: the reader keeps u = ~(pos + 63), pos = the stream index of the
+// next bit not yet in C.  Then the window (w0 = word K - 1, w1 = word K,
+// K = ceil(pos / 32)) starts at bit offset (-pos) & 31 = u & 31 from w1's
+// start, which is alignbit's shift operand as it stands; a move by n bits
+// is u -= n, crossing into the next word exactly when u and u - n differ
+// above bit 4; and word K + 1 (nextw) sits in ring slot 15 - ((K + 1) % 16)
+// = bits [8:5] of u -- the ring is laid out in reverse so that no position
+// arithmetic is left on the per-decision path.  The two rare events, a carry
+// event (below) and a dry ring, are one unsigned compare against `ulim`.
 // ---------------------------------------------------------------------------
 constexpr uint32_t FB_RING = 16;  // words per lane
 struct FlatBits {
     uint32_t *ring;         // this lane's ring (see above)
     uint32_t rsh;           // slot stride = 1 << rsh words
-    uint32_t rp, wp;        // ring word of `nextw` (BitDecT), words put into the ring
+    uint32_t wp;            // words put into the ring
     uint32_t chunk;         // next chunk of the stream to fetch
     uint32_t nchunks;
     const uint4 *base;
@@ -108,18 +118,21 @@ struct FlatBits {
 // the last chunk (no branch around the load, no select on its result)
 GRK_HD uint4 fb_load(const FlatBits &b, uint32_t ci) { return b.base[ci < b.nchunks ? ci : b.nchunks - 1]; }
 
+// stream word j lives in ring slot 15 - j % 16
+GRK_HD uint32_t &fb_slot(const FlatBits &b, uint32_t j) { return b.ring[(FB_RING - 1 - (j % FB_RING)) << b.rsh]; }
+
 GRK_HD void fb_put(FlatBits &b, const uint4 &c) {
-    b.ring[((b.wp + 0) % FB_RING) << b.rsh] = c.x;
-    b.ring[((b.wp + 1) % FB_RING) << b.rsh] = c.y;
-    b.ring[((b.wp + 2) % FB_RING) << b.rsh] = c.z;
-    b.ring[((b.wp + 3) % FB_RING) << b.rsh] = c.w;
+    fb_slot(b, b.wp + 0) = c.x;
+    fb_slot(b, b.wp + 1) = c.y;
+    fb_slot(b, b.wp + 2) = c.z;
+    fb_slot(b, b.wp + 3) = c.w;
     b.wp += 4;
 }
 
 // top the ring up (both chunk loads issued before either is stored); never
-// past FB_RING words from rp, the slot the reader still re-reads
-GRK_HD void fb_fill(FlatBits &b) {
-    const uint32_t held = b.wp - b.rp;
+// past FB_RING words from rp, the oldest word the reader still reads
+GRK_HD void fb_fill(FlatBits &b, uint32_t rp) {
+    const uint32_t held = b.wp - rp;
     if (held <= FB_RING - 8) {
         const uint4 c0 = fb_load(b, b.chunk), c1 = fb_load(b, b.chunk + 1);
         b.chunk += 2;
@@ -135,17 +148,8 @@ GRK_HD void fb_start(FlatBits &b, const uint32_t *words, uint32_t nwords) {
     b.base = (const uint4 *)words;
     b.nchunks = (nwords + 3) >> 2;
     b.chunk = 0;
-    b.rp = b.wp = 0;
-    fb_fill(b);
-}
-
-// ring word rp (the ring holds it: rp < wp, or a dry ring is refilled from HBM)
-GRK_HD uint32_t fb_at(FlatBits &b) {
-    if (b.rp >= b.wp) {  // dry: straight from HBM
-        const uint4 c0 = fb_load(b, b.chunk++);
-        fb_put(b, c0);
-    }
-    return b.ring[(b.rp % FB_RING) << b.rsh];
+    b.wp = 0;
+    fb_fill(b, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -158,13 +162,13 @@ template <bool LAZY>
 struct BitDecT {
     static constexpr bool kLazy = LAZY;
     FlatBits bits;
-    uint32_t A, C, consumed, cq, cqn;  // cq: next carry event, cqn: the one after
-    // the stream bits not yet in C: the window {w0, w1} from bit offset 32 - t
-    // of w0 (t in [0, 31]; t = 0: w0 is used up, the bits start with w1), so
-    // alignbit(w0, w1, t) is the next 32 of them.  nextw: the ring word after
-    // w1 (ring slot bits.rp), re-read from the ring at every decision -- the
-    // read needs no branch, and by the next word advance it has landed
-    uint32_t w0, w1, t, nextw;
+    uint32_t A, C;
+    uint32_t cq, cqn;  // next carry event (a stream bit index, Unstuff), the one after
+    // the window {w0, w1}, the position u (see FlatBits) and nextw, word
+    // K + 1, re-read from the ring at every decision -- the read needs no
+    // branch, and by the next word advance it has landed
+    uint32_t w0, w1, u, nextw;
+    uint32_t ulim;  // u below it: a carry event is due or the ring is dry
     const uint32_t *cp;
     bool raw;  // the current segment is raw (BYPASS): bits straight from the stream
     // the lane's word ring (FlatBits), set once before the first init
@@ -172,60 +176,92 @@ struct BitDecT {
         bits.ring = ring;
         bits.rsh = rsh;
     }
-    // stripe start (t1_decode_passes): top the word ring up from HBM
-    GRK_HD void fill() { fb_fill(bits); }
-    GRK_HD void load_window() {
-        w0 = fb_at(bits);
-        ++bits.rp;
-        w1 = fb_at(bits);
-        ++bits.rp;
-        nextw = fb_at(bits);
+    GRK_HD uint32_t next_word() const { return ~u >> 5; }  // K + 1 = (pos + 63) >> 5
+    // u < ulim: pos passed the carry event cq (pos > cq: u < ~(cq + 63)), or
+    // word K + 1 is not in the ring (K + 1 >= wp: u <= ~(32 wp))
+    GRK_HD void set_limit() {
+        const uint32_t lc = cq == 0xffffffffu ? 0u : ~(cq + 63u);
+        const uint32_t ld = ~(32u * bits.wp) + 1u;
+        ulim = lc > ld ? lc : ld;
     }
-    // n bits consumed: the window moves by n (n <= 16); a move past w0 takes
-    // the next word (a select, no branch) and reads the one after from the ring
+    // stripe start (t1_decode_passes): top the word ring up from HBM
+    GRK_HD void fill() {
+        fb_fill(bits, next_word());
+        set_limit();
+    }
+    // the rare path of a move to u1: a carry event, a dry ring (a chunk
+    // straight from HBM), or both; the carry is added to C after its shift
+    GRK_HD void slow(const uint32_t u1) {
+        const uint32_t pos1 = ~u1 - 63u;
+        if (cq != 0xffffffffu && cq < pos1) {  // carry event (see Unstuff)
+            C += 1u << (16 + pos1 - cq);
+            next_carry();
+        }
+        if ((~u1 >> 5) >= bits.wp) {
+            const uint4 c0 = fb_load(bits, bits.chunk++);
+            fb_put(bits, c0);
+        }
+        set_limit();
+    }
+    // the window moves by n bits (n <= 16): a move past w0 takes the next
+    // word (a select, no branch) and reads the one after from the ring
     GRK_HD void advance(uint32_t n) {
-        const bool cross = t < n;
-        t = (t - n) & 31u;
+        const bool cross = (u & 31u) < n;  // fewer than n bits left in w0
         w0 = cross ? w1 : w0;
         w1 = cross ? nextw : w1;
-        bits.rp += cross ? 1u : 0u;
-        nextw = fb_at(bits);
+        u -= n;
+        if (u < ulim) slow(u);
+        nextw = bits.ring[ring_slot(u) << bits.rsh];
+    }
+    // bits [8:5] of u, as one v_bfe_u32 (the compiler's shift-and-mask form
+    // of it costs an op more on the address)
+    GRK_HD static uint32_t ring_slot(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        uint32_t r;
+        asm("v_bfe_u32 %0, %1, 5, 4" : "=v"(r) : "v"(v));
+        return r;
+#else
+        return (v >> 5) & (FB_RING - 1);
+#endif
     }
     // raw segment (mqc_raw_init_dec / mqc_raw_decode, mqc_dec.cpp:195-200,
     // mqc_dec_inl.h:90-112): the unstuffed stream IS the raw bit sequence --
     // 7 bits from the byte after a 0xFF, 1-bits from a marker on
     GRK_HD void init_raw(const uint32_t *words, uint32_t nwords) {
         fb_start(bits, words, nwords);
-        // the first bit is the first word's MSB, offset 0 of the window -- which
-        // t cannot express -- so the window starts one word earlier, at its
-        // end: w0 = (none), w1 = word 0, t = 0, nextw = word 1
+        // pos 0: K = 0, so w1 = word 0 and w0 = (none); nextw = word 1
         w0 = 0;
-        w1 = fb_at(bits);
-        ++bits.rp;
-        nextw = fb_at(bits);
-        t = 0;
+        w1 = fb_slot(bits, 0);
+        nextw = fb_slot(bits, 1);
+        u = ~63u;
+        cq = cqn = 0xffffffffu;
+        set_limit();
         raw = true;
     }
     GRK_HD uint32_t rawbit() {
-        const uint32_t b = alignbit32(w0, w1, t) >> 31;
+        const uint32_t b = alignbit32(w0, w1, u) >> 31;
         advance(1);
         return b;
     }
     GRK_HD void init(const uint32_t *words, uint32_t nwords, const uint32_t *carries) {
         raw = false;
         fb_start(bits, words, nwords);
-        load_window();
-        C = w0 >> 1;  // first 31 stream bits (INITDEC: consumed 24, then 7 shifts)
-        t = 1;        // the next bit is w0's last
+        // pos 31 (INITDEC: consumed 24, then 7 shifts): C = the first 31
+        // stream bits, K = 1 (w0 = word 0, w1 = word 1), nextw = word 2
+        w0 = fb_slot(bits, 0);
+        w1 = fb_slot(bits, 1);
+        nextw = fb_slot(bits, 2);
+        C = w0 >> 1;
+        u = ~(31u + 63u);
         A = 0x80000000u;  // 0x8000 << 16
-        consumed = 31;
         cq = carries[0];
         cp = carries + 1;
         if (cq < 31) { C += 1u << (16 + 31 - cq); cq = *cp++; }
         cqn = cq == 0xffffffffu ? cq : *cp++;  // the sentinel ends the list: never read past it
+        set_limit();
     }
     // the carry event after the one just applied: cqn was loaded one event
-    // earlier, so the per-decision compare never waits on a load
+    // earlier, so the rare path never waits on a load
     GRK_HD void next_carry() {
         cq = cqn;
         cqn = cq == 0xffffffffu ? cq : *cp++;
@@ -272,16 +308,19 @@ struct BitDecT {
         const bool keep = !lo && (int32_t)a < 0;  // MPS, no renormalisation
         C = lo ? C : C - qe;
         a = lo ? qe : a;
-        const uint32_t tw = tab[(wd >> (lps ? 7 : 0)) & 127u];
+        const uint32_t tw = tab[(wd >> (lps ? 8 : 1)) & 127u];
         const uint32_t n = clz32(a);
-        const uint32_t win = alignbit32(w0, w1, t);
+        const uint32_t win = alignbit32(w0, w1, u);
         C = (C << n) | bfe32(win, 32 - n, n);
         A = a << n;
-        const uint32_t c1 = consumed + n;
-        if (cq < c1) { C += 1u << (16 + c1 - cq); next_carry(); }  // carry event (see Unstuff)
-        consumed = c1;
         advance(n);
-        const uint32_t bit = ((wd >> 15) & 1u) ^ (uint32_t)lps;
+        // the bit as (wd ^ lps) & 1 on a materialised lps (one select and
+        // one 3-input op), not the mask logic the compiler would form
+        uint32_t lv = lps ? 1u : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(lv));
+#endif
+        const uint32_t bit = (wd ^ lv) & 1u;
         wd = keep ? wd : tw;
         return bit;
     }

@@ -142,15 +142,16 @@ GRK_HD void mq_reset_words(uint32_t *cxw, const uint32_t *tab) {
 
 // The DECODER's context words (t1_flat.h BitDecT::step): one word per
 // (state, MPS) pair i = 2 state + mps, so an LPS exchange needs no MPS
-// arithmetic -- Qe[31:16] | MPS[15] | next pair on LPS [13:7] | next pair on
-// MPS [6:0] (the LPS successor already carries SWITCH's MPS flip).  Qe sits
+// arithmetic -- Qe[31:16] | next pair on LPS [14:8] | next pair on MPS [7:1]
+// | MPS [0] (the LPS successor already carries SWITCH's MPS flip).  Qe sits
 // where the decoder's A and C registers compare against it (A held << 16,
-// C[31:16] = Chigh), so the decision needs no shifts of it.  94 entries
-// generated from the encoder table (ISO 15444-1 Table C.2).
+// C[31:16] = Chigh), so the decision needs no shifts of it, and the decoded
+// bit is (word ^ LPS) & 1.  94 entries generated from the encoder table
+// (ISO 15444-1 Table C.2).
 GRK_HD uint32_t mq_dec_word(const uint32_t *tab47, uint32_t i) {
     const uint32_t st = i >> 1, m = i & 1, t = tab47[st];
     const uint32_t qe = t & 0xffffu, nm = (t >> 16) & 63u, nl = (t >> 22) & 63u, sw = (t >> 28) & 1u;
-    return (qe << 16) | (m << 15) | ((2 * nl + (m ^ sw)) << 7) | (2 * nm + m);
+    return (qe << 16) | ((2 * nl + (m ^ sw)) << 8) | ((2 * nm + m) << 1) | m;
 }
 constexpr uint32_t MQ_DEC_WORDS = 94;
 // mqc_resetstates (mqc_dec.cpp:207-215) in decoder words: UNI -> 46, AGG -> 3,

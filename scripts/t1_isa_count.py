@@ -2,8 +2,8 @@
 (the innermost loop of k_t1_decode_ub<64, false, 4, 4> that holds both the
 ctz of the refinement word and the MQ renormalisation's clz), from the
 gfx950 assembly: VALU / SALU / LDS / VMEM per iteration along the common
-path (the carry-event and dry-ring blocks excluded, the word-ring refill
-counted both ways).
+path (every exec-masked region of the loop skipped: the carry-event and
+dry-ring blocks, entered only when a lane needs them).
   python scripts/t1_isa_count.py [kernels.hip]"""
 import os
 import re
@@ -68,18 +68,32 @@ def kind(x):
 
 
 tot = {"valu": 0, "salu": 0, "lds": 0, "vmem": 0, "other": 0}
-used, rare = [], []
-for b in best[1]:
-    ins = blocks[b]
-    # blocks entered only for a carry event (global_load of the next event)
-    # or a dry word ring (global_load_dwordx4 of a chunk) are off the common path
-    if any(x.startswith("global_load") for x in ins):
-        rare.append(b)
-        continue
+# the common path: from the header, every exec-masked region inside the loop
+# skipped (its s_cbranch_execz taken: the carry-event / dry-ring paths, which
+# a wavefront enters only when one of its lanes needs them), back to the header
+inloop = set(best[1])
+pos = order.index(best[0])
+used, seen = [], set()
+while True:
+    b = order[pos]
+    if b in seen:
+        break
+    seen.add(b)
     used.append(b)
-    for x in ins:
+    nxt = pos + 1
+    for x in blocks[b]:
         tot[kind(x)] += 1
-print("MRP decision loop of %s (header %s): common-path blocks %s; rare blocks %s" % (
+        m = re.match(r"s_(cbranch_execz|branch)\s+(\S+)", x)
+        if m:
+            tgt = m.group(2).replace(".L", ".L")
+            if m.group(1) == "branch" or tgt in inloop:
+                nxt = order.index(tgt)
+            break
+    if nxt >= len(order) or order[nxt] not in inloop:
+        break
+    pos = nxt
+rare = [b for b in best[1] if b not in used]
+print("MRP decision loop of %s (header %s): common-path blocks %s; skipped %s" % (
     name[:48], best[0], " ".join(used), " ".join(rare)))
-print("per decision (common path, ring refill taken by some lane): VALU %d  SALU %d  LDS %d  VMEM %d"
+print("per decision (common path: no lane in a carry event or on a dry ring): VALU %d  SALU %d  LDS %d  VMEM %d"
       % (tot["valu"], tot["salu"], tot["lds"], tot["vmem"]))
