@@ -100,6 +100,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         nz = CUP ? 0xFu : z;
     }
     uint32_t todo = nz & ~sig4 & ~vis4 & rows;
+    const uint32_t todo0 = todo;
     uint32_t kind = 0, r = 0;  // 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo)
     if (CUP && nr == 4 && P == 0 && vis4 == 0) {
         kind = 2;
@@ -110,7 +111,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     // the sign window, read at the column start by every lane: a lane's first
     // sign symbol comes at almost every decision step of a wavefront, so a
     // lazy read would be a branch entered at every step
-    uint32_t Q = win18(s.neg, x), newsig = 0, newneg = 0, newvis = 0, si = 0;
+    uint32_t Q = win18(s.neg, x), si = 0;
     // The symbol-kind transitions are selects, not branches: the 64 lanes of
     // a wavefront sit in different kinds, and every branch taken by any lane
     // costs the whole wavefront its exec-mask bookkeeping.
@@ -126,13 +127,12 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const uint32_t bit = d.decode(cxw, T.mq, cx);
         if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
         const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;
-        newvis |= (!CUP && k0) ? 1u << r : 0u;
         // SC: the sample is significant with sign sg
         const uint32_t sg = bit ^ ((D::kLazy && d.raw) ? 0u : (si >> 7));  // a raw sign is the sign itself
+        // the new significance and sign go into the windows only: the
+        // column's new rows are read back from them once, after the loop
         P |= k1 ? 1u << (sh + 4) : 0u;
         Q |= k1 ? sg << (sh + 4) : 0u;
-        newsig |= k1 ? 1u << r : 0u;
-        newneg |= k1 ? sg << r : 0u;
         // the sample below now has a significant neighbour (SPP)
         todo |= (!CUP && k1) ? (rows & ~(sig4 | vis4)) & (2u << r) : 0u;
         // UNI, UNI: the run position; the rows after it are plain ZC
@@ -145,10 +145,14 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         if (advance && !todo) break;
         r = advance ? (uint32_t)__builtin_ctz(todo | 0x10u) : r;
     }
+    const uint32_t newsig = win_self4(P) & ~sig4;
+    // SPP: every row of the column's candidates was visited (a ZC symbol),
+    // the rows a new significant sample above made candidates included
+    const uint32_t newvis = todo0 | ((newsig << 1) & rows & ~(sig4 | vis4));
     if (!CUP && newvis) setcol4(s.vis, x, newvis);
     if (newsig) {
         setcol4(s.sig + 1, x, newsig);
-        setcol4(s.neg + 1, x, newneg);
+        setcol4(s.neg + 1, x, win_self4(Q) & newsig);
         return true;
     }
     return false;

@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "grokimagecompression_amd", "csrc", "kernels.hip")
+src = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else os.path.join(ROOT, "grokimagecompression_amd", "csrc", "kernels.hip")
 out = "/tmp/t1_isa_%d.s" % os.getpid()
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                 "--cuda-device-only", "-S", src, "-o", out], check=True, cwd=os.path.dirname(src),
@@ -67,33 +67,64 @@ def kind(x):
     return "other"
 
 
-tot = {"valu": 0, "salu": 0, "lds": 0, "vmem": 0, "other": 0}
-# the common path: from the header, every exec-masked region inside the loop
-# skipped (its s_cbranch_execz taken: the carry-event / dry-ring paths, which
-# a wavefront enters only when one of its lanes needs them), back to the header
-inloop = set(best[1])
-pos = order.index(best[0])
-used, seen = [], set()
-while True:
-    b = order[pos]
-    if b in seen:
-        break
-    seen.add(b)
-    used.append(b)
-    nxt = pos + 1
-    for x in blocks[b]:
-        tot[kind(x)] += 1
-        m = re.match(r"s_(cbranch_execz|branch)\s+(\S+)", x)
-        if m:
-            tgt = m.group(2).replace(".L", ".L")
-            if m.group(1) == "branch" or tgt in inloop:
-                nxt = order.index(tgt)
+def common_path(hdr, loop_blocks):
+    """instruction counts along the loop's common path: from the header, every
+    exec-masked region inside the loop skipped (its s_cbranch_execz taken:
+    the carry-event / dry-ring paths, entered only when one of the
+    wavefront's lanes needs them), back to the header"""
+    tot = {"valu": 0, "salu": 0, "lds": 0, "vmem": 0, "other": 0}
+    inloop = set(loop_blocks)
+    pos = order.index(hdr)
+    used, seen = [], set()
+    while True:
+        b = order[pos]
+        if b in seen:
             break
-    if nxt >= len(order) or order[nxt] not in inloop:
-        break
-    pos = nxt
+        seen.add(b)
+        used.append(b)
+        nxt = pos + 1
+        for x in blocks[b]:
+            tot[kind(x)] += 1
+            m = re.match(r"s_(cbranch_execz|branch)\s+(\S+)", x)
+            if m:
+                if m.group(1) == "branch" or m.group(2) in inloop:
+                    nxt = order.index(m.group(2))
+                break
+        if nxt >= len(order) or order[nxt] not in inloop:
+            break
+        pos = nxt
+    return tot, used
+
+
+tot, used = common_path(best[0], best[1])
 rare = [b for b in best[1] if b not in used]
 print("MRP decision loop of %s (header %s): common-path blocks %s; skipped %s" % (
     name[:48], best[0], " ".join(used), " ".join(rare)))
 print("per decision (common path: no lane in a carry event or on a dry ring): VALU %d  SALU %d  LDS %d  VMEM %d"
       % (tot["valu"], tot["salu"], tot["lds"], tot["vmem"]))
+if "--all" in sys.argv:
+    # every innermost loop with a decode site (the MQ table read), in code order
+    for hb in order:
+        key = hb.lstrip(".L")
+        lb = [b for b in order if loopof.get(b) == key or b == hb]
+        if len(lb) < 2 or not any("offset:" in x and x.startswith("ds_read_b32") and "v_ffbh_u32" in " ".join(blocks[hb] + sum((blocks[c] for c in lb), []))
+                                  for b in lb for x in blocks[b]):
+            continue
+        if not any(x.startswith("v_ffbh_u32") for b in lb for x in blocks[b]):
+            continue
+        # the whole body less the bit reader's rare region: the blocks from
+        # the one after the renormalisation's limit branch (the block with
+        # the window alignbit ends in it) up to that branch's target
+        rare = set()
+        for b in lb:
+            if any(x.startswith("v_alignbit_b32") for x in blocks[b]) and blocks[b][-1].startswith("s_cbranch_execz"):
+                tgt = blocks[b][-1].split()[1]
+                i, j = order.index(b) + 1, order.index(tgt)
+                rare.update(order[i:j])
+        t = {"valu": 0, "salu": 0, "lds": 0, "vmem": 0, "other": 0}
+        for b in lb:
+            if b not in rare:
+                for x in blocks[b]:
+                    t[kind(x)] += 1
+        print("  loop %s: %d blocks; all but the bit reader's rare path (every masked region entered): VALU %d SALU %d LDS %d"
+              % (hb, len(lb), t["valu"], t["salu"], t["lds"]))
