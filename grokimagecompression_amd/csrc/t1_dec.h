@@ -73,6 +73,16 @@ GRK_HD void keep_here(uint32_t v) {
 #endif
 }
 
+// true if p holds on any active lane of the wavefront (wave-uniform); the
+// host build runs one block at a time
+GRK_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(p) != 0;
+#else
+    return p;
+#endif
+}
+
 struct DecTables {
     const uint8_t *zc;   // 512 entries for this block's orientation
     const uint8_t *sc;   // 256, window order
@@ -201,6 +211,20 @@ GRK_HD void d3_mrp_stripe(D &d, uint32_t *cxw, const DecTables &T, const uint64_
         uint32_t E = nib4(e, sh);
         const uint32_t R = nib4(ref, sh), N = nib4(nb, sh);
         uint32_t res = 0;
+        // context 14 (a first refinement without a significant neighbour) is
+        // rare (~1 in 10^5 refinement decisions): a group no lane of the
+        // wavefront needs it for picks between 15 and 16 on one mask bit
+        if (REG && !wave_any((E & ~R & ~N) != 0)) {
+            while (E) {
+                const uint32_t pos = (uint32_t)__builtin_ctz(E);
+                E &= E - 1;
+                const bool r2 = (R >> pos) & 1;
+                uint32_t wd = r2 ? w2 : w1;
+                res |= d.decode_reg(wd, T.mq, CX_MAG + (r2 ? 2u : 1u)) << pos;
+                w1 = r2 ? w1 : wd;
+                w2 = r2 ? wd : w2;
+            }
+        }
         while (E) {
             const uint32_t pos = (uint32_t)__builtin_ctz(E);
             E &= E - 1;

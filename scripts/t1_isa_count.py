@@ -44,14 +44,19 @@ for ln in lines:
 # the MRP loop: the innermost loop whose header starts with the ctz (v_ffbl)
 # of the refinement word and whose body holds the renormalisation clz
 hdrs = [b for b in order if blocks[b] and blocks[b][0].startswith("v_ffbl_b32")]
-best = None
+mrp = []
 for hb in hdrs:
     key = hb.lstrip(".L")
     body_blocks = [b for b in order if loopof.get(b) == key or b == hb]
     if any(x.startswith("v_ffbh_u32") for b in body_blocks for x in blocks[b]):
-        best = (hb, body_blocks)
-if best is None:
+        mrp.append((hb, body_blocks))
+if not mrp:
     sys.exit("MRP loop not found")
+# the single-segment path comes last in the kernel: its two MRP loops are the
+# two-way one (contexts 15 / 16, taken unless a lane needs context 14) and the
+# three-way one
+mrp = mrp[-2:]
+best = mrp[0]
 
 
 def kind(x):
@@ -96,12 +101,13 @@ def common_path(hdr, loop_blocks):
     return tot, used
 
 
-tot, used = common_path(best[0], best[1])
-rare = [b for b in best[1] if b not in used]
-print("MRP decision loop of %s (header %s): common-path blocks %s; skipped %s" % (
-    name[:48], best[0], " ".join(used), " ".join(rare)))
-print("per decision (common path: no lane in a carry event or on a dry ring): VALU %d  SALU %d  LDS %d  VMEM %d"
-      % (tot["valu"], tot["salu"], tot["lds"], tot["vmem"]))
+for label, lp in zip(("two-way (15 / 16)", "three-way (14 / 15 / 16)"), mrp):
+    tot, used = common_path(lp[0], lp[1])
+    rare = [b for b in lp[1] if b not in used]
+    print("MRP decision loop, %s contexts, of %s (header %s): common-path blocks %s; skipped %s" % (
+        label, name[:48], lp[0], " ".join(used), " ".join(rare)))
+    print("  per decision (common path: no lane in a carry event or on a dry ring): VALU %d  SALU %d  LDS %d  VMEM %d"
+          % (tot["valu"], tot["salu"], tot["lds"], tot["vmem"]))
 if "--all" in sys.argv:
     # every innermost loop with a decode site (the MQ table read), in code order
     for hb in order:
