@@ -94,6 +94,11 @@ struct grkgpu_ctx {
     HostBuf h_results, h_packed, h_gather, h_blocks, h_out, h_symoff, h_dwtjobs, h_segs;
     DevBuf dwtjobs53;  // decode: the 5/3 tile-components' job table when 9/7 ones share the call
     DevBuf t1order;    // encode: the MQ coder's work order (keys, permutation, bucket counters)
+    // encode with rate control: the pass records formed on the device
+    // (launch_pass_records): per block its distortion factor and record slots
+    // (in), its summary and records (out)
+    DevBuf pinfo, precs;
+    HostBuf h_pinfo, h_psum, h_precs;
     // encode: the pass records of the last call, kept so that a frame of the
     // same size does not zero ~20 MB again before overwriting every record
     std::vector<EncPass> enc_passes;
@@ -1183,6 +1188,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     };
     std::vector<BlkInfo> binfo;
     std::vector<uint64_t> symoff;  // per-block symbol-stream slots, sized by the band's numbps bound
+    std::vector<uint32_t> pcap;    // per-block pass-record slots (3 numbps - 2 of that bound)
     uint64_t sym_total = 0;
     uint32_t maxdepth = 1;
     // tile geometry (independent per tile) on the host pool, then the block
@@ -1237,6 +1243,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
                 binfo.push_back({k, tc.numres - 1 - resno, band.bandno, band.stepsize, tile.index, resno, precno,
                                  cblkno, cb.r});
                 const uint32_t bound = std::min<uint32_t>(band.numbps, 32);
+                pcap.push_back(bound ? 3 * bound - 2 : 0);
                 symoff.push_back(sym_total);
                 sym_total += (uint64_t)bound * sym_slot_bytes(b.w, b.h);
                 maxdepth = std::max(maxdepth, bound);
@@ -1383,27 +1390,6 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
     bool need_rc = force_dist != 0;
     for (uint32_t l = 0; l < cp.numlayers; ++l)
         need_rc = need_rc || (cp.disto_alloc && cp.rates[l] > 0.0) || (cp.fixed_quality && cp.distoratio[l] > 0.0f);
-    if (need_rc)
-        HIPCHK(launch_t1_dist(c->blocks.as<EncBlock>(), nblk, maxdepth, c->coef.as<int32_t>(), c->scratch.p,
-                              c->results.as<EncResult>(), s));
-    HIPCHK(hipEventRecord(c->ev[4], s));
-    if (nblk)
-        HIPCHK(hipMemcpy2DAsync(c->h_results.p, sizeof(EncResult), c->results.p, sizeof(EncResult),
-                                need_rc ? sizeof(EncResult) : ENC_RESULT_RATE_BYTES, nblk, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const EncResult *res = c->h_results.as<EncResult>();
-
-    // Tier-2 + headers on the host (j2k_encode :2059, j2k_post_write_tile
-    // :2196, T2::encode_packets): only header BITS are produced here; the
-    // code-block bytes never visit the host -- a gather kernel assembles the
-    // codestream in HBM and one D2H copies it into the pinned output buffer.
-    double t_t2 = now_ms();
-    const uint32_t L = cp.numlayers;
-    std::vector<EncCblkState> cst(nblk);
-    std::vector<EncPass> &passes = c->enc_passes;  // [0, npass) filled below; the tail is unused
-    uint32_t npass = 0;
-    std::vector<EncLayer> layers((size_t)nblk * L, EncLayer{0, 0, 0, 0.0});
-    std::vector<double> blk_disto(nblk, 0.0);
     const double *mct_norms = nullptr;
     uint32_t mct_numcomps = 0;
     if (cp.mct == 1) {  // TileProcessor::t1_encode (TileProcessor.cpp:1535-1551), mct.cpp:65-79
@@ -1414,60 +1400,147 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         mct_numcomps = nc;
         if (cp.mct == 2) mct_norms = cp.mct_norms;
     }
-    // per-block pass records: validate and lay the blocks' passes out (prefix
-    // sum), then fill them on the host pool (blocks are independent)
-    uint64_t nsym = 0;
-    {
+    // With rate control the pass records are formed on the device
+    // (launch_pass_records): the host fills each block's distortion factor
+    // and record slots while the GPU codes, and after the coders only the
+    // records and per-block summaries come back.  Without it the host forms
+    // them from the coders' results (rates only: no distortion to weigh).
+    const bool dev_rec = need_rc && nblk;
+    uint64_t ptotal = 0;
+    if (dev_rec) {
+        HIPCHK(c->h_pinfo.ensure((size_t)nblk * 16 + 8 + 256));
+        double *wf = c->h_pinfo.as<double>();
+        uint64_t *p0 = (uint64_t *)(wf + nblk);
         for (uint32_t i = 0; i < nblk; ++i) {
-            const EncResult &r = res[i];
-            if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
-            if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
-            const uint32_t np = r.numpasses;
-            if (np && r.rate[np - 1] > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
-            nsym += r.nsym;
-            EncCblkState &st = cst[i];
-            st.numbps = r.numbps;
-            st.numpasses = np;
-            st.pass0 = npass;
-            st.dev_off = eb[i].out_off;
-            npass += np;
-        }
-        if (passes.size() < npass) passes.resize(npass);
-    }
-    host_parallel_for(nblk, 1024, [&](size_t b0, size_t b1) {
-        for (size_t i = b0; i < b1; ++i) {
-            const EncResult &r = res[i];
-            const uint32_t np = r.numpasses;
-            EncPass *out = passes.data() + cst[i].pass0;
-            double cum = 0.0;
             const BlkInfo &bi = binfo[i];
-            const double wfac = need_rc ? t1_wmsedec_factor(bi.compno, bi.level, bi.orient, cp.irrev ? 0 : 1,
-                                                            (double)bi.stepsize, mct_norms, mct_numcomps)
-                                        : 0.0;
-            for (uint32_t k = 0; k < np; ++k) {
-                EncPass ps;
-                ps.rate = r.rate[k];
-                ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
-                // t1_enc_is_term_pass (t1.cpp:1131-1151)
-                {
-                    const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
-                    const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
-                    ps.term = t1_pass_term(cp.cblksty, bp, pt, r.numbps);
-                }
-                ps.slope = 0;
-                if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
-                    const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
-                    cum += t1_wmsedec_at(wfac, r.nmsedec[k], bpno);
-                }
-                ps.dd = cum;
-                out[k] = ps;
-            }
-            // the simple PCRD's slope range over this block's passes, from
-            // the records just written (pcrd_simple's own loop, TileEnc::slopes)
-            block_slopes(cst[i], out);
-            blk_disto[i] = cum;
+            wf[i] = t1_wmsedec_factor(bi.compno, bi.level, bi.orient, cp.irrev ? 0 : 1, (double)bi.stepsize, mct_norms,
+                                      mct_numcomps);
+            p0[i] = ptotal;
+            ptotal += pcap[i];
         }
-    });
+        p0[nblk] = ptotal;
+        HIPCHK(c->pinfo.ensure((size_t)nblk * 16 + 8 + 256));
+        HIPCHK(hipMemcpyAsync(c->pinfo.p, c->h_pinfo.p, (size_t)nblk * 16 + 8, hipMemcpyHostToDevice, s));
+    }
+    if (need_rc)
+        HIPCHK(launch_t1_dist(c->blocks.as<EncBlock>(), nblk, maxdepth, c->coef.as<int32_t>(), c->scratch.p,
+                              c->results.as<EncResult>(), s));
+    HIPCHK(hipEventRecord(c->ev[4], s));
+    if (dev_rec) {
+        const size_t sum_bytes = ((size_t)nblk * sizeof(PassSum) + 255) & ~(size_t)255;
+        HIPCHK(c->precs.ensure(sum_bytes + ptotal * sizeof(DevPass) + 256));
+        HIPCHK(c->h_psum.ensure(sum_bytes + 256));
+        HIPCHK(c->h_precs.ensure(ptotal * sizeof(DevPass) + 256));
+        PassSum *dsum = c->precs.as<PassSum>();
+        DevPass *dpass = (DevPass *)(c->precs.as<uint8_t>() + sum_bytes);
+        const double *dwf = c->pinfo.as<double>();
+        HIPCHK(launch_pass_records(c->blocks.as<EncBlock>(), c->results.as<EncResult>(), dwf,
+                                   (const uint64_t *)(dwf + nblk), nblk, cp.cblksty, dpass, dsum, s));
+        HIPCHK(hipMemcpyAsync(c->h_psum.p, dsum, (size_t)nblk * sizeof(PassSum), hipMemcpyDeviceToHost, s));
+        if (ptotal)
+            HIPCHK(hipMemcpyAsync(c->h_precs.p, dpass, ptotal * sizeof(DevPass), hipMemcpyDeviceToHost, s));
+    } else if (nblk) {
+        HIPCHK(hipMemcpy2DAsync(c->h_results.p, sizeof(EncResult), c->results.p, sizeof(EncResult),
+                                ENC_RESULT_RATE_BYTES, nblk, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    const EncResult *res = c->h_results.as<EncResult>();
+
+    // Tier-2 + headers on the host (j2k_encode :2059, j2k_post_write_tile
+    // :2196, T2::encode_packets): only header BITS are produced here; the
+    // code-block bytes never visit the host -- a gather kernel assembles the
+    // codestream in HBM and one D2H copies it into the pinned output buffer.
+    double t_t2 = now_ms();
+    const uint32_t L = cp.numlayers;
+    std::vector<EncCblkState> cst(nblk);
+    std::vector<EncPass> &passes = c->enc_passes;  // host-formed records: [0, npass) filled below
+    EncPass *precs = nullptr;                      // the records Tier-2 reads: these, or the device's
+    uint64_t npass = 0;
+    std::vector<EncLayer> layers((size_t)nblk * L, EncLayer{0, 0, 0, 0.0});
+    std::vector<double> blk_disto(nblk, 0.0);
+    std::vector<uint32_t> blen(nblk, 0);  // each block's MQ bytes
+    uint64_t nsym = 0;
+    if (dev_rec) {
+        const PassSum *sm = c->h_psum.as<PassSum>();
+        const uint64_t *p0 = (const uint64_t *)(c->h_pinfo.as<double>() + nblk);
+        for (uint32_t i = 0; i < nblk; ++i) {
+            const PassSum &q = sm[i];
+            if (q.bad & 1u) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
+            if (q.bad & 2u) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
+            if (q.bad & 4u) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+            nsym += q.nsym;
+            EncCblkState &st = cst[i];
+            st.numbps = q.numbps;
+            st.numpasses = q.numpasses;
+            st.pass0 = (uint32_t)p0[i];
+            st.dev_off = eb[i].out_off;
+            st.smin = q.smin;
+            st.smax = q.smax;
+            st.s0max = q.s0max;
+            st.z0 = q.z0 != 0;
+            blk_disto[i] = q.disto;
+            blen[i] = q.len;
+        }
+        if (ptotal > 0xffffffffu) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
+        npass = ptotal;
+        precs = c->h_precs.as<EncPass>();
+    } else {
+        // per-block pass records: validate and lay the blocks' passes out (prefix
+        // sum), then fill them on the host pool (blocks are independent)
+        {
+            for (uint32_t i = 0; i < nblk; ++i) {
+                const EncResult &r = res[i];
+                if (r.pad) return set_err(GRKGPU_EUNSUPPORTED, "code-block numbps exceeds its band's bound");
+                if (r.numpasses > GRK_MAX_PASSES) return set_err(GRKGPU_EUNSUPPORTED, "too many coding passes");
+                const uint32_t np = r.numpasses;
+                if (np && r.rate[np - 1] > eb[i].w * eb[i].h * 4 + 64) return set_err(GRKGPU_EUNSUPPORTED, "MQ slab overflow");
+                nsym += r.nsym;
+                EncCblkState &st = cst[i];
+                st.numbps = r.numbps;
+                st.numpasses = np;
+                st.pass0 = (uint32_t)npass;
+                st.dev_off = eb[i].out_off;
+                npass += np;
+            }
+            if (passes.size() < npass) passes.resize(npass);
+        }
+        host_parallel_for(nblk, 1024, [&](size_t b0, size_t b1) {
+            for (size_t i = b0; i < b1; ++i) {
+                const EncResult &r = res[i];
+                const uint32_t np = r.numpasses;
+                EncPass *out = passes.data() + cst[i].pass0;
+                double cum = 0.0;
+                const BlkInfo &bi = binfo[i];
+                const double wfac = need_rc ? t1_wmsedec_factor(bi.compno, bi.level, bi.orient, cp.irrev ? 0 : 1,
+                                                                (double)bi.stepsize, mct_norms, mct_numcomps)
+                                            : 0.0;
+                for (uint32_t k = 0; k < np; ++k) {
+                    EncPass ps;
+                    ps.rate = r.rate[k];
+                    ps.len = r.rate[k] - (k ? r.rate[k - 1] : 0);
+                    // t1_enc_is_term_pass (t1.cpp:1131-1151)
+                    {
+                        const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                        const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
+                        ps.term = t1_pass_term(cp.cblksty, bp, pt, r.numbps);
+                    }
+                    ps.slope = 0;
+                    if (need_rc) {  // t1_encode_cblk's cumulative distortion (t1.cpp:1249-1254)
+                        const int32_t bpno = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+                        cum += t1_wmsedec_at(wfac, r.nmsedec[k], bpno);
+                    }
+                    ps.dd = cum;
+                    out[k] = ps;
+                }
+                // the simple PCRD's slope range over this block's passes, from
+                // the records just written (pcrd_simple's own loop, TileEnc::slopes)
+                block_slopes(cst[i], out);
+                blk_disto[i] = cum;
+            }
+        });
+        precs = passes.data();
+        for (uint32_t i = 0; i < nblk; ++i) blen[i] = res[i].len;
+    }
     const double t_passrec = now_ms() - t_t2;
     if (export_blocks) {
         // the MQ slab to pinned host memory, then one record per block
@@ -1478,8 +1551,8 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
         c->bexp_rate.resize((size_t)npass + 1);
         c->bexp_dist.resize((size_t)npass + 1);
         for (size_t k = 0; k < npass; ++k) {
-            c->bexp_rate[k] = passes[k].rate;
-            c->bexp_dist[k] = passes[k].dd;
+            c->bexp_rate[k] = precs[k].rate;
+            c->bexp_dist[k] = precs[k].dd;
         }
         for (uint32_t i = 0; i < nblk; ++i) {
             grkgpu_block_info &o = c->bexp[i];
@@ -1489,7 +1562,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             o.x0 = bi.r.x0; o.y0 = bi.r.y0; o.x1 = bi.r.x1; o.y1 = bi.r.y1;
             o.numbps = cst[i].numbps;
             o.numpasses = cst[i].numpasses;
-            o.len = res[i].len;
+            o.len = blen[i];
             o.stepsize = bi.stepsize;
             o.data = c->h_slab.as<uint8_t>() + eb[i].out_off;
             o.rate = c->bexp_rate.data() + cst[i].pass0;
@@ -1624,7 +1697,7 @@ static int compress_impl(grkgpu_ctx *c, const grkgpu_image_desc *img, const grkg
             TileEnc tenc;
             tenc.tile = &tile;
             tenc.cblk = &cst;
-            tenc.passes = &passes;
+            tenc.passes = precs;
             tenc.layers = &layers;
             tenc.slopes = true;  // the pass-record fill above computed every block's slope range
             init_enc_pocs(cp, tenc);
@@ -2946,6 +3019,10 @@ extern "C" int grkgpu_dwt_inv(int32_t *buf, int32_t *scratch, uint32_t x0, uint3
 }
 
 static_assert(sizeof(grkgpu_enc_block) == sizeof(EncBlock), "EncBlock ABI");
+// the device's pass records are read in place as the host's (launch_pass_records)
+static_assert(sizeof(DevPass) == sizeof(EncPass) && offsetof(DevPass, dd) == offsetof(EncPass, dd) &&
+                  offsetof(DevPass, slope) == offsetof(EncPass, slope) && offsetof(DevPass, term) == offsetof(EncPass, term),
+              "DevPass layout");
 static_assert(sizeof(grkgpu_enc_result) == sizeof(EncResult), "EncResult ABI");
 static_assert(sizeof(grkgpu_dec_block) == sizeof(DecBlock), "DecBlock ABI");
 

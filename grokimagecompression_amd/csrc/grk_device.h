@@ -167,6 +167,29 @@ uint32_t t1_order_words(uint32_t nblocks);
 // Per-pass distortion sums of the blocks k_t1_model coded (same scratch and
 // maxdepth): nmsedec[pass] of every block, in the pass order of
 // t1_encode_cblk (t1.cpp:1222-1260).
+// Pass records formed on the device when a layer is rate-controlled: the
+// host's per-pass loop of the encoder (codec.cpp: rate, length, termination
+// t1.cpp:1131-1151, cumulative distortion t1.cpp:1249-1254 with
+// t1_getwmsedec :912-930, and the block's slope range, t2.cpp block_slopes)
+// moved next to the results it reads, so only records cross PCIe and the
+// host's Tier-2 starts at the layer formation.  DevPass has EncPass's layout
+// (t2.h; static_assert in codec.cpp); block i's records go to
+// out[pass0[i] .. pass0[i + 1]) -- slots sized from the band's bit-plane
+// bound -- and its summary to sum[i].
+struct DevPass {
+    uint32_t rate, len;
+    double dd;
+    uint16_t slope;
+    uint8_t term;
+};
+struct PassSum {
+    uint32_t numbps, numpasses, len, nsym;
+    uint32_t bad;  // 1: numbps above the band's bound, 2: more passes than slots, 4: MQ slab overflow
+    uint32_t z0;   // EncCblkState::z0
+    double smin, smax, s0max, disto;
+};
+hipError_t launch_pass_records(const EncBlock *blocks, const EncResult *res, const double *wfac, const uint64_t *pass0,
+                               uint32_t n, uint32_t cblksty, DevPass *out, PassSum *sum, hipStream_t s);
 hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, uint32_t maxdepth, const int32_t *coef,
                           const void *scratch, EncResult *res, hipStream_t s);
 // ubuf: unstuffed-stream arena; block i's region at ubuf + i * fixed_words

@@ -10,6 +10,7 @@
 
 #include "grk_device.h"
 #include "t1_flat.h"
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -934,6 +935,76 @@ hipError_t launch_t1_dist(const EncBlock *blocks, uint32_t n, uint32_t maxdepth,
     if (maxdepth < 1) maxdepth = 1;
     hipLaunchKernelGGL(k_t1_dist, dim3(n), dim3(64), 0, s, blocks, n, maxdepth, coef, (const uint8_t *)scratch, res,
                        nmse_lut());
+    return hipGetLastError();
+}
+
+// One thread per block (grk_device.h DevPass / PassSum).  The arithmetic is
+// the host's, operation for operation in IEEE double (no contraction: the
+// library builds with -ffp-contract=off), so the records are bit-identical.
+__global__ __launch_bounds__(256) void k_pass_records(const EncBlock *__restrict__ blocks,
+                                                      const EncResult *__restrict__ res, const double *__restrict__ wfac,
+                                                      const uint64_t *__restrict__ pass0, uint32_t n, uint32_t sty,
+                                                      DevPass *__restrict__ out, PassSum *__restrict__ sum) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const EncResult &r = res[i];
+    const EncBlock &b = blocks[i];
+    PassSum ps{};
+    ps.numbps = r.numbps;
+    ps.numpasses = r.numpasses;
+    ps.len = r.len;
+    ps.nsym = r.nsym;
+    const uint64_t p0 = pass0[i], cap = pass0[i + 1] - p0;
+    uint32_t np = r.numpasses;
+    if (r.pad) ps.bad |= 1u;
+    if (np > cap || np > GRK_MAX_PASSES) { ps.bad |= 2u; np = 0; }
+    if (np && r.rate[np - 1] > b.w * b.h * 4 + 64) ps.bad |= 4u;
+    if (ps.bad) np = 0;
+    const double f = wfac[i];
+    double cum = 0.0, mn = DBL_MAX, mx = -1, m0 = -HUGE_VAL;
+    uint32_t prev = 0, z0 = 0;
+    double prevdd = 0.0;
+    DevPass *o = out + p0;
+    for (uint32_t k = 0; k < np; ++k) {
+        DevPass d;
+        d.rate = r.rate[k];
+        d.len = d.rate - prev;
+        const int32_t bp = k == 0 ? (int32_t)r.numbps - 1 : (int32_t)r.numbps - 2 - (int32_t)((k - 1) / 3);
+        const int pt = k == 0 ? 2 : (int)((k - 1) % 3);
+        d.term = t1_pass_term(sty, bp, pt, r.numbps) ? 1 : 0;
+        d.slope = 0;
+        // t1_wmsedec_at (t2.h): factor * 2^bpno, squared with nmsedec / 8192
+        double w = f * (1 << bp);
+        w *= w * r.nmsedec[k] / 8192.0;
+        cum += w;
+        d.dd = cum;
+        o[k] = d;
+        // block_slopes (t2.cpp)
+        if (d.rate) { const double q = d.dd / d.rate; m0 = m0 < q ? q : m0; }
+        else if (d.dd != 0) z0 = 1;
+        const int32_t dr = k == 0 ? (int32_t)d.rate : (int32_t)(d.rate - prev);
+        const double ddd = k == 0 ? d.dd : d.dd - prevdd;
+        if (dr != 0) {
+            const double q = ddd / dr;
+            if (q < mn) mn = q;
+            if (q > mx) mx = q;
+        }
+        prev = d.rate;
+        prevdd = d.dd;
+    }
+    ps.z0 = z0;
+    ps.smin = mn;
+    ps.smax = mx;
+    ps.s0max = m0;
+    ps.disto = cum;
+    sum[i] = ps;
+}
+
+hipError_t launch_pass_records(const EncBlock *blocks, const EncResult *res, const double *wfac, const uint64_t *pass0,
+                               uint32_t n, uint32_t cblksty, DevPass *out, PassSum *sum, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pass_records, dim3((n + 255) / 256), dim3(256), 0, s, blocks, res, wfac, pass0, n, cblksty,
+                       out, sum);
     return hipGetLastError();
 }
 

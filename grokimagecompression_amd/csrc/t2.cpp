@@ -584,7 +584,7 @@ template <class W>
 void packet_header(const CodingParams &cp, TileEnc &te, Resolution &res, uint32_t precno, uint32_t layno, W &w) {
     std::vector<EncCblkState> &cs = *te.cblk;
     std::vector<EncLayer> &lay = *te.layers;
-    const std::vector<EncPass> &passes = *te.passes;
+    const EncPass *passes = te.passes;
     const uint32_t L = cp.numlayers;
     if (layno == 0) {
         for (uint32_t bandno = 0; bandno < res.numbands; ++bandno) {
@@ -1028,7 +1028,7 @@ void for_each_block(TileEnc &te, F f) {
 void set_layer(TileEnc &te, uint32_t gidx, uint32_t layno, uint32_t L, uint32_t cumul) {
     EncCblkState &s = (*te.cblk)[gidx];
     EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
-    const std::vector<EncPass> &P = *te.passes;
+    const EncPass *P = te.passes;
     ly.numpasses = cumul - s.incl_prev;
     if (!ly.numpasses) {
         ly.disto = 0;
@@ -1182,21 +1182,21 @@ uint32_t header_bits_ub(const RateProbe &rp, size_t i, const EncCblkState &s, co
 template <bool FEASIBLE, class T>
 void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool final, bool need_sum, RateProbe &rp) {
     const uint32_t L = cp.numlayers;
-    const std::vector<EncPass> &P = *te.passes;
+    const EncPass *P = te.passes;
     const size_t nb = te.blist.size();
     // true if the block's layer record changed; *dlen = its change of bytes
     auto eval = [&](size_t i, int64_t *dlen) -> bool {
         const uint32_t gidx = rp.gidx[i];
         EncCblkState &s = (*te.cblk)[gidx];
         uint32_t cumul;
-        if constexpr (FEASIBLE) cumul = feasible_cumul(s, P.data() + s.pass0, (uint32_t)thresh, &rp.bu[i].lo, &rp.bu[i].hi);
-        else cumul = simple_cumul(s, P.data() + s.pass0, te.slopes, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
+        if constexpr (FEASIBLE) cumul = feasible_cumul(s, P + s.pass0, (uint32_t)thresh, &rp.bu[i].lo, &rp.bu[i].hi);
+        else cumul = simple_cumul(s, P + s.pass0, te.slopes, (double)thresh, &rp.bd[i].lo, &rp.bd[i].hi);
         EncLayer &ly = (*te.layers)[(size_t)gidx * L + layno];
         const uint32_t old = ly.numpasses;
         const int64_t oldlen = old ? (int64_t)ly.len : 0;
         set_layer(te, gidx, layno, L, cumul);
         *dlen = (ly.numpasses ? (int64_t)ly.len : 0) - oldlen;
-        if (layno == 0) rp.ub[i] = header_bits_ub(rp, i, s, ly, P.data() + s.pass0);
+        if (layno == 0) rp.ub[i] = header_bits_ub(rp, i, s, ly, P + s.pass0);
         return ly.numpasses != old;
     };
     std::vector<uint32_t> &redo = rp.redo;
@@ -1239,7 +1239,7 @@ void form_layer(CodingParams &cp, TileEnc &te, uint32_t layno, T thresh, bool fi
     constexpr size_t PF = 6;
     auto prefetch = [&](size_t j) {
         const EncCblkState &sp = (*te.cblk)[rp.gidx[redo[j]]];
-        const char *pp = (const char *)(P.data() + sp.pass0);
+        const char *pp = (const char *)(P + sp.pass0);
         for (size_t o = 0; o < (size_t)sp.numpasses * sizeof(EncPass); o += 64) __builtin_prefetch(pp + o);
     };
     auto eval_range = [&](size_t a, size_t b) {
@@ -1396,7 +1396,7 @@ bool pcrd_simple(CodingParams &cp, TileEnc &te, uint64_t len) {
     const double K = 1;
     double min_slope = DBL_MAX, max_slope = -1;
     if (single_lossless(cp, te)) return true;
-    const std::vector<EncPass> &P = *te.passes;
+    const EncPass *P = te.passes;
     const double h0 = g_rt.on ? t2_ms() : 0;
     {  // min / max over every pass of every block (order-free), per chunk then combined
         std::mutex mu;
@@ -1525,11 +1525,11 @@ bool pcrd_feasible(CodingParams &cp, TileEnc &te, uint64_t len) {
         const double h0 = g_rt.on ? t2_ms() : 0;
         blocks_parallel(te, [&](Cblk &c) {
             EncCblkState &s = (*te.cblk)[c.gidx];
-            convex_hull(te.passes->data() + s.pass0, s.numpasses);
+            convex_hull(te.passes + s.pass0, s.numpasses);
         });
         for (Cblk *c : te.blist) {
             const EncCblkState &s = (*te.cblk)[c->gidx];
-            const EncPass *P = te.passes->data() + s.pass0;
+            const EncPass *P = te.passes + s.pass0;
             for (uint32_t pn = 0; pn < s.numpasses; ++pn)
                 if (P[pn].slope && P[pn].slope < min_slope) min_slope = P[pn].slope;
         }

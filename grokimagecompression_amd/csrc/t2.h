@@ -72,7 +72,7 @@ struct EncPoc {
 struct TileEnc {
     Tile *tile = nullptr;
     std::vector<EncCblkState> *cblk = nullptr;  // indexed by Cblk::gidx
-    std::vector<EncPass> *passes = nullptr;
+    EncPass *passes = nullptr;  // the pass records, block b's at passes[cblk[b].pass0 ...]
     std::vector<EncLayer> *layers = nullptr;    // [gidx * numlayers + layno]
     std::vector<EncPoc> pocs;                   // numpocs + 1 entries (at least one)
     uint32_t packno = 0;                        // SOP packet counter

@@ -147,7 +147,7 @@ int main(int argc, char **argv) {
         TileEnc te;
         te.tile = &tile;
         te.cblk = &cs;
-        te.passes = &ps;
+        te.passes = ps.data();
         te.layers = &layers;
         te.slopes = slopes;
         init_enc_pocs(cp, te);
