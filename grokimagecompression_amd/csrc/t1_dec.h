@@ -112,6 +112,10 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     uint32_t todo = nz & ~sig4 & ~vis4 & rows;
     const uint32_t todo0 = todo;
     uint32_t kind = 0, r = 0;  // 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo)
+    // the context of the next symbol when it is not a ZC one: AGG, then UNI
+    // after an aggregation 1, or the SC context read with the sign LUT -- set
+    // at the transitions, so a step only selects between it and the ZC LUT's
+    uint32_t cxn = CX_AGG;
     if (CUP && nr == 4 && P == 0 && vis4 == 0) {
         kind = 2;
     } else {
@@ -129,11 +133,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const uint32_t sh = 3 * r;
         const uint32_t zcx = T.zc[(P >> sh) & 0x1FF];  // read for every kind (LDS, in bounds)
         keep_here(zcx);
-        // context of the symbol kind, as mask arithmetic (a select chain
-        // here compiled to exec-mask branches around each arm)
-        const uint32_t m0 = 0u - (uint32_t)(kind == 0), m1 = 0u - (uint32_t)(kind == 1);
-        const uint32_t cx = (zcx & m0) | ((si & 0x7fu) & m1) |
-                            (((uint32_t)CX_AGG + (uint32_t)(kind > 2)) & ~(m0 | m1));
+        const uint32_t cx = kind == 0 ? zcx : cxn;
         const uint32_t bit = d.decode(cxw, T.mq, cx);
         if (kind == 2 && !bit) break;  // aggregation symbol 0: the column is done
         const bool k0 = kind == 0, k1 = kind == 1, k3 = kind == 3, k4 = kind == 4;
@@ -149,8 +149,12 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         r = k3 ? bit << 1 : k4 ? (r | bit) : r;
         todo = k4 ? rows & ~((2u << r) - 1) : todo;
         const bool advance = k1 || (k0 && !bit);
+        cxn = kind == 2 ? (uint32_t)CX_UNI : cxn;  // aggregation 1: the run position in UNI
         kind = k0 ? bit : k1 ? 0u : kind == 2 ? 3u : k3 ? 4u : 1u;
-        if (kind == 1 && !advance) si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
+        if (kind == 1 && !advance) {
+            si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
+            cxn = si & 0x7fu;
+        }
         todo = advance ? todo & ~((2u << r) - 1) : todo;
         if (advance && !todo) break;
         r = advance ? (uint32_t)__builtin_ctz(todo | 0x10u) : r;
