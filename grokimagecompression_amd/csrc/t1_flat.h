@@ -209,6 +209,12 @@ struct BitDecT {
         const bool cross = (u & 31u) < n;  // fewer than n bits left in w0
         w0 = cross ? w1 : w0;
         w1 = cross ? nextw : w1;
+        // the window moves here, before the rare branch: the old u and
+        // nextw die at once and their registers carry the new ones (left to
+        // itself the compiler sinks the selects past the branch and copies
+        // both at every step)
+        keep_here(w0);
+        keep_here(w1);
         u -= n;
         if (u < ulim) slow(u);
         nextw = bits.ring[ring_slot(u) << bits.rsh];
