@@ -633,13 +633,13 @@ __global__ __launch_bounds__(LANES * WAVES) __attribute__((amdgpu_waves_per_eu(W
                                                         const uint8_t *__restrict__ roi, uint32_t bpw) {
     __shared__ uint8_t s_zc[2048];
     __shared__ uint8_t s_sc[256];
-    __shared__ uint32_t s_mq[MQ_DEC_WORDS + 2];  // decoder words (t1_lane.h mq_dec_word)
+    __shared__ uint32_t s_mq[MQ_DEC_WORDS + 2];  // decoder successor table (t1_lane.h mq_dec_table_entry)
     __shared__ uint32_t s_cx[WAVES * LANES * DEC_CX_STRIDE];
     __shared__ uint32_t s_ring[WAVES * LANES * FB_RING];  // bit readers' word rings (t1_flat.h FlatBits), slot stride 64
     static_assert(LANES == 64, "the word rings interleave 64 lanes");
     for (uint32_t k = threadIdx.x; k < 2048; k += LANES * WAVES) s_zc[k] = zc_lut_entry(k >> 9, k & 511);
     for (uint32_t k = threadIdx.x; k < 256; k += LANES * WAVES) s_sc[k] = sc_win_entry(k);
-    for (uint32_t k = threadIdx.x; k < MQ_DEC_WORDS; k += LANES * WAVES) s_mq[k] = mq_dec_word(c_mq_tab, k);
+    for (uint32_t k = threadIdx.x; k < MQ_DEC_WORDS; k += LANES * WAVES) s_mq[k] = mq_dec_table_entry(c_mq_tab, k);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane >= bpw) return;  // bpw blocks per wavefront (t1_blocks_per_wave)

@@ -86,7 +86,7 @@ GRK_HD bool wave_any(bool p) {
 struct DecTables {
     const uint8_t *zc;   // 512 entries for this block's orientation
     const uint8_t *sc;   // 256, window order
-    const uint32_t *mq;  // MQ_DEC_WORDS decoder words (t1_lane.h mq_dec_word)
+    const uint32_t *mq;  // MQ_DEC_WORDS successor-table entries (t1_lane.h mq_dec_table_entry)
 };
 
 // significance propagation (CUP = false) or cleanup (CUP = true) of one

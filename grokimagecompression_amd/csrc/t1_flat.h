@@ -303,8 +303,9 @@ struct BitDecT {
     // << 16 and the context word carries Qe << 16 (mq_dec_word), so the
     // interval and the code register compare against Qe as it is loaded:
     // C < Qe << 16  <=>  C[31:16] < Qe, and the renormalisation shift is
-    // clz(A) directly.  The next word comes from the (state, MPS) table with
-    // the MPS flip already in it.  The renormalisation shifts the next n
+    // clz(A) directly.  The next word comes from the successor table
+    // (mq_dec_table_entry: the MPS flip already in it) at the word's own
+    // byte offset, + 512 for the LPS successor.  The renormalisation shifts the next n
     // window bits into C (a bit-field extract of the 32 window bits).
     GRK_HD uint32_t step(uint32_t &wd, const uint32_t *tab) {
         const uint32_t qe = wd & 0xffff0000u;
@@ -314,7 +315,7 @@ struct BitDecT {
         const bool keep = !lo && (int32_t)a < 0;  // MPS, no renormalisation
         C = lo ? C : C - qe;
         a = lo ? qe : a;
-        const uint32_t tw = tab[(wd >> (lps ? 8 : 1)) & 127u];
+        const uint32_t tw = *(const uint32_t *)((const char *)tab + ((wd & 0x1FCu) | (lps ? 512u : 0u)));
         const uint32_t n = clz32(a);
         const uint32_t win = alignbit32(w0, w1, u);
         C = (C << n) | bfe32(win, 32 - n, n);

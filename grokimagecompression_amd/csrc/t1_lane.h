@@ -141,26 +141,46 @@ GRK_HD void mq_reset_words(uint32_t *cxw, const uint32_t *tab) {
 }
 
 // The DECODER's context words (t1_flat.h BitDecT::step): one word per
-// (state, MPS) pair i = 2 state + mps, so an LPS exchange needs no MPS
-// arithmetic -- Qe[31:16] | next pair on LPS [14:8] | next pair on MPS [7:1]
-// | MPS [0] (the LPS successor already carries SWITCH's MPS flip).  Qe sits
-// where the decoder's A and C registers compare against it (A held << 16,
-// C[31:16] = Chigh), so the decision needs no shifts of it, and the decoded
-// bit is (word ^ LPS) & 1.  94 entries generated from the encoder table
-// (ISO 15444-1 Table C.2).
+// (state, MPS) pair i = 2 state + mps -- Qe[31:16] | i << 2 | MPS [0].  Qe
+// sits where the decoder's A and C registers compare against it (A held
+// << 16, C[31:16] = Chigh), so the decision needs no shifts of it; bits
+// [8:2] are the pair's byte offset in the successor table below, and the
+// decoded bit is (word ^ LPS) & 1.
 GRK_HD uint32_t mq_dec_word(const uint32_t *tab47, uint32_t i) {
-    const uint32_t st = i >> 1, m = i & 1, t = tab47[st];
-    const uint32_t qe = t & 0xffffu, nm = (t >> 16) & 63u, nl = (t >> 22) & 63u, sw = (t >> 28) & 1u;
-    return (qe << 16) | ((2 * nl + (m ^ sw)) << 8) | ((2 * nm + m) << 1) | m;
+    const uint32_t qe = tab47[i >> 1] & 0xffffu;
+    return (qe << 16) | (i << 2) | (i & 1u);
 }
-constexpr uint32_t MQ_DEC_WORDS = 94;
-// mqc_resetstates (mqc_dec.cpp:207-215) in decoder words: UNI -> 46, AGG -> 3,
-// ZC0 -> 4, every other context state 0, MPS 0
-GRK_HD void mq_reset_words_dec(uint32_t *cxw, const uint32_t *tab94) {
-    for (int i = 0; i < NUM_CX; ++i) cxw[i] = tab94[0];
-    cxw[CX_UNI] = tab94[2 * 46];
-    cxw[CX_AGG] = tab94[2 * 3];
-    cxw[CX_ZC] = tab94[2 * 4];
+// The successor table the decoder reads after every decision (LDS):
+// entry i (< 94) is the word of pair i's MPS successor, entry 128 + i that
+// of its LPS successor (SWITCH's MPS flip folded in), so the address is
+// (word & 0x1FC) | (LPS ? 512 : 0) bytes -- one op on the decision chain.
+// Entries 94..97 hold the reset words (mqc_resetstates, mqc_dec.cpp:207-215:
+// every context state 0 MPS 0, UNI -> 46, AGG -> 3, ZC0 -> 4).  ISO 15444-1
+// Table C.2 via the encoder table (Qe | NMPS<<16 | NLPS<<22 | SWITCH<<28).
+constexpr uint32_t MQ_DEC_WORDS = 128 + 94;
+GRK_HD uint32_t mq_dec_table_entry(const uint32_t *tab47, uint32_t k) {
+    if (k >= 128) {
+        const uint32_t i = k - 128, t = tab47[i >> 1], m = i & 1u;
+        return mq_dec_word(tab47, 2 * ((t >> 22) & 63u) + (m ^ ((t >> 28) & 1u)));
+    }
+    if (k < 94) {
+        const uint32_t t = tab47[k >> 1];
+        return mq_dec_word(tab47, 2 * ((t >> 16) & 63u) + (k & 1u));
+    }
+    switch (k) {
+        case 94: return mq_dec_word(tab47, 0);
+        case 95: return mq_dec_word(tab47, 2 * 46);
+        case 96: return mq_dec_word(tab47, 2 * 3);
+        case 97: return mq_dec_word(tab47, 2 * 4);
+        default: return 0;
+    }
+}
+// mqc_resetstates in decoder words, from the table's entries 94..97
+GRK_HD void mq_reset_words_dec(uint32_t *cxw, const uint32_t *dtab) {
+    for (int i = 0; i < NUM_CX; ++i) cxw[i] = dtab[94];
+    cxw[CX_UNI] = dtab[95];
+    cxw[CX_AGG] = dtab[96];
+    cxw[CX_ZC] = dtab[97];
 }
 
 // ---------------------------------------------------------------------------

@@ -113,8 +113,7 @@ if "--all" in sys.argv:
     for hb in order:
         key = hb.lstrip(".L")
         lb = [b for b in order if loopof.get(b) == key or b == hb]
-        if len(lb) < 2 or not any("offset:" in x and x.startswith("ds_read_b32") and "v_ffbh_u32" in " ".join(blocks[hb] + sum((blocks[c] for c in lb), []))
-                                  for b in lb for x in blocks[b]):
+        if len(lb) < 2 or not any(x.startswith("ds_read_b32") for b in lb for x in blocks[b]):
             continue
         if not any(x.startswith("v_ffbh_u32") for b in lb for x in blocks[b]):
             continue

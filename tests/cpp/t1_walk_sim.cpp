@@ -42,7 +42,7 @@ static uint64_t g_bypass[3];
 using namespace grkgpu;
 static const uint32_t kTab[47] = GRK_MQ_TABLE_INIT;
 static uint32_t kDecTab[MQ_DEC_WORDS];
-static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_word(kTab, i); return true; }();
+static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_table_entry(kTab, i); return true; }();
 static T1Scratch scr;
 
 // per block: passes -> stripes -> columns -> decisions

@@ -13,7 +13,7 @@
 using namespace grkgpu;
 static const uint32_t kTab[47] = GRK_MQ_TABLE_INIT;
 static uint32_t kDecTab[MQ_DEC_WORDS];
-static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_word(kTab, i); return true; }();
+static const bool kDecInit = [] { for (uint32_t i = 0; i < MQ_DEC_WORDS; ++i) kDecTab[i] = mq_dec_table_entry(kTab, i); return true; }();
 
 static uint64_t rng = 88172645463325252ull;
 static uint32_t rnd() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return (uint32_t)rng; }
