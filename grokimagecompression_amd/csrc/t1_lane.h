@@ -195,10 +195,13 @@ struct MqEncLane {
     uint32_t *out;     // 4-byte aligned
 };
 
+// acc's byte at pos is zero until pos is committed (acc starts at zero, is
+// zeroed with every store, and mqel_step_back clears the byte it re-opens),
+// so a commit is one shift-or
 GRK_HD void sink_commit(MqEncLane &e, int32_t pos, uint32_t byte) {
     if (pos < 0) return;  // the zero pad byte before the block
-    uint32_t sh = ((uint32_t)pos & 3u) * 8u;
-    e.acc = (e.acc & ~(0xFFu << sh)) | (byte << sh);
+    const uint32_t sh = ((uint32_t)pos & 3u) * 8u;
+    e.acc |= byte << sh;
     if ((pos & 3) == 3) { e.out[pos >> 2] = e.acc; e.acc = 0; }
 }
 
@@ -287,6 +290,7 @@ GRK_HD void mqel_step_back(MqEncLane &e) {
     } else {
         if ((nb >> 2) != (e.bp >> 2)) e.acc = e.out[nb >> 2];
         e.cur = (e.acc >> ((nb & 3) * 8)) & 0xffu;
+        e.acc &= ~(0xffu << ((nb & 3) * 8));  // open again (sink_commit ORs into it)
     }
     e.bp = nb;
 }
@@ -827,16 +831,21 @@ GRK_HD void t1_model_plane(uint32_t w, uint32_t h, uint32_t orient, const R &bit
 
 // BYTEOUT without data-dependent branches (mqc_enc.cpp:168-199): the carry
 // into a non-0xFF byte, then 7 or 8 bits out depending on whether the byte
-// before is 0xFF.  Clearing bit 27 before the 8-bit case is harmless: that bit
-// lands in bit 8 of the emitted value, which the byte store drops.
+// before is 0xFF.  Bit 27 of C is the carry into the previous byte unless
+// that byte is 0xFF, where it is the top bit of the 8 going out; the 8-bit
+// case drops it with the byte's mask (it lands in bit 8), the 7-bit case
+// after a carry made the byte 0xFF clears it (mqc_enc.cpp:186), and the new
+// C keeps only the sh bits below the byte either way.
 GRK_HD void mqel_byteout_bf(MqEncLane &e) {
-    const uint32_t carry = e.cur == 0xff ? 0u : (e.c >> 27) & 1u;
+    const bool big0 = e.cur == 0xff;
+    const uint32_t carry = big0 ? 0u : (e.c >> 27) & 1u;
     e.cur += carry;
-    e.c &= ~(carry << 27);
     const bool big = e.cur == 0xff;
-    const uint32_t byte = big ? (e.c >> 20) : (e.c >> 19);
-    e.c &= big ? 0xfffffu : 0x7ffffu;
-    e.ct = big ? 7u : 8u;
+    const uint32_t cm = big0 ? e.c : e.c & 0x7ffffffu;
+    const uint32_t sh = big ? 20u : 19u;
+    const uint32_t byte = (cm >> sh) & 0xffu;
+    e.c &= (1u << sh) - 1u;
+    e.ct = 27u - sh;
     mqel_emit(e, byte);
 }
 
