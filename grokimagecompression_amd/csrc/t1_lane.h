@@ -197,9 +197,11 @@ struct MqEncLane {
 
 // acc's byte at pos is zero until pos is committed (acc starts at zero, is
 // zeroed with every store, and mqel_step_back clears the byte it re-opens),
-// so a commit is one shift-or
+// so a commit is one shift-or.  The pad byte before the block (pos -1) is
+// committed like any other and lands in out[-1]: the caller leaves a dword
+// of headroom before `out` (codec.cpp's MQ slab: 16 bytes between blocks),
+// and nothing reads it back (mqel_byte_at answers 0 for pos < 0).
 GRK_HD void sink_commit(MqEncLane &e, int32_t pos, uint32_t byte) {
-    if (pos < 0) return;  // the zero pad byte before the block
     const uint32_t sh = ((uint32_t)pos & 3u) * 8u;
     e.acc |= byte << sh;
     if ((pos & 3) == 3) { e.out[pos >> 2] = e.acc; e.acc = 0; }

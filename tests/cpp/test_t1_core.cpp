@@ -64,10 +64,12 @@ int main(int argc, char **argv) {
                 t1_model_plane<const uint64_t *, uint64_t *>(w, h, orient, scr.pa + p * 64, scr.pb + p * 64, ref,
                                                              p + 1 < lnb, scr.st.neg, tmp, sc, base, scr.cnt + p * 4);
             }
-            std::vector<uint32_t> sout(w * h * 2 + 64, 0);
+            // a dword of headroom before the output (the pad byte's commit)
+            std::vector<uint32_t> sbuf(w * h * 2 + 64 + 1, 0);
+            uint32_t *sout = sbuf.data() + 1;
             uint32_t srate[100], slen = 0;
-            uint32_t snp = t1_mq_block(lnb, sym.data(), slot / 4, scr.cnt, kTab, cx, sout.data(), srate, &slen);
-            bool sok = lnb == onb && (int)snp == onp && slen == olen && memcmp(sout.data(), obuf.data() + 1, olen) == 0;
+            uint32_t snp = t1_mq_block(lnb, sym.data(), slot / 4, scr.cnt, kTab, cx, sout, srate, &slen);
+            bool sok = lnb == onb && (int)snp == onp && slen == olen && memcmp(sout, obuf.data() + 1, olen) == 0;
             for (int p = 0; sok && p < onp; ++p) sok = srate[p] == op[p].rate;
             if (!sok) {
                 printf("ENC MISMATCH it=%d w=%u h=%u orient=%u q=%d np %u/%d nb %u/%u len %u/%u\n", it, w, h, orient,
