@@ -524,7 +524,12 @@ int grkgpu_dwt_inv(int32_t *buf, int32_t *scratch, uint32_t x0, uint32_t y0, uin
 /* Code-block descriptors for the T1 entry points (all device memory). */
 typedef struct {
     uint64_t coef_off;    /* element offset of the block's top-left in `coef` */
-    uint64_t out_off;     /* byte offset in `out`; out[out_off - 1] must be 0 */
+    uint64_t out_off;     /* byte offset in `out`, a multiple of 4 and >= 4: the
+                             block's bytes start there, and the encoder writes
+                             zeros to out[out_off - 4 .. out_off - 1] (the MQ
+                             coder's pad byte before the block, Grok's
+                             bp = start - 1, committed with its dword), so no
+                             other block's bytes may lie there */
     uint32_t stride, w, h, orient; /* orient = band number 0:LL 1:HL 2:LH 3:HH */
     int32_t qmfbid, inv_step;      /* qmfbid 1 = 5/3, 0 = 9/7 (13-bit inv step) */
 } grkgpu_enc_block;
