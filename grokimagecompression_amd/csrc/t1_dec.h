@@ -40,12 +40,14 @@ GRK_HD uint8_t sc_win_entry(uint32_t i) {
 }
 
 // 18-bit 3x6 window of column x: bits 3i..3i+2 = row i (k-1+i), columns x-1..x+1
+// (column 0: the rows' bits 0..2 moved up one, the left column zero -- one
+// shift and mask of the whole window instead of a per-row shift)
 GRK_HD uint32_t win18(const uint64_t *r6, uint32_t x) {
-    const uint32_t s1 = x ? x - 1 : 0, m = x ? 7u : 3u, s2 = x ? 0u : 1u;
+    const uint32_t s1 = x ? x - 1 : 0;
     uint32_t P = 0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) P |= ((((uint32_t)(r6[i] >> s1)) & m) << s2) << (3 * i);
-    return P;
+    for (int i = 0; i < 6; ++i) P |= (((uint32_t)(r6[i] >> s1)) & 7u) << (3 * i);
+    return x ? P : (P << 1) & 0x36DB6u;
 }
 
 GRK_HD uint32_t col4(const uint64_t *r4, uint32_t x) {
