@@ -50,20 +50,23 @@ GRK_HD uint32_t win18(const uint64_t *r6, uint32_t x) {
     return x ? P : (P << 1) & 0x36DB6u;
 }
 
-GRK_HD uint32_t col4(const uint64_t *r4, uint32_t x) {
+// A column's four rows as a mask in the window's row spacing: row i at bit
+// 3i (SPREAD), so a row's bit position is also its window shift
+constexpr uint32_t SPREAD4 = 0x249u;  // rows 0..3
+GRK_HD uint32_t col4s(const uint64_t *r4, uint32_t x) {
     uint32_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v |= (uint32_t)((r4[i] >> x) & 1) << i;
+    for (int i = 0; i < 4; ++i) v |= (uint32_t)((r4[i] >> x) & 1) << (3 * i);
     return v;
 }
 
-GRK_HD void setcol4(uint64_t *r4, uint32_t x, uint32_t bits) {
+GRK_HD void setcol4s(uint64_t *r4, uint32_t x, uint32_t bits) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r4[i] |= (uint64_t)((bits >> i) & 1) << x;
+    for (int i = 0; i < 4; ++i) r4[i] |= (uint64_t)((bits >> (3 * i)) & 1) << x;
 }
 
-// self bits of the window (rows k..k+3 of column x)
-GRK_HD uint32_t win_self4(uint32_t P) { return ((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 8) & 4) | ((P >> 10) & 8); }
+// self bits of the window (rows k..k+3 of column x), spread
+GRK_HD uint32_t win_self4s(uint32_t P) { return (P >> 4) & SPREAD4; }
 
 // Keep v computed at this point for every lane: stops the compiler from
 // sinking its producer (an LDS read) into a branch around its one use.
@@ -100,20 +103,22 @@ template <int CUP_, class D>
 GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32_t x, uint32_t nr, bool cup_rt = false) {
     const bool CUP = CUP_ < 0 ? cup_rt : CUP_ != 0;
     T1_WALK(2, x);
+    // row masks are spread (row r at bit 3r: col4s), so the current row's
+    // position p = 3r is its window shift as it stands
     uint32_t P = win18(s.sig, x);
-    const uint32_t vis4 = col4(s.vis, x);
-    const uint32_t rows = (1u << nr) - 1;
-    const uint32_t sig4 = win_self4(P);
-    uint32_t nz = 0xF;  // SPP: rows with a significant neighbour
+    const uint32_t vis4 = col4s(s.vis, x);
+    const uint32_t rows = SPREAD4 >> (12 - 3 * nr);
+    const uint32_t sig4 = win_self4s(P);
+    uint32_t nz = SPREAD4;  // SPP: rows with a significant neighbour
     if (CUP_ <= 0) {
         uint32_t z = 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) z |= (((P >> (3 * r)) & 0x1EF) != 0 ? 1u : 0u) << r;
-        nz = CUP ? 0xFu : z;
+        for (int r = 0; r < 4; ++r) z |= (((P >> (3 * r)) & 0x1EF) != 0 ? 1u : 0u) << (3 * r);
+        nz = CUP ? SPREAD4 : z;
     }
     uint32_t todo = nz & ~sig4 & ~vis4 & rows;
     const uint32_t todo0 = todo;
-    uint32_t kind = 0, r = 0;  // 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo)
+    uint32_t kind = 0, p = 0;  // kind: 0 ZC, 1 SC, 2 AGG, 3 UNI(hi), 4 UNI(lo); p = 3 x row
     // the context of the next symbol when it is not a ZC one: AGG, then UNI
     // after an aggregation 1, or the SC context read with the sign LUT -- set
     // at the transitions, so a step only selects between it and the ZC LUT's
@@ -122,7 +127,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         kind = 2;
     } else {
         if (!todo) return false;
-        r = (uint32_t)__builtin_ctz(todo);
+        p = (uint32_t)__builtin_ctz(todo);
     }
     // the sign window, read at the column start by every lane: a lane's first
     // sign symbol comes at almost every decision step of a wavefront, so a
@@ -132,8 +137,7 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
     // a wavefront sit in different kinds, and every branch taken by any lane
     // costs the whole wavefront its exec-mask bookkeeping.
     for (;;) {
-        const uint32_t sh = 3 * r;
-        const uint32_t zcx = T.zc[(P >> sh) & 0x1FF];  // read for every kind (LDS, in bounds)
+        const uint32_t zcx = T.zc[(P >> p) & 0x1FF];  // read for every kind (LDS, in bounds)
         keep_here(zcx);
         const uint32_t cx = kind == 0 ? zcx : cxn;
         const uint32_t bit = d.decode(cxw, T.mq, cx);
@@ -143,32 +147,32 @@ GRK_HD bool d3_column(D &d, uint32_t *cxw, const DecTables &T, Stripe &s, uint32
         const uint32_t sg = bit ^ ((D::kLazy && d.raw) ? 0u : (si >> 7));  // a raw sign is the sign itself
         // the new significance and sign go into the windows only: the
         // column's new rows are read back from them once, after the loop
-        P |= k1 ? 1u << (sh + 4) : 0u;
-        Q |= k1 ? sg << (sh + 4) : 0u;
+        P |= k1 ? 1u << (p + 4) : 0u;
+        Q |= k1 ? sg << (p + 4) : 0u;
         // the sample below now has a significant neighbour (SPP)
-        todo |= (!CUP && k1) ? (rows & ~(sig4 | vis4)) & (2u << r) : 0u;
-        // UNI, UNI: the run position; the rows after it are plain ZC
-        r = k3 ? bit << 1 : k4 ? (r | bit) : r;
-        todo = k4 ? rows & ~((2u << r) - 1) : todo;
+        todo |= (!CUP && k1) ? (rows & ~(sig4 | vis4)) & (8u << p) : 0u;
+        // UNI, UNI: the run position (row 2 bit1 + bit0); the rows after it are plain ZC
+        p = k3 ? (bit ? 6u : 0u) : k4 ? p + (bit ? 3u : 0u) : p;
+        todo = k4 ? rows & ~((8u << p) - 1) : todo;
         const bool advance = k1 || (k0 && !bit);
         cxn = kind == 2 ? (uint32_t)CX_UNI : cxn;  // aggregation 1: the run position in UNI
         kind = k0 ? bit : k1 ? 0u : kind == 2 ? 3u : k3 ? 4u : 1u;
         if (kind == 1 && !advance) {
-            si = T.sc[(((P >> (3 * r)) & 0xAA) >> 1) | ((Q >> (3 * r)) & 0xAA)];
+            si = T.sc[(((P >> p) & 0xAA) >> 1) | ((Q >> p) & 0xAA)];
             cxn = si & 0x7fu;
         }
-        todo = advance ? todo & ~((2u << r) - 1) : todo;
+        todo = advance ? todo & ~((8u << p) - 1) : todo;
         if (advance && !todo) break;
-        r = advance ? (uint32_t)__builtin_ctz(todo | 0x10u) : r;
+        p = advance ? (uint32_t)__builtin_ctz(todo | (1u << 12)) : p;
     }
-    const uint32_t newsig = win_self4(P) & ~sig4;
+    const uint32_t newsig = win_self4s(P) & ~sig4;
     // SPP: every row of the column's candidates was visited (a ZC symbol),
     // the rows a new significant sample above made candidates included
-    const uint32_t newvis = todo0 | ((newsig << 1) & rows & ~(sig4 | vis4));
-    if (!CUP && newvis) setcol4(s.vis, x, newvis);
+    const uint32_t newvis = todo0 | ((newsig << 3) & rows & ~(sig4 | vis4));
+    if (!CUP && newvis) setcol4s(s.vis, x, newvis);
     if (newsig) {
-        setcol4(s.sig + 1, x, newsig);
-        setcol4(s.neg + 1, x, win_self4(Q) & newsig);
+        setcol4s(s.sig + 1, x, newsig);
+        setcol4s(s.neg + 1, x, win_self4s(Q) & newsig);
         return true;
     }
     return false;
